@@ -1,0 +1,136 @@
+"""Weight ingestion: reference checkpoints -> plain float32 tensors under reference names.
+
+Handles the on-disk formats of the path:
+  - RVC ``.pth`` (zip dict with ``weight``/``config``/``f0``/``version``/``sr``),
+    fp16 tensors, weight-norm pairs ``*.weight_g``/``*.weight_v``
+    (rvc/train/process/extract_model.py:57-109), loaded with
+    ``torch.load(weights_only=True)`` only.
+  - live torch parametrization names ``*.parametrizations.weight.original0/1``.
+  - MLX ``.npz`` / ``.safetensors`` exported by tools/convert_rvc_model.py are
+    NOT accepted here (their fusion adds +1e-8 to the norm,
+    tools/convert_rvc_model.py:357); they carry already-fused weights under
+    remapped keys, see ``unmap_mlx_keys``.
+
+Weight-norm fusion matches torch exactly (``torch._weight_norm``: w = g * v / ||v||,
+norm over every dim except ``dim``, no epsilon). ``dim`` is 0 for every RVC conv
+(for ConvTranspose1d that is the input-channel axis) and 2 for the HuBERT
+positional conv (modeling_hubert.py HubertPositionalConvEmbedding).
+"""
+from __future__ import annotations
+
+import re
+from typing import Dict, Mapping
+
+import numpy as np
+
+_WN_PAIRS = (
+    (".weight_g", ".weight_v"),
+    (".parametrizations.weight.original0", ".parametrizations.weight.original1"),
+)
+
+
+def _wn_dim(g_shape) -> int:
+    """Infer the weight-norm ``dim`` from the shape of g (all ones except ``dim``)."""
+    non1 = [i for i, s in enumerate(g_shape) if s != 1]
+    if len(non1) == 1:
+        return non1[0]
+    if len(non1) == 0:
+        return 0
+    raise ValueError(f"cannot infer weight_norm dim from g shape {tuple(g_shape)}")
+
+
+def fuse_weight_norm(v: np.ndarray, g: np.ndarray) -> np.ndarray:
+    import torch
+
+    dim = _wn_dim(g.shape)
+    tv = torch.from_numpy(np.ascontiguousarray(v, dtype=np.float32))
+    tg = torch.from_numpy(np.ascontiguousarray(g, dtype=np.float32))
+    return torch._weight_norm(tv, tg, dim).numpy().astype(np.float32)
+
+
+def normalize_state(sd: Mapping[str, object]) -> Dict[str, np.ndarray]:
+    """Fuse weight-norm pairs, cast to float32 numpy, drop non-float bookkeeping."""
+    arrs: Dict[str, np.ndarray] = {}
+    for k, v in sd.items():
+        if hasattr(v, "detach"):
+            v = v.detach().cpu()
+            v = v.float().numpy() if v.is_floating_point() else v.numpy()
+        arrs[k] = np.asarray(v)
+    out: Dict[str, np.ndarray] = {}
+    used = set()
+    for k, v in arrs.items():
+        for gs, vs in _WN_PAIRS:
+            if k.endswith(gs):
+                base = k[: -len(gs)]
+                vk = base + vs
+                if vk not in arrs:
+                    raise KeyError(f"weight-norm pair incomplete: {k} without {vk}")
+                out[base + ".weight"] = fuse_weight_norm(arrs[vk], v)
+                used.update((k, vk))
+    for k, v in arrs.items():
+        if k in used:
+            continue
+        if k.endswith("num_batches_tracked"):
+            continue
+        if not np.issubdtype(v.dtype, np.floating):
+            raise TypeError(f"non-float tensor {k} ({v.dtype}) in a weight dict")
+        out[k] = np.ascontiguousarray(v, dtype=np.float32)
+    return out
+
+
+def load_rvc_checkpoint(path: str):
+    """Load an RVC ``.pth`` with the non-executing loader. Returns (state, cfg_list, meta)."""
+    import torch
+
+    cpt = torch.load(path, map_location="cpu", weights_only=True)
+    if "weight" not in cpt:
+        raise ValueError(f"{path}: not an RVC inference checkpoint (no 'weight' key)")
+    state = {k: v for k, v in cpt["weight"].items() if not k.startswith("enc_q.")}
+    meta = {k: cpt.get(k) for k in ("f0", "version", "sr", "vocoder")}
+    return normalize_state(state), list(cpt.get("config", [])), meta
+
+
+def load_state_file(path: str) -> Dict[str, np.ndarray]:
+    """Load a bare state dict (``rmvpe.pt``, ``pytorch_model.bin``, ``.safetensors``, ``.npz``)."""
+    if path.endswith(".safetensors"):
+        from safetensors.numpy import load_file
+
+        return normalize_state(load_file(path))
+    if path.endswith(".npz"):
+        with np.load(path, allow_pickle=False) as z:
+            return normalize_state({k: z[k] for k in z.files})
+    import torch
+
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    if isinstance(sd, dict) and "weight" in sd and isinstance(sd["weight"], dict):
+        sd = sd["weight"]
+    return normalize_state(sd)
+
+
+_MLX_RULES = [
+    (re.compile(r"^dec\.resblock_(\d+)\.c([12])_(\d+)\.(.*)$"), r"dec.resblocks.\1.convs\2.\3.\4"),
+    (re.compile(r"^dec\.up_(\d+)\.(.*)$"), r"dec.ups.\1.\2"),
+    (re.compile(r"^dec\.noise_conv_(\d+)\.(.*)$"), r"dec.noise_convs.\1.\2"),
+    (re.compile(r"^enc_p\.encoder\.attn_(\d+)\.(.*)$"), r"enc_p.encoder.attn_layers.\1.\2"),
+    (re.compile(r"^enc_p\.encoder\.norm1_(\d+)\.(.*)$"), r"enc_p.encoder.norm_layers_1.\1.\2"),
+    (re.compile(r"^enc_p\.encoder\.norm2_(\d+)\.(.*)$"), r"enc_p.encoder.norm_layers_2.\1.\2"),
+    (re.compile(r"^enc_p\.encoder\.ffn_(\d+)\.(.*)$"), r"enc_p.encoder.ffn_layers.\1.\2"),
+    (re.compile(r"^flow\.flow_(\d+)\.enc\.in_layer_(\d+)\.(.*)$"), r"flow.flows.\1.enc.in_layers.\2.\3"),
+    (re.compile(r"^flow\.flow_(\d+)\.enc\.res_skip_layer_(\d+)\.(.*)$"), r"flow.flows.\1.enc.res_skip_layers.\2.\3"),
+    (re.compile(r"^flow\.flow_(\d+)\.(.*)$"), r"flow.flows.\1.\2"),
+]
+
+
+def unmap_mlx_keys(keys) -> Dict[str, str]:
+    """Inverse of rvc_mlx/infer/infer_mlx.py:17-89 ``remap_keys`` (name mapping only)."""
+    out = {}
+    for k in keys:
+        n = k
+        for pat, rep in _MLX_RULES:
+            if pat.match(n):
+                n = pat.sub(rep, n)
+                break
+        if n.startswith("enc_p.encoder.norm_layers_"):
+            n = n.replace(".weight", ".gamma").replace(".bias", ".beta")
+        out[k] = n
+    return out
