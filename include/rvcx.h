@@ -1,0 +1,130 @@
+/*
+ * rvcx — MI355X-native RVC v2 inference engine: public C ABI.
+ *
+ * Plain pointers and sizes only. All d_* pointers are device (HBM) pointers owned by the
+ * caller (e.g. torch tensors' data_ptr()); every compute call is asynchronous on the given
+ * hipStream_t (passed as void*; NULL = the null stream). The context owns the uploaded
+ * weights, the workspace and the RNG state; one context = one device, one host thread at a
+ * time. Every function returns an rvcx_status (0 = ok, < 0 = error); the message of the
+ * last error is rvcx_last_error(ctx). Nothing prints and continues.
+ *
+ * The reference (Acelogic/Retrieval-based-Voice-Conversion-MLX) has no native code on this
+ * path; each entry point below replaces a Python-level interface of the reference, cited
+ * file:line (paths relative to the reference root).
+ */
+#ifndef RVCX_H_
+#define RVCX_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct rvcx_ctx rvcx_ctx;
+
+typedef enum {
+  RVCX_OK = 0,
+  RVCX_E_INVALID = -1, /* bad argument (null pointer, negative size, unknown name) */
+  RVCX_E_SHAPE = -2,   /* tensor shape / length does not match the model */
+  RVCX_E_HIP = -3,     /* HIP runtime error or kernel launch failure */
+  RVCX_E_OOM = -4,     /* device allocation failed */
+  RVCX_E_STATE = -5,   /* model not finalized / weights missing */
+  RVCX_E_CAPACITY = -6 /* caller's output buffer too small */
+} rvcx_status;
+
+typedef enum { RVCX_MODEL_SYNTH = 0, RVCX_MODEL_HUBERT = 1, RVCX_MODEL_RMVPE = 2 } rvcx_model;
+
+/* Synthesizer hyper-parameters = the 18-element ``cpt["config"]`` list of an RVC .pth
+ * (rvc/train/process/extract_model.py:62-81) plus text_enc_hidden_dim (768 for v2). */
+typedef struct {
+  int inter_channels, hidden_channels, filter_channels, n_heads, n_layers, kernel_size;
+  int n_resblocks;                  /* len(resblock_kernel_sizes) (3) */
+  int resblock_kernel_sizes[4];
+  int resblock_dilation_sizes[4][4];
+  int n_dilations;                  /* len of each dilation list (3) */
+  int n_upsample;                   /* len(upsample_rates) (4) */
+  int upsample_rates[8];
+  int upsample_initial_channel;
+  int upsample_kernel_sizes[8];
+  int spk_embed_dim, gin_channels, sr, text_enc_hidden_dim;
+} rvcx_synth_desc;
+
+/* Create a context on HIP device `device`. */
+int rvcx_create(rvcx_ctx** out, int device);
+int rvcx_destroy(rvcx_ctx* ctx);
+const char* rvcx_last_error(const rvcx_ctx* ctx);
+
+/* Model structure (replaces Synthesizer(*cpt["config"]) in rvc/infer/infer.py:467-488 and
+ * the hard-coded defaults of rvc_mlx/infer/infer_mlx.py:130-244). */
+int rvcx_set_synth_config(rvcx_ctx* ctx, const rvcx_synth_desc* desc);
+
+/* Weight ingestion: one fp32 host tensor in the REFERENCE layout under its REFERENCE
+ * state-dict name (weight-norm already fused to ``.weight``; BatchNorm as its 4 tensors).
+ * Replaces load_state_dict in rvc/infer/infer.py:480-486 (synth), HubertModel
+ * from_pretrained in rvc/lib/utils.py:125-153 (hubert), RMVPE0Predictor.__init__
+ * torch.load in rvc/lib/predictors/RMVPE.py:429-434 (rmvpe). */
+int rvcx_upload(rvcx_ctx* ctx, int model, const char* name, const float* host, const int64_t* shape, int ndim);
+/* Validate names/shapes, fold BatchNorm, repack to kernel layouts, copy to HBM. */
+int rvcx_finalize(rvcx_ctx* ctx, int model);
+
+/* HuBERT/ContentVec: hubert_model(audio[1,N])["last_hidden_state"] -> [L][768] (v2) or final_proj
+ * [L][256] (v1). Replaces transformers HubertModel.forward as called at rvc/infer/pipeline.py:331-334
+ * and rvc_mlx/lib/mlx/hubert.py:174-201 (pipeline_mlx.py:172-173). */
+int rvcx_hubert(rvcx_ctx* ctx, const float* d_audio, int64_t n, int version, float* d_feats, int64_t cap_rows,
+                int64_t* rows_out, void* stream);
+
+/* RMVPE: RMVPE0Predictor.infer_from_audio(audio, thred) -> f0 (fp64, [F], F = 1 + n/160).
+ * Replaces rvc/lib/predictors/RMVPE.py:497-513 and rvc_mlx/lib/mlx/rmvpe.py:408-412.
+ * d_hidden (optional, [F][360] fp32) receives the salience (mel2hidden output). */
+int rvcx_rmvpe(rvcx_ctx* ctx, const float* d_audio, int64_t n, float thred, double* d_f0, int64_t cap_frames,
+               int64_t* frames_out, float* d_hidden, void* stream);
+
+/* f0 post-processing of Pipeline.get_f0 (rvc/infer/pipeline.py:278-291): f0 *= 2^(semitones/12),
+ * mel quantisation to coarse 1..255. Writes coarse (int32), pitchf (fp32) and shifted f0 (fp64, optional). */
+int rvcx_f0_post(rvcx_ctx* ctx, const double* d_f0, int64_t F, double semitones, int32_t* d_coarse, float* d_pitchf,
+                 double* d_f0_shifted, void* stream);
+
+/* Synthesizer.infer (rvc/lib/algorithm/synthesizers.py:206-243; rvc_mlx/lib/mlx/synthesizers.py:193-235).
+ * phone [B][T][E], lengths [B], pitch [B][T], pitchf [B][T], sid [B] -> out [B][T*upp].
+ * d_eps_z ([B][I][T], reference layout of randn_like(m_p)) and d_eps_src ([B][T*upp], randn_like at
+ * generators/hifigan.py:223) are optional injected noise; when NULL the noise is drawn from the
+ * context's Philox stream keyed by `seed`. d_zp / d_z (optional, [B][T][I]) receive z_p and z. */
+int rvcx_synth_infer(rvcx_ctx* ctx, int B, int T, const float* d_phone, const int32_t* d_lengths,
+                     const int32_t* d_pitch, const float* d_pitchf, const int32_t* d_sid, const float* d_eps_z,
+                     const float* d_eps_src, uint64_t seed, float* d_out, float* d_zp, float* d_z, void* stream);
+
+/* HiFiGAN-NSF generator alone (config C3): dec(z, f0, g=emb_g(sid)) with z in reference layout
+ * [B][I][T] (rvc/lib/algorithm/generators/hifigan_nsf.py:173-212). out [B][T*upp]. */
+int rvcx_dec_only(rvcx_ctx* ctx, int B, int T, const float* d_z, const float* d_f0, const int32_t* d_sid,
+                  const float* d_eps_src, uint64_t seed, float* d_out, void* stream);
+
+/* Pipeline.voice_conversion on one padded chunk (rvc/infer/pipeline.py:293-376 with index_rate = 0;
+ * rvc_mlx/infer/pipeline_mlx.py:166-261): HuBERT -> x2 nearest upsample -> protect blend ->
+ * Synthesizer.infer, all on device. d_audio [n] @16 kHz (already filtered and padded);
+ * d_pitch/d_pitchf [>= n/160]. Output out [p_len*upp], p_len = min(n/160, 2L). */
+int rvcx_voice_conversion(rvcx_ctx* ctx, const float* d_audio, int64_t n, const int32_t* d_pitch,
+                          const float* d_pitchf, int sid, float protect, const float* d_eps_z, const float* d_eps_src,
+                          uint64_t seed, float* d_out, int64_t cap, int64_t* n_out, void* stream);
+
+/* Pipeline high-pass (rvc/infer/pipeline.py:22-27: signal.butter(5, 48, 'high', fs=16000)) as
+ * transfer-function coefficients b[order+1], a[order+1] and lfilter_zi(b, a) zi[order]; used by
+ * rvcx_pipeline's zero-phase filtfilt (padtype 'odd', padlen 3*(order+1)). */
+int rvcx_set_highpass(rvcx_ctx* ctx, const double* b, const double* a, const double* zi, int order);
+
+/* Pipeline.pipeline for one utterance whose padded length fits one chunk (<= t_max), all on device
+ * (rvc/infer/pipeline.py:390-558 with pitch_guidance, index_rate 0, volume_envelope 1;
+ * rvc_mlx/infer/pipeline_mlx.py:263-373): filtfilt(audio) -> reflect pad t_pad -> RMVPE (thred 0.03)
+ * -> f0 * 2^(semitones/12), coarse -> voice_conversion -> trim t_pad_tgt per side -> peak-normalise.
+ * d_audio [n] fp64 @16 kHz; out fp32 @tgt_sr; d_f0 (optional) receives the shifted f0 [1 + (n+2 t_pad)/160]. */
+int rvcx_pipeline(rvcx_ctx* ctx, const double* d_audio, int64_t n, int sid, double semitones, float protect,
+                  int64_t t_pad, int64_t t_pad_tgt, const float* d_eps_z, const float* d_eps_src, uint64_t seed,
+                  float* d_out, int64_t cap, int64_t* n_out, double* d_f0, void* stream);
+
+/* Upsampling factor of the loaded synthesizer (prod(upsample_rates); net_g.dec.upp). */
+int rvcx_synth_upp(const rvcx_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RVCX_H_ */

@@ -1,0 +1,805 @@
+// Non-GEMM kernels of the RVC path: NSF source (SineGen), noise convs, conv_post, norms,
+// softmax with relative-position bands, layout transforms, RNG, RMVPE front/back end.
+// Elementwise / reduction work here is HBM- or latency-bound; every kernel keeps channels
+// contiguous (time-major rows) so a wave reads whole 128-B lines.
+#include <cmath>
+
+#include "rvcx_kernels.h"
+
+namespace rvcx {
+
+namespace {
+
+constexpr int TB = 256;
+
+inline unsigned nblocks(long long n, int per = TB) {
+  long long b = (n + per - 1) / per;
+  if (b > 65535LL * 32) b = 65535LL * 32;
+  return (unsigned)(b < 1 ? 1 : b);
+}
+
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float warp_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---- Philox4x32-10 (counter-based; one 128-bit block per 4 normals)
+__device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+    c[1] = (uint32_t)p1;
+    c[3] = (uint32_t)p0;
+    c[0] = n0;
+    c[2] = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+__device__ __forceinline__ float normal_at(uint64_t seed, uint64_t idx) {
+  uint32_t c[4] = {(uint32_t)(idx >> 1), (uint32_t)(idx >> 33), 0x52564358u, 0u};
+  philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  const float u1 = ((c[0] >> 8) + 1) * (1.0f / 16777217.0f);
+  const float u2 = (c[1] >> 8) * (1.0f / 16777216.0f);
+  const float r = sqrtf(-2.f * logf(u1));
+  const float th = 6.283185307179586f * u2;
+  return (idx & 1) ? r * sinf(th) : r * cosf(th);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ simple maps
+__global__ void k_fill(float* p, float v, long long n) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+hipError_t fill(float* p, float v, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(k_fill, dim3(nblocks(n)), dim3(TB), 0, s, p, v, n);
+  return hipGetLastError();
+}
+
+__global__ void k_randn(float* y, long long n, uint64_t seed, uint64_t off) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    y[i] = normal_at(seed, off + i);
+}
+hipError_t randn(float* y, long long n, uint64_t seed, uint64_t offset, hipStream_t s) {
+  hipLaunchKernelGGL(k_randn, dim3(nblocks(n)), dim3(TB), 0, s, y, n, seed, offset);
+  return hipGetLastError();
+}
+
+__global__ void k_act(float* x, long long n, int act, float slope) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    float v = x[i];
+    switch (act) {
+      case ACT_LRELU: v = v > 0.f ? v : v * slope; break;
+      case ACT_RELU: v = v > 0.f ? v : 0.f; break;
+      case ACT_GELU: v = 0.5f * v * (1.f + erff(v * 0.70710678118654752440f)); break;
+      case ACT_TANH: v = tanhf(v); break;
+      case ACT_SIGMOID: v = 1.f / (1.f + expf(-v)); break;
+      default: break;
+    }
+    x[i] = v;
+  }
+}
+hipError_t act_inplace(float* x, long long n, int act, float slope, hipStream_t s) {
+  hipLaunchKernelGGL(k_act, dim3(nblocks(n)), dim3(TB), 0, s, x, n, act, slope);
+  return hipGetLastError();
+}
+
+__global__ void k_affine(float* x, long long n, float a, float b) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    x[i] = x[i] * a + b;
+}
+hipError_t affine_inplace(float* x, long long n, float a, float b, hipStream_t s) {
+  hipLaunchKernelGGL(k_affine, dim3(nblocks(n)), dim3(TB), 0, s, x, n, a, b);
+  return hipGetLastError();
+}
+
+// [B][C][T] -> [B][T][C] and back, 32x32 LDS tiles
+__global__ void k_tr(const float* x, float* y, int R, int Cc, long long ld_in, long long ld_out, long long bs_in,
+                     long long bs_out) {
+  __shared__ float t[32][33];
+  const int b = blockIdx.z;
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const float* X = x + b * bs_in;
+  float* Y = y + b * bs_out;
+  for (int i = threadIdx.y; i < 32; i += 8) {
+    const int r = r0 + i, c = c0 + threadIdx.x;
+    if (r < R && c < Cc) t[i][threadIdx.x] = X[(long long)r * ld_in + c];
+  }
+  __syncthreads();
+  for (int i = threadIdx.y; i < 32; i += 8) {
+    const int c = c0 + i, r = r0 + threadIdx.x;
+    if (r < R && c < Cc) Y[(long long)c * ld_out + r] = t[threadIdx.x][i];
+  }
+}
+hipError_t transpose_bct_btc(const float* x, float* y, int B, int C, int T, hipStream_t s) {
+  dim3 g((T + 31) / 32, (C + 31) / 32, B);
+  hipLaunchKernelGGL(k_tr, g, dim3(32, 8), 0, s, x, y, C, T, (long long)T, (long long)C, (long long)C * T,
+                     (long long)C * T);
+  return hipGetLastError();
+}
+hipError_t transpose_btc_bct(const float* x, float* y, int B, int T, int C, int ldx, hipStream_t s) {
+  dim3 g((C + 31) / 32, (T + 31) / 32, B);
+  hipLaunchKernelGGL(k_tr, g, dim3(32, 8), 0, s, x, y, T, C, (long long)ldx, (long long)T, (long long)T * ldx,
+                     (long long)C * T);
+  return hipGetLastError();
+}
+
+__global__ void k_flip(const float* x, float* y, long long rows, int C) {
+  const long long n = rows * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / C;
+    const int c = (int)(i - r * C);
+    y[i] = x[r * C + (C - 1 - c)];
+  }
+}
+hipError_t channel_flip(const float* x, float* y, int rows, int C, hipStream_t s) {
+  hipLaunchKernelGGL(k_flip, dim3(nblocks((long long)rows * C)), dim3(TB), 0, s, x, y, (long long)rows, C);
+  return hipGetLastError();
+}
+
+__global__ void k_gather(const float* table, int ld, const int32_t* idx, float* y, long long rows, int C) {
+  const long long n = rows * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / C;
+    const int c = (int)(i - r * C);
+    y[i] = table[(long long)idx[r] * ld + c];
+  }
+}
+hipError_t gather_rows(const float* table, int ld_table, const int32_t* idx, float* y, int rows, int C,
+                       hipStream_t s) {
+  hipLaunchKernelGGL(k_gather, dim3(nblocks((long long)rows * C)), dim3(TB), 0, s, table, ld_table, idx, y,
+                     (long long)rows, C);
+  return hipGetLastError();
+}
+
+__global__ void k_seqmask(const int32_t* len, float* mask, int B, int T) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < B * T) mask[i] = (i % T) < len[i / T] ? 1.f : 0.f;
+}
+hipError_t seq_mask(const int32_t* lengths, float* mask, int B, int T, hipStream_t s) {
+  hipLaunchKernelGGL(k_seqmask, dim3(nblocks((long long)B * T)), dim3(TB), 0, s, lengths, mask, B, T);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ LayerNorm over rows (one wave per row)
+__global__ void k_layernorm(const float* x, const float* r, float* y, const float* gamma, const float* beta,
+                            int rows, int D, float eps, const float* mask) {
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= rows) return;
+  const float* xr = x + (long long)wave * D;
+  const float* rr = r ? r + (long long)wave * D : nullptr;
+  float v[16];
+  float s = 0.f;
+  const int per = (D + 63) / 64;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int c = lane + j * 64;
+    float t = 0.f;
+    if (j < per && c < D) {
+      t = xr[c];
+      if (rr) t = t + rr[c];
+    }
+    v[j] = t;
+    s += t;
+  }
+  const float mean = warp_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int c = lane + j * 64;
+    if (j < per && c < D) {
+      const float d = v[j] - mean;
+      q += d * d;
+    }
+  }
+  const float var = warp_sum(q) / (float)D;
+  const float rstd = 1.f / sqrtf(var + eps);
+  const float mk = mask ? mask[wave] : 1.f;
+  float* yr = y + (long long)wave * D;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int c = lane + j * 64;
+    if (j < per && c < D) {
+      float o = (v[j] - mean) * rstd * gamma[c] + beta[c];
+      if (mask) o *= mk;
+      yr[c] = o;
+    }
+  }
+}
+hipError_t layernorm_rows(const float* x, const float* r, float* y, const float* gamma, const float* beta,
+                          int rows, int D, float eps, const float* mask, hipStream_t s) {
+  if (D > 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_layernorm, dim3((rows + 3) / 4), dim3(256), 0, s, x, r, y, gamma, beta, rows, D, eps, mask);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ WaveNet gate
+__global__ void k_gate(const float* xin, int ldx, const float* g, long long g_bs, float* acts, int B, int T,
+                       int H) {
+  const long long n = (long long)B * T * H;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % H);
+    const long long bt = i / H;
+    const int b = (int)(bt / T);
+    const float* xr = xin + bt * ldx;
+    const float* gb = g + b * g_bs;
+    const float a = xr[c] + gb[c];
+    const float z = xr[H + c] + gb[H + c];
+    acts[i] = tanhf(a) * (1.f / (1.f + expf(-z)));
+  }
+}
+hipError_t gate_tanh_sigmoid(const float* xin, int ldx, const float* g, long long g_bs, float* acts, int B,
+                             int T, int H, hipStream_t s) {
+  hipLaunchKernelGGL(k_gate, dim3(nblocks((long long)B * T * H)), dim3(TB), 0, s, xin, ldx, g, g_bs, acts, B, T, H);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ softmax with relative-position band
+// scores: [B*heads][T][T] (already (q/sqrt(d)).k); rel: [B*heads][T][2w+1] ((q/sqrt(d)).emb_rel_k);
+// mask: [B][T] (attention mask = mask[i]*mask[j], fill -1e4); pband out: [B*heads][T][2w+1].
+__global__ void k_softmax_rel(float* scores, int T, int n_heads, const float* rel, int window, const float* mask,
+                              float* pband) {
+  const int row = blockIdx.x;  // over B*heads*T
+  const int bh = row / T, i = row % T;
+  const int b = bh / n_heads;
+  float* sr = scores + (long long)row * T;
+  const int nw = 2 * window + 1;
+  const float* rr = rel ? rel + (long long)row * nw : nullptr;
+  const float* mk = mask ? mask + (long long)b * T : nullptr;
+  const float mi = mk ? mk[i] : 1.f;
+  __shared__ float red[8];
+  float mx = -INFINITY;
+  for (int j = threadIdx.x; j < T; j += blockDim.x) {
+    float v = sr[j];
+    const int o = j - i + window;
+    if (rr && o >= 0 && o < nw) v = v + rr[o];
+    if (mk && mi * mk[j] == 0.f) v = -1e4f;
+    sr[j] = v;
+    mx = fmaxf(mx, v);
+  }
+  mx = warp_max(mx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = red[0];
+  for (int w = 1; w < (int)(blockDim.x >> 6); ++w) mx = fmaxf(mx, red[w]);
+  __syncthreads();
+  float sum = 0.f;
+  for (int j = threadIdx.x; j < T; j += blockDim.x) {
+    const float e = expf(sr[j] - mx);
+    sr[j] = e;
+    sum += e;
+  }
+  sum = warp_sum(sum);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sum;
+  __syncthreads();
+  sum = 0.f;
+  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) sum += red[w];
+  const float inv = 1.f / sum;
+  for (int j = threadIdx.x; j < T; j += blockDim.x) sr[j] = sr[j] * inv;
+  if (pband) {
+    __syncthreads();
+    for (int o = threadIdx.x; o < nw; o += blockDim.x) {
+      const int j = i + o - window;
+      pband[(long long)row * nw + o] = (j >= 0 && j < T) ? sr[j] : 0.f;
+    }
+  }
+}
+hipError_t softmax_rel(float* scores, int T, int n_heads, int B, const float* rel, int window, const float* mask,
+                       float* pband, int, hipStream_t s) {
+  hipLaunchKernelGGL(k_softmax_rel, dim3(B * n_heads * T), dim3(256), 0, s, scores, T, n_heads, rel, window, mask,
+                     pband);
+  return hipGetLastError();
+}
+hipError_t softmax_rows(float* scores, int rows, int cols, hipStream_t s) {
+  hipLaunchKernelGGL(k_softmax_rel, dim3(rows), dim3(256), 0, s, scores, cols, 1, nullptr, 0, nullptr, nullptr);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ feature x2 upsample + protect blend
+// pipeline.py:344-362: feats = interpolate(x2, nearest); pitchff = 1 if pitchf > 0 else protect;
+// feats = feats * pitchff + feats0 * (1 - pitchff)   (feats0 == feats without index retrieval).
+__global__ void k_up2(const float* feats, int L, int D, float* out, int T, const float* pitchf, float protect) {
+  const long long n = (long long)T * D;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int t = (int)(i / D), c = (int)(i % D);
+    const int src = t >> 1 < L ? t >> 1 : L - 1;
+    const float f = feats[(long long)src * D + c];
+    float v = f;
+    if (pitchf) {
+      const float pf = pitchf[t];
+      const float p = pf > 0.f ? 1.f : (pf < 1.f ? protect : pf);
+      v = f * p + f * (1.f - p);
+    }
+    out[i] = v;
+  }
+}
+hipError_t upsample2_protect(const float* feats, int L, int D, float* out, int T, const float* pitchf, float protect,
+                             hipStream_t s) {
+  hipLaunchKernelGGL(k_up2, dim3(nblocks((long long)T * D)), dim3(TB), 0, s, feats, L, D, out, T, pitchf, protect);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ NSF harmonic source (SineGen, harmonic_num=0)
+// generators/hifigan.py:156-228 + hifigan_nsf.py:48-52. Phase carry: rem[l] = fmod(f0[l]/sr*upp + .5, 1) - .5,
+// cumsum accumulated in fp64 and rounded per element (torch CPU cumsum acc_type<float> = double), then fmod 1.
+__global__ void k_sine_cum(const float* f0, int B, int L, int upp, float sr, double* cum) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float* fb = f0 + (long long)b * L;
+  float* cf = reinterpret_cast<float*>(cum + (long long)b * L);
+  double acc = 0.0;
+  for (int l = 0; l < L - 1; ++l) {
+    const float inc = (fb[l] / sr) * (float)upp;
+    const float rem = fmodf(inc + 0.5f, 1.0f) - 0.5f;
+    acc += (double)rem;
+    cf[l] = fmodf((float)acc, 1.0f);
+  }
+}
+__global__ void k_sine(const float* f0, int B, int L, int upp, float sr, const double* cum, const float* eps,
+                       uint64_t seed, float lin_w, float lin_b, float* har) {
+  const long long n = (long long)B * L * upp;
+  const float two_pi = 6.283185307179586f;
+  const float amp_unv = (float)(0.1 / 3.0);
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int u = (int)(i % upp);
+    const long long bl = i / upp;
+    const int b = (int)(bl / L), l = (int)(bl % L);
+    const float f = f0[bl];
+    float ph = (f / sr) * (float)(u + 1);
+    if (l > 0) ph = ph + reinterpret_cast<const float*>(cum + (long long)b * L)[l - 1];
+    const float sine = sinf(two_pi * ph) * 0.1f;
+    const float uv = f > 0.f ? 1.f : 0.f;
+    const float amp = uv * 0.003f + (1.f - uv) * amp_unv;
+    const float e = eps ? eps[i] : normal_at(seed, (uint64_t)i);
+    const float merged = sine * uv + amp * e;
+    har[i] = tanhf(merged * lin_w + lin_b);
+  }
+}
+hipError_t sine_source(const float* f0, int B, int L, int upp, float sr, const float* eps, uint64_t seed,
+                       float lin_w, float lin_b, double* cum_ws, float* har, hipStream_t s) {
+  hipLaunchKernelGGL(k_sine_cum, dim3((B + 63) / 64), dim3(64), 0, s, f0, B, L, upp, sr, cum_ws);
+  hipLaunchKernelGGL(k_sine, dim3(nblocks((long long)B * L * upp)), dim3(TB), 0, s, f0, B, L, upp, sr, cum_ws, eps,
+                     seed, lin_w, lin_b, har);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ noise_convs: y[b][t][c] += b[c] + sum_k har[t*s-p+k] w[c][k]
+__global__ void k_noise_conv(const float* har, int Nh, float* y, int T, int C, long long y_bs, const float* w,
+                             const float* bias, int K, int stride, int pad) {
+  extern __shared__ float seg[];
+  const int b = blockIdx.y;
+  const int t0 = blockIdx.x * 32;
+  const int span = 31 * stride + K;
+  const float* hb = har + (long long)b * Nh;
+  for (int k = threadIdx.x; k < span; k += blockDim.x) {
+    const long long g = (long long)t0 * stride - pad + k;
+    seg[k] = (g >= 0 && g < Nh) ? hb[g] : 0.f;
+  }
+  __syncthreads();
+  float* yb = y + (long long)b * y_bs;
+  for (int idx = threadIdx.x; idx < 32 * C; idx += blockDim.x) {
+    const int tt = idx / C, c = idx % C;
+    const int t = t0 + tt;
+    if (t >= T) continue;
+    const float* wc = w + (long long)c * K;
+    const float* sg = seg + tt * stride;
+    float acc = 0.f;
+    for (int k = 0; k < K; ++k) acc = fmaf(sg[k], wc[k], acc);
+    float* dst = yb + (long long)t * C + c;
+    *dst = *dst + (acc + bias[c]);
+  }
+}
+hipError_t noise_conv_add(const float* har, int Nh, float* y, int B, int T, int C, long long y_bs, const float* w,
+                          const float* b, int K, int stride, int pad, hipStream_t s) {
+  const int span = 31 * stride + K;
+  hipLaunchKernelGGL(k_noise_conv, dim3((T + 31) / 32, B), dim3(256), span * sizeof(float), s, har, Nh, y, T, C,
+                     y_bs, w, b, K, stride, pad);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ conv_post: tanh(conv1d(lrelu(x, 0.01), w[1][C][K], pad K/2)), no bias
+__global__ void k_conv_post(const float* x, int T, int C, const float* w, int K, float slope, float* y) {
+  extern __shared__ float tile[];  // [(256+K-1)][C+1]
+  const int b = blockIdx.y;
+  const int t0 = blockIdx.x * 256;
+  const int pad = K / 2;
+  const int rows = 256 + K - 1;
+  const int ldt = C + 1;
+  const float* xb = x + (long long)b * T * C;
+  for (int idx = threadIdx.x; idx < rows * C; idx += blockDim.x) {
+    const int r = idx / C, c = idx % C;
+    const int g = t0 - pad + r;
+    float v = 0.f;
+    if (g >= 0 && g < T) {
+      v = xb[(long long)g * C + c];
+      v = v > 0.f ? v : v * slope;
+    }
+    tile[r * ldt + c] = v;
+  }
+  __syncthreads();
+  const int t = t0 + threadIdx.x;
+  if (t >= T) return;
+  float acc = 0.f;
+  for (int c = 0; c < C; ++c)
+    for (int k = 0; k < K; ++k) acc = fmaf(tile[(threadIdx.x + k) * ldt + c], w[c * K + k], acc);
+  y[(long long)b * T + t] = tanhf(acc);
+}
+hipError_t conv_post_tanh(const float* x, int B, int T, int C, const float* w, int K, float slope, float* y,
+                          hipStream_t s) {
+  const size_t smem = (size_t)(256 + K - 1) * (C + 1) * sizeof(float);
+  hipLaunchKernelGGL(k_conv_post, dim3((T + 255) / 256, B), dim3(256), smem, s, x, T, C, w, K, slope, y);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ z_p = (m + exp(logs) * eps * 0.66666) * mask
+// stats: [B][T][2I] (m | logs); eps (reference layout [B][I][T]) or generated.
+__global__ void k_zp(const float* stats, int B, int T, int I, const float* eps, uint64_t seed, const float* mask,
+                     float* zp) {
+  const long long n = (long long)B * T * I;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % I);
+    const long long bt = i / I;
+    const int b = (int)(bt / T), t = (int)(bt % T);
+    const float m = stats[bt * 2 * I + c];
+    const float lg = stats[bt * 2 * I + I + c];
+    const long long ei = ((long long)b * I + c) * T + t;
+    const float e = eps ? eps[ei] : normal_at(seed, (uint64_t)ei);
+    zp[i] = (m + expf(lg) * e * 0.66666f) * mask[bt];
+  }
+}
+hipError_t zp_sample(const float* stats, int B, int T, int I, const float* eps, uint64_t seed, const float* mask,
+                     float* zp, hipStream_t s) {
+  hipLaunchKernelGGL(k_zp, dim3(nblocks((long long)B * T * I)), dim3(TB), 0, s, stats, B, T, I, eps, seed, mask, zp);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ GroupNorm(C groups of 1 channel) over time + GELU (HuBERT conv0)
+__global__ void k_gn_stats(const float* x, int T, int C, int chunk, double* ws) {
+  // grid (C/64, nchunks); block 256 = 64 channels x 4 row lanes
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;
+  const int t0 = blockIdx.y * chunk;
+  const int t1 = min(T, t0 + chunk);
+  double s = 0.0, q = 0.0;
+  if (c < C) {
+    for (int t = t0 + rl; t < t1; t += 4) {
+      const double v = x[(long long)t * C + c];
+      s += v;
+      q += v * v;
+    }
+  }
+  __shared__ double ss[4][64], qq[4][64];
+  ss[rl][threadIdx.x & 63] = s;
+  qq[rl][threadIdx.x & 63] = q;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    s = ss[0][threadIdx.x] + ss[1][threadIdx.x] + ss[2][threadIdx.x] + ss[3][threadIdx.x];
+    q = qq[0][threadIdx.x] + qq[1][threadIdx.x] + qq[2][threadIdx.x] + qq[3][threadIdx.x];
+    ws[((long long)blockIdx.y * C + c) * 2] = s;
+    ws[((long long)blockIdx.y * C + c) * 2 + 1] = q;
+  }
+}
+__global__ void k_gn_apply(float* x, int T, int C, int nchunks, const double* ws, const float* gamma,
+                           const float* beta, float eps) {
+  const long long n = (long long)T * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    double s = 0.0, q = 0.0;
+    for (int k = 0; k < nchunks; ++k) {
+      s += ws[((long long)k * C + c) * 2];
+      q += ws[((long long)k * C + c) * 2 + 1];
+    }
+    const double mean = s / T;
+    double var = q / T - mean * mean;
+    if (var < 0) var = 0;
+    const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+    float v = (x[i] - (float)mean) * rstd * gamma[c] + beta[c];
+    x[i] = 0.5f * v * (1.f + erff(v * 0.70710678118654752440f));
+  }
+}
+hipError_t groupnorm_time_gelu(float* x, int T, int C, const float* gamma, const float* beta, float eps, double* ws,
+                               hipStream_t s) {
+  const int nchunks = 64;
+  const int chunk = (T + nchunks - 1) / nchunks;
+  hipLaunchKernelGGL(k_gn_stats, dim3((C + 63) / 64, nchunks), dim3(256), 0, s, x, T, C, chunk, ws);
+  hipLaunchKernelGGL(k_gn_apply, dim3(nblocks((long long)T * C)), dim3(TB), 0, s, x, T, C, nchunks, ws, gamma, beta,
+                     eps);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ RMVPE front end
+__global__ void k_reflect1d(const float* x, int n, int pl, int pr, float* y) {
+  const int m = n + pl + pr;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+    int j = i - pl;
+    if (j < 0) j = -j;
+    if (j >= n) j = 2 * (n - 1) - j;
+    y[i] = x[j];
+  }
+}
+hipError_t reflect_pad_1d(const float* x, int n, int pad_l, int pad_r, float* y, hipStream_t s) {
+  if (pad_l >= n || pad_r >= n) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_reflect1d, dim3(nblocks(n + pad_l + pad_r)), dim3(TB), 0, s, x, n, pad_l, pad_r, y);
+  return hipGetLastError();
+}
+__global__ void k_reflect_rows(const float* x, int rows, int C, int pr, float* y) {
+  const long long n = (long long)(rows + pr) * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int r = (int)(i / C), c = (int)(i % C);
+    const int src = r < rows ? r : 2 * (rows - 1) - r;
+    y[i] = x[(long long)src * C + c];
+  }
+}
+hipError_t reflect_pad_rows(const float* x, int rows, int C, int pad_r, float* y, hipStream_t s) {
+  if (pad_r >= rows) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_reflect_rows, dim3(nblocks((long long)(rows + pad_r) * C)), dim3(TB), 0, s, x, rows, C, pad_r,
+                     y);
+  return hipGetLastError();
+}
+__global__ void k_stftmag(const float* spec, int F, int nb, float* mag, int ldm) {
+  const long long n = (long long)F * nb;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int f = (int)(i / nb), k = (int)(i % nb);
+    const float re = spec[(long long)f * 2 * nb + k];
+    const float im = spec[(long long)f * 2 * nb + nb + k];
+    mag[(long long)f * ldm + k] = sqrtf(re * re + im * im);
+  }
+}
+hipError_t stft_magnitude(const float* spec, int F, int nbins, float* mag, int ldm, hipStream_t s) {
+  hipLaunchKernelGGL(k_stftmag, dim3(nblocks((long long)F * nbins)), dim3(TB), 0, s, spec, F, nbins, mag, ldm);
+  return hipGetLastError();
+}
+
+__global__ void k_avgpool2(const float* x, int H, int W, int C, int ldx, float* y) {
+  const int Ho = H / 2, Wo = W / 2;
+  const long long n = (long long)Ho * Wo * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long long p = i / C;
+    const int h = (int)(p / Wo), w = (int)(p % Wo);
+    const float* a = x + ((long long)(2 * h) * W + 2 * w) * ldx + c;
+    const float* bb = a + (long long)W * ldx;
+    y[i] = (((a[0] + a[ldx]) + bb[0]) + bb[ldx]) / 4.f;
+  }
+}
+hipError_t avgpool2(const float* x, int H, int W, int C, int ldx, float* y, hipStream_t s) {
+  hipLaunchKernelGGL(k_avgpool2, dim3(nblocks((long long)(H / 2) * (W / 2) * C)), dim3(TB), 0, s, x, H, W, C, ldx, y);
+  return hipGetLastError();
+}
+
+__global__ void k_nhwc_hcw(const float* x, int H, int W, int C, float* y) {
+  const long long n = (long long)H * W * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int h = (int)(i / (W * C));
+    const int rem = (int)(i % (W * C));
+    const int c = rem / W, w = rem % W;
+    y[i] = x[((long long)h * W + w) * C + c];
+  }
+}
+hipError_t nhwc_to_hcw(const float* x, int H, int W, int C, float* y, hipStream_t s) {
+  hipLaunchKernelGGL(k_nhwc_hcw, dim3(nblocks((long long)H * W * C)), dim3(TB), 0, s, x, H, W, C, y);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ RMVPE decode (RMVPE.py:484-540), fp64 like numpy
+__global__ void k_decode(const float* sal, int F, int ncls, float thred, double* f0) {
+  const int f = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (f >= F) return;
+  const float* s = sal + (long long)f * ncls;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int k = lane; k < ncls; k += 64) {
+    const float v = s[k];
+    if (v > best) {
+      best = v;
+      bi = k;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > best || (ov == best && oi < bi)) {
+      best = ov;
+      bi = oi;
+    }
+  }
+  if (lane == 0) {
+    double ps = 0.0, ws = 0.0;
+    for (int k = bi - 4; k <= bi + 4; ++k) {
+      if (k < 0 || k >= ncls) continue;
+      const double sv = (double)s[k];
+      const double cm = 20.0 * k + 1997.3794084376191;
+      ps += sv * cm;
+      ws += sv;
+    }
+    double cents = ps / ws;
+    if ((double)best <= (double)thred) cents = 0.0;
+    double v = 10.0 * exp2(cents / 1200.0);
+    if (v == 10.0) v = 0.0;
+    f0[f] = v;
+  }
+}
+hipError_t rmvpe_decode(const float* sal, int F, int ncls, float thred, double* f0, hipStream_t s) {
+  hipLaunchKernelGGL(k_decode, dim3((F + 3) / 4), dim3(256), 0, s, sal, F, ncls, thred, f0);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ f0 shift + coarse quantisation (pipeline.py:280-291)
+__global__ void k_f0post(const double* f0, int F, double shift, int32_t* coarse, float* pitchf, double* f0_out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= F) return;
+  const double f = f0[i] * shift;
+  const double mel_min = 1127.0 * log(1.0 + 50.0 / 700.0);
+  const double mel_max = 1127.0 * log(1.0 + 1100.0 / 700.0);
+  double m = 1127.0 * log(1.0 + f / 700.0);
+  if (m > 0) m = (m - mel_min) * 254.0 / (mel_max - mel_min) + 1.0;
+  if (m <= 1) m = 1;
+  if (m > 255) m = 255;
+  coarse[i] = (int32_t)rint(m);
+  pitchf[i] = (float)f;
+  if (f0_out) f0_out[i] = f;
+}
+hipError_t f0_post(const double* f0, int F, double shift, int32_t* coarse, float* pitchf, double* f0_out,
+                   hipStream_t s) {
+  hipLaunchKernelGGL(k_f0post, dim3(nblocks(F)), dim3(TB), 0, s, f0, F, shift, coarse, pitchf, f0_out);
+  return hipGetLastError();
+}
+
+}  // namespace rvcx
+
+// =================================================================== pipeline DSP on device
+namespace rvcx {
+
+// scipy.signal.filtfilt(b, a, x) with padtype='odd', padlen = 3*max(len(a), len(b)) (pipeline.py:439),
+// lfilter in direct form II transposed, fp64. Each pass is a chunked linear recurrence:
+//   (1) every chunk of IIR_L samples runs from a zero state -> end state e_c;
+//   (2) one thread propagates true chunk start states s_{c+1} = F^L s_c + e_c;
+//   (3) every chunk reruns from s_c and writes its outputs.
+constexpr int IIR_L = 256;
+
+struct IirCoef {
+  double b[IIR_MAXO + 1], a[IIR_MAXO + 1], zi[IIR_MAXO], FL[IIR_MAXO * IIR_MAXO];
+  int order;
+};
+
+__device__ __forceinline__ double iir_step(const IirCoef& c, double* z, double x) {
+  const double y = c.b[0] * x + z[0];
+  for (int i = 0; i < c.order - 1; ++i) z[i] = c.b[i + 1] * x + z[i + 1] - c.a[i + 1] * y;
+  z[c.order - 1] = c.b[c.order] * x - c.a[c.order] * y;
+  return y;
+}
+
+// input sequence element j of pass `rev`: forward pass reads the odd extension of x lazily,
+// backward pass reads the forward output reversed.
+__device__ __forceinline__ double iir_in(const double* x, long long n, int padlen, const double* yf, long long ne,
+                                         int rev, long long j) {
+  if (rev) return yf[ne - 1 - j];
+  const long long k = j - padlen;
+  if (k < 0) return 2.0 * x[0] - x[-k];
+  if (k >= n) return 2.0 * x[n - 1] - x[2 * (n - 1) - k];
+  return x[k];
+}
+
+__global__ void k_iir_chunks(const IirCoef c, const double* x, long long n, int padlen, const double* yf, long long ne,
+                             int rev, double* ends, const double* starts, double* out) {
+  const long long ch = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const long long nch = (ne + IIR_L - 1) / IIR_L;
+  if (ch >= nch) return;
+  double z[IIR_MAXO];
+  for (int i = 0; i < c.order; ++i) z[i] = starts ? starts[ch * IIR_MAXO + i] : 0.0;
+  const long long j0 = ch * IIR_L, j1 = min(ne, j0 + IIR_L);
+  for (long long j = j0; j < j1; ++j) {
+    const double y = iir_step(c, z, iir_in(x, n, padlen, yf, ne, rev, j));
+    if (out) out[j] = y;
+  }
+  if (ends)
+    for (int i = 0; i < c.order; ++i) ends[ch * IIR_MAXO + i] = z[i];
+}
+
+__global__ void k_iir_combine(const IirCoef c, const double* x, long long n, int padlen, const double* yf,
+                              long long ne, int rev, const double* ends, double* starts) {
+  const long long nch = (ne + IIR_L - 1) / IIR_L;
+  const double x0 = iir_in(x, n, padlen, yf, ne, rev, 0);
+  double s[IIR_MAXO];
+  for (int i = 0; i < c.order; ++i) s[i] = c.zi[i] * x0;
+  for (long long ch = 0; ch < nch; ++ch) {
+    for (int i = 0; i < c.order; ++i) starts[ch * IIR_MAXO + i] = s[i];
+    double t[IIR_MAXO];
+    for (int i = 0; i < c.order; ++i) {
+      double acc = ends[ch * IIR_MAXO + i];
+      for (int k = 0; k < c.order; ++k) acc += c.FL[i * IIR_MAXO + k] * s[k];
+      t[i] = acc;
+    }
+    for (int i = 0; i < c.order; ++i) s[i] = t[i];
+  }
+}
+
+// audio_pad[k] = y[reflect(k - t_pad)] with y the filtfilt output (backward pass result yb reversed, trimmed)
+__global__ void k_filt_pad(const double* yb, long long ne, int padlen, long long n, long long t_pad, double* pad64,
+                           float* pad32) {
+  const long long m = n + 2 * t_pad;
+  for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < m; k += (long long)gridDim.x * blockDim.x) {
+    long long j = k - t_pad;
+    if (j < 0) j = -j;
+    if (j >= n) j = 2 * (n - 1) - j;
+    const double v = yb[ne - 1 - (j + padlen)];
+    if (pad64) pad64[k] = v;
+    pad32[k] = (float)v;
+  }
+}
+
+hipError_t filtfilt_pad(const double* x, long long n, const double* b, const double* a, const double* zi,
+                        const double* FL, int order, long long t_pad, double* ws, double* pad64, float* pad32,
+                        hipStream_t s) {
+  if (order < 1 || order > IIR_MAXO) return hipErrorInvalidValue;
+  const int padlen = 3 * (order + 1);
+  if (n <= padlen || t_pad >= n) return hipErrorInvalidValue;
+  IirCoef c;
+  c.order = order;
+  for (int i = 0; i <= order; ++i) {
+    c.b[i] = b[i];
+    c.a[i] = a[i];
+  }
+  for (int i = 0; i < order; ++i) c.zi[i] = zi[i];
+  for (int i = 0; i < IIR_MAXO * IIR_MAXO; ++i) c.FL[i] = FL[i];
+  const long long ne = n + 2 * padlen;
+  const long long nch = (ne + IIR_L - 1) / IIR_L;
+  double* yf = ws;
+  double* yb = yf + ne;
+  double* ends = yb + ne;
+  double* starts = ends + nch * IIR_MAXO;
+  const unsigned g = (unsigned)((nch + 127) / 128);
+  for (int rev = 0; rev < 2; ++rev) {
+    double* out = rev ? yb : yf;
+    hipLaunchKernelGGL(k_iir_chunks, dim3(g), dim3(128), 0, s, c, x, n, padlen, yf, ne, rev, ends, nullptr, nullptr);
+    hipLaunchKernelGGL(k_iir_combine, dim3(1), dim3(1), 0, s, c, x, n, padlen, yf, ne, rev, ends, starts);
+    hipLaunchKernelGGL(k_iir_chunks, dim3(g), dim3(128), 0, s, c, x, n, padlen, yf, ne, rev, nullptr, starts, out);
+  }
+  hipLaunchKernelGGL(k_filt_pad, dim3(nblocks(n + 2 * t_pad)), dim3(TB), 0, s, yb, ne, padlen, n, t_pad, pad64,
+                     pad32);
+  return hipGetLastError();
+}
+
+size_t filtfilt_ws_doubles(long long n, int order) {
+  const long long ne = n + 2 * 3 * (order + 1);
+  const long long nch = (ne + IIR_L - 1) / IIR_L;
+  return (size_t)(2 * ne + 2 * nch * IIR_MAXO);
+}
+
+// peak normalisation (pipeline.py:550-552): m = max|x| / 0.99 ; if m > 1: x /= m
+__global__ void k_absmax(const float* x, long long n, unsigned* out) {
+  float m = 0.f;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    m = fmaxf(m, fabsf(x[i]));
+  m = warp_max(m);
+  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+}
+__global__ void k_peak_scale(float* x, long long n, const unsigned* mx) {
+  const float m = __uint_as_float(*mx) / 0.99f;
+  if (!(m > 1.f)) return;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    x[i] = x[i] / m;
+}
+hipError_t peak_normalize(float* x, long long n, unsigned* ws, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(ws, 0, sizeof(unsigned), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_absmax, dim3(std::min<long long>(1024, (n + TB - 1) / TB)), dim3(TB), 0, s, x, n, ws);
+  hipLaunchKernelGGL(k_peak_scale, dim3(nblocks(n)), dim3(TB), 0, s, x, n, ws);
+  return hipGetLastError();
+}
+
+}  // namespace rvcx

@@ -1,0 +1,247 @@
+// extern "C" boundary (include/rvcx.h). Every entry point converts C++ exceptions into an
+// rvcx_status and stores the message for rvcx_last_error.
+#include <cstring>
+
+#include "runtime.h"
+
+using namespace rvcx;
+
+struct rvcx_ctx : public Ctx {};
+
+namespace {
+
+template <class F>
+int guard(rvcx_ctx* c, F&& f) {
+  if (!c) return RVCX_E_INVALID;
+  try {
+    c->err.clear();
+    f();
+    return RVCX_OK;
+  } catch (const Error& e) {
+    c->err = e.what();
+    return e.code;
+  } catch (const std::exception& e) {
+    c->err = e.what();
+    return RVCX_E_INVALID;
+  }
+}
+
+void set_device(rvcx_ctx* c) { RVCX_HIP(hipSetDevice(c->device)); }
+
+}  // namespace
+
+namespace rvcx {
+__global__ void k_set_i32(int32_t* p, int32_t v) { p[0] = v; }
+void set_i32(int32_t* p, int32_t v, hipStream_t s) {
+  hipLaunchKernelGGL(k_set_i32, dim3(1), dim3(1), 0, s, p, v);
+  check(hipGetLastError(), "set_i32");
+}
+}  // namespace rvcx
+
+extern "C" {
+
+int rvcx_create(rvcx_ctx** out, int device) {
+  if (!out) return RVCX_E_INVALID;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return RVCX_E_HIP;
+  auto* c = new rvcx_ctx();
+  c->device = device;
+  *out = c;
+  return RVCX_OK;
+}
+
+int rvcx_destroy(rvcx_ctx* ctx) {
+  if (!ctx) return RVCX_E_INVALID;
+  (void)hipSetDevice(ctx->device);
+  (void)hipDeviceSynchronize();
+  delete ctx;
+  return RVCX_OK;
+}
+
+const char* rvcx_last_error(const rvcx_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int rvcx_set_synth_config(rvcx_ctx* ctx, const rvcx_synth_desc* d) {
+  return guard(ctx, [&] {
+    if (!d) throw Error(RVCX_E_INVALID, "null desc");
+    SynthCfg g;
+    g.I = d->inter_channels;
+    g.H = d->hidden_channels;
+    g.F = d->filter_channels;
+    g.n_heads = d->n_heads;
+    g.n_layers = d->n_layers;
+    g.ksize = d->kernel_size;
+    if (d->n_resblocks < 1 || d->n_resblocks > 4 || d->n_dilations < 1 || d->n_dilations > 4)
+      throw Error(RVCX_E_INVALID, "resblock config out of range");
+    g.rb_k.assign(d->resblock_kernel_sizes, d->resblock_kernel_sizes + d->n_resblocks);
+    g.rb_d.clear();
+    for (int j = 0; j < d->n_resblocks; ++j)
+      g.rb_d.emplace_back(d->resblock_dilation_sizes[j], d->resblock_dilation_sizes[j] + d->n_dilations);
+    if (d->n_upsample < 1 || d->n_upsample > 8) throw Error(RVCX_E_INVALID, "n_upsample out of range");
+    g.ups.assign(d->upsample_rates, d->upsample_rates + d->n_upsample);
+    g.up_k.assign(d->upsample_kernel_sizes, d->upsample_kernel_sizes + d->n_upsample);
+    g.C0 = d->upsample_initial_channel;
+    g.n_spk = d->spk_embed_dim;
+    g.gin = d->gin_channels;
+    g.sr = d->sr;
+    g.emb_dim = d->text_enc_hidden_dim;
+    if (g.H % g.n_heads || g.I % 2 || g.C0 % (1 << g.ups.size()))
+      throw Error(RVCX_E_INVALID, "inconsistent synthesizer dimensions");
+    ctx->scfg = g;
+    ctx->synth_cfg_set = true;
+    ctx->ready[0] = false;
+  });
+}
+
+int rvcx_upload(rvcx_ctx* ctx, int model, const char* name, const float* host, const int64_t* shape, int ndim) {
+  return guard(ctx, [&] {
+    if (model < 0 || model > 2 || !name || !host || (ndim > 0 && !shape) || ndim < 0 || ndim > 8)
+      throw Error(RVCX_E_INVALID, "rvcx_upload: bad arguments");
+    HostTensor t;
+    size_t n = 1;
+    for (int i = 0; i < ndim; ++i) {
+      if (shape[i] < 0) throw Error(RVCX_E_INVALID, "negative dim");
+      t.shape.push_back(shape[i]);
+      n *= (size_t)shape[i];
+    }
+    t.v.assign(host, host + n);
+    ctx->host[model][name] = std::move(t);
+    ctx->ready[model] = false;
+  });
+}
+
+int rvcx_finalize(rvcx_ctx* ctx, int model) {
+  return guard(ctx, [&] {
+    set_device(ctx);
+    if (model == RVCX_MODEL_SYNTH) {
+      finalize_synth(*ctx);
+    } else if (model == RVCX_MODEL_HUBERT) {
+      finalize_hubert(*ctx);
+    } else if (model == RVCX_MODEL_RMVPE) {
+      finalize_rmvpe(*ctx);
+    } else {
+      throw Error(RVCX_E_INVALID, "unknown model");
+    }
+    RVCX_HIP(hipDeviceSynchronize());
+    ctx->ready[model] = true;
+  });
+}
+
+int rvcx_synth_upp(const rvcx_ctx* ctx) { return ctx ? ctx->scfg.upp() : 0; }
+
+int rvcx_hubert(rvcx_ctx* ctx, const float* d_audio, int64_t n, int version, float* d_feats, int64_t cap_rows,
+                int64_t* rows_out, void* stream) {
+  return guard(ctx, [&] {
+    if (!ctx->ready[1]) throw Error(RVCX_E_STATE, "hubert weights not finalized");
+    if (!d_audio || !d_feats || n <= 0) throw Error(RVCX_E_INVALID, "rvcx_hubert: bad arguments");
+    set_device(ctx);
+    const int64_t L = hubert_forward(*ctx, d_audio, n, version == 1 ? 1 : 2, d_feats, cap_rows,
+                                     static_cast<hipStream_t>(stream));
+    if (rows_out) *rows_out = L;
+  });
+}
+
+int rvcx_rmvpe(rvcx_ctx* ctx, const float* d_audio, int64_t n, float thred, double* d_f0, int64_t cap_frames,
+               int64_t* frames_out, float* d_hidden, void* stream) {
+  return guard(ctx, [&] {
+    if (!ctx->ready[2]) throw Error(RVCX_E_STATE, "rmvpe weights not finalized");
+    if (!d_audio || !d_f0 || n <= 0) throw Error(RVCX_E_INVALID, "rvcx_rmvpe: bad arguments");
+    set_device(ctx);
+    const int64_t F = rmvpe_forward(*ctx, d_audio, n, thred, d_f0, cap_frames, d_hidden,
+                                    static_cast<hipStream_t>(stream));
+    if (frames_out) *frames_out = F;
+  });
+}
+
+int rvcx_f0_post(rvcx_ctx* ctx, const double* d_f0, int64_t F, double semitones, int32_t* d_coarse, float* d_pitchf,
+                 double* d_f0_shifted, void* stream) {
+  return guard(ctx, [&] {
+    if (!d_f0 || !d_coarse || !d_pitchf || F < 0) throw Error(RVCX_E_INVALID, "rvcx_f0_post: bad arguments");
+    set_device(ctx);
+    check(f0_post(d_f0, (int)F, std::pow(2.0, semitones / 12.0), d_coarse, d_pitchf, d_f0_shifted,
+                  static_cast<hipStream_t>(stream)),
+          "f0_post");
+  });
+}
+
+int rvcx_synth_infer(rvcx_ctx* ctx, int B, int T, const float* d_phone, const int32_t* d_lengths,
+                     const int32_t* d_pitch, const float* d_pitchf, const int32_t* d_sid, const float* d_eps_z,
+                     const float* d_eps_src, uint64_t seed, float* d_out, float* d_zp, float* d_z, void* stream) {
+  return guard(ctx, [&] {
+    if (!ctx->ready[0]) throw Error(RVCX_E_STATE, "synthesizer weights not finalized");
+    if (B <= 0 || T <= 0 || !d_phone || !d_lengths || !d_pitch || !d_pitchf || !d_sid || !d_out)
+      throw Error(RVCX_E_INVALID, "rvcx_synth_infer: bad arguments");
+    set_device(ctx);
+    synth_forward(*ctx, B, T, d_phone, d_lengths, d_pitch, d_pitchf, d_sid, d_eps_z, d_eps_src, seed, d_out, d_zp,
+                  d_z, static_cast<hipStream_t>(stream));
+  });
+}
+
+int rvcx_dec_only(rvcx_ctx* ctx, int B, int T, const float* d_z, const float* d_f0, const int32_t* d_sid,
+                  const float* d_eps_src, uint64_t seed, float* d_out, void* stream) {
+  return guard(ctx, [&] {
+    if (!ctx->ready[0]) throw Error(RVCX_E_STATE, "synthesizer weights not finalized");
+    if (B <= 0 || T <= 0 || !d_z || !d_f0 || !d_sid || !d_out) throw Error(RVCX_E_INVALID, "rvcx_dec_only: bad arguments");
+    set_device(ctx);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int I = ctx->scfg.I;
+    float* zt = ctx->buf<float>("dec_only.z", (size_t)B * T * I, s);
+    check(transpose_bct_btc(d_z, zt, B, I, T, s), "transpose");
+    float* g = ctx->buf<float>("dec_only.g", (size_t)B * ctx->scfg.gin, s);
+    check(gather_rows(ctx->W("emb_g"), ctx->scfg.gin, d_sid, g, B, ctx->scfg.gin, s), "emb_g");
+    dec_forward(*ctx, B, T, zt, nullptr, d_f0, g, d_eps_src, seed, d_out, s);
+  });
+}
+
+int rvcx_voice_conversion(rvcx_ctx* ctx, const float* d_audio, int64_t n, const int32_t* d_pitch,
+                          const float* d_pitchf, int sid, float protect, const float* d_eps_z, const float* d_eps_src,
+                          uint64_t seed, float* d_out, int64_t cap, int64_t* n_out, void* stream) {
+  return guard(ctx, [&] {
+    if (!ctx->ready[0] || !ctx->ready[1]) throw Error(RVCX_E_STATE, "synthesizer/hubert not finalized");
+    if (!d_audio || !d_pitch || !d_pitchf || !d_out || n <= 0) throw Error(RVCX_E_INVALID, "bad arguments");
+    if (sid < 0 || sid >= ctx->scfg.n_spk) throw Error(RVCX_E_INVALID, "sid out of range");
+    set_device(ctx);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int E = ctx->scfg.emb_dim;
+    // HuBERT frames for n samples (upper bound n/320)
+    const int64_t cap_rows = n / 320 + 8;
+    float* feats = ctx->buf<float>("vc.feats", (size_t)cap_rows * E, s);
+    const int64_t L = hubert_forward(*ctx, d_audio, n, 2, feats, cap_rows, s);
+    const int T = (int)std::min<int64_t>(n / 160, 2 * L);
+    const int upp = ctx->scfg.upp();
+    if ((int64_t)T * upp > cap) throw Error(RVCX_E_CAPACITY, "voice_conversion: output needs " +
+                                                                 std::to_string((int64_t)T * upp) + " samples");
+    float* phone = ctx->buf<float>("vc.phone", (size_t)T * E, s);
+    check(upsample2_protect(feats, (int)L, E, phone, T, protect < 0.5f ? d_pitchf : nullptr, protect, s), "upsample");
+    int32_t* lens = ctx->buf<int32_t>("vc.len", 4, s);
+    int32_t* sids = lens + 1;
+    set_i32(lens, T, s);
+    set_i32(sids, sid, s);
+    synth_forward(*ctx, 1, T, phone, lens, d_pitch, d_pitchf, sids, d_eps_z, d_eps_src, seed, d_out, nullptr,
+                  nullptr, s);
+    if (n_out) *n_out = (int64_t)T * upp;
+  });
+}
+
+int rvcx_set_highpass(rvcx_ctx* ctx, const double* b, const double* a, const double* zi, int order) {
+  return guard(ctx, [&] {
+    if (!b || !a || !zi) throw Error(RVCX_E_INVALID, "null coefficients");
+    set_highpass(*ctx, b, a, zi, order);
+  });
+}
+
+int rvcx_pipeline(rvcx_ctx* ctx, const double* d_audio, int64_t n, int sid, double semitones, float protect,
+                  int64_t t_pad, int64_t t_pad_tgt, const float* d_eps_z, const float* d_eps_src, uint64_t seed,
+                  float* d_out, int64_t cap, int64_t* n_out, double* d_f0, void* stream) {
+  return guard(ctx, [&] {
+    if (!ctx->ready[0] || !ctx->ready[1] || !ctx->ready[2]) throw Error(RVCX_E_STATE, "models not finalized");
+    if (!d_audio || !d_out || n <= 0 || t_pad < 0 || t_pad_tgt < 0) throw Error(RVCX_E_INVALID, "bad arguments");
+    if (sid < 0 || sid >= ctx->scfg.n_spk) throw Error(RVCX_E_INVALID, "sid out of range");
+    set_device(ctx);
+    const int64_t no = pipeline_forward(*ctx, d_audio, n, sid, semitones, protect, t_pad, t_pad_tgt, d_eps_z,
+                                        d_eps_src, seed, d_out, cap, d_f0, static_cast<hipStream_t>(stream));
+    if (n_out) *n_out = no;
+  });
+}
+
+}  // extern "C"

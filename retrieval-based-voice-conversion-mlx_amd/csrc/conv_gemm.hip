@@ -1,0 +1,314 @@
+// Implicit-GEMM convolution on CDNA4 fp32 MFMA (v_mfma_f32_32x32x2_f32).
+//
+// One kernel family covers every contraction of the RVC path:
+//   * 1-D conv (time-major [T][C]): NSF ResBlock dilated convs, conv_pre, flow WaveNet,
+//     TextEncoder FFN, HuBERT strided feature convs, the grouped positional conv (batch=group),
+//     ConvTranspose1d as a polyphase conv (u*C_out virtual outputs), STFT-as-GEMM framing;
+//   * GEMM (taps=1): all Linear / 1x1 convs, attention QK^T and PV (batch = head);
+//   * 2-D 3x3 conv on NHWC images (RMVPE U-Net), ConvTranspose2d as a 2x2-tap phase conv.
+//
+// Tiling: a 256-thread block (4 waves) owns BM output rows x BN output channels. The A tile is
+// staged once per 32-channel chunk with its full tap halo ((BM-1)*stride + (taps-1)*dil + 1 rows,
+// or the (RH+KH-1) x (RW+KW-1) pixel window in 2-D), the pre-activation applied on the way into
+// LDS; each tap then re-reads shifted rows of that tile (no im2col in HBM). B (weights packed
+// [tap][N][C]) is staged per tap. Each wave holds TM x TN 32x32 fp32 accumulators; one
+// ds_read_b128 per operand feeds 4 MFMAs (the k-pair of MFMA j is channels {8kk+j, 8kk+4+j}).
+// fp32 in / fp32 accumulate MFMA is a bit-exact fp32 fma chain at the FP32 vector peak rate.
+#include "rvcx_kernels.h"
+
+namespace rvcx {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int CK = 32;   // contraction channels per LDS chunk
+constexpr int CKP = 36;  // padded LDS row: rows i..i+15 land on distinct 16-B bank slots
+constexpr int NTHREADS = 256;
+
+__device__ __forceinline__ float act_fn(float v, int act, float slope) {
+  switch (act) {
+    case ACT_LRELU: return v > 0.f ? v : v * slope;
+    case ACT_RELU: return v > 0.f ? v : 0.f;
+    case ACT_GELU: return 0.5f * v * (1.f + erff(v * 0.70710678118654752440f));
+    case ACT_TANH: return tanhf(v);
+    case ACT_SIGMOID: return 1.f / (1.f + expf(-v));
+    case ACT_LOGCLAMP: return logf(fmaxf(v, slope));
+    default: return v;
+  }
+}
+
+__device__ __forceinline__ void epilogue_store(const ConvArgs& a, float v, float bn, long long m, int n, int oh,
+                                               int ow, const float* R, const float* MK, float* Y) {
+  if (a.bias) v += bn;
+  if (a.res_mode == RES_ADD_PRE) v = v + R[m * a.ldr + n];
+  if (a.alpha != 1.f) v *= a.alpha;
+  v = act_fn(v, a.act, a.slope);
+  if (a.res_mode == RES_ADD_POST) v = v + R[m * a.ldr + n];
+  else if (a.res_mode == RES_RSUB_POST) v = R[m * a.ldr + n] - v;
+  float* dst;
+  if (a.out_map == OUT_UPSAMPLE2D) {
+    const int cv = a.out_cv;
+    const int ph = n / (2 * cv), pw = (n / cv) & 1, co = n % cv;
+    dst = Y + ((long long)(2 * oh + ph) * (2 * a.W_out) + (2 * ow + pw)) * a.ldy + co;
+  } else {
+    dst = Y + m * a.ldy + n;
+  }
+  if (a.acc_mode == ACC_ADD) v = *dst + v;
+  else if (a.acc_mode == ACC_ADD_DIV) v = (*dst + v) / a.acc_div;
+  if (MK) v *= MK[m];
+  *dst = v;
+}
+
+template <int BM, int BN, int WM, int WN, bool TWO_D>
+__global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a, const int nrows_a, const int rw,
+                                                             const int rh, const int tiles_w, const int vec_a,
+                                                             const int vec_b) {
+  constexpr int TM = BM / (WM * 32);
+  constexpr int TN = BN / (WN * 32);
+  static_assert(WM * WN == 4, "4 waves per block");
+  static_assert(TM >= 1 && TN >= 1, "tile too small");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* As = smem;
+  float* Bs = smem + nrows_a * CKP;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int li = lane & 31, hk = lane >> 5;
+  const int b = blockIdx.z / a.batch_inner;   // outer batch
+  const int bi = blockIdx.z % a.batch_inner;  // inner batch (heads / groups)
+  const int n0 = blockIdx.y * BN;
+  int m0 = 0, h0 = 0, w0 = 0;
+  if (!TWO_D) {
+    m0 = blockIdx.x * BM;
+  } else {
+    h0 = (blockIdx.x / tiles_w) * rh;
+    w0 = (blockIdx.x % tiles_w) * rw;
+  }
+  const float* X = a.x + (long long)b * a.x_bs + (long long)bi * a.x_bs2;
+  const float* Wb = a.w + (long long)b * a.w_bs + (long long)bi * a.w_bs2;
+  const float* PM = a.pre_mask ? a.pre_mask + (long long)b * a.pre_mask_bs : nullptr;
+  const int aw = TWO_D ? rw + a.KW - 1 : 0;
+  const int row0 = TWO_D ? 0 : m0 * a.stride - a.pad;
+
+  int base[TM];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+    const int ml = wm * TM * 32 + tm * 32 + li;
+    if (!TWO_D) {
+      base[tm] = ml * a.stride;
+    } else {
+      base[tm] = (ml < rh * rw) ? (ml / rw) * aw + (ml % rw) : 0;
+    }
+  }
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[tm][tn][r] = 0.f;
+
+  for (int c0 = 0; c0 < a.C_in; c0 += CK) {
+    __syncthreads();
+    // ---- stage A: nrows_a x 32 channels, pre-activation applied, zero outside the input
+    for (int idx = tid; idx < nrows_a * (CK / 4); idx += NTHREADS) {
+      const int r = idx >> 3;
+      const int c4 = (idx & 7) << 2;
+      const int c = c0 + c4;
+      long long grow;
+      bool valid;
+      if (!TWO_D) {
+        const int g = row0 + r;
+        valid = (g >= 0) && (g < a.T_in);
+        grow = g;
+      } else {
+        const int ah = r / aw, awi = r - ah * aw;
+        const int gh = h0 - a.padh + ah, gw = w0 - a.padw + awi;
+        valid = (gh >= 0) && (gh < a.T_in) && (gw >= 0) && (gw < a.W_in);
+        grow = (long long)gh * a.W_in + gw;
+      }
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (valid && c < a.C_in) {
+        const float* src = X + grow * a.ldx + c;
+        if (vec_a && c + 4 <= a.C_in) {
+          v = *reinterpret_cast<const f32x4*>(src);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = (c + j < a.C_in) ? src[j] : 0.f;
+        }
+        if (a.pre_act != ACT_NONE) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = act_fn(v[j], a.pre_act, a.pre_slope);
+        }
+        if (PM) {
+          const float mk = PM[grow];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] *= mk;
+        }
+      }
+      *reinterpret_cast<f32x4*>(&As[r * CKP + c4]) = v;
+    }
+    for (int tap = 0; tap < a.taps; ++tap) {
+      if (tap) __syncthreads();
+      // ---- stage B for (tap, chunk): Bs[n][c]
+      const float* Wt = Wb + (long long)tap * a.w_ts;
+      if (!a.b_kn) {
+        for (int idx = tid; idx < BN * (CK / 4); idx += NTHREADS) {
+          const int n = idx >> 3;
+          const int c4 = (idx & 7) << 2;
+          const int gn = n0 + n, c = c0 + c4;
+          f32x4 v = {0.f, 0.f, 0.f, 0.f};
+          if (gn < a.N && c < a.C_in) {
+            const float* src = Wt + (long long)gn * a.ldw + c;
+            if (vec_b && c + 4 <= a.C_in) {
+              v = *reinterpret_cast<const f32x4*>(src);
+            } else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) v[j] = (c + j < a.C_in) ? src[j] : 0.f;
+            }
+          }
+          *reinterpret_cast<f32x4*>(&Bs[n * CKP + c4]) = v;
+        }
+      } else {
+        for (int idx = tid; idx < CK * (BN / 4); idx += NTHREADS) {
+          const int c = idx / (BN / 4);
+          const int n4 = (idx - c * (BN / 4)) << 2;
+          const int gc = c0 + c, gn = n0 + n4;
+          f32x4 v = {0.f, 0.f, 0.f, 0.f};
+          if (gc < a.C_in && gn < a.N) {
+            const float* src = Wt + (long long)gc * a.ldw + gn;
+            if (vec_b && gn + 4 <= a.N) {
+              v = *reinterpret_cast<const f32x4*>(src);
+            } else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) v[j] = (gn + j < a.N) ? src[j] : 0.f;
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) Bs[(n4 + j) * CKP + c] = v[j];
+        }
+      }
+      __syncthreads();
+      // ---- MFMA over the chunk
+      const int toff = TWO_D ? (tap / a.KW) * aw + (tap % a.KW) : tap * a.dil;
+#pragma unroll
+      for (int kk = 0; kk < CK; kk += 8) {
+        float av[TM][4], bv[TN][4];
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+          const f32x4 t = *reinterpret_cast<const f32x4*>(&As[(base[tm] + toff) * CKP + kk + hk * 4]);
+          av[tm][0] = t[0]; av[tm][1] = t[1]; av[tm][2] = t[2]; av[tm][3] = t[3];
+        }
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+          const f32x4 t = *reinterpret_cast<const f32x4*>(&Bs[(wn * TN * 32 + tn * 32 + li) * CKP + kk + hk * 4]);
+          bv[tn][0] = t[0]; bv[tn][1] = t[1]; bv[tn][2] = t[2]; bv[tn][3] = t[3];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn)
+              acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[tm][j], bv[tn][j], acc[tm][tn], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- epilogue
+  const float* bias = a.bias ? a.bias + (long long)b * a.bias_bs + (long long)bi * a.bias_bs2 : nullptr;
+  const float* R = a.res ? a.res + (long long)b * a.res_bs + (long long)bi * a.res_bs2 : nullptr;
+  const float* MK = a.mask ? a.mask + (long long)b * a.mask_bs : nullptr;
+  float* Y = a.y + (long long)b * a.y_bs + (long long)bi * a.y_bs2;
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const int n = n0 + wn * TN * 32 + tn * 32 + li;
+      const bool n_ok = n < a.N;
+      const float bn = (bias && n_ok) ? bias[n] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ml = wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hk;
+        long long m;
+        int oh = 0, ow = 0;
+        bool ok;
+        if (!TWO_D) {
+          m = m0 + ml;
+          ok = n_ok && (m < a.T_out);
+        } else {
+          oh = h0 + ml / rw;
+          ow = w0 + ml % rw;
+          ok = n_ok && (ml < rh * rw) && (oh < a.T_out) && (ow < a.W_out);
+          m = (long long)oh * a.W_out + ow;
+        }
+        if (ok) epilogue_store(a, acc[tm][tn][r], bn, m, n, oh, ow, R, MK, Y);
+      }
+    }
+  }
+}
+
+namespace {
+
+struct TileCfg {
+  int BM, BN;
+};
+
+template <int BM, int BN, int WM, int WN, bool TWO_D>
+hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
+  int nrows_a, rw = 0, rh = 0, tiles_w = 1, mtiles;
+  if (!TWO_D) {
+    nrows_a = (BM - 1) * a.stride + (a.taps - 1) * a.dil + 1;
+    mtiles = (a.T_out + BM - 1) / BM;
+  } else {
+    rw = a.W_out < BM ? a.W_out : BM;
+    rh = BM / rw;
+    tiles_w = (a.W_out + rw - 1) / rw;
+    mtiles = ((a.T_out + rh - 1) / rh) * tiles_w;
+    nrows_a = (rh + a.KH - 1) * (rw + a.KW - 1);
+  }
+  const size_t smem = (size_t)(nrows_a + BN) * CKP * sizeof(float);
+  if (smem > 160 * 1024) return hipErrorInvalidValue;
+  const int vec_a = ((a.ldx & 3) == 0) && ((reinterpret_cast<uintptr_t>(a.x) & 15) == 0) &&
+                    ((a.x_bs & 3) == 0) && ((a.x_bs2 & 3) == 0);
+  const int vec_b = ((a.ldw & 3) == 0) && ((reinterpret_cast<uintptr_t>(a.w) & 15) == 0) &&
+                    ((a.w_bs & 3) == 0) && ((a.w_bs2 & 3) == 0) && ((a.w_ts & 3) == 0);
+  if (a.batch_inner < 1) return hipErrorInvalidValue;
+  dim3 grid(mtiles, (a.N + BN - 1) / BN, a.batch * a.batch_inner);
+  auto kern = conv_gemm_kernel<BM, BN, WM, WN, TWO_D>;
+  if (smem > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(kern, grid, dim3(NTHREADS), smem, s, a, nrows_a, rw, rh, tiles_w, vec_a, vec_b);
+  return hipGetLastError();
+}
+
+template <bool TWO_D>
+hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
+  if (a.N <= 0 || a.T_out <= 0 || a.batch <= 0) return hipSuccess;
+  if (a.C_in <= 0 || a.taps <= 0) return hipErrorInvalidValue;
+  const long long M = TWO_D ? (long long)a.T_out * a.W_out : a.T_out;
+  const long long work = M * a.batch * a.batch_inner;
+  if (a.N <= 32) {
+    if (work >= 256 * 256) return launch_cfg<256, 32, 4, 1, TWO_D>(a, s);
+    return launch_cfg<128, 32, 4, 1, TWO_D>(a, s);
+  }
+  if (a.N <= 64) {
+    if (work >= 128 * 512) return launch_cfg<128, 64, 2, 2, TWO_D>(a, s);
+    return launch_cfg<64, 64, 2, 2, TWO_D>(a, s);
+  }
+  if (((work + 127) / 128) * ((a.N + 63) / 64) >= 512) return launch_cfg<128, 64, 2, 2, TWO_D>(a, s);
+  return launch_cfg<64, 64, 2, 2, TWO_D>(a, s);
+}
+
+}  // namespace
+
+hipError_t conv1d(const ConvArgs& a, hipStream_t s) { return dispatch<false>(a, s); }
+hipError_t conv2d(const ConvArgs& a, hipStream_t s) { return dispatch<true>(a, s); }
+
+}  // namespace rvcx

@@ -1,0 +1,135 @@
+// rvcx runtime internals: context, weight store, workspace.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/rvcx.h"
+#include "rvcx_kernels.h"
+
+namespace rvcx {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define RVCX_HIP(expr)                                                                                 \
+  do {                                                                                                 \
+    hipError_t e_ = (expr);                                                                            \
+    if (e_ != hipSuccess)                                                                              \
+      throw ::rvcx::Error(RVCX_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_) + " at " +     \
+                                          __FILE__ + ":" + std::to_string(__LINE__));                  \
+  } while (0)
+
+struct HostTensor {
+  std::vector<float> v;
+  std::vector<int64_t> shape;
+  size_t numel() const { return v.size(); }
+};
+
+// Device buffer (owned).
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+struct SynthCfg {
+  int I = 192, H = 192, F = 768, n_heads = 2, n_layers = 6, ksize = 3;
+  std::vector<int> rb_k{3, 7, 11};
+  std::vector<std::vector<int>> rb_d{{1, 3, 5}, {1, 3, 5}, {1, 3, 5}};
+  std::vector<int> ups{12, 10, 2, 2};
+  int C0 = 512;
+  std::vector<int> up_k{24, 20, 4, 4};
+  int n_spk = 109, gin = 256, sr = 48000, emb_dim = 768;
+  int window = 10, flow_k = 5, flow_layers = 3, flow_n = 4;
+  int upp() const {
+    int u = 1;
+    for (int x : ups) u *= x;
+    return u;
+  }
+};
+
+// ConvTranspose1d lowered to a polyphase conv: input row for output q, tap t is q + t - pad.
+struct UpsLayer {
+  int cin = 0, cout = 0, u = 0, k = 0, taps = 0, pad = 0;
+  float* w = nullptr;     // [taps][u*cout][cin]
+  float* b = nullptr;     // [u*cout]
+};
+
+struct Ctx {
+  int device = 0;
+  std::string err;
+  SynthCfg scfg;
+  bool synth_cfg_set = false;
+  std::map<std::string, HostTensor> host[3];
+  std::map<std::string, std::unique_ptr<DevBuf>> dev;  // packed weights
+  bool ready[3] = {false, false, false};
+  std::vector<UpsLayer> ups;
+  // pipeline high-pass (rvc/infer/pipeline.py:22-27), normalised so a[0] = 1
+  int hp_order = 0;
+  std::vector<double> hp_b, hp_a, hp_zi, hp_FL;
+  // workspace pool
+  std::map<std::string, std::unique_ptr<DevBuf>> ws;
+  uint64_t call_counter = 0;
+
+  float* W(const std::string& name) const;
+  float* alloc_weight(const std::string& name, const std::vector<float>& data);
+  template <class T>
+  T* buf(const std::string& name, size_t count, hipStream_t s);
+};
+
+template <class T>
+T* Ctx::buf(const std::string& name, size_t count, hipStream_t s) {
+  size_t bytes = count * sizeof(T);
+  if (bytes == 0) bytes = 16;
+  bytes = (bytes + 255) & ~size_t(255);
+  auto& slot = ws[name];
+  if (!slot || slot->bytes < bytes) {
+    if (slot && slot->p) RVCX_HIP(hipStreamSynchronize(s));
+    slot.reset(new DevBuf());
+    if (hipMalloc(&slot->p, bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      throw Error(RVCX_E_OOM, "workspace allocation failed: " + name + " (" + std::to_string(bytes) + " B)");
+    }
+    slot->bytes = bytes;
+  }
+  return static_cast<T*>(slot->p);
+}
+
+// model forward passes (runtime_*.cpp)
+void finalize_synth(Ctx& c);
+void finalize_hubert(Ctx& c);
+void finalize_rmvpe(Ctx& c);
+int64_t hubert_forward(Ctx& c, const float* audio, int64_t n, int version, float* feats, int64_t cap,
+                       hipStream_t s);
+int64_t rmvpe_forward(Ctx& c, const float* audio, int64_t n, float thred, double* f0, int64_t cap, float* hidden,
+                      hipStream_t s);
+void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* lengths, const int32_t* pitch,
+                   const float* pitchf, const int32_t* sid, const float* eps_z, const float* eps_src, uint64_t seed,
+                   float* out, float* zp_out, float* z_out, hipStream_t s);
+void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, const float* f0, const float* g,
+                 const float* eps_src, uint64_t seed, float* out, hipStream_t s);
+
+void set_highpass(Ctx& c, const double* b, const double* a, const double* zi, int order);
+int64_t pipeline_forward(Ctx& c, const double* audio, int64_t n, int sid, double semitones, float protect,
+                         int64_t t_pad, int64_t t_pad_tgt, const float* eps_z, const float* eps_src, uint64_t seed,
+                         float* out, int64_t cap, double* f0_out, hipStream_t s);
+void set_i32(int32_t* p, int32_t v, hipStream_t s);
+
+inline void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw Error(RVCX_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+}  // namespace rvcx

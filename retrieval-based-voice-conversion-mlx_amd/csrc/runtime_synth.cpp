@@ -1,0 +1,538 @@
+// Synthesizer (TextEncoder -> flow reverse -> HiFiGAN-NSF) on device: weight repacking and
+// the forward pass as a sequence of MFMA conv-GEMM launches plus small fused kernels.
+// Reference semantics: rvc/lib/algorithm/{synthesizers,encoders,attentions,modules,residuals}.py,
+// generators/{hifigan_nsf,hifigan}.py (see each block's comment for file:line).
+#include <cmath>
+#include <cstring>
+
+#include "runtime.h"
+
+namespace rvcx {
+
+namespace {
+
+uint64_t splitmix(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+const HostTensor& get(Ctx& c, int model, const std::string& n, std::vector<int64_t> shape) {
+  auto it = c.host[model].find(n);
+  if (it == c.host[model].end()) throw Error(RVCX_E_STATE, "missing weight: " + n);
+  if (it->second.shape != shape) {
+    std::string got, want;
+    for (auto s : it->second.shape) got += std::to_string(s) + ",";
+    for (auto s : shape) want += std::to_string(s) + ",";
+    throw Error(RVCX_E_SHAPE, "weight " + n + " has shape (" + got + ") expected (" + want + ")");
+  }
+  return it->second;
+}
+
+// torch Conv1d weight [O][I][K] -> [K][O][I]
+std::vector<float> pack_conv1d(const HostTensor& t) {
+  const int64_t O = t.shape[0], I = t.shape[1], K = t.shape[2];
+  std::vector<float> out(t.v.size());
+  for (int64_t o = 0; o < O; ++o)
+    for (int64_t i = 0; i < I; ++i)
+      for (int64_t k = 0; k < K; ++k) out[(k * O + o) * I + i] = t.v[(o * I + i) * K + k];
+  return out;
+}
+
+std::vector<float> cat(std::initializer_list<const std::vector<float>*> parts) {
+  std::vector<float> out;
+  for (auto* p : parts) out.insert(out.end(), p->begin(), p->end());
+  return out;
+}
+
+ConvArgs lin(const float* x, int ldx, int rows, int K, const float* w, int N, const float* bias, float* y, int ldy) {
+  ConvArgs a;
+  a.x = x;
+  a.ldx = ldx;
+  a.T_in = rows;
+  a.C_in = K;
+  a.w = w;
+  a.ldw = K;
+  a.taps = 1;
+  a.y = y;
+  a.ldy = ldy;
+  a.T_out = rows;
+  a.N = N;
+  a.bias = bias;
+  return a;
+}
+
+// 1-D conv over B independent sequences of T rows ([B][T][ld]); weights packed [taps][N][Cin].
+ConvArgs conv(const float* x, int ldx, int Tin, int Cin, const float* w, int N, int taps, int dil, int pad,
+              const float* bias, float* y, int ldy, int Tout, int B) {
+  ConvArgs a;
+  a.x = x;
+  a.ldx = ldx;
+  a.T_in = Tin;
+  a.C_in = Cin;
+  a.x_bs = (long long)Tin * ldx;
+  a.w = w;
+  a.ldw = Cin;
+  a.w_ts = (long long)N * Cin;
+  a.taps = taps;
+  a.dil = dil;
+  a.pad = pad;
+  a.stride = 1;
+  a.y = y;
+  a.ldy = ldy;
+  a.y_bs = (long long)Tout * ldy;
+  a.T_out = Tout;
+  a.N = N;
+  a.bias = bias;
+  a.batch = B;
+  return a;
+}
+
+void run(const ConvArgs& a, hipStream_t s) { check(conv1d(a, s), "conv1d"); }
+
+}  // namespace
+
+float* Ctx::W(const std::string& name) const {
+  auto it = dev.find(name);
+  if (it == dev.end()) throw Error(RVCX_E_STATE, "packed weight not found: " + name);
+  return static_cast<float*>(it->second->p);
+}
+
+float* Ctx::alloc_weight(const std::string& name, const std::vector<float>& data) {
+  std::unique_ptr<DevBuf> b(new DevBuf());
+  size_t bytes = data.size() * sizeof(float);
+  if (bytes == 0) bytes = 16;
+  if (hipMalloc(&b->p, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    throw Error(RVCX_E_OOM, "weight allocation failed: " + name);
+  }
+  b->bytes = bytes;
+  RVCX_HIP(hipMemcpy(b->p, data.data(), data.size() * sizeof(float), hipMemcpyHostToDevice));
+  float* p = static_cast<float*>(b->p);
+  dev[name] = std::move(b);
+  return p;
+}
+
+// ------------------------------------------------------------------ weight repacking
+void finalize_synth(Ctx& c) {
+  const SynthCfg& g = c.scfg;
+  const int H = g.H, I = g.I, F = g.F, E = g.emb_dim, dk = H / g.n_heads, nw = 2 * g.window + 1;
+  const int M = 0;
+  // TextEncoder (encoders.py:88-144)
+  c.alloc_weight("te.emb_phone.w", get(c, M, "enc_p.emb_phone.weight", {H, E}).v);
+  c.alloc_weight("te.emb_phone.b", get(c, M, "enc_p.emb_phone.bias", {H}).v);
+  c.alloc_weight("te.emb_pitch", get(c, M, "enc_p.emb_pitch.weight", {256, H}).v);
+  for (int i = 0; i < g.n_layers; ++i) {
+    const std::string p = "enc_p.encoder.attn_layers." + std::to_string(i);
+    const std::string q = "te." + std::to_string(i);
+    auto& wq = get(c, M, p + ".conv_q.weight", {H, H, 1}).v;
+    auto& wk = get(c, M, p + ".conv_k.weight", {H, H, 1}).v;
+    auto& wv = get(c, M, p + ".conv_v.weight", {H, H, 1}).v;
+    c.alloc_weight(q + ".qkv.w", cat({&wq, &wk, &wv}));
+    auto& bq = get(c, M, p + ".conv_q.bias", {H}).v;
+    auto& bk = get(c, M, p + ".conv_k.bias", {H}).v;
+    auto& bv = get(c, M, p + ".conv_v.bias", {H}).v;
+    c.alloc_weight(q + ".qkv.b", cat({&bq, &bk, &bv}));
+    c.alloc_weight(q + ".o.w", get(c, M, p + ".conv_o.weight", {H, H, 1}).v);
+    c.alloc_weight(q + ".o.b", get(c, M, p + ".conv_o.bias", {H}).v);
+    c.alloc_weight(q + ".rel_k", get(c, M, p + ".emb_rel_k", {1, nw, dk}).v);
+    c.alloc_weight(q + ".rel_v", get(c, M, p + ".emb_rel_v", {1, nw, dk}).v);
+    const std::string n1 = "enc_p.encoder.norm_layers_1." + std::to_string(i);
+    const std::string n2 = "enc_p.encoder.norm_layers_2." + std::to_string(i);
+    c.alloc_weight(q + ".ln1.g", get(c, M, n1 + ".gamma", {H}).v);
+    c.alloc_weight(q + ".ln1.b", get(c, M, n1 + ".beta", {H}).v);
+    c.alloc_weight(q + ".ln2.g", get(c, M, n2 + ".gamma", {H}).v);
+    c.alloc_weight(q + ".ln2.b", get(c, M, n2 + ".beta", {H}).v);
+    const std::string f = "enc_p.encoder.ffn_layers." + std::to_string(i);
+    c.alloc_weight(q + ".ffn1.w", pack_conv1d(get(c, M, f + ".conv_1.weight", {F, H, g.ksize})));
+    c.alloc_weight(q + ".ffn1.b", get(c, M, f + ".conv_1.bias", {F}).v);
+    c.alloc_weight(q + ".ffn2.w", pack_conv1d(get(c, M, f + ".conv_2.weight", {H, F, g.ksize})));
+    c.alloc_weight(q + ".ffn2.b", get(c, M, f + ".conv_2.bias", {H}).v);
+  }
+  c.alloc_weight("te.proj.w", get(c, M, "enc_p.proj.weight", {2 * I, H, 1}).v);
+  c.alloc_weight("te.proj.b", get(c, M, "enc_p.proj.bias", {2 * I}).v);
+  // flow (residuals.py:103-258, modules.py:5-117)
+  for (int f = 0; f < g.flow_n; ++f) {
+    const std::string p = "flow.flows." + std::to_string(2 * f);
+    const std::string q = "flow." + std::to_string(f);
+    c.alloc_weight(q + ".pre.w", get(c, M, p + ".pre.weight", {H, I / 2, 1}).v);
+    c.alloc_weight(q + ".pre.b", get(c, M, p + ".pre.bias", {H}).v);
+    const int cl = 2 * H * g.flow_layers;
+    c.alloc_weight(q + ".cond.w", get(c, M, p + ".enc.cond_layer.weight", {cl, g.gin, 1}).v);
+    c.alloc_weight(q + ".cond.b", get(c, M, p + ".enc.cond_layer.bias", {cl}).v);
+    for (int L = 0; L < g.flow_layers; ++L) {
+      const std::string l = std::to_string(L);
+      c.alloc_weight(q + ".in" + l + ".w",
+                     pack_conv1d(get(c, M, p + ".enc.in_layers." + l + ".weight", {2 * H, H, g.flow_k})));
+      c.alloc_weight(q + ".in" + l + ".b", get(c, M, p + ".enc.in_layers." + l + ".bias", {2 * H}).v);
+      const int rs = (L == g.flow_layers - 1) ? H : 2 * H;
+      c.alloc_weight(q + ".rs" + l + ".w", get(c, M, p + ".enc.res_skip_layers." + l + ".weight", {rs, H, 1}).v);
+      c.alloc_weight(q + ".rs" + l + ".b", get(c, M, p + ".enc.res_skip_layers." + l + ".bias", {rs}).v);
+    }
+    c.alloc_weight(q + ".post.w", get(c, M, p + ".post.weight", {I / 2, H, 1}).v);
+    c.alloc_weight(q + ".post.b", get(c, M, p + ".post.bias", {I / 2}).v);
+  }
+  c.alloc_weight("emb_g", get(c, M, "emb_g.weight", {g.n_spk, g.gin}).v);
+  // HiFiGAN-NSF (generators/hifigan_nsf.py:55-171)
+  const int C0 = g.C0;
+  c.alloc_weight("dec.pre.w", pack_conv1d(get(c, M, "dec.conv_pre.weight", {C0, I, 7})));
+  c.alloc_weight("dec.pre.b", get(c, M, "dec.conv_pre.bias", {C0}).v);
+  c.alloc_weight("dec.cond.w", get(c, M, "dec.cond.weight", {C0, g.gin, 1}).v);
+  c.alloc_weight("dec.cond.b", get(c, M, "dec.cond.bias", {C0}).v);
+  {
+    auto& lw = get(c, M, "dec.m_source.l_linear.weight", {1, 1}).v;
+    auto& lb = get(c, M, "dec.m_source.l_linear.bias", {1}).v;
+    c.alloc_weight("dec.src.lin", {lw[0], lb[0]});
+    c.host[M]["__src_lin__"] = HostTensor{{lw[0], lb[0]}, {2}};
+  }
+  c.ups.clear();
+  const int nu = (int)g.ups.size();
+  for (int i = 0; i < nu; ++i) {
+    const int cin = C0 >> i, cout = C0 >> (i + 1), u = g.ups[i], k = g.up_k[i];
+    const int p = (u % 2 == 0) ? (k - u) / 2 : u / 2 + u % 2;
+    const int op = u % 2;
+    if (k + op - 2 * p != u)
+      throw Error(RVCX_E_SHAPE, "ConvTranspose1d stage " + std::to_string(i) + ": output length != T*u unsupported");
+    const std::string n = "dec.ups." + std::to_string(i);
+    auto& w = get(c, M, n + ".weight", {cin, cout, k});
+    auto& b = get(c, M, n + ".bias", {cout});
+    auto fdiv = [](int a, int bb) { return (a >= 0) ? a / bb : -((-a + bb - 1) / bb); };
+    int smin = 1 << 30, smax = -(1 << 30);
+    for (int r = 0; r < u; ++r) {
+      const int lo = -fdiv(r + p, u);                // ceil(-(r+p)/u)
+      const int hi = fdiv(k - 1 - r - p, u);         // floor((k-1-r-p)/u)
+      smin = std::min(smin, lo);
+      smax = std::max(smax, hi);
+    }
+    UpsLayer L;
+    L.cin = cin;
+    L.cout = cout;
+    L.u = u;
+    L.k = k;
+    L.taps = smax - smin + 1;
+    L.pad = smax;
+    std::vector<float> wv((size_t)L.taps * u * cout * cin, 0.f), bv((size_t)u * cout);
+    for (int tau = 0; tau < L.taps; ++tau) {
+      const int s = smax - tau;
+      for (int r = 0; r < u; ++r) {
+        const int kk = s * u + r + p;
+        if (kk < 0 || kk >= k) continue;
+        for (int co = 0; co < cout; ++co)
+          for (int ci = 0; ci < cin; ++ci)
+            wv[(((size_t)tau * u + r) * cout + co) * cin + ci] = w.v[((size_t)ci * cout + co) * k + kk];
+      }
+    }
+    for (int r = 0; r < u; ++r)
+      for (int co = 0; co < cout; ++co) bv[(size_t)r * cout + co] = b.v[co];
+    L.w = c.alloc_weight(n + ".vw", wv);
+    L.b = c.alloc_weight(n + ".vb", bv);
+    c.ups.push_back(L);
+    // noise conv (C_in = 1)
+    int stride = 1;
+    for (int j = i + 1; j < nu; ++j) stride *= g.ups[j];
+    const int kern = stride == 1 ? 1 : stride * 2 - stride % 2;
+    const std::string nn = "dec.noise_convs." + std::to_string(i);
+    c.alloc_weight(nn + ".w", get(c, M, nn + ".weight", {cout, 1, kern}).v);
+    c.alloc_weight(nn + ".b", get(c, M, nn + ".bias", {cout}).v);
+  }
+  const int nk = (int)g.rb_k.size();
+  for (int i = 0; i < nu; ++i) {
+    const int C = C0 >> (i + 1);
+    for (int j = 0; j < nk; ++j) {
+      const int k = g.rb_k[j];
+      const std::string rb = "dec.resblocks." + std::to_string(i * nk + j);
+      for (size_t m = 0; m < g.rb_d[j].size(); ++m) {
+        for (const char* cv : {"convs1", "convs2"}) {
+          const std::string n = rb + "." + cv + "." + std::to_string(m);
+          c.alloc_weight(n + ".w", pack_conv1d(get(c, M, n + ".weight", {C, C, k})));
+          c.alloc_weight(n + ".b", get(c, M, n + ".bias", {C}).v);
+        }
+      }
+    }
+  }
+  const int Cl = C0 >> nu;
+  c.alloc_weight("dec.post.w", get(c, M, "dec.conv_post.weight", {1, Cl, 7}).v);
+}
+
+// ------------------------------------------------------------------ generator
+// HiFiGANNSFGenerator.forward (generators/hifigan_nsf.py:173-212); z_btc [B][T][I] time-major.
+void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, const float* f0, const float* g,
+                 const float* eps_src, uint64_t seed, float* out, hipStream_t s) {
+  const SynthCfg& cf = c.scfg;
+  const int I = cf.I, C0 = cf.C0, upp = cf.upp();
+  const long long Nh = (long long)T * upp;
+  // NSF source (SineGen + l_linear + tanh)
+  float* har = c.buf<float>("dec.har", (size_t)B * Nh, s);
+  double* cum = c.buf<double>("dec.cum", (size_t)B * T, s);
+  const auto& lin_wb = c.host[0].at("__src_lin__").v;
+  check(sine_source(f0, B, T, upp, (float)cf.sr, eps_src, splitmix(seed ^ 0x5352434e4f495345ull), lin_wb[0],
+                    lin_wb[1], cum, har, s),
+        "sine_source");
+  // conv_pre + cond(g)
+  float* cv = c.buf<float>("dec.cvec", (size_t)B * C0, s);
+  run(lin(g, cf.gin, B, cf.gin, c.W("dec.cond.w"), C0, c.W("dec.cond.b"), cv, C0), s);
+  // stage buffers sized for the largest stage
+  size_t maxe = (size_t)T * C0;
+  {
+    long long t = T;
+    for (size_t i = 0; i < cf.ups.size(); ++i) {
+      t *= cf.ups[i];
+      maxe = std::max(maxe, (size_t)t * (C0 >> (i + 1)));
+    }
+  }
+  float* xin = c.buf<float>("dec.x", (size_t)B * maxe, s);
+  float* y = c.buf<float>("dec.y", (size_t)B * maxe, s);
+  float* R = c.buf<float>("dec.r", (size_t)B * maxe, s);
+  float* t1 = c.buf<float>("dec.t", (size_t)B * maxe, s);
+  {
+    ConvArgs a = conv(z_btc, I, T, I, c.W("dec.pre.w"), C0, 7, 1, 3, c.W("dec.pre.b"), xin, C0, T, B);
+    a.pre_mask = mask;
+    a.pre_mask_bs = T;
+    a.res = cv;
+    a.ldr = 0;
+    a.res_bs = C0;
+    a.res_mode = RES_ADD_PRE;
+    run(a, s);
+  }
+  float* cur = xin;
+  int curT = T, Cin = C0;
+  const int nk = (int)cf.rb_k.size();
+  for (size_t i = 0; i < cf.ups.size(); ++i) {
+    const UpsLayer& L = c.ups[i];
+    const int C = L.cout, u = L.u, Ti = curT * u;
+    // LeakyReLU(0.1) -> ConvTranspose1d (polyphase) ; output [B][curT][u*C] == [B][Ti][C]
+    ConvArgs a = conv(cur, Cin, curT, Cin, L.w, u * C, L.taps, 1, L.pad, L.b, y, u * C, curT, B);
+    a.pre_act = ACT_LRELU;
+    a.pre_slope = 0.1f;
+    run(a, s);
+    // + noise_convs[i](har)
+    int stride = 1;
+    for (size_t j = i + 1; j < cf.ups.size(); ++j) stride *= cf.ups[j];
+    const int kern = stride == 1 ? 1 : stride * 2 - stride % 2;
+    const int npad = stride == 1 ? 0 : (kern - stride) / 2;
+    const std::string nn = "dec.noise_convs." + std::to_string(i);
+    check(noise_conv_add(har, (int)Nh, y, B, Ti, C, (long long)Ti * C, c.W(nn + ".w"), c.W(nn + ".b"), kern, stride,
+                         npad, s),
+          "noise_conv_add");
+    // mean of the ResBlocks (residuals.py:71-80) accumulated into S. `cur` (= xin) is dead once the
+    // ConvTranspose above has consumed it, so S reuses it and becomes the next stage's input.
+    float* S = xin;
+    float* T1 = t1;
+    float* RR = R;
+    for (int j = 0; j < nk; ++j) {
+      const int k = cf.rb_k[j];
+      const auto& dil = cf.rb_d[j];
+      const std::string rb = "dec.resblocks." + std::to_string(i * nk + j);
+      const float* r_in = y;
+      for (size_t m = 0; m < dil.size(); ++m) {
+        const int d = dil[m];
+        const std::string n1 = rb + ".convs1." + std::to_string(m);
+        const std::string n2 = rb + ".convs2." + std::to_string(m);
+        ConvArgs a1 = conv(r_in, C, Ti, C, c.W(n1 + ".w"), C, k, d, (k * d - d) / 2, c.W(n1 + ".b"), T1, C, Ti, B);
+        a1.pre_act = ACT_LRELU;
+        a1.pre_slope = 0.1f;
+        a1.act = ACT_LRELU;
+        a1.slope = 0.1f;
+        run(a1, s);
+        const bool last = (m + 1 == dil.size());
+        float* dst = last ? S : RR;
+        ConvArgs a2 = conv(T1, C, Ti, C, c.W(n2 + ".w"), C, k, 1, (k - 1) / 2, c.W(n2 + ".b"), dst, C, Ti, B);
+        a2.res = r_in;
+        a2.ldr = C;
+        a2.res_bs = (long long)Ti * C;
+        a2.res_mode = RES_ADD_POST;
+        if (last) {
+          a2.acc_mode = (j == 0) ? ACC_STORE : ((j + 1 == nk) ? ACC_ADD_DIV : ACC_ADD);
+          a2.acc_div = (float)nk;
+        }
+        run(a2, s);
+        r_in = RR;
+      }
+    }
+    cur = S;
+    curT = Ti;
+    Cin = C;
+  }
+  // LeakyReLU(0.01) -> conv_post (no bias) -> tanh
+  check(conv_post_tanh(cur, B, curT, Cin, c.W("dec.post.w"), 7, 0.01f, out, s), "conv_post");
+}
+
+// ------------------------------------------------------------------ Synthesizer.infer
+void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* lengths, const int32_t* pitch,
+                   const float* pitchf, const int32_t* sid, const float* eps_z, const float* eps_src, uint64_t seed,
+                   float* out, float* zp_out, float* z_out, hipStream_t s) {
+  const SynthCfg& cf = c.scfg;
+  const int H = cf.H, I = cf.I, F = cf.F, E = cf.emb_dim, nh = cf.n_heads, dk = H / nh, nw = 2 * cf.window + 1;
+  const long long BT = (long long)B * T;
+  float* mask = c.buf<float>("te.mask", BT, s);
+  check(seq_mask(lengths, mask, B, T, s), "seq_mask");
+  float* g = c.buf<float>("spk.g", (size_t)B * cf.gin, s);
+  check(gather_rows(c.W("emb_g"), cf.gin, sid, g, B, cf.gin, s), "emb_g");
+  // ---- TextEncoder (encoders.py:128-144)
+  float* pe = c.buf<float>("te.pe", BT * H, s);
+  check(gather_rows(c.W("te.emb_pitch"), H, pitch, pe, (int)BT, H, s), "emb_pitch");
+  float* x = c.buf<float>("te.x", BT * H, s);
+  {
+    ConvArgs a = lin(phone, E, (int)BT, E, c.W("te.emb_phone.w"), H, c.W("te.emb_phone.b"), x, H);
+    a.res = pe;
+    a.ldr = H;
+    a.res_mode = RES_ADD_PRE;
+    a.alpha = (float)std::sqrt((double)H);
+    a.act = ACT_LRELU;
+    a.slope = 0.1f;
+    a.mask = mask;
+    run(a, s);
+  }
+  float* qkv = c.buf<float>("te.qkv", BT * 3 * H, s);
+  float* sc = c.buf<float>("te.scores", (size_t)B * nh * T * T, s);
+  float* rel = c.buf<float>("te.rel", (size_t)B * nh * T * nw, s);
+  float* pband = c.buf<float>("te.pband", (size_t)B * nh * T * nw, s);
+  float* att = c.buf<float>("te.att", BT * H, s);
+  float* o = c.buf<float>("te.o", BT * H, s);
+  float* h1 = c.buf<float>("te.h1", BT * F, s);
+  const float qscale = (float)(1.0 / std::sqrt((double)dk));
+  for (int i = 0; i < cf.n_layers; ++i) {
+    const std::string q = "te." + std::to_string(i);
+    run(lin(x, H, (int)BT, H, c.W(q + ".qkv.w"), 3 * H, c.W(q + ".qkv.b"), qkv, 3 * H), s);
+    {  // scores = (q / sqrt(dk)) k^T   (attentions.py:96)
+      ConvArgs a = lin(qkv, 3 * H, T, dk, qkv + H, T, nullptr, sc, T);
+      a.ldw = 3 * H;
+      a.alpha = qscale;
+      a.batch = B;
+      a.batch_inner = nh;
+      a.x_bs = (long long)T * 3 * H;
+      a.x_bs2 = dk;
+      a.w_bs = (long long)T * 3 * H;
+      a.w_bs2 = dk;
+      a.y_bs = (long long)nh * T * T;
+      a.y_bs2 = (long long)T * T;
+      run(a, s);
+    }
+    {  // relative key logits (attentions.py:127-132)
+      ConvArgs a = lin(qkv, 3 * H, T, dk, c.W(q + ".rel_k"), nw, nullptr, rel, nw);
+      a.alpha = qscale;
+      a.batch = B;
+      a.batch_inner = nh;
+      a.x_bs = (long long)T * 3 * H;
+      a.x_bs2 = dk;
+      a.y_bs = (long long)nh * T * nw;
+      a.y_bs2 = (long long)T * nw;
+      run(a, s);
+    }
+    check(softmax_rel(sc, T, nh, B, rel, cf.window, mask, pband, 0, s), "softmax_rel");
+    {  // p v   (attentions.py:120)
+      ConvArgs a = lin(sc, T, T, T, qkv + 2 * H, dk, nullptr, att, H);
+      a.ldw = 3 * H;
+      a.b_kn = 1;
+      a.batch = B;
+      a.batch_inner = nh;
+      a.x_bs = (long long)nh * T * T;
+      a.x_bs2 = (long long)T * T;
+      a.w_bs = (long long)T * 3 * H;
+      a.w_bs2 = dk;
+      a.y_bs = (long long)T * H;
+      a.y_bs2 = dk;
+      run(a, s);
+    }
+    {  // + relative values (attentions.py:122-123, 134-141)
+      ConvArgs a = lin(pband, nw, T, nw, c.W(q + ".rel_v"), dk, nullptr, att, H);
+      a.ldw = dk;
+      a.b_kn = 1;
+      a.batch = B;
+      a.batch_inner = nh;
+      a.x_bs = (long long)nh * T * nw;
+      a.x_bs2 = (long long)T * nw;
+      a.y_bs = (long long)T * H;
+      a.y_bs2 = dk;
+      a.acc_mode = ACC_ADD;
+      run(a, s);
+    }
+    run(lin(att, H, (int)BT, H, c.W(q + ".o.w"), H, c.W(q + ".o.b"), o, H), s);
+    check(layernorm_rows(x, o, x, c.W(q + ".ln1.g"), c.W(q + ".ln1.b"), (int)BT, H, 1e-5f, nullptr, s), "ln1");
+    {  // FFN (attentions.py:221-231): conv_1(pad(x*mask)) -> relu -> conv_2(pad(.*mask)) * mask
+      ConvArgs a = conv(x, H, T, H, c.W(q + ".ffn1.w"), F, cf.ksize, 1, (cf.ksize - 1) / 2, c.W(q + ".ffn1.b"), h1,
+                        F, T, B);
+      a.pre_mask = mask;
+      a.pre_mask_bs = T;
+      a.act = ACT_RELU;
+      run(a, s);
+      ConvArgs b = conv(h1, F, T, F, c.W(q + ".ffn2.w"), H, cf.ksize, 1, (cf.ksize - 1) / 2, c.W(q + ".ffn2.b"), o,
+                        H, T, B);
+      b.pre_mask = mask;
+      b.pre_mask_bs = T;
+      b.mask = mask;
+      b.mask_bs = T;
+      run(b, s);
+    }
+    check(layernorm_rows(x, o, x, c.W(q + ".ln2.g"), c.W(q + ".ln2.b"), (int)BT, H, 1e-5f, nullptr, s), "ln2");
+  }
+  float* stats = c.buf<float>("te.stats", BT * 2 * I, s);
+  {
+    ConvArgs a = lin(x, H, (int)BT, H, c.W("te.proj.w"), 2 * I, c.W("te.proj.b"), stats, 2 * I);
+    a.pre_mask = mask;
+    a.mask = mask;
+    run(a, s);
+  }
+  // ---- z_p = (m + exp(logs) * eps * 0.66666) * mask   (synthesizers.py:228)
+  float* z = c.buf<float>("flow.z", BT * I, s);
+  float* xf = c.buf<float>("flow.xf", BT * I, s);
+  check(zp_sample(stats, B, T, I, eps_z, splitmix(seed ^ 0x5a505f4e4f495345ull), mask, z, s), "zp_sample");
+  if (zp_out) RVCX_HIP(hipMemcpyAsync(zp_out, z, BT * I * sizeof(float), hipMemcpyDeviceToDevice, s));
+  // ---- flow reverse (residuals.py:151-164, 233-258; modules.py:78-109)
+  float* hb = c.buf<float>("flow.h", BT * H, s);
+  float* outb = c.buf<float>("flow.out", BT * H, s);
+  float* xin = c.buf<float>("flow.xin", BT * 2 * H, s);
+  float* acts = c.buf<float>("flow.acts", BT * H, s);
+  const int cl = 2 * H * cf.flow_layers;
+  float* gc = c.buf<float>("flow.gc", (size_t)B * cl, s);
+  for (int f = cf.flow_n - 1; f >= 0; --f) {
+    const std::string q = "flow." + std::to_string(f);
+    check(channel_flip(z, xf, (int)BT, I, s), "flip");
+    {
+      ConvArgs a = lin(xf, I, (int)BT, I / 2, c.W(q + ".pre.w"), H, c.W(q + ".pre.b"), hb, H);
+      a.mask = mask;
+      run(a, s);
+    }
+    run(lin(g, cf.gin, B, cf.gin, c.W(q + ".cond.w"), cl, c.W(q + ".cond.b"), gc, cl), s);
+    for (int L = 0; L < cf.flow_layers; ++L) {
+      const std::string l = std::to_string(L);
+      run(conv(hb, H, T, H, c.W(q + ".in" + l + ".w"), 2 * H, cf.flow_k, 1, (cf.flow_k - 1) / 2,
+               c.W(q + ".in" + l + ".b"), xin, 2 * H, T, B),
+          s);
+      check(gate_tanh_sigmoid(xin, 2 * H, gc + L * 2 * H, cl, acts, B, T, H, s), "gate");
+      const float* wrs = c.W(q + ".rs" + l + ".w");
+      const float* brs = c.W(q + ".rs" + l + ".b");
+      if (L < cf.flow_layers - 1) {
+        ConvArgs a = lin(acts, H, (int)BT, H, wrs, H, brs, hb, H);
+        a.res = hb;
+        a.ldr = H;
+        a.res_mode = RES_ADD_POST;
+        a.mask = mask;
+        run(a, s);
+        ConvArgs b = lin(acts, H, (int)BT, H, wrs + (size_t)H * H, H, brs + H, outb, H);
+        b.acc_mode = (L == 0) ? ACC_STORE : ACC_ADD;
+        run(b, s);
+      } else {
+        ConvArgs a = lin(acts, H, (int)BT, H, wrs, H, brs, outb, H);
+        a.acc_mode = (L == 0) ? ACC_STORE : ACC_ADD;
+        a.mask = mask;
+        run(a, s);
+      }
+    }
+    {  // x1 = (x1 - m) * mask, m = post(h) * mask
+      ConvArgs a = lin(outb, H, (int)BT, H, c.W(q + ".post.w"), I / 2, c.W(q + ".post.b"), xf + I / 2, I);
+      a.res = xf + I / 2;
+      a.ldr = I;
+      a.res_mode = RES_RSUB_POST;
+      a.mask = mask;
+      run(a, s);
+    }
+    std::swap(z, xf);
+  }
+  if (z_out) RVCX_HIP(hipMemcpyAsync(z_out, z, BT * I * sizeof(float), hipMemcpyDeviceToDevice, s));
+  // ---- dec(z * mask, nsff0, g)
+  dec_forward(c, B, T, z, mask, pitchf, g, eps_src, seed, out, s);
+}
+
+}  // namespace rvcx

@@ -1,0 +1,145 @@
+// rvcx kernel launchers (internal; the public C-ABI is include/rvcx.h).
+//
+// Tensor convention on device: frame-major ("time-major") rows, channels
+// contiguous: a [T][C] matrix with row stride ld (floats). 2-D images (RMVPE
+// U-Net) are NHWC: pixel-major rows (h*W + w), channels contiguous.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace rvcx {
+
+enum Act : int {
+  ACT_NONE = 0,
+  ACT_LRELU = 1,    // leaky relu with slope
+  ACT_RELU = 2,
+  ACT_GELU = 3,     // exact erf GELU (HF "gelu", torch F.gelu default)
+  ACT_TANH = 4,
+  ACT_SIGMOID = 5,
+  ACT_LOGCLAMP = 6, // log(max(v, slope))  (RMVPE mel: log(clamp(.,1e-5)))
+};
+
+enum ResMode : int {
+  RES_NONE = 0,
+  RES_ADD_PRE = 1,   // v = (acc + bias) + R, then alpha, act
+  RES_ADD_POST = 2,  // v = act(alpha*(acc + bias)) + R
+  RES_RSUB_POST = 3, // v = R - act(alpha*(acc + bias))
+};
+
+enum AccMode : int {
+  ACC_STORE = 0,   // y = v
+  ACC_ADD = 1,     // y = y + v
+  ACC_ADD_DIV = 2, // y = (y + v) / acc_div
+};
+
+enum OutMap : int {
+  OUT_ROWS = 0,       // y[b][m][n]
+  OUT_UPSAMPLE2D = 1, // 2-D ConvTranspose phase scatter: n = (ph*2+pw)*Cv + co -> pixel (2h+ph, 2w+pw)
+};
+
+// Implicit-GEMM convolution:  y[b][m][n] = epi( sum_tap sum_c pre(X[b][row(m,tap)][c]) * W[tap][n][c] )
+struct ConvArgs {
+  // A operand (activations)
+  const float* x = nullptr;
+  long long x_bs = 0;   // batch stride (floats)
+  int ldx = 0;          // row stride
+  int T_in = 0;         // valid input rows (1-D) ; for 2-D: H_in
+  int W_in = 0;         // 2-D: input width
+  int C_in = 0;         // contraction channels per tap
+  int pre_act = ACT_NONE;
+  float pre_slope = 0.f;
+  const float* pre_mask = nullptr;  // [b][row] multiplier applied to input rows (1-D only)
+  long long pre_mask_bs = 0;
+  // B operand (weights): NK: w + tap*w_ts + n*ldw + c ; KN: w + tap*w_ts + c*ldw + n
+  const float* w = nullptr;
+  long long w_bs = 0;
+  long long w_ts = 0;
+  int ldw = 0;
+  int b_kn = 0;
+  // geometry
+  int taps = 1;
+  int stride = 1, dil = 1, pad = 0;     // 1-D
+  int KH = 1, KW = 1, padh = 0, padw = 0; // 2-D (taps = KH*KW; tap = kh*KW + kw)
+  // output
+  float* y = nullptr;
+  long long y_bs = 0;
+  int ldy = 0;
+  int T_out = 0;   // output rows (1-D) ; 2-D: H_out (tile grid), W_out
+  int W_out = 0;
+  int N = 0;
+  int out_map = OUT_ROWS;
+  int out_cv = 0;  // OUT_UPSAMPLE2D: real output channels
+  // epilogue
+  const float* bias = nullptr;
+  long long bias_bs = 0;
+  float alpha = 1.f;
+  int act = ACT_NONE;
+  float slope = 0.f;
+  const float* res = nullptr;
+  long long res_bs = 0;
+  int ldr = 0;
+  int res_mode = RES_NONE;
+  const float* mask = nullptr;  // [b][m] output-row multiplier (applied last, after acc_mode)
+  long long mask_bs = 0;
+  int acc_mode = ACC_STORE;
+  float acc_div = 1.f;
+  // grid z = batch * batch_inner; pointer offset = zo * *_bs + zi * *_bs2 (mask: zo only)
+  int batch = 1;
+  int batch_inner = 1;
+  long long x_bs2 = 0, w_bs2 = 0, y_bs2 = 0, res_bs2 = 0, bias_bs2 = 0;
+};
+
+hipError_t conv1d(const ConvArgs& a, hipStream_t s);
+hipError_t conv2d(const ConvArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------- misc kernels
+hipError_t fill(float* p, float v, long long n, hipStream_t s);
+hipError_t transpose_bct_btc(const float* x, float* y, int B, int C, int T, hipStream_t s); // [B][C][T] -> [B][T][C]
+hipError_t transpose_btc_bct(const float* x, float* y, int B, int T, int C, int ldx, hipStream_t s);
+hipError_t channel_flip(const float* x, float* y, int rows, int C, hipStream_t s);
+hipError_t gather_rows(const float* table, int ld_table, const int32_t* idx, float* y, int rows, int C,
+                       hipStream_t s);
+hipError_t seq_mask(const int32_t* lengths, float* mask, int B, int T, hipStream_t s);
+hipError_t layernorm_rows(const float* x, const float* r, float* y, const float* gamma, const float* beta,
+                          int rows, int D, float eps, const float* mask, hipStream_t s);
+hipError_t gate_tanh_sigmoid(const float* xin, int ldx, const float* g, long long g_bs, float* acts, int B,
+                             int T, int H, hipStream_t s);
+hipError_t softmax_rel(float* scores, int T, int n_heads, int B, const float* rel, int window,
+                       const float* mask, float* pband, int rows_scaled_by_band, hipStream_t s);
+hipError_t softmax_rows(float* scores, int rows, int cols, hipStream_t s);
+hipError_t upsample2_protect(const float* feats, int L, int D, float* out, int T, const float* pitchf, float protect,
+                             hipStream_t s);
+hipError_t sine_source(const float* f0, int B, int L, int upp, float sr, const float* eps, uint64_t seed,
+                       float lin_w, float lin_b, double* cum_ws, float* har, hipStream_t s);
+hipError_t noise_conv_add(const float* har, int Nh, float* y, int B, int T, int C, long long y_bs,
+                          const float* w, const float* b, int K, int stride, int pad, hipStream_t s);
+hipError_t conv_post_tanh(const float* x, int B, int T, int C, const float* w, int K, float slope, float* y,
+                          hipStream_t s);
+hipError_t randn(float* y, long long n, uint64_t seed, uint64_t offset, hipStream_t s);
+hipError_t zp_sample(const float* stats, int B, int T, int I, const float* eps, uint64_t seed, const float* mask,
+                     float* zp, hipStream_t s);
+hipError_t groupnorm_time_gelu(float* x, int T, int C, const float* gamma, const float* beta, float eps,
+                               double* ws, hipStream_t s);
+hipError_t act_inplace(float* x, long long n, int act, float slope, hipStream_t s);
+hipError_t reflect_pad_1d(const float* x, int n, int pad_l, int pad_r, float* y, hipStream_t s);
+hipError_t reflect_pad_rows(const float* x, int rows, int C, int pad_r, float* y, hipStream_t s);
+hipError_t stft_magnitude(const float* spec, int F, int nbins, float* mag, int ldm, hipStream_t s);
+hipError_t affine_inplace(float* x, long long n, float a, float b, hipStream_t s);
+hipError_t avgpool2(const float* x, int H, int W, int C, int ldx, float* y, hipStream_t s);
+hipError_t nhwc_to_hcw(const float* x, int H, int W, int C, float* y, hipStream_t s);
+hipError_t gru_bidir(const float* gi, const float* whh_f, const float* bhh_f, const float* whh_b,
+                     const float* bhh_b, int T, float* out, unsigned long long* xchg, unsigned* status,
+                     hipStream_t s);
+hipError_t rmvpe_decode(const float* sal, int F, int ncls, float thred, double* f0, hipStream_t s);
+hipError_t f0_post(const double* f0, int F, double shift, int32_t* coarse, float* pitchf, double* f0_out,
+                   hipStream_t s);
+
+// pipeline DSP
+constexpr int IIR_MAXO = 8;
+hipError_t filtfilt_pad(const double* x, long long n, const double* b, const double* a, const double* zi,
+                        const double* FL, int order, long long t_pad, double* ws, double* pad64, float* pad32,
+                        hipStream_t s);
+size_t filtfilt_ws_doubles(long long n, int order);
+hipError_t peak_normalize(float* x, long long n, unsigned* ws, hipStream_t s);
+
+}  // namespace rvcx

@@ -1,0 +1,100 @@
+"""ctypes binding of librvcx.so (the C-ABI declared in include/rvcx.h).
+
+There is no CPU fallback: if the HIP library is missing or cannot be loaded, importing
+the compute path raises ``RvcxLibraryError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("RVCX_LIB", os.path.join(_HERE, "librvcx.so"))
+
+RVCX_MODEL_SYNTH, RVCX_MODEL_HUBERT, RVCX_MODEL_RMVPE = 0, 1, 2
+
+STATUS = {
+    0: "RVCX_OK", -1: "RVCX_E_INVALID", -2: "RVCX_E_SHAPE", -3: "RVCX_E_HIP", -4: "RVCX_E_OOM",
+    -5: "RVCX_E_STATE", -6: "RVCX_E_CAPACITY",
+}
+
+EXPORTS = [
+    "rvcx_create", "rvcx_destroy", "rvcx_last_error", "rvcx_set_synth_config", "rvcx_upload", "rvcx_finalize",
+    "rvcx_hubert", "rvcx_rmvpe", "rvcx_f0_post", "rvcx_synth_infer", "rvcx_dec_only", "rvcx_voice_conversion",
+    "rvcx_synth_upp", "rvcx_set_highpass", "rvcx_pipeline",
+]
+
+
+class RvcxLibraryError(ImportError):
+    pass
+
+
+class RvcxError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{STATUS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class SynthDesc(ctypes.Structure):
+    _fields_ = [
+        ("inter_channels", ctypes.c_int), ("hidden_channels", ctypes.c_int), ("filter_channels", ctypes.c_int),
+        ("n_heads", ctypes.c_int), ("n_layers", ctypes.c_int), ("kernel_size", ctypes.c_int),
+        ("n_resblocks", ctypes.c_int), ("resblock_kernel_sizes", ctypes.c_int * 4),
+        ("resblock_dilation_sizes", (ctypes.c_int * 4) * 4), ("n_dilations", ctypes.c_int),
+        ("n_upsample", ctypes.c_int), ("upsample_rates", ctypes.c_int * 8),
+        ("upsample_initial_channel", ctypes.c_int), ("upsample_kernel_sizes", ctypes.c_int * 8),
+        ("spk_embed_dim", ctypes.c_int), ("gin_channels", ctypes.c_int), ("sr", ctypes.c_int),
+        ("text_enc_hidden_dim", ctypes.c_int),
+    ]
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def load(path: Optional[str] = None) -> ctypes.CDLL:
+    """Load librvcx.so and declare every prototype. Raises RvcxLibraryError when absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RvcxLibraryError(f"librvcx.so not found at {p}; build it with __graft_entry__.build() "
+                               "(make -C retrieval-based-voice-conversion-mlx_amd/csrc)")
+    try:
+        lib = ctypes.CDLL(p)
+    except OSError as e:
+        raise RvcxLibraryError(f"cannot load {p}: {e}") from e
+    vp, i64, i32, f32, f64, u64 = (ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_float, ctypes.c_double,
+                                   ctypes.c_uint64)
+    P = ctypes.POINTER
+    sig = {
+        "rvcx_create": (i32, [P(vp), i32]),
+        "rvcx_destroy": (i32, [vp]),
+        "rvcx_last_error": (ctypes.c_char_p, [vp]),
+        "rvcx_set_synth_config": (i32, [vp, P(SynthDesc)]),
+        "rvcx_upload": (i32, [vp, i32, ctypes.c_char_p, vp, P(i64), i32]),
+        "rvcx_finalize": (i32, [vp, i32]),
+        "rvcx_hubert": (i32, [vp, vp, i64, i32, vp, i64, P(i64), vp]),
+        "rvcx_rmvpe": (i32, [vp, vp, i64, f32, vp, i64, P(i64), vp, vp]),
+        "rvcx_f0_post": (i32, [vp, vp, i64, f64, vp, vp, vp, vp]),
+        "rvcx_synth_infer": (i32, [vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, u64, vp, vp, vp, vp]),
+        "rvcx_dec_only": (i32, [vp, i32, i32, vp, vp, vp, vp, u64, vp, vp]),
+        "rvcx_voice_conversion": (i32, [vp, vp, i64, vp, vp, i32, f32, vp, vp, u64, vp, i64, P(i64), vp]),
+        "rvcx_synth_upp": (i32, [vp]),
+        "rvcx_set_highpass": (i32, [vp, vp, vp, vp, i32]),
+        "rvcx_pipeline": (i32, [vp, vp, i64, i32, f64, f32, i64, i64, vp, vp, u64, vp, i64, P(i64), vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def exported_symbols(path: Optional[str] = None):
+    """Names of the C-ABI entry points that resolve in the library (no compute call)."""
+    lib = load(path)
+    return [n for n in EXPORTS if hasattr(lib, n)]

@@ -1,0 +1,239 @@
+"""Device engine: one rvcx context (weights + workspace in HBM) driven through the C-ABI.
+
+torch is used only for device memory and the current HIP stream; every computation runs in
+librvcx.so (HIP kernels for gfx950).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Mapping, Optional
+
+import numpy as np
+
+from . import _lib
+from .config import SYNTH_48K_V2, SynthConfig
+from .weights import normalize_state
+
+
+def _ptr(t) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+class Engine:
+    """Owns an ``rvcx_ctx`` on one GPU. Not thread-safe (one host thread at a time)."""
+
+    def __init__(self, device: int = 0):
+        import torch
+
+        self.lib = _lib.load()
+        if not torch.cuda.is_available():
+            raise RuntimeError("rvcx needs a ROCm GPU: torch.cuda.is_available() is False")
+        self.torch = torch
+        self.device_index = int(device)
+        self.device = torch.device(f"cuda:{self.device_index}")
+        ctx = ctypes.c_void_p()
+        rc = self.lib.rvcx_create(ctypes.byref(ctx), self.device_index)
+        if rc != 0:
+            raise _lib.RvcxError(rc, f"rvcx_create(device={device}) failed")
+        self.ctx = ctx
+        self.synth_cfg: Optional[SynthConfig] = None
+        self.loaded = {"synth": False, "hubert": False, "rmvpe": False}
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.rvcx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ plumbing
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            msg = self.lib.rvcx_last_error(self.ctx)
+            raise _lib.RvcxError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+    def stream(self) -> int:
+        return self.torch.cuda.current_stream(self.device).cuda_stream
+
+    def _dev(self, x, dtype):
+        t = self.torch
+        if isinstance(x, t.Tensor):
+            return x.to(device=self.device, dtype=dtype).contiguous()
+        return t.as_tensor(np.ascontiguousarray(x), dtype=dtype, device=self.device).contiguous()
+
+    # ------------------------------------------------------------------ weights
+    def set_synth_config(self, cfg: SynthConfig = SYNTH_48K_V2):
+        d = _lib.SynthDesc()
+        d.inter_channels, d.hidden_channels, d.filter_channels = cfg.inter_channels, cfg.hidden_channels, \
+            cfg.filter_channels
+        d.n_heads, d.n_layers, d.kernel_size = cfg.n_heads, cfg.n_layers, cfg.kernel_size
+        d.n_resblocks = len(cfg.resblock_kernel_sizes)
+        d.n_dilations = len(cfg.resblock_dilation_sizes[0])
+        for j, k in enumerate(cfg.resblock_kernel_sizes):
+            d.resblock_kernel_sizes[j] = k
+            for m, dd in enumerate(cfg.resblock_dilation_sizes[j]):
+                d.resblock_dilation_sizes[j][m] = dd
+        d.n_upsample = len(cfg.upsample_rates)
+        for i, (u, k) in enumerate(zip(cfg.upsample_rates, cfg.upsample_kernel_sizes)):
+            d.upsample_rates[i] = u
+            d.upsample_kernel_sizes[i] = k
+        d.upsample_initial_channel = cfg.upsample_initial_channel
+        d.spk_embed_dim, d.gin_channels, d.sr = cfg.spk_embed_dim, cfg.gin_channels, cfg.sr
+        d.text_enc_hidden_dim = cfg.text_enc_hidden_dim
+        self._check(self.lib.rvcx_set_synth_config(self.ctx, ctypes.byref(d)), "set_synth_config")
+        self.synth_cfg = cfg
+
+    def upload_state(self, model: int, state: Mapping[str, np.ndarray]):
+        """Upload a fused fp32 state dict (reference names and layouts) and finalize it."""
+        for name, arr in state.items():
+            a = np.ascontiguousarray(arr, dtype=np.float32)
+            shape = (ctypes.c_int64 * max(1, a.ndim))(*a.shape)
+            self._check(self.lib.rvcx_upload(self.ctx, model, name.encode(), a.ctypes.data, shape, a.ndim),
+                        f"upload {name}")
+        self._check(self.lib.rvcx_finalize(self.ctx, model), "finalize")
+
+    def load_synth(self, state: Mapping[str, np.ndarray], cfg: SynthConfig = SYNTH_48K_V2):
+        self.set_synth_config(cfg)
+        st = {k: v for k, v in normalize_state(state).items() if not k.startswith("enc_q.")}
+        self.upload_state(_lib.RVCX_MODEL_SYNTH, st)
+        self.loaded["synth"] = True
+
+    def load_hubert(self, state: Mapping[str, np.ndarray]):
+        st = {k: v for k, v in normalize_state(state).items() if k != "masked_spec_embed"}
+        self.upload_state(_lib.RVCX_MODEL_HUBERT, st)
+        self.loaded["hubert"] = True
+
+    def load_rmvpe(self, state: Mapping[str, np.ndarray]):
+        self.upload_state(_lib.RVCX_MODEL_RMVPE, normalize_state(state))
+        self.loaded["rmvpe"] = True
+
+    @property
+    def upp(self) -> int:
+        return int(self.lib.rvcx_synth_upp(self.ctx))
+
+    # ------------------------------------------------------------------ compute
+    def hubert(self, audio, version: str = "v2"):
+        """audio [N] (16 kHz) -> feats [L, 768] (v2) / [L, 256] (v1), fp32 on device."""
+        t = self.torch
+        a = self._dev(audio, t.float32).reshape(-1)
+        n = a.numel()
+        cap = n // 320 + 8
+        D = 256 if version == "v1" else 768
+        out = t.empty((cap, D), dtype=t.float32, device=self.device)
+        rows = ctypes.c_int64(0)
+        self._check(self.lib.rvcx_hubert(self.ctx, a.data_ptr(), n, 1 if version == "v1" else 2, out.data_ptr(), cap,
+                                         ctypes.byref(rows), self.stream()), "hubert")
+        return out[: rows.value]
+
+    def rmvpe(self, audio, thred: float = 0.03, want_hidden: bool = False):
+        """audio [N] (16 kHz) -> f0 fp64 [1 + N//160] on device (and salience [F, 360])."""
+        t = self.torch
+        a = self._dev(audio, t.float32).reshape(-1)
+        n = a.numel()
+        F = 1 + n // 160
+        f0 = t.empty((F,), dtype=t.float64, device=self.device)
+        hid = t.empty((F, 360), dtype=t.float32, device=self.device) if want_hidden else None
+        fo = ctypes.c_int64(0)
+        self._check(self.lib.rvcx_rmvpe(self.ctx, a.data_ptr(), n, float(thred), f0.data_ptr(), F, ctypes.byref(fo),
+                                        _ptr(hid), self.stream()), "rmvpe")
+        return (f0, hid) if want_hidden else f0
+
+    def f0_post(self, f0, semitones: float):
+        """Pitch shift + coarse quantisation on device: (coarse int32, pitchf fp32, f0 fp64)."""
+        t = self.torch
+        f = self._dev(f0, t.float64).reshape(-1)
+        F = f.numel()
+        coarse = t.empty((F,), dtype=t.int32, device=self.device)
+        pitchf = t.empty((F,), dtype=t.float32, device=self.device)
+        fs = t.empty((F,), dtype=t.float64, device=self.device)
+        self._check(self.lib.rvcx_f0_post(self.ctx, f.data_ptr(), F, float(semitones), coarse.data_ptr(),
+                                          pitchf.data_ptr(), fs.data_ptr(), self.stream()), "f0_post")
+        return coarse, pitchf, fs
+
+    def synth_infer(self, phone, lengths, pitch, pitchf, sid, eps_z=None, eps_src=None, seed: int = 0,
+                    want_latents: bool = False):
+        t = self.torch
+        ph = self._dev(phone, t.float32)
+        B, T = int(ph.shape[0]), int(ph.shape[1])
+        ln = self._dev(lengths, t.int32).reshape(B)
+        pc = self._dev(pitch, t.int32).reshape(B, T)
+        pf = self._dev(pitchf, t.float32).reshape(B, T)
+        sd = self._dev(sid, t.int32).reshape(B)
+        ez = None if eps_z is None else self._dev(eps_z, t.float32)
+        es = None if eps_src is None else self._dev(eps_src, t.float32)
+        out = t.empty((B, T * self.upp), dtype=t.float32, device=self.device)
+        I = self.synth_cfg.inter_channels
+        zp = t.empty((B, T, I), dtype=t.float32, device=self.device) if want_latents else None
+        z = t.empty((B, T, I), dtype=t.float32, device=self.device) if want_latents else None
+        self._check(self.lib.rvcx_synth_infer(self.ctx, B, T, ph.data_ptr(), ln.data_ptr(), pc.data_ptr(),
+                                              pf.data_ptr(), sd.data_ptr(), _ptr(ez), _ptr(es),
+                                              ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), out.data_ptr(), _ptr(zp),
+                                              _ptr(z), self.stream()), "synth_infer")
+        return (out, zp, z) if want_latents else out
+
+    def dec_only(self, z, f0, sid, eps_src=None, seed: int = 0):
+        t = self.torch
+        zz = self._dev(z, t.float32)
+        B, I, T = zz.shape
+        f = self._dev(f0, t.float32).reshape(B, T)
+        sd = self._dev(sid, t.int32).reshape(B)
+        es = None if eps_src is None else self._dev(eps_src, t.float32)
+        out = t.empty((B, T * self.upp), dtype=t.float32, device=self.device)
+        self._check(self.lib.rvcx_dec_only(self.ctx, B, T, zz.data_ptr(), f.data_ptr(), sd.data_ptr(), _ptr(es),
+                                           ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), out.data_ptr(),
+                                           self.stream()), "dec_only")
+        return out
+
+    def voice_conversion(self, audio_pad, pitch, pitchf, sid: int, protect: float, eps_z=None, eps_src=None,
+                         seed: int = 0):
+        """HuBERT -> x2 upsample -> protect -> Synthesizer.infer on one padded chunk (device in/out)."""
+        t = self.torch
+        a = self._dev(audio_pad, t.float32).reshape(-1)
+        n = a.numel()
+        pc = self._dev(pitch, t.int32).reshape(-1)
+        pf = self._dev(pitchf, t.float32).reshape(-1)
+        cap = (n // 160) * self.upp
+        out = t.empty((cap,), dtype=t.float32, device=self.device)
+        no = ctypes.c_int64(0)
+        ez = None if eps_z is None else self._dev(eps_z, t.float32)
+        es = None if eps_src is None else self._dev(eps_src, t.float32)
+        self._check(self.lib.rvcx_voice_conversion(self.ctx, a.data_ptr(), n, pc.data_ptr(), pf.data_ptr(), int(sid),
+                                                   float(protect), _ptr(ez), _ptr(es),
+                                                   ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), out.data_ptr(), cap,
+                                                   ctypes.byref(no), self.stream()), "voice_conversion")
+        return out[: no.value]
+
+    # ------------------------------------------------------------------ whole pipeline
+    def set_highpass(self, b, a, zi):
+        b = np.ascontiguousarray(b, dtype=np.float64)
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        zi = np.ascontiguousarray(zi, dtype=np.float64)
+        self._check(self.lib.rvcx_set_highpass(self.ctx, b.ctypes.data, a.ctypes.data, zi.ctypes.data, len(a) - 1),
+                    "set_highpass")
+        self._hp = (b, a, zi)
+
+    def pipeline(self, audio, sid: int = 0, semitones: float = 0.0, protect: float = 0.33, t_pad: int = 16000,
+                 t_pad_tgt: int = 48000, eps_z=None, eps_src=None, seed: int = 0, out=None, want_f0: bool = False):
+        """One utterance (padded length <= t_max) through the whole device pipeline.
+        audio: fp64 [n] @16 kHz (device tensor or numpy). Returns fp32 [n_out] on device."""
+        t = self.torch
+        a = self._dev(audio, t.float64).reshape(-1)
+        n = a.numel()
+        m = n + 2 * t_pad
+        cap = (m // 160) * self.upp
+        if out is None:
+            out = t.empty((cap,), dtype=t.float32, device=self.device)
+        f0 = t.empty((1 + m // 160,), dtype=t.float64, device=self.device) if want_f0 else None
+        no = ctypes.c_int64(0)
+        ez = None if eps_z is None else self._dev(eps_z, t.float32)
+        es = None if eps_src is None else self._dev(eps_src, t.float32)
+        self._check(self.lib.rvcx_pipeline(self.ctx, a.data_ptr(), n, int(sid), float(semitones), float(protect),
+                                           int(t_pad), int(t_pad_tgt), _ptr(ez), _ptr(es),
+                                           ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), out.data_ptr(), out.numel(),
+                                           ctypes.byref(no), _ptr(f0), self.stream()), "pipeline")
+        res = out[: no.value]
+        return (res, f0) if want_f0 else res
