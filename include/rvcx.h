@@ -121,6 +121,13 @@ int rvcx_pipeline(rvcx_ctx* ctx, const double* d_audio, int64_t n, int sid, doub
                   int64_t t_pad, int64_t t_pad_tgt, const float* d_eps_z, const float* d_eps_src, uint64_t seed,
                   float* d_out, int64_t cap, int64_t* n_out, double* d_f0, void* stream);
 
+/* Kernel timing for roofline reporting: when enabled, every implicit-GEMM conv launch (the MFMA
+ * kernel family that carries ~all FLOPs) is bracketed by hipEvents recorded on its own stream.
+ * rvcx_profile_read synchronises those events and returns the summed kernel time (ms), the
+ * summed ALGORITHMIC FLOPs of those launches and the launch count, then clears the record. */
+int rvcx_profile(rvcx_ctx* ctx, int enable);
+int rvcx_profile_read(rvcx_ctx* ctx, double* total_ms, double* total_flops, int64_t* launches);
+
 /* Upsampling factor of the loaded synthesizer (prod(upsample_rates); net_g.dec.upp). */
 int rvcx_synth_upp(const rvcx_ctx* ctx);
 

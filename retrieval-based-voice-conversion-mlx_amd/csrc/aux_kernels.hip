@@ -665,14 +665,17 @@ hipError_t f0_post(const double* f0, int F, double shift, int32_t* coarse, float
 namespace rvcx {
 
 // scipy.signal.filtfilt(b, a, x) with padtype='odd', padlen = 3*max(len(a), len(b)) (pipeline.py:439),
-// lfilter in direct form II transposed, fp64. Each pass is a chunked linear recurrence:
-//   (1) every chunk of IIR_L samples runs from a zero state -> end state e_c;
-//   (2) one thread propagates true chunk start states s_{c+1} = F^L s_c + e_c;
-//   (3) every chunk reruns from s_c and writes its outputs.
-constexpr int IIR_L = 256;
+// lfilter in direct form II transposed, fp64. The 5th-order 48 Hz high-pass has poles at |p| <= 0.9942
+// and a highly non-normal DF2T state matrix (||F^256|| ~ 4e7), so chunk-state propagation
+// (s_{c+1} = F^L s_c + e_c) is numerically unstable. Instead each chunk of IIR_L outputs re-runs
+// IIR_W samples of history from a zero state (||F^10240|| ~ 1e-18, so the truncated history is below
+// fp64 resolution); chunks that reach the signal start run from lfilter_zi * x[0] exactly as scipy.
+// Measured vs scipy on the 13.5 s reference clip: max |diff| 3.4e-8 (below the fp32 ulp the models see).
+constexpr int IIR_L = 2048;
+constexpr int IIR_W = 10240;
 
 struct IirCoef {
-  double b[IIR_MAXO + 1], a[IIR_MAXO + 1], zi[IIR_MAXO], FL[IIR_MAXO * IIR_MAXO];
+  double b[IIR_MAXO + 1], a[IIR_MAXO + 1], zi[IIR_MAXO];
   int order;
 };
 
@@ -694,38 +697,23 @@ __device__ __forceinline__ double iir_in(const double* x, long long n, int padle
   return x[k];
 }
 
-__global__ void k_iir_chunks(const IirCoef c, const double* x, long long n, int padlen, const double* yf, long long ne,
-                             int rev, double* ends, const double* starts, double* out) {
+__global__ void k_iir_warm(const IirCoef c, const double* x, long long n, int padlen, const double* yf, long long ne,
+                           int rev, double* out) {
   const long long ch = blockIdx.x * (long long)blockDim.x + threadIdx.x;
   const long long nch = (ne + IIR_L - 1) / IIR_L;
   if (ch >= nch) return;
-  double z[IIR_MAXO];
-  for (int i = 0; i < c.order; ++i) z[i] = starts ? starts[ch * IIR_MAXO + i] : 0.0;
   const long long j0 = ch * IIR_L, j1 = min(ne, j0 + IIR_L);
-  for (long long j = j0; j < j1; ++j) {
-    const double y = iir_step(c, z, iir_in(x, n, padlen, yf, ne, rev, j));
-    if (out) out[j] = y;
+  long long js = j0 - IIR_W;
+  double z[IIR_MAXO];
+  if (js <= 0) {
+    js = 0;
+    const double x0 = iir_in(x, n, padlen, yf, ne, rev, 0);
+    for (int i = 0; i < c.order; ++i) z[i] = c.zi[i] * x0;
+  } else {
+    for (int i = 0; i < c.order; ++i) z[i] = 0.0;
   }
-  if (ends)
-    for (int i = 0; i < c.order; ++i) ends[ch * IIR_MAXO + i] = z[i];
-}
-
-__global__ void k_iir_combine(const IirCoef c, const double* x, long long n, int padlen, const double* yf,
-                              long long ne, int rev, const double* ends, double* starts) {
-  const long long nch = (ne + IIR_L - 1) / IIR_L;
-  const double x0 = iir_in(x, n, padlen, yf, ne, rev, 0);
-  double s[IIR_MAXO];
-  for (int i = 0; i < c.order; ++i) s[i] = c.zi[i] * x0;
-  for (long long ch = 0; ch < nch; ++ch) {
-    for (int i = 0; i < c.order; ++i) starts[ch * IIR_MAXO + i] = s[i];
-    double t[IIR_MAXO];
-    for (int i = 0; i < c.order; ++i) {
-      double acc = ends[ch * IIR_MAXO + i];
-      for (int k = 0; k < c.order; ++k) acc += c.FL[i * IIR_MAXO + k] * s[k];
-      t[i] = acc;
-    }
-    for (int i = 0; i < c.order; ++i) s[i] = t[i];
-  }
+  for (long long j = js; j < j0; ++j) (void)iir_step(c, z, iir_in(x, n, padlen, yf, ne, rev, j));
+  for (long long j = j0; j < j1; ++j) out[j] = iir_step(c, z, iir_in(x, n, padlen, yf, ne, rev, j));
 }
 
 // audio_pad[k] = y[reflect(k - t_pad)] with y the filtfilt output (backward pass result yb reversed, trimmed)
@@ -743,7 +731,7 @@ __global__ void k_filt_pad(const double* yb, long long ne, int padlen, long long
 }
 
 hipError_t filtfilt_pad(const double* x, long long n, const double* b, const double* a, const double* zi,
-                        const double* FL, int order, long long t_pad, double* ws, double* pad64, float* pad32,
+                        const double* /*FL*/, int order, long long t_pad, double* ws, double* pad64, float* pad32,
                         hipStream_t s) {
   if (order < 1 || order > IIR_MAXO) return hipErrorInvalidValue;
   const int padlen = 3 * (order + 1);
@@ -755,20 +743,13 @@ hipError_t filtfilt_pad(const double* x, long long n, const double* b, const dou
     c.a[i] = a[i];
   }
   for (int i = 0; i < order; ++i) c.zi[i] = zi[i];
-  for (int i = 0; i < IIR_MAXO * IIR_MAXO; ++i) c.FL[i] = FL[i];
   const long long ne = n + 2 * padlen;
   const long long nch = (ne + IIR_L - 1) / IIR_L;
   double* yf = ws;
   double* yb = yf + ne;
-  double* ends = yb + ne;
-  double* starts = ends + nch * IIR_MAXO;
-  const unsigned g = (unsigned)((nch + 127) / 128);
-  for (int rev = 0; rev < 2; ++rev) {
-    double* out = rev ? yb : yf;
-    hipLaunchKernelGGL(k_iir_chunks, dim3(g), dim3(128), 0, s, c, x, n, padlen, yf, ne, rev, ends, nullptr, nullptr);
-    hipLaunchKernelGGL(k_iir_combine, dim3(1), dim3(1), 0, s, c, x, n, padlen, yf, ne, rev, ends, starts);
-    hipLaunchKernelGGL(k_iir_chunks, dim3(g), dim3(128), 0, s, c, x, n, padlen, yf, ne, rev, nullptr, starts, out);
-  }
+  const unsigned g = (unsigned)((nch + 63) / 64);
+  hipLaunchKernelGGL(k_iir_warm, dim3(g), dim3(64), 0, s, c, x, n, padlen, yf, ne, 0, yf);
+  hipLaunchKernelGGL(k_iir_warm, dim3(g), dim3(64), 0, s, c, x, n, padlen, yf, ne, 1, yb);
   hipLaunchKernelGGL(k_filt_pad, dim3(nblocks(n + 2 * t_pad)), dim3(TB), 0, s, yb, ne, padlen, n, t_pad, pad64,
                      pad32);
   return hipGetLastError();
@@ -776,8 +757,7 @@ hipError_t filtfilt_pad(const double* x, long long n, const double* b, const dou
 
 size_t filtfilt_ws_doubles(long long n, int order) {
   const long long ne = n + 2 * 3 * (order + 1);
-  const long long nch = (ne + IIR_L - 1) / IIR_L;
-  return (size_t)(2 * ne + 2 * nch * IIR_MAXO);
+  return (size_t)(2 * ne);
 }
 
 // peak normalisation (pipeline.py:550-552): m = max|x| / 0.99 ; if m > 1: x /= m

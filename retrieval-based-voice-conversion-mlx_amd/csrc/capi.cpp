@@ -31,6 +31,32 @@ void set_device(rvcx_ctx* c) { RVCX_HIP(hipSetDevice(c->device)); }
 }  // namespace
 
 namespace rvcx {
+void launch_conv(Ctx& c, const ConvArgs& a, bool two_d, hipStream_t s, double flops) {
+  if (flops < 0) {
+    const double M = two_d ? (double)a.T_out * a.W_out : (double)a.T_out;
+    flops = 2.0 * M * a.N * (double)a.C_in * a.taps * a.batch * a.batch_inner;
+  }
+  if (!c.prof) {
+    check(two_d ? conv2d(a, s) : conv1d(a, s), two_d ? "conv2d" : "conv1d");
+    return;
+  }
+  auto get_ev = [&]() {
+    hipEvent_t e;
+    if (!c.prof_pool.empty()) {
+      e = c.prof_pool.back();
+      c.prof_pool.pop_back();
+    } else {
+      RVCX_HIP(hipEventCreate(&e));
+    }
+    return e;
+  };
+  Ctx::ProfRec r{get_ev(), get_ev(), flops};
+  RVCX_HIP(hipEventRecord(r.a, s));
+  check(two_d ? conv2d(a, s) : conv1d(a, s), two_d ? "conv2d" : "conv1d");
+  RVCX_HIP(hipEventRecord(r.b, s));
+  c.prof_recs.push_back(r);
+}
+
 __global__ void k_set_i32(int32_t* p, int32_t v) { p[0] = v; }
 void set_i32(int32_t* p, int32_t v, hipStream_t s) {
   hipLaunchKernelGGL(k_set_i32, dim3(1), dim3(1), 0, s, p, v);
@@ -241,6 +267,30 @@ int rvcx_pipeline(rvcx_ctx* ctx, const double* d_audio, int64_t n, int sid, doub
     const int64_t no = pipeline_forward(*ctx, d_audio, n, sid, semitones, protect, t_pad, t_pad_tgt, d_eps_z,
                                         d_eps_src, seed, d_out, cap, d_f0, static_cast<hipStream_t>(stream));
     if (n_out) *n_out = no;
+  });
+}
+
+int rvcx_profile(rvcx_ctx* ctx, int enable) {
+  return guard(ctx, [&] { ctx->prof = enable != 0; });
+}
+
+int rvcx_profile_read(rvcx_ctx* ctx, double* total_ms, double* total_flops, int64_t* launches) {
+  return guard(ctx, [&] {
+    set_device(ctx);
+    double ms = 0.0, fl = 0.0;
+    for (auto& r : ctx->prof_recs) {
+      RVCX_HIP(hipEventSynchronize(r.b));
+      float t = 0.f;
+      RVCX_HIP(hipEventElapsedTime(&t, r.a, r.b));
+      ms += t;
+      fl += r.flops;
+      ctx->prof_pool.push_back(r.a);
+      ctx->prof_pool.push_back(r.b);
+    }
+    if (total_ms) *total_ms = ms;
+    if (total_flops) *total_flops = fl;
+    if (launches) *launches = (int64_t)ctx->prof_recs.size();
+    ctx->prof_recs.clear();
   });
 }
 

@@ -83,6 +83,14 @@ struct Ctx {
   // workspace pool
   std::map<std::string, std::unique_ptr<DevBuf>> ws;
   uint64_t call_counter = 0;
+  // kernel timing (rvcx_profile): event pairs around every conv-GEMM launch, on its stream
+  bool prof = false;
+  struct ProfRec {
+    hipEvent_t a, b;
+    double flops;
+  };
+  std::vector<ProfRec> prof_recs;
+  std::vector<hipEvent_t> prof_pool;
 
   float* W(const std::string& name) const;
   float* alloc_weight(const std::string& name, const std::vector<float>& data);
@@ -127,6 +135,8 @@ int64_t pipeline_forward(Ctx& c, const double* audio, int64_t n, int sid, double
                          int64_t t_pad, int64_t t_pad_tgt, const float* eps_z, const float* eps_src, uint64_t seed,
                          float* out, int64_t cap, double* f0_out, hipStream_t s);
 void set_i32(int32_t* p, int32_t v, hipStream_t s);
+// launch one implicit-GEMM conv (1-D or 2-D) with optional event timing; flops = algorithmic FLOPs
+void launch_conv(Ctx& c, const ConvArgs& a, bool two_d, hipStream_t s, double flops = -1.0);
 
 inline void check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw Error(RVCX_E_HIP, std::string(what) + ": " + hipGetErrorString(e));

@@ -49,8 +49,9 @@ ConvArgs lin(const float* x, int ldx, int rows, int K, const float* w, int N, co
   return a;
 }
 
-void run1(const ConvArgs& a, hipStream_t s) { check(conv1d(a, s), "conv1d"); }
-void run2(const ConvArgs& a, hipStream_t s) { check(conv2d(a, s), "conv2d"); }
+
+void run1(Ctx& c, const ConvArgs& a, hipStream_t s, double flops = -1.0) { launch_conv(c, a, false, s, flops); }
+void run2(Ctx& c, const ConvArgs& a, hipStream_t s, double flops = -1.0) { launch_conv(c, a, true, s, flops); }
 
 constexpr int HD = 768, HHEADS = 12, HFF = 3072, HCONV = 512;
 const int HK[7] = {10, 3, 3, 3, 3, 2, 2};
@@ -144,7 +145,7 @@ int64_t hubert_forward(Ctx& c, const float* audio, int64_t n, int version, float
     a0.w_ts = (long long)HCONV * 5;
     a0.ldw = 5;
     a0.T_out = (int)T[1];
-    run1(a0, s);
+    run1(c, a0, s);
   }
   check(groupnorm_time_gelu(a, (int)T[1], HCONV, c.W("hb.gn.g"), c.W("hb.gn.b"), 1e-5f, gnws, s), "groupnorm");
   float* cur = a;
@@ -156,14 +157,14 @@ int64_t hubert_forward(Ctx& c, const float* audio, int64_t n, int version, float
     ci.w_ts = (long long)HCONV * HCONV;
     ci.T_out = (int)T[i + 1];
     ci.act = ACT_GELU;
-    run1(ci, s);
+    run1(c, ci, s);
     std::swap(cur, nxt);
   }
   // feature projection: LayerNorm(512) -> Linear(512, 768)
   float* hs = c.buf<float>("hb.hs", (size_t)L * HD, s);
   float* hs2 = c.buf<float>("hb.hs2", (size_t)L * HD, s);
   check(layernorm_rows(cur, nullptr, nxt, c.W("hb.fp.ln.g"), c.W("hb.fp.ln.b"), L, HCONV, 1e-5f, nullptr, s), "fp_ln");
-  run1(lin(nxt, HCONV, L, HCONV, c.W("hb.fp.w"), HD, c.W("hb.fp.b"), hs, HD), s);
+  run1(c, lin(nxt, HCONV, L, HCONV, c.W("hb.fp.w"), HD, c.W("hb.fp.b"), hs, HD), s);
   {  // hs + gelu(pos_conv(hs)) (groups as inner batch), then encoder LayerNorm
     const int cg = HD / POS_G;
     ConvArgs p = lin(hs, HD, L, cg, c.W("hb.pos.w"), cg, c.W("hb.pos.b"), hs2, HD);
@@ -181,7 +182,7 @@ int64_t hubert_forward(Ctx& c, const float* audio, int64_t n, int version, float
     p.ldr = HD;
     p.res_bs2 = cg;
     p.res_mode = RES_ADD_POST;
-    run1(p, s);
+    run1(c, p, s);
     check(layernorm_rows(hs2, nullptr, hs, c.W("hb.enc.ln.g"), c.W("hb.enc.ln.b"), L, HD, 1e-5f, nullptr, s),
           "enc_ln");
   }
@@ -192,7 +193,7 @@ int64_t hubert_forward(Ctx& c, const float* audio, int64_t n, int version, float
   const int hd = HD / HHEADS;
   for (int i = 0; i < 12; ++i) {
     const std::string q = "hb." + std::to_string(i);
-    run1(lin(hs, HD, L, HD, c.W(q + ".qkv.w"), 3 * HD, c.W(q + ".qkv.b"), qkv, 3 * HD), s);
+    run1(c, lin(hs, HD, L, HD, c.W(q + ".qkv.w"), 3 * HD, c.W(q + ".qkv.b"), qkv, 3 * HD), s);
     {
       ConvArgs a1 = lin(qkv, 3 * HD, L, hd, qkv + HD, L, nullptr, sc, L);
       a1.ldw = 3 * HD;
@@ -201,7 +202,7 @@ int64_t hubert_forward(Ctx& c, const float* audio, int64_t n, int version, float
       a1.x_bs2 = hd;
       a1.w_bs2 = hd;
       a1.y_bs2 = (long long)L * L;
-      run1(a1, s);
+      run1(c, a1, s);
     }
     check(softmax_rows(sc, HHEADS * L, L, s), "softmax");
     {
@@ -212,31 +213,31 @@ int64_t hubert_forward(Ctx& c, const float* audio, int64_t n, int version, float
       a2.x_bs2 = (long long)L * L;
       a2.w_bs2 = hd;
       a2.y_bs2 = hd;
-      run1(a2, s);
+      run1(c, a2, s);
     }
     {
       ConvArgs a3 = lin(att, HD, L, HD, c.W(q + ".o.w"), HD, c.W(q + ".o.b"), hs2, HD);
       a3.res = hs;
       a3.ldr = HD;
       a3.res_mode = RES_ADD_POST;
-      run1(a3, s);
+      run1(c, a3, s);
     }
     check(layernorm_rows(hs2, nullptr, hs, c.W(q + ".ln1.g"), c.W(q + ".ln1.b"), L, HD, 1e-5f, nullptr, s), "ln1");
     {
       ConvArgs f1 = lin(hs, HD, L, HD, c.W(q + ".ff1.w"), HFF, c.W(q + ".ff1.b"), ff, HFF);
       f1.act = ACT_GELU;
-      run1(f1, s);
+      run1(c, f1, s);
       ConvArgs f2 = lin(ff, HFF, L, HFF, c.W(q + ".ff2.w"), HD, c.W(q + ".ff2.b"), hs2, HD);
       f2.res = hs;
       f2.ldr = HD;
       f2.res_mode = RES_ADD_POST;
-      run1(f2, s);
+      run1(c, f2, s);
     }
     check(layernorm_rows(hs2, nullptr, hs, c.W(q + ".ln2.g"), c.W(q + ".ln2.b"), L, HD, 1e-5f, nullptr, s), "ln2");
   }
   if (version == 1) {
     if (!c.dev.count("hb.final_proj.w")) throw Error(RVCX_E_STATE, "hubert: v1 needs final_proj weights");
-    run1(lin(hs, HD, L, HD, c.W("hb.final_proj.w"), 256, c.W("hb.final_proj.b"), feats, 256), s);
+    run1(c, lin(hs, HD, L, HD, c.W("hb.final_proj.w"), 256, c.W("hb.final_proj.b"), feats, 256), s);
   } else {
     RVCX_HIP(hipMemcpyAsync(feats, hs, (size_t)L * outD * sizeof(float), hipMemcpyDeviceToDevice, s));
   }
@@ -364,12 +365,12 @@ void conv_block(Ctx& c, const std::string& q, const float* x, int ldx, int H, in
   float* t = c.buf<float>("rm.blk.t", P * cout, s);
   ConvArgs a = c2d(x, ldx, H, W, cin, c.W(q + ".c1.w"), cout, c.W(q + ".c1.b"), t, cout);
   a.act = ACT_RELU;
-  run2(a, s);
+  run2(c, a, s);
   const float* res = x;
   int ldr = ldx;
   if (cin != cout) {
     float* sc = c.buf<float>("rm.blk.sc", P * cout, s);
-    run1(lin(x, ldx, (int)P, cin, c.W(q + ".sc.w"), cout, c.W(q + ".sc.b"), sc, cout), s);
+    run1(c, lin(x, ldx, (int)P, cin, c.W(q + ".sc.w"), cout, c.W(q + ".sc.b"), sc, cout), s);
     res = sc;
     ldr = cout;
   }
@@ -378,7 +379,7 @@ void conv_block(Ctx& c, const std::string& q, const float* x, int ldx, int H, in
   b.res = res;
   b.ldr = ldr;
   b.res_mode = RES_ADD_POST;
-  run2(b, s);
+  run2(c, b, s);
 }
 
 }  // namespace
@@ -547,7 +548,7 @@ static void e2e_chunk(Ctx& c, float* img, int Fc, float* sal, hipStream_t s) {
       a.out_cv = co;
       a.bias = c.W(q + ".up.b");
       a.act = ACT_RELU;
-      run2(a, s);
+      run2(c, a, s, 2.0 * H * W * (double)C * co * 9);
     }
     H *= 2;
     W *= 2;
@@ -568,11 +569,11 @@ static void e2e_chunk(Ctx& c, float* img, int Fc, float* sal, hipStream_t s) {
   }
   // cnn (16 -> 3, 3x3, bias) -> [Fc][3*128] (index c*128 + w) -> BiGRU -> Linear + sigmoid
   float* cn = c.buf<float>("rm.cnn", (size_t)Fc * NMEL * 3, s);
-  run2(c2d(x, ldx, H, W, C_BASE, c.W("rm.cnn.w"), 3, c.W("rm.cnn.b"), cn, 3), s);
+  run2(c, c2d(x, ldx, H, W, C_BASE, c.W("rm.cnn.w"), 3, c.W("rm.cnn.b"), cn, 3), s);
   float* feat = c.buf<float>("rm.feat", (size_t)Fc * 3 * NMEL, s);
   check(nhwc_to_hcw(cn, Fc, NMEL, 3, feat, s), "nhwc_to_hcw");
   float* gi = c.buf<float>("rm.gi", (size_t)Fc * 6 * GRU_H, s);
-  run1(lin(feat, 3 * NMEL, Fc, 3 * NMEL, c.W("rm.gru.wih"), 6 * GRU_H, c.W("rm.gru.bih"), gi, 6 * GRU_H), s);
+  run1(c, lin(feat, 3 * NMEL, Fc, 3 * NMEL, c.W("rm.gru.wih"), 6 * GRU_H, c.W("rm.gru.bih"), gi, 6 * GRU_H), s);
   float* go = c.buf<float>("rm.gruout", (size_t)Fc * 2 * GRU_H, s);
   unsigned long long* xchg = c.buf<unsigned long long>("rm.xchg", 4 * 2 * 128, s);
   unsigned* status = c.buf<unsigned>("rm.status", 4, s);
@@ -582,7 +583,7 @@ static void e2e_chunk(Ctx& c, float* img, int Fc, float* sal, hipStream_t s) {
         "gru");
   ConvArgs f = lin(go, 2 * GRU_H, Fc, 2 * GRU_H, c.W("rm.fc.w"), NCLS, c.W("rm.fc.b"), sal, NCLS);
   f.act = ACT_SIGMOID;
-  run1(f, s);
+  run1(c, f, s);
 }
 
 int64_t rmvpe_forward(Ctx& c, const float* audio, int64_t n, float thred, double* f0, int64_t cap, float* hidden,
@@ -603,7 +604,7 @@ int64_t rmvpe_forward(Ctx& c, const float* audio, int64_t n, float thred, double
     a.stride = 5;
     a.w_ts = (long long)2 * NBIN * 32;
     a.T_out = F;
-    run1(a, s);
+    run1(c, a, s, 0.0);
   }
   const int ldm = 516;
   float* mag = c.buf<float>("rm.mag", (size_t)F * ldm, s);
@@ -613,7 +614,7 @@ int64_t rmvpe_forward(Ctx& c, const float* audio, int64_t n, float thred, double
     ConvArgs a = lin(mag, ldm, F, NBIN, c.W("rm.mel"), NMEL, nullptr, mel, NMEL);
     a.act = ACT_LOGCLAMP;
     a.slope = 1e-5f;
-    run1(a, s);
+    run1(c, a, s);
   }
   // mel2hidden (RMVPE.py:445-482): reflect-pad frames to a multiple of 32, E2E per 32000-frame chunk
   const int Fp = 32 * ((F - 1) / 32 + 1);

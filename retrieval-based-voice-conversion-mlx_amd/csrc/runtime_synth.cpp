@@ -89,9 +89,12 @@ ConvArgs conv(const float* x, int ldx, int Tin, int Cin, const float* w, int N, 
   return a;
 }
 
-void run(const ConvArgs& a, hipStream_t s) { check(conv1d(a, s), "conv1d"); }
 
 }  // namespace
+
+static void run(Ctx& c, const ConvArgs& a, hipStream_t s, double flops = -1.0) {
+  launch_conv(c, a, false, s, flops);
+}
 
 float* Ctx::W(const std::string& name) const {
   auto it = dev.find(name);
@@ -271,7 +274,7 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
         "sine_source");
   // conv_pre + cond(g)
   float* cv = c.buf<float>("dec.cvec", (size_t)B * C0, s);
-  run(lin(g, cf.gin, B, cf.gin, c.W("dec.cond.w"), C0, c.W("dec.cond.b"), cv, C0), s);
+  run(c, lin(g, cf.gin, B, cf.gin, c.W("dec.cond.w"), C0, c.W("dec.cond.b"), cv, C0), s);
   // stage buffers sized for the largest stage
   size_t maxe = (size_t)T * C0;
   {
@@ -293,7 +296,7 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
     a.ldr = 0;
     a.res_bs = C0;
     a.res_mode = RES_ADD_PRE;
-    run(a, s);
+    run(c, a, s);
   }
   float* cur = xin;
   int curT = T, Cin = C0;
@@ -305,7 +308,7 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
     ConvArgs a = conv(cur, Cin, curT, Cin, L.w, u * C, L.taps, 1, L.pad, L.b, y, u * C, curT, B);
     a.pre_act = ACT_LRELU;
     a.pre_slope = 0.1f;
-    run(a, s);
+    run(c, a, s, 2.0 * B * curT * (double)Cin * C * L.k);
     // + noise_convs[i](har)
     int stride = 1;
     for (size_t j = i + 1; j < cf.ups.size(); ++j) stride *= cf.ups[j];
@@ -334,7 +337,7 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
         a1.pre_slope = 0.1f;
         a1.act = ACT_LRELU;
         a1.slope = 0.1f;
-        run(a1, s);
+        run(c, a1, s);
         const bool last = (m + 1 == dil.size());
         float* dst = last ? S : RR;
         ConvArgs a2 = conv(T1, C, Ti, C, c.W(n2 + ".w"), C, k, 1, (k - 1) / 2, c.W(n2 + ".b"), dst, C, Ti, B);
@@ -346,7 +349,7 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
           a2.acc_mode = (j == 0) ? ACC_STORE : ((j + 1 == nk) ? ACC_ADD_DIV : ACC_ADD);
           a2.acc_div = (float)nk;
         }
-        run(a2, s);
+        run(c, a2, s);
         r_in = RR;
       }
     }
@@ -382,7 +385,7 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
     a.act = ACT_LRELU;
     a.slope = 0.1f;
     a.mask = mask;
-    run(a, s);
+    run(c, a, s);
   }
   float* qkv = c.buf<float>("te.qkv", BT * 3 * H, s);
   float* sc = c.buf<float>("te.scores", (size_t)B * nh * T * T, s);
@@ -394,7 +397,7 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
   const float qscale = (float)(1.0 / std::sqrt((double)dk));
   for (int i = 0; i < cf.n_layers; ++i) {
     const std::string q = "te." + std::to_string(i);
-    run(lin(x, H, (int)BT, H, c.W(q + ".qkv.w"), 3 * H, c.W(q + ".qkv.b"), qkv, 3 * H), s);
+    run(c, lin(x, H, (int)BT, H, c.W(q + ".qkv.w"), 3 * H, c.W(q + ".qkv.b"), qkv, 3 * H), s);
     {  // scores = (q / sqrt(dk)) k^T   (attentions.py:96)
       ConvArgs a = lin(qkv, 3 * H, T, dk, qkv + H, T, nullptr, sc, T);
       a.ldw = 3 * H;
@@ -407,7 +410,7 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
       a.w_bs2 = dk;
       a.y_bs = (long long)nh * T * T;
       a.y_bs2 = (long long)T * T;
-      run(a, s);
+      run(c, a, s);
     }
     {  // relative key logits (attentions.py:127-132)
       ConvArgs a = lin(qkv, 3 * H, T, dk, c.W(q + ".rel_k"), nw, nullptr, rel, nw);
@@ -418,7 +421,7 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
       a.x_bs2 = dk;
       a.y_bs = (long long)nh * T * nw;
       a.y_bs2 = (long long)T * nw;
-      run(a, s);
+      run(c, a, s);
     }
     check(softmax_rel(sc, T, nh, B, rel, cf.window, mask, pband, 0, s), "softmax_rel");
     {  // p v   (attentions.py:120)
@@ -433,7 +436,7 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
       a.w_bs2 = dk;
       a.y_bs = (long long)T * H;
       a.y_bs2 = dk;
-      run(a, s);
+      run(c, a, s);
     }
     {  // + relative values (attentions.py:122-123, 134-141)
       ConvArgs a = lin(pband, nw, T, nw, c.W(q + ".rel_v"), dk, nullptr, att, H);
@@ -446,9 +449,9 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
       a.y_bs = (long long)T * H;
       a.y_bs2 = dk;
       a.acc_mode = ACC_ADD;
-      run(a, s);
+      run(c, a, s);
     }
-    run(lin(att, H, (int)BT, H, c.W(q + ".o.w"), H, c.W(q + ".o.b"), o, H), s);
+    run(c, lin(att, H, (int)BT, H, c.W(q + ".o.w"), H, c.W(q + ".o.b"), o, H), s);
     check(layernorm_rows(x, o, x, c.W(q + ".ln1.g"), c.W(q + ".ln1.b"), (int)BT, H, 1e-5f, nullptr, s), "ln1");
     {  // FFN (attentions.py:221-231): conv_1(pad(x*mask)) -> relu -> conv_2(pad(.*mask)) * mask
       ConvArgs a = conv(x, H, T, H, c.W(q + ".ffn1.w"), F, cf.ksize, 1, (cf.ksize - 1) / 2, c.W(q + ".ffn1.b"), h1,
@@ -456,14 +459,14 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
       a.pre_mask = mask;
       a.pre_mask_bs = T;
       a.act = ACT_RELU;
-      run(a, s);
+      run(c, a, s);
       ConvArgs b = conv(h1, F, T, F, c.W(q + ".ffn2.w"), H, cf.ksize, 1, (cf.ksize - 1) / 2, c.W(q + ".ffn2.b"), o,
                         H, T, B);
       b.pre_mask = mask;
       b.pre_mask_bs = T;
       b.mask = mask;
       b.mask_bs = T;
-      run(b, s);
+      run(c, b, s);
     }
     check(layernorm_rows(x, o, x, c.W(q + ".ln2.g"), c.W(q + ".ln2.b"), (int)BT, H, 1e-5f, nullptr, s), "ln2");
   }
@@ -472,7 +475,7 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
     ConvArgs a = lin(x, H, (int)BT, H, c.W("te.proj.w"), 2 * I, c.W("te.proj.b"), stats, 2 * I);
     a.pre_mask = mask;
     a.mask = mask;
-    run(a, s);
+    run(c, a, s);
   }
   // ---- z_p = (m + exp(logs) * eps * 0.66666) * mask   (synthesizers.py:228)
   float* z = c.buf<float>("flow.z", BT * I, s);
@@ -492,12 +495,12 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
     {
       ConvArgs a = lin(xf, I, (int)BT, I / 2, c.W(q + ".pre.w"), H, c.W(q + ".pre.b"), hb, H);
       a.mask = mask;
-      run(a, s);
+      run(c, a, s);
     }
-    run(lin(g, cf.gin, B, cf.gin, c.W(q + ".cond.w"), cl, c.W(q + ".cond.b"), gc, cl), s);
+    run(c, lin(g, cf.gin, B, cf.gin, c.W(q + ".cond.w"), cl, c.W(q + ".cond.b"), gc, cl), s);
     for (int L = 0; L < cf.flow_layers; ++L) {
       const std::string l = std::to_string(L);
-      run(conv(hb, H, T, H, c.W(q + ".in" + l + ".w"), 2 * H, cf.flow_k, 1, (cf.flow_k - 1) / 2,
+      run(c, conv(hb, H, T, H, c.W(q + ".in" + l + ".w"), 2 * H, cf.flow_k, 1, (cf.flow_k - 1) / 2,
                c.W(q + ".in" + l + ".b"), xin, 2 * H, T, B),
           s);
       check(gate_tanh_sigmoid(xin, 2 * H, gc + L * 2 * H, cl, acts, B, T, H, s), "gate");
@@ -509,15 +512,15 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
         a.ldr = H;
         a.res_mode = RES_ADD_POST;
         a.mask = mask;
-        run(a, s);
+        run(c, a, s);
         ConvArgs b = lin(acts, H, (int)BT, H, wrs + (size_t)H * H, H, brs + H, outb, H);
         b.acc_mode = (L == 0) ? ACC_STORE : ACC_ADD;
-        run(b, s);
+        run(c, b, s);
       } else {
         ConvArgs a = lin(acts, H, (int)BT, H, wrs, H, brs, outb, H);
         a.acc_mode = (L == 0) ? ACC_STORE : ACC_ADD;
         a.mask = mask;
-        run(a, s);
+        run(c, a, s);
       }
     }
     {  // x1 = (x1 - m) * mask, m = post(h) * mask
@@ -526,7 +529,7 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
       a.ldr = I;
       a.res_mode = RES_RSUB_POST;
       a.mask = mask;
-      run(a, s);
+      run(c, a, s);
     }
     std::swap(z, xf);
   }

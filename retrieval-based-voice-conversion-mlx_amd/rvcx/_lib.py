@@ -22,7 +22,7 @@ STATUS = {
 EXPORTS = [
     "rvcx_create", "rvcx_destroy", "rvcx_last_error", "rvcx_set_synth_config", "rvcx_upload", "rvcx_finalize",
     "rvcx_hubert", "rvcx_rmvpe", "rvcx_f0_post", "rvcx_synth_infer", "rvcx_dec_only", "rvcx_voice_conversion",
-    "rvcx_synth_upp", "rvcx_set_highpass", "rvcx_pipeline",
+    "rvcx_synth_upp", "rvcx_set_highpass", "rvcx_pipeline", "rvcx_profile", "rvcx_profile_read",
 ]
 
 
@@ -83,6 +83,8 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "rvcx_voice_conversion": (i32, [vp, vp, i64, vp, vp, i32, f32, vp, vp, u64, vp, i64, P(i64), vp]),
         "rvcx_synth_upp": (i32, [vp]),
         "rvcx_set_highpass": (i32, [vp, vp, vp, vp, i32]),
+        "rvcx_profile": (i32, [vp, i32]),
+        "rvcx_profile_read": (i32, [vp, P(f64), P(f64), P(i64)]),
         "rvcx_pipeline": (i32, [vp, vp, i64, i32, f64, f32, i64, i64, vp, vp, u64, vp, i64, P(i64), vp, vp]),
     }
     for name, (res, args) in sig.items():

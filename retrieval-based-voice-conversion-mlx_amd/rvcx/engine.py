@@ -237,3 +237,14 @@ class Engine:
                                            ctypes.byref(no), _ptr(f0), self.stream()), "pipeline")
         res = out[: no.value]
         return (res, f0) if want_f0 else res
+
+    # ------------------------------------------------------------------ kernel timing
+    def profile(self, enable: bool):
+        self._check(self.lib.rvcx_profile(self.ctx, 1 if enable else 0), "profile")
+
+    def profile_read(self):
+        """(summed conv-GEMM kernel ms, summed algorithmic FLOPs, launches) since the last read."""
+        ms, fl, n = ctypes.c_double(0), ctypes.c_double(0), ctypes.c_int64(0)
+        self._check(self.lib.rvcx_profile_read(self.ctx, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(n)),
+                    "profile_read")
+        return ms.value, fl.value, n.value
