@@ -679,10 +679,12 @@ struct IirCoef {
   int order;
 };
 
+template <int O>
 __device__ __forceinline__ double iir_step(const IirCoef& c, double* z, double x) {
   const double y = c.b[0] * x + z[0];
-  for (int i = 0; i < c.order - 1; ++i) z[i] = c.b[i + 1] * x + z[i + 1] - c.a[i + 1] * y;
-  z[c.order - 1] = c.b[c.order] * x - c.a[c.order] * y;
+#pragma unroll
+  for (int i = 0; i < O - 1; ++i) z[i] = c.b[i + 1] * x + z[i + 1] - c.a[i + 1] * y;
+  z[O - 1] = c.b[O] * x - c.a[O] * y;
   return y;
 }
 
@@ -697,6 +699,7 @@ __device__ __forceinline__ double iir_in(const double* x, long long n, int padle
   return x[k];
 }
 
+template <int O>
 __global__ void k_iir_warm(const IirCoef c, const double* x, long long n, int padlen, const double* yf, long long ne,
                            int rev, double* out) {
   const long long ch = blockIdx.x * (long long)blockDim.x + threadIdx.x;
@@ -704,16 +707,39 @@ __global__ void k_iir_warm(const IirCoef c, const double* x, long long n, int pa
   if (ch >= nch) return;
   const long long j0 = ch * IIR_L, j1 = min(ne, j0 + IIR_L);
   long long js = j0 - IIR_W;
-  double z[IIR_MAXO];
+  double z[O];
   if (js <= 0) {
     js = 0;
     const double x0 = iir_in(x, n, padlen, yf, ne, rev, 0);
-    for (int i = 0; i < c.order; ++i) z[i] = c.zi[i] * x0;
+#pragma unroll
+    for (int i = 0; i < O; ++i) z[i] = c.zi[i] * x0;
   } else {
-    for (int i = 0; i < c.order; ++i) z[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < O; ++i) z[i] = 0.0;
   }
-  for (long long j = js; j < j0; ++j) (void)iir_step(c, z, iir_in(x, n, padlen, yf, ne, rev, j));
-  for (long long j = j0; j < j1; ++j) out[j] = iir_step(c, z, iir_in(x, n, padlen, yf, ne, rev, j));
+  // inputs are independent of the recurrence: fetch them 16 at a time, one batch ahead, so the
+  // sequential loop only waits on its own 2-FMA dependency chain, not on memory latency
+  constexpr int NB = 16;
+  double cur[NB], nxt[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) cur[i] = (js + i < j1) ? iir_in(x, n, padlen, yf, ne, rev, js + i) : 0.0;
+  for (long long jb = js; jb < j1; jb += NB) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const long long j = jb + NB + i;
+      nxt[i] = (j < j1) ? iir_in(x, n, padlen, yf, ne, rev, j) : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const long long j = jb + i;
+      if (j < j1) {
+        const double y = iir_step<O>(c, z, cur[i]);
+        if (j >= j0) out[j] = y;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) cur[i] = nxt[i];
+  }
 }
 
 // audio_pad[k] = y[reflect(k - t_pad)] with y the filtfilt output (backward pass result yb reversed, trimmed)
@@ -748,8 +774,17 @@ hipError_t filtfilt_pad(const double* x, long long n, const double* b, const dou
   double* yf = ws;
   double* yb = yf + ne;
   const unsigned g = (unsigned)((nch + 63) / 64);
-  hipLaunchKernelGGL(k_iir_warm, dim3(g), dim3(64), 0, s, c, x, n, padlen, yf, ne, 0, yf);
-  hipLaunchKernelGGL(k_iir_warm, dim3(g), dim3(64), 0, s, c, x, n, padlen, yf, ne, 1, yb);
+  for (int rev = 0; rev < 2; ++rev) {
+    double* o = rev ? yb : yf;
+    switch (order) {
+#define RVCX_IIR_CASE(O_) \
+  case O_: hipLaunchKernelGGL(k_iir_warm<O_>, dim3(g), dim3(64), 0, s, c, x, n, padlen, yf, ne, rev, o); break;
+      RVCX_IIR_CASE(1) RVCX_IIR_CASE(2) RVCX_IIR_CASE(3) RVCX_IIR_CASE(4)
+      RVCX_IIR_CASE(5) RVCX_IIR_CASE(6) RVCX_IIR_CASE(7) RVCX_IIR_CASE(8)
+#undef RVCX_IIR_CASE
+      default: return hipErrorInvalidValue;
+    }
+  }
   hipLaunchKernelGGL(k_filt_pad, dim3(nblocks(n + 2 * t_pad)), dim3(TB), 0, s, yb, ne, padlen, n, t_pad, pad64,
                      pad32);
   return hipGetLastError();

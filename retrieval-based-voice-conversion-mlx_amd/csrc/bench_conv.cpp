@@ -1,0 +1,188 @@
+// Standalone micro-benchmark + correctness check of the implicit-GEMM conv kernel
+// (not part of librvcx.so). Build: make bench_conv ; run on the GPU box.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "rvcx_kernels.h"
+
+using namespace rvcx;
+
+#define CK_(x)                                                                      \
+  do {                                                                               \
+    hipError_t e = (x);                                                              \
+    if (e != hipSuccess) {                                                           \
+      fprintf(stderr, "%s failed: %s (line %d)\n", #x, hipGetErrorString(e), __LINE__); \
+      exit(1);                                                                       \
+    }                                                                                \
+  } while (0)
+
+__global__ void naive_conv1d(const float* x, const float* w, const float* b, float* y, int Tin, int Cin, int Tout,
+                             int N, int taps, int dil, int pad, int stride) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= (long long)Tout * N) return;
+  const int t = (int)(i / N), n = (int)(i % N);
+  double acc = 0.0;
+  for (int k = 0; k < taps; ++k) {
+    const int r = t * stride - pad + k * dil;
+    if (r < 0 || r >= Tin) continue;
+    for (int c = 0; c < Cin; ++c) {
+      float xv = x[(long long)r * Cin + c];
+      xv = xv > 0.f ? xv : 0.1f * xv;
+      acc += (double)xv * w[((long long)k * N + n) * Cin + c];
+    }
+  }
+  y[i] = (float)acc + b[n];
+}
+
+static void fill_rand(std::vector<float>& v, unsigned seed) {
+  srand(seed);
+  for (auto& x : v) x = (float)rand() / RAND_MAX * 2.f - 1.f;
+}
+
+struct Case {
+  const char* name;
+  int T, Cin, N, taps, dil;
+};
+
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? atoi(argv[1]) : 20;
+  // correctness on a small shape for every forced config x pipe
+  {
+    const int T = 1000, C = 128, N = 128, taps = 7, dil = 3, pad = (taps * dil - dil) / 2;
+    std::vector<float> hx((size_t)T * C), hw((size_t)taps * N * C), hb(N);
+    fill_rand(hx, 1);
+    fill_rand(hw, 2);
+    fill_rand(hb, 3);
+    float *x, *w, *b, *y, *yr;
+    CK_(hipMalloc(&x, hx.size() * 4));
+    CK_(hipMalloc(&w, hw.size() * 4));
+    CK_(hipMalloc(&b, N * 4));
+    CK_(hipMalloc(&y, (size_t)T * N * 4));
+    CK_(hipMalloc(&yr, (size_t)T * N * 4));
+    CK_(hipMemcpy(x, hx.data(), hx.size() * 4, hipMemcpyHostToDevice));
+    CK_(hipMemcpy(w, hw.data(), hw.size() * 4, hipMemcpyHostToDevice));
+    CK_(hipMemcpy(b, hb.data(), N * 4, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(naive_conv1d, dim3((T * N + 255) / 256), dim3(256), 0, 0, x, w, b, yr, T, C, T, N, taps, dil,
+                       pad, 1);
+    std::vector<float> ref((size_t)T * N), out((size_t)T * N);
+    CK_(hipMemcpy(ref.data(), yr, ref.size() * 4, hipMemcpyDeviceToHost));
+    for (int cfg = 0; cfg < 6; ++cfg)
+      for (int pipe = 0; pipe < 2; ++pipe) {
+        ConvArgs a;
+        a.x = x; a.ldx = C; a.T_in = T; a.C_in = C;
+        a.w = w; a.ldw = C; a.w_ts = (long long)N * C; a.taps = taps; a.dil = dil; a.pad = pad;
+        a.y = y; a.ldy = N; a.T_out = T; a.N = N; a.bias = b;
+        a.pre_act = ACT_LRELU; a.pre_slope = 0.1f;
+        a.force_cfg = cfg; a.pipe = pipe;
+        CK_(hipMemset(y, 0, (size_t)T * N * 4));
+        CK_(conv1d(a, 0));
+        CK_(hipDeviceSynchronize());
+        CK_(hipMemcpy(out.data(), y, out.size() * 4, hipMemcpyDeviceToHost));
+        double md = 0, mr = 0;
+        for (size_t i = 0; i < out.size(); ++i) {
+          md = std::max(md, (double)fabsf(out[i] - ref[i]));
+          mr = std::max(mr, (double)fabsf(ref[i]));
+        }
+        printf("check cfg=%d pipe=%d max|diff|/max|ref| = %.3e %s\n", cfg, pipe, md / mr, md / mr < 1e-5 ? "OK" : "FAIL");
+      }
+  }
+  // split-K correctness on a small-M shape
+  {
+    const int T = 150, C = 512, N = 384, taps = 3, dil = 1, pad = 1;
+    std::vector<float> hx((size_t)T * C), hw((size_t)taps * N * C), hb(N);
+    fill_rand(hx, 11);
+    fill_rand(hw, 12);
+    fill_rand(hb, 13);
+    float *x, *w, *b, *y, *yr, *ws;
+    CK_(hipMalloc(&x, hx.size() * 4));
+    CK_(hipMalloc(&w, hw.size() * 4));
+    CK_(hipMalloc(&b, N * 4));
+    CK_(hipMalloc(&y, (size_t)T * N * 4));
+    CK_(hipMalloc(&yr, (size_t)T * N * 4));
+    CK_(hipMemcpy(x, hx.data(), hx.size() * 4, hipMemcpyHostToDevice));
+    CK_(hipMemcpy(w, hw.data(), hw.size() * 4, hipMemcpyHostToDevice));
+    CK_(hipMemcpy(b, hb.data(), N * 4, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(naive_conv1d, dim3((T * N + 255) / 256), dim3(256), 0, 0, x, w, b, yr, T, C, T, N, taps, dil,
+                       pad, 1);
+    ConvArgs a;
+    a.x = x; a.ldx = C; a.T_in = T; a.C_in = C;
+    a.w = w; a.ldw = C; a.w_ts = (long long)N * C; a.taps = taps; a.dil = dil; a.pad = pad;
+    a.y = y; a.ldy = N; a.T_out = T; a.N = N; a.bias = b;
+    a.pre_act = ACT_LRELU; a.pre_slope = 0.1f;
+    const long long need = conv_plan_splitk(a, false);
+    CK_(hipMalloc(&ws, (need > 0 ? need : 1) * 4));
+    a.ws = ws;
+    CK_(conv1d(a, 0));
+    CK_(hipDeviceSynchronize());
+    std::vector<float> ref((size_t)T * N), out((size_t)T * N);
+    CK_(hipMemcpy(ref.data(), yr, ref.size() * 4, hipMemcpyDeviceToHost));
+    CK_(hipMemcpy(out.data(), y, out.size() * 4, hipMemcpyDeviceToHost));
+    double md = 0, mr = 0;
+    for (size_t i = 0; i < out.size(); ++i) {
+      md = std::max(md, (double)fabsf(out[i] - ref[i]));
+      mr = std::max(mr, (double)fabsf(ref[i]));
+    }
+    printf("check splitk ksplit=%d max|diff|/max|ref| = %.3e %s\n", a.ksplit, md / mr, md / mr < 1e-5 ? "OK" : "FAIL");
+  }
+  // timing
+  std::vector<Case> cases = {
+      {"gen.s1 C256 k11 d5", 18600, 256, 256, 11, 5}, {"gen.s2 C128 k3 d1", 186000, 128, 128, 3, 1},
+      {"gen.s2 C128 k7 d3", 186000, 128, 128, 7, 3},  {"gen.s2 C128 k11 d5", 186000, 128, 128, 11, 5},
+      {"gen.s3 C64 k11 d5", 372000, 64, 64, 11, 5},   {"gen.s4 C32 k11 d5", 744000, 32, 32, 11, 5},
+      {"hubert ffn1 775x768->3072", 775, 768, 3072, 1, 1}, {"hubert qkv 775x768->2304", 775, 768, 2304, 1, 1},
+      {"hubert conv1 24808 k3 s2", 24808, 512, 512, 3, 1},
+      {"hubert ffn2 775x3072->768", 775, 3072, 768, 1, 1}, {"te ffn1 1550 k3 192->768", 1550, 192, 768, 3, 1},
+      {"te qkv 1550x192->576", 1550, 192, 576, 1, 1}, {"flow in 1550 k5 192->384", 1550, 192, 384, 5, 1},
+  };
+  for (auto& cs : cases) {
+    const size_t nx = (size_t)cs.T * cs.Cin, nw = (size_t)cs.taps * cs.N * cs.Cin, ny = (size_t)cs.T * cs.N;
+    float *x, *w, *b, *y;
+    CK_(hipMalloc(&x, nx * 4));
+    CK_(hipMalloc(&w, nw * 4));
+    CK_(hipMalloc(&b, cs.N * 4));
+    CK_(hipMalloc(&y, ny * 4));
+    std::vector<float> hx(nx), hw(nw);
+    fill_rand(hx, 5);
+    fill_rand(hw, 6);
+    CK_(hipMemcpy(x, hx.data(), nx * 4, hipMemcpyHostToDevice));
+    CK_(hipMemcpy(w, hw.data(), nw * 4, hipMemcpyHostToDevice));
+    CK_(hipMemset(b, 0, cs.N * 4));
+    const double flops = 2.0 * cs.T * cs.N * (double)cs.Cin * cs.taps;
+    for (int cfg : {-1, 1, 3})
+      for (int pipe = 0; pipe < 1; ++pipe) {
+        ConvArgs a;
+        a.x = x; a.ldx = cs.Cin; a.T_in = cs.T; a.C_in = cs.Cin;
+        a.w = w; a.ldw = cs.Cin; a.w_ts = (long long)cs.N * cs.Cin; a.taps = cs.taps; a.dil = cs.dil;
+        a.pad = (cs.taps * cs.dil - cs.dil) / 2;
+        a.y = y; a.ldy = cs.N; a.T_out = cs.T; a.N = cs.N; a.bias = b;
+        a.pre_act = ACT_LRELU; a.pre_slope = 0.1f; a.act = ACT_LRELU; a.slope = 0.1f;
+        a.force_cfg = cfg; a.pipe = pipe;
+        float* wsp = nullptr;
+        if (cfg < 0) {
+          const long long need = conv_plan_splitk(a, false);
+          if (need > 0) { CK_(hipMalloc(&wsp, need * 4)); a.ws = wsp; }
+        }
+        if (conv1d(a, 0) != hipSuccess) { (void)hipGetLastError(); continue; }
+        CK_(hipDeviceSynchronize());
+        hipEvent_t e0, e1;
+        CK_(hipEventCreate(&e0));
+        CK_(hipEventCreate(&e1));
+        CK_(hipEventRecord(e0, 0));
+        for (int i = 0; i < iters; ++i) CK_(conv1d(a, 0));
+        CK_(hipEventRecord(e1, 0));
+        CK_(hipEventSynchronize(e1));
+        float ms = 0;
+        CK_(hipEventElapsedTime(&ms, e0, e1));
+        ms /= iters;
+        printf("%-28s cfg=%2d pipe=%d ks=%2d %8.3f ms  %7.2f TFLOP/s\n", cs.name, cfg, pipe, a.ksplit, ms, flops / ms / 1e9);
+        if (wsp) (void)hipFree(wsp);
+      }
+    (void)hipFree(x); (void)hipFree(w); (void)hipFree(b); (void)hipFree(y);
+  }
+  return 0;
+}

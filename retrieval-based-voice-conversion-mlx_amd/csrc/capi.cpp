@@ -31,7 +31,10 @@ void set_device(rvcx_ctx* c) { RVCX_HIP(hipSetDevice(c->device)); }
 }  // namespace
 
 namespace rvcx {
-void launch_conv(Ctx& c, const ConvArgs& a, bool two_d, hipStream_t s, double flops) {
+void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double flops) {
+  ConvArgs a = a_in;
+  const long long need = conv_plan_splitk(a, two_d);
+  if (need > 0) a.ws = c.buf<float>("conv.splitk", (size_t)need, s);
   if (flops < 0) {
     const double M = two_d ? (double)a.T_out * a.W_out : (double)a.T_out;
     flops = 2.0 * M * a.N * (double)a.C_in * a.taps * a.batch * a.batch_inner;

@@ -14,6 +14,8 @@
 // [tap][N][C]) is staged per tap. Each wave holds TM x TN 32x32 fp32 accumulators; one
 // ds_read_b128 per operand feeds 4 MFMAs (the k-pair of MFMA j is channels {8kk+j, 8kk+4+j}).
 // fp32 in / fp32 accumulate MFMA is a bit-exact fp32 fma chain at the FP32 vector peak rate.
+#include <algorithm>
+
 #include "rvcx_kernels.h"
 
 namespace rvcx {
@@ -25,16 +27,23 @@ constexpr int CK = 32;   // contraction channels per LDS chunk
 constexpr int CKP = 36;  // padded LDS row: rows i..i+15 land on distinct 16-B bank slots
 constexpr int NTHREADS = 256;
 
-__device__ __forceinline__ float act_fn(float v, int act, float slope) {
+__device__ __noinline__ float act_fn_slow(float v, int act, float slope) {
   switch (act) {
-    case ACT_LRELU: return v > 0.f ? v : v * slope;
-    case ACT_RELU: return v > 0.f ? v : 0.f;
     case ACT_GELU: return 0.5f * v * (1.f + erff(v * 0.70710678118654752440f));
     case ACT_TANH: return tanhf(v);
     case ACT_SIGMOID: return 1.f / (1.f + expf(-v));
     case ACT_LOGCLAMP: return logf(fmaxf(v, slope));
     default: return v;
   }
+}
+
+// cheap activations inline, transcendental ones out of line (keeps the unrolled epilogue small
+// enough that the accumulators stay in registers)
+__device__ __forceinline__ float act_fn(float v, int act, float slope) {
+  if (act == ACT_NONE) return v;
+  if (act == ACT_LRELU) return v > 0.f ? v : v * slope;
+  if (act == ACT_RELU) return v > 0.f ? v : 0.f;
+  return act_fn_slow(v, act, slope);
 }
 
 __device__ __forceinline__ void epilogue_store(const ConvArgs& a, float v, float bn, long long m, int n, int oh,
@@ -59,25 +68,28 @@ __device__ __forceinline__ void epilogue_store(const ConvArgs& a, float v, float
   *dst = v;
 }
 
-template <int BM, int BN, int WM, int WN, bool TWO_D>
+template <int BM, int BN, int WM, int WN, bool TWO_D, bool PIPE>
 __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a, const int nrows_a, const int rw,
                                                              const int rh, const int tiles_w, const int vec_a,
-                                                             const int vec_b) {
+                                                             const int vec_b, const int ksplit) {
   constexpr int TM = BM / (WM * 32);
   constexpr int TN = BN / (WN * 32);
   static_assert(WM * WN == 4, "4 waves per block");
   static_assert(TM >= 1 && TN >= 1, "tile too small");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* As = smem;
-  float* Bs = smem + nrows_a * CKP;
+  float* Bs0 = smem + nrows_a * CKP;        // PIPE: two B buffers [2][BN][CKP]
+  float* Bs1 = Bs0 + BN * CKP;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int li = lane & 31, hk = lane >> 5;
-  const int b = blockIdx.z / a.batch_inner;   // outer batch
-  const int bi = blockIdx.z % a.batch_inner;  // inner batch (heads / groups)
+  const int zsplit = blockIdx.z % ksplit;     // split-K slice
+  const int zb = blockIdx.z / ksplit;
+  const int b = zb / a.batch_inner;           // outer batch
+  const int bi = zb % a.batch_inner;          // inner batch (heads / groups)
   const int n0 = blockIdx.y * BN;
   int m0 = 0, h0 = 0, w0 = 0;
   if (!TWO_D) {
@@ -111,9 +123,64 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[tm][tn][r] = 0.f;
 
-  for (int c0 = 0; c0 < a.C_in; c0 += CK) {
-    __syncthreads();
-    // ---- stage A: nrows_a x 32 channels, pre-activation applied, zero outside the input
+  // B tile loader: global -> registers (BN x 32 floats of (tap, chunk)); NK or KN weight layout
+  constexpr int BV = (BN * (CK / 4) + NTHREADS - 1) / NTHREADS;  // float4 per thread
+  auto load_b = [&](int tap, int c0, f32x4 (&reg)[BV]) {
+    const float* Wt = Wb + (long long)tap * a.w_ts;
+#pragma unroll
+    for (int v = 0; v < BV; ++v) {
+      const int idx = tid + v * NTHREADS;
+      f32x4 val = {0.f, 0.f, 0.f, 0.f};
+      if (idx < BN * (CK / 4)) {
+        if (!a.b_kn) {
+          const int n = idx >> 3;
+          const int c = c0 + ((idx & 7) << 2);
+          const int gn = n0 + n;
+          if (gn < a.N && c < a.C_in) {
+            const float* src = Wt + (long long)gn * a.ldw + c;
+            if (vec_b && c + 4 <= a.C_in) {
+              val = *reinterpret_cast<const f32x4*>(src);
+            } else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) val[j] = (c + j < a.C_in) ? src[j] : 0.f;
+            }
+          }
+        } else {
+          const int cc = idx / (BN / 4);
+          const int n4 = (idx - cc * (BN / 4)) << 2;
+          const int gc = c0 + cc, gn = n0 + n4;
+          if (gc < a.C_in && gn < a.N) {
+            const float* src = Wt + (long long)gc * a.ldw + gn;
+            if (vec_b && gn + 4 <= a.N) {
+              val = *reinterpret_cast<const f32x4*>(src);
+            } else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) val[j] = (gn + j < a.N) ? src[j] : 0.f;
+            }
+          }
+        }
+      }
+      reg[v] = val;
+    }
+  };
+  auto store_b = [&](float* Bs, const f32x4 (&reg)[BV]) {
+#pragma unroll
+    for (int v = 0; v < BV; ++v) {
+      const int idx = tid + v * NTHREADS;
+      if (idx < BN * (CK / 4)) {
+        if (!a.b_kn) {
+          *reinterpret_cast<f32x4*>(&Bs[(idx >> 3) * CKP + ((idx & 7) << 2)]) = reg[v];
+        } else {
+          const int cc = idx / (BN / 4);
+          const int n4 = (idx - cc * (BN / 4)) << 2;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) Bs[(n4 + j) * CKP + cc] = reg[v][j];
+        }
+      }
+    }
+  };
+  // A tile: nrows_a x 32 channels of chunk c0 -> LDS, pre-activation applied, zero outside the input
+  auto stage_a = [&](int c0) {
     for (int idx = tid; idx < nrows_a * (CK / 4); idx += NTHREADS) {
       const int r = idx >> 3;
       const int c4 = (idx & 7) << 2;
@@ -151,70 +218,82 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
       }
       *reinterpret_cast<f32x4*>(&As[r * CKP + c4]) = v;
     }
-    for (int tap = 0; tap < a.taps; ++tap) {
-      if (tap) __syncthreads();
-      // ---- stage B for (tap, chunk): Bs[n][c]
-      const float* Wt = Wb + (long long)tap * a.w_ts;
-      if (!a.b_kn) {
-        for (int idx = tid; idx < BN * (CK / 4); idx += NTHREADS) {
-          const int n = idx >> 3;
-          const int c4 = (idx & 7) << 2;
-          const int gn = n0 + n, c = c0 + c4;
-          f32x4 v = {0.f, 0.f, 0.f, 0.f};
-          if (gn < a.N && c < a.C_in) {
-            const float* src = Wt + (long long)gn * a.ldw + c;
-            if (vec_b && c + 4 <= a.C_in) {
-              v = *reinterpret_cast<const f32x4*>(src);
-            } else {
+  };
+  auto compute = [&](const float* Bs, int tap) {
+    const int toff = TWO_D ? (tap / a.KW) * aw + (tap % a.KW) : tap * a.dil;
 #pragma unroll
-              for (int j = 0; j < 4; ++j) v[j] = (c + j < a.C_in) ? src[j] : 0.f;
-            }
-          }
-          *reinterpret_cast<f32x4*>(&Bs[n * CKP + c4]) = v;
+    for (int kk = 0; kk < CK; kk += 8) {
+      float av[TM][4], bv[TN][4];
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const f32x4 t = *reinterpret_cast<const f32x4*>(&As[(base[tm] + toff) * CKP + kk + hk * 4]);
+        av[tm][0] = t[0]; av[tm][1] = t[1]; av[tm][2] = t[2]; av[tm][3] = t[3];
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const f32x4 t = *reinterpret_cast<const f32x4*>(&Bs[(wn * TN * 32 + tn * 32 + li) * CKP + kk + hk * 4]);
+        bv[tn][0] = t[0]; bv[tn][1] = t[1]; bv[tn][2] = t[2]; bv[tn][3] = t[3];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < TN; ++tn)
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[tm][j], bv[tn][j], acc[tm][tn], 0, 0, 0);
+    }
+  };
+
+  const int nchunks = (a.C_in + CK - 1) / CK;
+  if (!PIPE) {
+    f32x4 breg[BV];
+    const int total = nchunks * a.taps;
+    const int per = (total + ksplit - 1) / ksplit;
+    const int it0 = zsplit * per, it1 = min(total, it0 + per);
+    int it = it0;
+    while (it < it1) {
+      const int ch = it / a.taps;
+      __syncthreads();
+      stage_a(ch * CK);
+      for (int tap = it - ch * a.taps; tap < a.taps && it < it1; ++tap, ++it) {
+        if (it > it0 && tap != it0 - ch * a.taps) __syncthreads();
+        load_b(tap, ch * CK, breg);
+        store_b(Bs0, breg);
+        __syncthreads();
+        compute(Bs0, tap);
+      }
+    }
+  } else {
+    // software pipeline over the (chunk, tap) sequence: the next B tile is fetched into registers
+    // while the MFMAs consume the current one from LDS; one barrier per tap (two at chunk change).
+    f32x4 breg[BV];
+    stage_a(0);
+    load_b(0, 0, breg);
+    store_b(Bs0, breg);
+    __syncthreads();
+    const int total = nchunks * a.taps;
+    int ch = 0, tap = 0;
+    for (int it = 0; it < total; ++it) {
+      float* Bcur = (it & 1) ? Bs1 : Bs0;
+      float* Bnxt = (it & 1) ? Bs0 : Bs1;
+      int nch = ch, ntap = tap + 1;
+      if (ntap == a.taps) {
+        ntap = 0;
+        ++nch;
+      }
+      const bool more = it + 1 < total;
+      if (more) load_b(ntap, nch * CK, breg);
+      compute(Bcur, tap);
+      if (more) {
+        if (ntap == 0) {
+          __syncthreads();  // every wave is done with this chunk's A tile
+          stage_a(nch * CK);
         }
-      } else {
-        for (int idx = tid; idx < CK * (BN / 4); idx += NTHREADS) {
-          const int c = idx / (BN / 4);
-          const int n4 = (idx - c * (BN / 4)) << 2;
-          const int gc = c0 + c, gn = n0 + n4;
-          f32x4 v = {0.f, 0.f, 0.f, 0.f};
-          if (gc < a.C_in && gn < a.N) {
-            const float* src = Wt + (long long)gc * a.ldw + gn;
-            if (vec_b && gn + 4 <= a.N) {
-              v = *reinterpret_cast<const f32x4*>(src);
-            } else {
-#pragma unroll
-              for (int j = 0; j < 4; ++j) v[j] = (gn + j < a.N) ? src[j] : 0.f;
-            }
-          }
-#pragma unroll
-          for (int j = 0; j < 4; ++j) Bs[(n4 + j) * CKP + c] = v[j];
-        }
+        store_b(Bnxt, breg);
       }
       __syncthreads();
-      // ---- MFMA over the chunk
-      const int toff = TWO_D ? (tap / a.KW) * aw + (tap % a.KW) : tap * a.dil;
-#pragma unroll
-      for (int kk = 0; kk < CK; kk += 8) {
-        float av[TM][4], bv[TN][4];
-#pragma unroll
-        for (int tm = 0; tm < TM; ++tm) {
-          const f32x4 t = *reinterpret_cast<const f32x4*>(&As[(base[tm] + toff) * CKP + kk + hk * 4]);
-          av[tm][0] = t[0]; av[tm][1] = t[1]; av[tm][2] = t[2]; av[tm][3] = t[3];
-        }
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn) {
-          const f32x4 t = *reinterpret_cast<const f32x4*>(&Bs[(wn * TN * 32 + tn * 32 + li) * CKP + kk + hk * 4]);
-          bv[tn][0] = t[0]; bv[tn][1] = t[1]; bv[tn][2] = t[2]; bv[tn][3] = t[3];
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-            for (int tn = 0; tn < TN; ++tn)
-              acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[tm][j], bv[tn][j], acc[tm][tn], 0, 0, 0);
-      }
+      ch = nch;
+      tap = ntap;
     }
   }
 
@@ -245,9 +324,43 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
           ok = n_ok && (ml < rh * rw) && (oh < a.T_out) && (ow < a.W_out);
           m = (long long)oh * a.W_out + ow;
         }
-        if (ok) epilogue_store(a, acc[tm][tn][r], bn, m, n, oh, ow, R, MK, Y);
+        if (ok) {
+          if (ksplit > 1) {
+            a.ws[(((long long)zb * ksplit + zsplit) * a.ws_rows + m) * a.N + n] = acc[tm][tn][r];
+          } else {
+            epilogue_store(a, acc[tm][tn][r], bn, m, n, oh, ow, R, MK, Y);
+          }
+        }
       }
     }
+  }
+}
+
+// split-K combine: sums the ksplit partial tiles in slice order (deterministic) and applies the epilogue
+__global__ void splitk_reduce_kernel(const ConvArgs a, const int ksplit, const int two_d) {
+  const long long rows = a.ws_rows;
+  const long long per_b = rows * a.N;
+  const long long total = per_b * a.batch * a.batch_inner;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long zb = i / per_b;
+    const long long rem = i - zb * per_b;
+    const long long m = rem / a.N;
+    const int n = (int)(rem - m * a.N);
+    const int b = (int)(zb / a.batch_inner), bi = (int)(zb % a.batch_inner);
+    const float* p = a.ws + (zb * ksplit) * per_b + m * a.N + n;
+    float v = 0.f;
+    for (int s = 0; s < ksplit; ++s) v += p[(long long)s * per_b];
+    const float* bias = a.bias ? a.bias + (long long)b * a.bias_bs + (long long)bi * a.bias_bs2 : nullptr;
+    const float* R = a.res ? a.res + (long long)b * a.res_bs + (long long)bi * a.res_bs2 : nullptr;
+    const float* MK = a.mask ? a.mask + (long long)b * a.mask_bs : nullptr;
+    float* Y = a.y + (long long)b * a.y_bs + (long long)bi * a.y_bs2;
+    int oh = 0, ow = 0;
+    if (two_d) {
+      oh = (int)(m / a.W_out);
+      ow = (int)(m % a.W_out);
+    }
+    epilogue_store(a, v, bias ? bias[n] : 0.f, m, n, oh, ow, R, MK, Y);
   }
 }
 
@@ -257,7 +370,7 @@ struct TileCfg {
   int BM, BN;
 };
 
-template <int BM, int BN, int WM, int WN, bool TWO_D>
+template <int BM, int BN, int WM, int WN, bool TWO_D, bool PIPE = false>
 hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
   int nrows_a, rw = 0, rh = 0, tiles_w = 1, mtiles;
   if (!TWO_D) {
@@ -270,43 +383,98 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
     mtiles = ((a.T_out + rh - 1) / rh) * tiles_w;
     nrows_a = (rh + a.KH - 1) * (rw + a.KW - 1);
   }
-  const size_t smem = (size_t)(nrows_a + BN) * CKP * sizeof(float);
+  const size_t smem = (size_t)(nrows_a + (PIPE ? 2 : 1) * BN) * CKP * sizeof(float);
   if (smem > 160 * 1024) return hipErrorInvalidValue;
   const int vec_a = ((a.ldx & 3) == 0) && ((reinterpret_cast<uintptr_t>(a.x) & 15) == 0) &&
                     ((a.x_bs & 3) == 0) && ((a.x_bs2 & 3) == 0);
   const int vec_b = ((a.ldw & 3) == 0) && ((reinterpret_cast<uintptr_t>(a.w) & 15) == 0) &&
                     ((a.w_bs & 3) == 0) && ((a.w_bs2 & 3) == 0) && ((a.w_ts & 3) == 0);
   if (a.batch_inner < 1) return hipErrorInvalidValue;
-  dim3 grid(mtiles, (a.N + BN - 1) / BN, a.batch * a.batch_inner);
-  auto kern = conv_gemm_kernel<BM, BN, WM, WN, TWO_D>;
+  int ksplit = 1;
+  if (!PIPE && a.ws && a.ksplit > 1) ksplit = a.ksplit;
+  dim3 grid(mtiles, (a.N + BN - 1) / BN, a.batch * a.batch_inner * ksplit);
+  auto kern = conv_gemm_kernel<BM, BN, WM, WN, TWO_D, PIPE>;
   if (smem > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(kern, grid, dim3(NTHREADS), smem, s, a, nrows_a, rw, rh, tiles_w, vec_a, vec_b);
+  hipLaunchKernelGGL(kern, grid, dim3(NTHREADS), smem, s, a, nrows_a, rw, rh, tiles_w, vec_a, vec_b, ksplit);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || ksplit == 1) return e;
+  const long long total = (long long)a.ws_rows * a.N * a.batch * a.batch_inner;
+  long long nb = (total + 255) / 256;
+  if (nb > 8192) nb = 8192;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, ksplit, TWO_D ? 1 : 0);
   return hipGetLastError();
+}
+
+template <bool TWO_D, bool PIPE>
+hipError_t launch_forced(const ConvArgs& a, hipStream_t s) {
+  switch (a.force_cfg) {
+    case 0: return launch_cfg<256, 32, 4, 1, TWO_D, PIPE>(a, s);
+    case 1: return launch_cfg<128, 32, 4, 1, TWO_D, PIPE>(a, s);
+    case 2: return launch_cfg<128, 64, 2, 2, TWO_D, PIPE>(a, s);
+    case 3: return launch_cfg<64, 64, 2, 2, TWO_D, PIPE>(a, s);
+    case 4: return launch_cfg<128, 128, 2, 2, TWO_D, PIPE>(a, s);
+    case 5: return launch_cfg<64, 128, 2, 2, TWO_D, PIPE>(a, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// Tile choice measured on MI355X (build/bench_conv): one 32x32 accumulator per wave with 4 waves
+// per block (128x32 or 64x64 tiles) beats larger per-wave tiles on every RVC shape (more resident
+// waves hide the LDS/staging latency); split-K when the output-tile grid cannot fill 256 CUs.
+template <bool TWO_D>
+int pick_cfg(const ConvArgs& a) {
+  if (a.force_cfg >= 0) return a.force_cfg;
+  return a.N <= 32 ? 1 : 3;
+}
+
+inline void cfg_tile(int cfg, int& BM, int& BN) {
+  static const int t[6][2] = {{256, 32}, {128, 32}, {128, 64}, {64, 64}, {128, 128}, {64, 128}};
+  BM = t[cfg][0];
+  BN = t[cfg][1];
 }
 
 template <bool TWO_D>
 hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
   if (a.N <= 0 || a.T_out <= 0 || a.batch <= 0) return hipSuccess;
   if (a.C_in <= 0 || a.taps <= 0) return hipErrorInvalidValue;
-  const long long M = TWO_D ? (long long)a.T_out * a.W_out : a.T_out;
-  const long long work = M * a.batch * a.batch_inner;
-  if (a.N <= 32) {
-    if (work >= 256 * 256) return launch_cfg<256, 32, 4, 1, TWO_D>(a, s);
-    return launch_cfg<128, 32, 4, 1, TWO_D>(a, s);
-  }
-  if (a.N <= 64) {
-    if (work >= 128 * 512) return launch_cfg<128, 64, 2, 2, TWO_D>(a, s);
-    return launch_cfg<64, 64, 2, 2, TWO_D>(a, s);
-  }
-  if (((work + 127) / 128) * ((a.N + 63) / 64) >= 512) return launch_cfg<128, 64, 2, 2, TWO_D>(a, s);
-  return launch_cfg<64, 64, 2, 2, TWO_D>(a, s);
+  const int cfg = pick_cfg<TWO_D>(a);
+  ConvArgs b = a;
+  b.force_cfg = cfg;
+  if (a.pipe && a.force_cfg >= 0) return launch_forced<TWO_D, true>(b, s);
+  return launch_forced<TWO_D, false>(b, s);
 }
 
 }  // namespace
+
+long long conv_plan_splitk(ConvArgs& a, bool two_d) {
+  a.ksplit = 1;
+  if (a.N <= 0 || a.T_out <= 0 || a.no_splitk) return 0;
+  const int cfg = two_d ? pick_cfg<true>(a) : pick_cfg<false>(a);
+  int BM, BN;
+  cfg_tile(cfg, BM, BN);
+  long long mtiles;
+  if (!two_d) {
+    mtiles = (a.T_out + BM - 1) / BM;
+  } else {
+    const int rw = a.W_out < BM ? a.W_out : BM;
+    const int rh = BM / rw;
+    mtiles = (long long)((a.T_out + rh - 1) / rh) * ((a.W_out + rw - 1) / rw);
+  }
+  const long long tiles = mtiles * ((a.N + BN - 1) / BN) * a.batch * a.batch_inner;
+  const int iters = ((a.C_in + CK - 1) / CK) * a.taps;
+  if (tiles >= 512 || iters < 4) return 0;
+  int ks = (int)((1024 + tiles - 1) / tiles);
+  ks = std::min(ks, iters / 2);
+  ks = std::min(ks, 32);
+  if (ks < 2) return 0;
+  a.ksplit = ks;
+  a.ws_rows = two_d ? (long long)a.T_out * a.W_out : a.T_out;
+  return (long long)ks * a.ws_rows * a.N * a.batch * a.batch_inner;
+}
 
 hipError_t conv1d(const ConvArgs& a, hipStream_t s) { return dispatch<false>(a, s); }
 hipError_t conv2d(const ConvArgs& a, hipStream_t s) { return dispatch<true>(a, s); }

@@ -136,7 +136,7 @@ int64_t pipeline_forward(Ctx& c, const double* audio, int64_t n, int sid, double
                          float* out, int64_t cap, double* f0_out, hipStream_t s);
 void set_i32(int32_t* p, int32_t v, hipStream_t s);
 // launch one implicit-GEMM conv (1-D or 2-D) with optional event timing; flops = algorithmic FLOPs
-void launch_conv(Ctx& c, const ConvArgs& a, bool two_d, hipStream_t s, double flops = -1.0);
+void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double flops = -1.0);
 
 inline void check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw Error(RVCX_E_HIP, std::string(what) + ": " + hipGetErrorString(e));

@@ -87,10 +87,20 @@ struct ConvArgs {
   int batch = 1;
   int batch_inner = 1;
   long long x_bs2 = 0, w_bs2 = 0, y_bs2 = 0, res_bs2 = 0, bias_bs2 = 0;
+  // tuning / benchmarking: force a tile configuration (0..5) and the software pipeline on/off
+  int force_cfg = -1;
+  int pipe = 0;
+  // split-K: set by conv_plan_splitk; ws holds ksplit partial [rows][N] tiles per batch entry
+  int ksplit = 1;
+  int no_splitk = 0;
+  long long ws_rows = 0;
+  float* ws = nullptr;
 };
 
 hipError_t conv1d(const ConvArgs& a, hipStream_t s);
 hipError_t conv2d(const ConvArgs& a, hipStream_t s);
+// choose split-K for small output grids; returns the workspace floats needed (0 = no split)
+long long conv_plan_splitk(ConvArgs& a, bool two_d);
 
 // ---------------------------------------------------------------- misc kernels
 hipError_t fill(float* p, float v, long long n, hipStream_t s);
