@@ -466,8 +466,12 @@ long long conv_plan_splitk(ConvArgs& a, bool two_d) {
   }
   const long long tiles = mtiles * ((a.N + BN - 1) / BN) * a.batch * a.batch_inner;
   const int iters = ((a.C_in + CK - 1) / CK) * a.taps;
-  if (tiles >= 512 || iters < 4) return 0;
-  int ks = (int)((1024 + tiles - 1) / tiles);
+  const double M = two_d ? (double)a.T_out * a.W_out : (double)a.T_out;
+  const double flops = 2.0 * M * a.N * (double)a.C_in * a.taps * a.batch * a.batch_inner;
+  // split only where the output grid leaves CUs idle AND the contraction is long enough to pay
+  // for the extra combine launch (~5-10 us)
+  if (tiles >= 384 || iters < 8 || flops < 1.0e8) return 0;
+  int ks = (int)((768 + tiles - 1) / tiles);
   ks = std::min(ks, iters / 2);
   ks = std::min(ks, 32);
   if (ks < 2) return 0;
