@@ -80,10 +80,18 @@ int rvcx_hubert(rvcx_ctx* ctx, const float* d_audio, int64_t n, int version, flo
 int rvcx_rmvpe(rvcx_ctx* ctx, const float* d_audio, int64_t n, float thred, double* d_f0, int64_t cap_frames,
                int64_t* frames_out, float* d_hidden, void* stream);
 
+/* RMVPE0Predictor.decode (rvc/lib/predictors/RMVPE.py:515-540; rvc_mlx/lib/mlx/rmvpe.py:357-406):
+ * salience [F][360] fp32 -> f0 [F] fp64 (argmax, +-4-bin weighted cents, threshold, 10 * 2^(c/1200), 10 -> 0). */
+int rvcx_rmvpe_decode(rvcx_ctx* ctx, const float* d_hidden, int64_t F, float thred, double* d_f0, void* stream);
+
 /* f0 post-processing of Pipeline.get_f0 (rvc/infer/pipeline.py:278-291): f0 *= 2^(semitones/12),
  * mel quantisation to coarse 1..255. Writes coarse (int32), pitchf (fp32) and shifted f0 (fp64, optional). */
 int rvcx_f0_post(rvcx_ctx* ctx, const double* d_f0, int64_t F, double semitones, int32_t* d_coarse, float* d_pitchf,
                  double* d_f0_shifted, void* stream);
+
+/* Autotune.autotune_f0 in place (rvc/infer/pipeline.py:151-162; rvc_mlx/infer/pipeline_mlx.py:72-80):
+ * f0 += (nearest note - f0) * strength. skip_unvoiced = 1 leaves f0 <= 0 frames untouched (MLX). */
+int rvcx_f0_autotune(rvcx_ctx* ctx, double* d_f0, int64_t F, double strength, int skip_unvoiced, void* stream);
 
 /* Synthesizer.infer (rvc/lib/algorithm/synthesizers.py:206-243; rvc_mlx/lib/mlx/synthesizers.py:193-235).
  * phone [B][T][E], lengths [B], pitch [B][T], pitchf [B][T], sid [B] -> out [B][T*upp].
@@ -112,11 +120,44 @@ int rvcx_voice_conversion(rvcx_ctx* ctx, const float* d_audio, int64_t n, const 
  * rvcx_pipeline's zero-phase filtfilt (padtype 'odd', padlen 3*(order+1)). */
 int rvcx_set_highpass(rvcx_ctx* ctx, const double* b, const double* a, const double* zi, int order);
 
-/* Pipeline.pipeline for one utterance whose padded length fits one chunk (<= t_max), all on device
- * (rvc/infer/pipeline.py:390-558 with pitch_guidance, index_rate 0, volume_envelope 1;
- * rvc_mlx/infer/pipeline_mlx.py:263-373): filtfilt(audio) -> reflect pad t_pad -> RMVPE (thred 0.03)
- * -> f0 * 2^(semitones/12), coarse -> voice_conversion -> trim t_pad_tgt per side -> peak-normalise.
- * d_audio [n] fp64 @16 kHz; out fp32 @tgt_sr; d_f0 (optional) receives the shifted f0 [1 + (n+2 t_pad)/160]. */
+/* Options of Pipeline.pipeline (rvc/infer/pipeline.py:390-408; rvc_mlx/infer/pipeline_mlx.py:263) that
+ * reach the device path. Fill with rvcx_pipeline_default_opts, then override. Times are in samples. */
+typedef struct {
+  int sid;                          /* speaker id (emb_g row) */
+  int version;                      /* 0 = from the synthesizer (768-d -> v2, 256-d -> v1), or 1 / 2 */
+  double pitch;                     /* semitones, f0 *= 2^(pitch/12) (pipeline.py:278-279) */
+  float protect;                    /* consonant protection, active when < 0.5 (pipeline.py:350-362) */
+  float rmvpe_threshold;            /* decode threshold (0.03, pipeline.py:237) */
+  int64_t t_pad, t_pad_tgt;         /* x_pad * 16000 and x_pad * tgt_sr (pipeline.py:176-177) */
+  int64_t t_query, t_center, t_max; /* x_query/x_center/x_max * 16000: long-input split search (:440-452);
+                                       t_max = 0 disables splitting */
+  int f0_autotune;                  /* Autotune.autotune_f0 (pipeline.py:151-162, :248-249) */
+  double f0_autotune_strength;
+  int proposed_pitch;               /* key offset from the median f0 (pipeline.py:250-277) */
+  double proposed_pitch_threshold;
+  double volume_envelope;           /* AudioProcessor.change_rms rate; 1 = off (pipeline.py:545-549) */
+  int mlx_semantics;                /* 1: f0 adjustments as rvc_mlx PipelineMLX.get_f0 (pipeline_mlx.py:135-164):
+                                       autotune skips f0 <= 0 and the pitch shift is applied after it */
+} rvcx_pipeline_opts;
+
+/* Defaults of the rvc/ Config (x_pad 1, x_query 6, x_center 38, x_max 41; rvc/configs/config.py) at
+ * 48 kHz, protect 0.33, volume_envelope 1. */
+int rvcx_pipeline_default_opts(rvcx_pipeline_opts* opts);
+
+/* Pipeline.pipeline, all on device (rvc/infer/pipeline.py:390-558 with pitch_guidance and
+ * index_rate 0; rvc_mlx/infer/pipeline_mlx.py:263-373): filtfilt(audio) -> reflect pad t_pad -> RMVPE
+ * -> get_f0 adjustments -> [split at the quietest points near every t_center when the input exceeds
+ * t_max] -> voice_conversion per chunk -> trim t_pad_tgt per side -> concatenate -> change_rms ->
+ * peak-normalise. d_audio [n] fp64 @16 kHz; out fp32 @tgt_sr, n_out samples (cap >=
+ * ((n + 2 t_pad)/160 + n/t_center + 2) * upp is always enough). d_eps_z / d_eps_src (optional)
+ * hold the injected noise of all chunks back to back ([192][T_i] then [T_i * upp] per chunk);
+ * d_f0 (optional) receives the adjusted f0 [1 + (n + 2 t_pad)/160]. The host synchronises the
+ * stream once to read the split points (long inputs only) and once for proposed_pitch. */
+int rvcx_pipeline_ex(rvcx_ctx* ctx, const double* d_audio, int64_t n, const rvcx_pipeline_opts* opts,
+                     const float* d_eps_z, const float* d_eps_src, uint64_t seed, float* d_out, int64_t cap,
+                     int64_t* n_out, double* d_f0, void* stream);
+
+/* Single-chunk shorthand of rvcx_pipeline_ex (t_max = 0, defaults otherwise). */
 int rvcx_pipeline(rvcx_ctx* ctx, const double* d_audio, int64_t n, int sid, double semitones, float protect,
                   int64_t t_pad, int64_t t_pad_tgt, const float* d_eps_z, const float* d_eps_src, uint64_t seed,
                   float* d_out, int64_t cap, int64_t* n_out, double* d_f0, void* stream);

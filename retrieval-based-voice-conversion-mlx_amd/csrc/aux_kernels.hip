@@ -595,6 +595,7 @@ hipError_t nhwc_to_hcw(const float* x, int H, int W, int C, float* y, hipStream_
 
 // ------------------------------------------------------------------ RMVPE decode (RMVPE.py:484-540), fp64 like numpy
 __global__ void k_decode(const float* sal, int F, int ncls, float thred, double* f0) {
+#pragma clang fp contract(off)  // numpy rounds every product and sum separately
   const int f = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (f >= F) return;
@@ -618,17 +619,24 @@ __global__ void k_decode(const float* sal, int F, int ncls, float thred, double*
     }
   }
   if (lane == 0) {
-    double ps = 0.0, ws = 0.0;
-    for (int k = bi - 4; k <= bi + 4; ++k) {
-      if (k < 0 || k >= ncls) continue;
-      const double sv = (double)s[k];
-      const double cm = 20.0 * k + 1997.3794084376191;
-      ps += sv * cm;
-      ws += sv;
+    // numpy reduces each 9-wide row with its pairwise kernel: 8 partials seeded by a[0..7], combined
+    // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then + a[8]. weight_sum stays float32 (salience dtype),
+    // product_sum is float64 (float32 * float64 cents map). Out-of-range slots are the zero padding.
+    float wv[9];
+    double pv[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int k = bi - 4 + j;
+      const bool in = k >= 0 && k < ncls;
+      wv[j] = in ? s[k] : 0.f;
+      pv[j] = in ? (double)wv[j] * (20.0 * k + 1997.3794084376191) : 0.0;
     }
+    const float wsf = (((wv[0] + wv[1]) + (wv[2] + wv[3])) + ((wv[4] + wv[5]) + (wv[6] + wv[7]))) + wv[8];
+    const double ps = (((pv[0] + pv[1]) + (pv[2] + pv[3])) + ((pv[4] + pv[5]) + (pv[6] + pv[7]))) + pv[8];
+    const double ws = (double)wsf;
     double cents = ps / ws;
     if ((double)best <= (double)thred) cents = 0.0;
-    double v = 10.0 * exp2(cents / 1200.0);
+    double v = 10.0 * pow(2.0, cents / 1200.0);
     if (v == 10.0) v = 0.0;
     f0[f] = v;
   }
@@ -640,6 +648,7 @@ hipError_t rmvpe_decode(const float* sal, int F, int ncls, float thred, double* 
 
 // ------------------------------------------------------------------ f0 shift + coarse quantisation (pipeline.py:280-291)
 __global__ void k_f0post(const double* f0, int F, double shift, int32_t* coarse, float* pitchf, double* f0_out) {
+#pragma clang fp contract(off)  // numpy rounds every product and sum separately
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= F) return;
   const double f = f0[i] * shift;
@@ -816,6 +825,148 @@ hipError_t peak_normalize(float* x, long long n, unsigned* ws, hipStream_t s) {
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_absmax, dim3(std::min<long long>(1024, (n + TB - 1) / TB)), dim3(TB), 0, s, x, n, ws);
   hipLaunchKernelGGL(k_peak_scale, dim3(nblocks(n)), dim3(TB), 0, s, x, n, ws);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ get_f0 adjustments
+// Autotune.autotune_f0 (rvc/infer/pipeline.py:151-162): snap to the nearest of 54 note
+// frequencies (first minimum wins, like Python's min()), blend by strength. The rvc/ path snaps
+// every frame (f0 = 0 -> 49 Hz * strength); rvc_mlx (pipeline_mlx.py:72-80) leaves f0 <= 0 alone.
+__constant__ double c_notes[54] = {
+    49.00,  51.91,  55.00,  58.27,  61.74,  65.41,  69.30,  73.42,  77.78,  82.41,  87.31,  92.50,  98.00,  103.83,
+    110.00, 116.54, 123.47, 130.81, 138.59, 146.83, 155.56, 164.81, 174.61, 185.00, 196.00, 207.65, 220.00, 233.08,
+    246.94, 261.63, 277.18, 293.66, 311.13, 329.63, 349.23, 369.99, 392.00, 415.30, 440.00, 466.16, 493.88, 523.25,
+    554.37, 587.33, 622.25, 659.25, 698.46, 739.99, 783.99, 830.61, 880.00, 932.33, 987.77, 1046.50};
+
+__global__ void k_autotune(double* f0, int F, double strength, int skip_unvoiced) {
+#pragma clang fp contract(off)  // numpy rounds every product and sum separately
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= F) return;
+  const double f = f0[i];
+  if (skip_unvoiced && f <= 0.0) return;
+  double best = c_notes[0], bd = fabs(c_notes[0] - f);
+  for (int j = 1; j < 54; ++j) {
+    const double d = fabs(c_notes[j] - f);
+    if (d < bd) {
+      bd = d;
+      best = c_notes[j];
+    }
+  }
+  f0[i] = f + (best - f) * strength;
+}
+hipError_t f0_autotune(double* f0, int F, double strength, int skip_unvoiced, hipStream_t s) {
+  hipLaunchKernelGGL(k_autotune, dim3(nblocks(F)), dim3(TB), 0, s, f0, F, strength, skip_unvoiced);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ long-input split points
+// Pipeline.pipeline opt_ts search (rvc/infer/pipeline.py:440-452): with xp = reflect-pad(x, w/2),
+// audio_sum[p] = sum_{i<w} xp[p+i] accumulated in i order (numpy's `audio_sum += audio_pad[i:i-w]`,
+// so the fp64 result is bit-identical), then for every t = t_center, 2 t_center, ... < n the split
+// is t - t_query + first argmin |audio_sum[t - t_query : t + t_query]|.
+__global__ void k_window_sum(const double* x, long long n, int w, double* sum) {
+  const long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const long long h = w / 2;
+  double acc = 0.0;
+  for (int i = 0; i < w; ++i) {
+    long long q = p + i - h;
+    if (q < 0) q = -q;
+    if (q >= n) q = 2 * (n - 1) - q;
+    acc += x[q];
+  }
+  sum[p] = acc;
+}
+__global__ void k_split_argmin(const double* sum, long long n, long long t_center, long long t_query,
+                               long long* ts) {
+  const long long t = t_center * (blockIdx.x + 1);
+  const long long lo = t - t_query;
+  const long long hi = t + t_query < n ? t + t_query : n;
+  double bv = INFINITY;
+  long long bi = hi;
+  for (long long p = lo + threadIdx.x; p < hi; p += blockDim.x) {
+    const double v = fabs(sum[p]);
+    if (v < bv) {  // ascending p per thread: keeps the first minimum
+      bv = v;
+      bi = p;
+    }
+  }
+  __shared__ double sv[TB];
+  __shared__ long long si[TB];
+  sv[threadIdx.x] = bv;
+  si[threadIdx.x] = bi;
+  __syncthreads();
+  for (int o = TB / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      const double v2 = sv[threadIdx.x + o];
+      const long long i2 = si[threadIdx.x + o];
+      if (v2 < sv[threadIdx.x] || (v2 == sv[threadIdx.x] && i2 < si[threadIdx.x])) {
+        sv[threadIdx.x] = v2;
+        si[threadIdx.x] = i2;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) ts[blockIdx.x] = si[0];
+}
+hipError_t split_points(const double* x, long long n, int window, long long t_center, long long t_query,
+                        double* sum_ws, long long* ts, int nts, hipStream_t s) {
+  hipLaunchKernelGGL(k_window_sum, dim3(nblocks(n)), dim3(TB), 0, s, x, n, window, sum_ws);
+  if (nts > 0) hipLaunchKernelGGL(k_split_argmin, dim3(nts), dim3(TB), 0, s, sum_ws, n, t_center, t_query, ts);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ volume envelope
+// AudioProcessor.change_rms (rvc/infer/pipeline.py:35-82): librosa.feature.rms (center=True, zero pad
+// frame/2, mean |x|^2 per frame, sqrt) of source and target, both linearly interpolated
+// (F.interpolate mode='linear', align_corners=False) to the target length, then
+// y *= rms1^(1-rate) * max(rms2, 1e-6)^(rate-1). One block per RMS frame, fp64 sums.
+template <class T>
+__global__ void k_rms_frames(const T* x, long long n, int frame, int hop, float* rms) {
+  const long long start = (long long)blockIdx.x * hop - frame / 2;
+  double acc = 0.0;
+  for (int j = threadIdx.x; j < frame; j += blockDim.x) {
+    const long long q = start + j;
+    if (q >= 0 && q < n) {
+      const double v = (double)x[q];
+      acc += v * v;
+    }
+  }
+  __shared__ double red[TB];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = TB / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) rms[blockIdx.x] = (float)sqrt(red[0] / frame);
+}
+__device__ __forceinline__ float interp_linear(const float* r, int n_in, long long i, long long n_out) {
+  const float scale = (float)n_in / (float)n_out;
+  float src = scale * ((float)i + 0.5f) - 0.5f;
+  if (src < 0.f) src = 0.f;
+  int i0 = (int)src;
+  if (i0 > n_in - 1) i0 = n_in - 1;
+  const int i1 = i0 + (i0 < n_in - 1 ? 1 : 0);
+  float l1 = src - (float)i0;
+  l1 = fminf(fmaxf(l1, 0.f), 1.f);
+  return (1.f - l1) * r[i0] + l1 * r[i1];
+}
+__global__ void k_apply_rms(float* y, long long n, const float* r1, int n1, const float* r2, int n2, float rate) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float a = interp_linear(r1, n1, i, n);
+    const float b = fmaxf(interp_linear(r2, n2, i, n), 1e-6f);
+    y[i] = y[i] * (powf(a, 1.f - rate) * powf(b, rate - 1.f));
+  }
+}
+int rms_frame_count(long long n, int sr) { return (int)(1 + n / (sr / 2)); }
+hipError_t change_rms(const double* src, long long n_src, int sr_src, float* y, long long n_y, int sr_y, float rate,
+                      float* ws, hipStream_t s) {
+  const int n1 = rms_frame_count(n_src, sr_src), n2 = rms_frame_count(n_y, sr_y);
+  hipLaunchKernelGGL(k_rms_frames<double>, dim3(n1), dim3(TB), 0, s, src, n_src, sr_src / 2 * 2, sr_src / 2, ws);
+  hipLaunchKernelGGL(k_rms_frames<float>, dim3(n2), dim3(TB), 0, s, (const float*)y, n_y, sr_y / 2 * 2, sr_y / 2,
+                     ws + n1);
+  hipLaunchKernelGGL(k_apply_rms, dim3(nblocks(n_y)), dim3(TB), 0, s, y, n_y, ws, n1, ws + n1, n2, rate);
   return hipGetLastError();
 }
 

@@ -182,6 +182,15 @@ int rvcx_rmvpe(rvcx_ctx* ctx, const float* d_audio, int64_t n, float thred, doub
   });
 }
 
+int rvcx_rmvpe_decode(rvcx_ctx* ctx, const float* d_hidden, int64_t F, float thred, double* d_f0, void* stream) {
+  return guard(ctx, [&] {
+    if (!d_hidden || !d_f0 || F < 0) throw Error(RVCX_E_INVALID, "rvcx_rmvpe_decode: bad arguments");
+    if (F == 0) return;
+    set_device(ctx);
+    check(rmvpe_decode(d_hidden, (int)F, 360, thred, d_f0, static_cast<hipStream_t>(stream)), "rmvpe_decode");
+  });
+}
+
 int rvcx_f0_post(rvcx_ctx* ctx, const double* d_f0, int64_t F, double semitones, int32_t* d_coarse, float* d_pitchf,
                  double* d_f0_shifted, void* stream) {
   return guard(ctx, [&] {
@@ -190,6 +199,15 @@ int rvcx_f0_post(rvcx_ctx* ctx, const double* d_f0, int64_t F, double semitones,
     check(f0_post(d_f0, (int)F, std::pow(2.0, semitones / 12.0), d_coarse, d_pitchf, d_f0_shifted,
                   static_cast<hipStream_t>(stream)),
           "f0_post");
+  });
+}
+
+int rvcx_f0_autotune(rvcx_ctx* ctx, double* d_f0, int64_t F, double strength, int skip_unvoiced, void* stream) {
+  return guard(ctx, [&] {
+    if (!d_f0 || F < 0) throw Error(RVCX_E_INVALID, "rvcx_f0_autotune: bad arguments");
+    if (F == 0) return;
+    set_device(ctx);
+    check(f0_autotune(d_f0, (int)F, strength, skip_unvoiced, static_cast<hipStream_t>(stream)), "f0_autotune");
   });
 }
 
@@ -228,27 +246,10 @@ int rvcx_voice_conversion(rvcx_ctx* ctx, const float* d_audio, int64_t n, const 
   return guard(ctx, [&] {
     if (!ctx->ready[0] || !ctx->ready[1]) throw Error(RVCX_E_STATE, "synthesizer/hubert not finalized");
     if (!d_audio || !d_pitch || !d_pitchf || !d_out || n <= 0) throw Error(RVCX_E_INVALID, "bad arguments");
-    if (sid < 0 || sid >= ctx->scfg.n_spk) throw Error(RVCX_E_INVALID, "sid out of range");
     set_device(ctx);
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    const int E = ctx->scfg.emb_dim;
-    // HuBERT frames for n samples (upper bound n/320)
-    const int64_t cap_rows = n / 320 + 8;
-    float* feats = ctx->buf<float>("vc.feats", (size_t)cap_rows * E, s);
-    const int64_t L = hubert_forward(*ctx, d_audio, n, 2, feats, cap_rows, s);
-    const int T = (int)std::min<int64_t>(n / 160, 2 * L);
-    const int upp = ctx->scfg.upp();
-    if ((int64_t)T * upp > cap) throw Error(RVCX_E_CAPACITY, "voice_conversion: output needs " +
-                                                                 std::to_string((int64_t)T * upp) + " samples");
-    float* phone = ctx->buf<float>("vc.phone", (size_t)T * E, s);
-    check(upsample2_protect(feats, (int)L, E, phone, T, protect < 0.5f ? d_pitchf : nullptr, protect, s), "upsample");
-    int32_t* lens = ctx->buf<int32_t>("vc.len", 4, s);
-    int32_t* sids = lens + 1;
-    set_i32(lens, T, s);
-    set_i32(sids, sid, s);
-    synth_forward(*ctx, 1, T, phone, lens, d_pitch, d_pitchf, sids, d_eps_z, d_eps_src, seed, d_out, nullptr,
-                  nullptr, s);
-    if (n_out) *n_out = (int64_t)T * upp;
+    const int64_t no = vc_forward(*ctx, d_audio, n, d_pitch, d_pitchf, n / 160, sid, protect, d_eps_z, d_eps_src,
+                                  seed, d_out, cap, static_cast<hipStream_t>(stream));
+    if (n_out) *n_out = no;
   });
 }
 
@@ -262,13 +263,31 @@ int rvcx_set_highpass(rvcx_ctx* ctx, const double* b, const double* a, const dou
 int rvcx_pipeline(rvcx_ctx* ctx, const double* d_audio, int64_t n, int sid, double semitones, float protect,
                   int64_t t_pad, int64_t t_pad_tgt, const float* d_eps_z, const float* d_eps_src, uint64_t seed,
                   float* d_out, int64_t cap, int64_t* n_out, double* d_f0, void* stream) {
+  rvcx_pipeline_opts o = default_pipeline_opts();
+  o.sid = sid;
+  o.pitch = semitones;
+  o.protect = protect;
+  o.t_pad = t_pad;
+  o.t_pad_tgt = t_pad_tgt;
+  o.t_max = 0;  // single chunk
+  return rvcx_pipeline_ex(ctx, d_audio, n, &o, d_eps_z, d_eps_src, seed, d_out, cap, n_out, d_f0, stream);
+}
+
+int rvcx_pipeline_default_opts(rvcx_pipeline_opts* opts) {
+  if (!opts) return RVCX_E_INVALID;
+  *opts = default_pipeline_opts();
+  return RVCX_OK;
+}
+
+int rvcx_pipeline_ex(rvcx_ctx* ctx, const double* d_audio, int64_t n, const rvcx_pipeline_opts* opts,
+                     const float* d_eps_z, const float* d_eps_src, uint64_t seed, float* d_out, int64_t cap,
+                     int64_t* n_out, double* d_f0, void* stream) {
   return guard(ctx, [&] {
     if (!ctx->ready[0] || !ctx->ready[1] || !ctx->ready[2]) throw Error(RVCX_E_STATE, "models not finalized");
-    if (!d_audio || !d_out || n <= 0 || t_pad < 0 || t_pad_tgt < 0) throw Error(RVCX_E_INVALID, "bad arguments");
-    if (sid < 0 || sid >= ctx->scfg.n_spk) throw Error(RVCX_E_INVALID, "sid out of range");
+    if (!d_audio || !d_out || !opts || n <= 0) throw Error(RVCX_E_INVALID, "bad arguments");
     set_device(ctx);
-    const int64_t no = pipeline_forward(*ctx, d_audio, n, sid, semitones, protect, t_pad, t_pad_tgt, d_eps_z,
-                                        d_eps_src, seed, d_out, cap, d_f0, static_cast<hipStream_t>(stream));
+    const int64_t no = pipeline_forward_ex(*ctx, d_audio, n, *opts, d_eps_z, d_eps_src, seed, d_out, cap, d_f0,
+                                           static_cast<hipStream_t>(stream));
     if (n_out) *n_out = no;
   });
 }

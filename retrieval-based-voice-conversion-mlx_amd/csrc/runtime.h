@@ -79,7 +79,7 @@ struct Ctx {
   std::vector<UpsLayer> ups;
   // pipeline high-pass (rvc/infer/pipeline.py:22-27), normalised so a[0] = 1
   int hp_order = 0;
-  std::vector<double> hp_b, hp_a, hp_zi, hp_FL;
+  std::vector<double> hp_b, hp_a, hp_zi;
   // workspace pool
   std::map<std::string, std::unique_ptr<DevBuf>> ws;
   uint64_t call_counter = 0;
@@ -131,9 +131,14 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
                  const float* eps_src, uint64_t seed, float* out, hipStream_t s);
 
 void set_highpass(Ctx& c, const double* b, const double* a, const double* zi, int order);
-int64_t pipeline_forward(Ctx& c, const double* audio, int64_t n, int sid, double semitones, float protect,
-                         int64_t t_pad, int64_t t_pad_tgt, const float* eps_z, const float* eps_src, uint64_t seed,
-                         float* out, int64_t cap, double* f0_out, hipStream_t s);
+int hubert_version_for(const Ctx& c);
+int64_t vc_forward(Ctx& c, const float* audio, int64_t n, const int32_t* pitch, const float* pitchf,
+                   int64_t pitch_len, int sid, float protect, const float* eps_z, const float* eps_src, uint64_t seed,
+                   float* out, int64_t cap, hipStream_t s);
+int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_pipeline_opts& o,
+                            const float* eps_z, const float* eps_src, uint64_t seed, float* out, int64_t cap,
+                            double* f0_out, hipStream_t s);
+rvcx_pipeline_opts default_pipeline_opts();
 void set_i32(int32_t* p, int32_t v, hipStream_t s);
 // launch one implicit-GEMM conv (1-D or 2-D) with optional event timing; flops = algorithmic FLOPs
 void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double flops = -1.0);

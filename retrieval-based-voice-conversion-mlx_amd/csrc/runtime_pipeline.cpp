@@ -1,6 +1,12 @@
-// Whole-utterance pipeline on device (Pipeline.pipeline, rvc/infer/pipeline.py:390-558, single-chunk
-// case audio_pad <= t_max; rvc_mlx/infer/pipeline_mlx.py:263-373): filtfilt -> reflect pad -> RMVPE ->
-// f0 post -> HuBERT -> x2 upsample + protect -> Synthesizer.infer -> trim -> peak normalise.
+// Whole-utterance pipeline on device: Pipeline.pipeline (rvc/infer/pipeline.py:390-558;
+// rvc_mlx/infer/pipeline_mlx.py:263-373) = filtfilt -> reflect pad -> RMVPE -> get_f0 adjustments ->
+// [split at quiet points when longer than t_max] -> per chunk HuBERT -> x2 upsample + protect ->
+// Synthesizer.infer -> trim -> concatenate -> change_rms -> peak normalise.
+//
+// Everything that touches samples runs as HIP kernels on the caller's stream. The host only plans:
+// it reads back the split points (long inputs) and, for proposed_pitch, the f0 track whose median
+// sets the key offset (pipeline.py:250-277) -- both are a few KB and need one stream sync each.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 
@@ -10,6 +16,7 @@ namespace rvcx {
 
 void set_highpass(Ctx& c, const double* b, const double* a, const double* zi, int order) {
   if (order < 1 || order > IIR_MAXO) throw Error(RVCX_E_INVALID, "highpass order out of range");
+  if (!(a[0] != 0.0)) throw Error(RVCX_E_INVALID, "highpass a[0] == 0");
   c.hp_order = order;
   c.hp_b.assign(b, b + order + 1);
   c.hp_a.assign(a, a + order + 1);
@@ -17,65 +24,182 @@ void set_highpass(Ctx& c, const double* b, const double* a, const double* zi, in
   const double a0 = a[0];
   for (auto& v : c.hp_b) v /= a0;
   for (auto& v : c.hp_a) v /= a0;
-  // state transition of DF2T with zero input: z'_i = z_{i+1} - a_{i+1} z_0 ; F^L for chunk length 256
-  std::vector<double> F(IIR_MAXO * IIR_MAXO, 0.0), P(IIR_MAXO * IIR_MAXO, 0.0), T(IIR_MAXO * IIR_MAXO);
-  for (int i = 0; i < order; ++i) {
-    F[i * IIR_MAXO + 0] = -c.hp_a[i + 1];
-    if (i + 1 < order) F[i * IIR_MAXO + i + 1] += 1.0;
-  }
-  for (int i = 0; i < order; ++i) P[i * IIR_MAXO + i] = 1.0;
-  for (int step = 0; step < 256; ++step) {
-    std::fill(T.begin(), T.end(), 0.0);
-    for (int i = 0; i < order; ++i)
-      for (int k = 0; k < order; ++k) {
-        double acc = 0.0;
-        for (int j = 0; j < order; ++j) acc += F[i * IIR_MAXO + j] * P[j * IIR_MAXO + k];
-        T[i * IIR_MAXO + k] = acc;
-      }
-    P = T;
-  }
-  c.hp_FL = P;
 }
 
-int64_t pipeline_forward(Ctx& c, const double* audio, int64_t n, int sid, double semitones, float protect,
-                         int64_t t_pad, int64_t t_pad_tgt, const float* eps_z, const float* eps_src, uint64_t seed,
-                         float* out, int64_t cap, double* f0_out, hipStream_t s) {
-  if (c.hp_order == 0) throw Error(RVCX_E_STATE, "pipeline: high-pass filter not configured");
-  const int64_t m = n + 2 * t_pad;
-  float* pad32 = c.buf<float>("pl.pad32", (size_t)m, s);
-  double* ws = c.buf<double>("pl.iirws", filtfilt_ws_doubles(n, c.hp_order), s);
-  check(filtfilt_pad(audio, n, c.hp_b.data(), c.hp_a.data(), c.hp_zi.data(), c.hp_FL.data(), c.hp_order, t_pad, ws,
-                     nullptr, pad32, s),
-        "filtfilt_pad");
-  const int64_t F = 1 + m / 160;
-  const int64_t p_len = m / 160;
-  double* f0 = c.buf<double>("pl.f0", (size_t)F, s);
-  rmvpe_forward(c, pad32, m, 0.03f, f0, F, nullptr, s);
-  int32_t* pitch = c.buf<int32_t>("pl.pitch", (size_t)p_len, s);
-  float* pitchf = c.buf<float>("pl.pitchf", (size_t)p_len, s);
-  check(f0_post(f0, (int)p_len, std::pow(2.0, semitones / 12.0), pitch, pitchf, f0_out, s), "f0_post");
-  // HuBERT -> upsample/protect -> synth
+int hubert_version_for(const Ctx& c) { return c.scfg.emb_dim == 256 ? 1 : 2; }
+
+int64_t vc_forward(Ctx& c, const float* audio, int64_t n, const int32_t* pitch, const float* pitchf,
+                   int64_t pitch_len, int sid, float protect, const float* eps_z, const float* eps_src, uint64_t seed,
+                   float* out, int64_t cap, hipStream_t s) {
+  if (sid < 0 || sid >= c.scfg.n_spk) throw Error(RVCX_E_INVALID, "sid out of range");
   const int E = c.scfg.emb_dim;
-  const int64_t cap_rows = m / 320 + 8;
+  const int64_t cap_rows = n / 320 + 8;  // HuBERT frames for n samples (upper bound n/320)
   float* feats = c.buf<float>("vc.feats", (size_t)cap_rows * E, s);
-  const int64_t L = hubert_forward(c, pad32, m, 2, feats, cap_rows, s);
-  const int T = (int)std::min<int64_t>(p_len, 2 * L);
+  const int64_t L = hubert_forward(c, audio, n, hubert_version_for(c), feats, cap_rows, s);
+  const int T = (int)std::min<int64_t>(n / 160, 2 * L);
+  if (T <= 0) throw Error(RVCX_E_SHAPE, "voice_conversion: input shorter than one frame");
+  if (T > pitch_len) throw Error(RVCX_E_SHAPE, "voice_conversion: pitch track shorter than the features");
   const int upp = c.scfg.upp();
-  const int64_t nvc = (int64_t)T * upp;
-  const int64_t nout = nvc - 2 * t_pad_tgt;
-  if (nout <= 0) throw Error(RVCX_E_SHAPE, "pipeline: input too short for the padding");
-  if (nout > cap) throw Error(RVCX_E_CAPACITY, "pipeline: output needs " + std::to_string(nout) + " samples");
+  if ((int64_t)T * upp > cap)
+    throw Error(RVCX_E_CAPACITY, "voice_conversion: output needs " + std::to_string((int64_t)T * upp) + " samples");
   float* phone = c.buf<float>("vc.phone", (size_t)T * E, s);
   check(upsample2_protect(feats, (int)L, E, phone, T, protect < 0.5f ? pitchf : nullptr, protect, s), "upsample");
   int32_t* lens = c.buf<int32_t>("vc.len", 4, s);
   set_i32(lens, T, s);
   set_i32(lens + 1, sid, s);
-  float* vc = c.buf<float>("pl.vc", (size_t)nvc, s);
-  synth_forward(c, 1, T, phone, lens, pitch, pitchf, lens + 1, eps_z, eps_src, seed, vc, nullptr, nullptr, s);
-  RVCX_HIP(hipMemcpyAsync(out, vc + t_pad_tgt, (size_t)nout * sizeof(float), hipMemcpyDeviceToDevice, s));
+  synth_forward(c, 1, T, phone, lens, pitch, pitchf, lens + 1, eps_z, eps_src, seed, out, nullptr, nullptr, s);
+  return (int64_t)T * upp;
+}
+
+namespace {
+
+// key offset of proposed_pitch (pipeline.py:250-277): median of the voiced-interpolated track
+int proposed_key(const std::vector<double>& f0, double threshold) {
+  std::vector<int64_t> valid;
+  for (size_t i = 0; i < f0.size(); ++i)
+    if (f0[i] > 0) valid.push_back((int64_t)i);
+  if (valid.size() < 2) return 0;
+  // np.interp(arange(F), valid, f0[valid]): clamps outside [valid[0], valid[-1]]
+  std::vector<double> v(f0.size());
+  size_t k = 0;
+  for (size_t i = 0; i < f0.size(); ++i) {
+    const int64_t x = (int64_t)i;
+    if (x <= valid.front()) {
+      v[i] = f0[valid.front()];
+    } else if (x >= valid.back()) {
+      v[i] = f0[valid.back()];
+    } else {
+      while (valid[k + 1] < x) ++k;
+      const double x0 = (double)valid[k], x1 = (double)valid[k + 1];
+      const double y0 = f0[valid[k]], y1 = f0[valid[k + 1]];
+      v[i] = (x == valid[k + 1]) ? y1 : y0 + (y1 - y0) * ((double)x - x0) / (x1 - x0);
+    }
+  }
+  std::sort(v.begin(), v.end());
+  const size_t m = v.size();
+  const double med = (m & 1) ? v[m / 2] : 0.5 * (v[m / 2 - 1] + v[m / 2]);
+  if (!(med > 0)) return 0;
+  const double key = std::nearbyint(12.0 * std::log2(threshold / med));  // np.round: half to even
+  return (int)std::max(-12.0, std::min(12.0, key));
+}
+
+}  // namespace
+
+int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_pipeline_opts& o,
+                            const float* eps_z, const float* eps_src, uint64_t seed, float* out, int64_t cap,
+                            double* f0_out, hipStream_t s) {
+  if (c.hp_order == 0) throw Error(RVCX_E_STATE, "pipeline: high-pass filter not configured");
+  if (o.t_pad < 0 || o.t_pad_tgt < 0 || o.t_pad >= n) throw Error(RVCX_E_INVALID, "pipeline: bad t_pad");
+  if (o.version != 0 && o.version != hubert_version_for(c))
+    throw Error(RVCX_E_INVALID, "pipeline: version does not match the synthesizer's embedding width");
+  const int64_t W = 160;  // Pipeline.window
+  const int64_t m = n + 2 * o.t_pad;
+  // 1. zero-phase high-pass, reflect pad t_pad (pipeline.py:439, :459); fp64 copy kept for the split
+  //    search and the RMS envelope, fp32 copy feeds the models (torch.from_numpy(...).float()).
+  float* pad32 = c.buf<float>("pl.pad32", (size_t)m, s);
+  double* pad64 = c.buf<double>("pl.pad64", (size_t)m, s);
+  double* ws = c.buf<double>("pl.iirws", filtfilt_ws_doubles(n, c.hp_order), s);
+  check(filtfilt_pad(audio, n, c.hp_b.data(), c.hp_a.data(), c.hp_zi.data(), nullptr, c.hp_order, o.t_pad, ws, pad64,
+                     pad32, s),
+        "filtfilt_pad");
+  const double* filtered = pad64 + o.t_pad;
+  // 2. split points for inputs longer than t_max (pipeline.py:440-452)
+  std::vector<int64_t> opt_ts;
+  if (o.t_max > 0 && n + W > o.t_max && o.t_center > 0) {
+    if (o.t_query <= 0 || o.t_query > o.t_center) throw Error(RVCX_E_INVALID, "pipeline: bad t_query/t_center");
+    const int nts = n > o.t_center ? (int)((n - 1 - o.t_center) / o.t_center + 1) : 0;
+    double* sum = c.buf<double>("pl.winsum", (size_t)n, s);
+    long long* dts = c.buf<long long>("pl.ts", (size_t)std::max(1, nts), s);
+    check(split_points(filtered, n, (int)W, o.t_center, o.t_query, sum, dts, nts, s), "split_points");
+    opt_ts.resize(nts);
+    if (nts > 0) {
+      RVCX_HIP(hipMemcpyAsync(opt_ts.data(), dts, sizeof(long long) * nts, hipMemcpyDeviceToHost, s));
+      RVCX_HIP(hipStreamSynchronize(s));
+    }
+  }
+  // 3. f0 over the whole padded input (pipeline.py:462-472) + get_f0 adjustments (:248-291)
+  const int64_t F = 1 + m / W;
+  const int64_t p_len = m / W;
+  double* f0 = c.buf<double>("pl.f0", (size_t)F, s);
+  rmvpe_forward(c, pad32, m, o.rmvpe_threshold > 0 ? o.rmvpe_threshold : 0.03f, f0, F, nullptr, s);
+  double shift_semitones = o.pitch;
+  if (o.f0_autotune) {
+    check(f0_autotune(f0, (int)F, o.f0_autotune_strength, o.mlx_semantics ? 1 : 0, s), "f0_autotune");
+    if (!o.mlx_semantics) shift_semitones = 0.0;  // rvc/: autotune replaces the shift (pipeline.py:248-279)
+  } else if (o.proposed_pitch) {
+    std::vector<double> h(F);
+    RVCX_HIP(hipMemcpyAsync(h.data(), f0, sizeof(double) * F, hipMemcpyDeviceToHost, s));
+    RVCX_HIP(hipStreamSynchronize(s));
+    shift_semitones = o.pitch + proposed_key(h, o.proposed_pitch_threshold);
+  }
+  int32_t* pitch = c.buf<int32_t>("pl.pitch", (size_t)F, s);
+  float* pitchf = c.buf<float>("pl.pitchf", (size_t)F, s);
+  check(f0_post(f0, (int)F, std::pow(2.0, shift_semitones / 12.0), pitch, pitchf, f0_out, s), "f0_post");
+  // 4. voice conversion per chunk (pipeline.py:486-512), outputs trimmed t_pad_tgt per side
+  const int upp = c.scfg.upp();
+  const int I = c.scfg.I;
+  int64_t written = 0, ez_off = 0, es_off = 0;
+  int64_t st = 0;
+  auto chunk = [&](int64_t a0, int64_t a1, int64_t f_lo, int64_t f_hi, uint64_t cseed) {
+    const int64_t len = a1 - a0;
+    const int64_t cap_vc = (len / W) * upp;
+    float* vc = c.buf<float>("pl.vc", (size_t)std::max<int64_t>(cap_vc, 1), s);
+    // pitch[:, f_lo:f_hi], then [:p_len] inside voice_conversion with p_len = min(len/160, 2L)
+    const int64_t nvc = vc_forward(c, pad32 + a0, len, pitch + f_lo, pitchf + f_lo, f_hi - f_lo, o.sid, o.protect,
+                                   eps_z ? eps_z + ez_off : nullptr, eps_src ? eps_src + es_off : nullptr, cseed, vc,
+                                   cap_vc, s);
+    const int64_t T = nvc / upp;
+    ez_off += (int64_t)I * T;
+    es_off += nvc;
+    const int64_t keep = nvc - 2 * o.t_pad_tgt;
+    if (keep <= 0) throw Error(RVCX_E_SHAPE, "pipeline: chunk too short for the padding");
+    if (written + keep > cap)
+      throw Error(RVCX_E_CAPACITY, "pipeline: output needs more than " + std::to_string(cap) + " samples");
+    RVCX_HIP(hipMemcpyAsync(out + written, vc + o.t_pad_tgt, (size_t)keep * sizeof(float), hipMemcpyDeviceToDevice,
+                            s));
+    written += keep;
+  };
+  uint64_t cseed = seed;
+  const int64_t t_pad2 = 2 * o.t_pad;
+  bool have_t = false;
+  int64_t t = 0;
+  for (int64_t t_raw : opt_ts) {
+    t = t_raw / W * W;
+    chunk(st, std::min(m, t + t_pad2 + W), st / W, (t + t_pad2) / W, cseed);
+    cseed += 0x9E3779B97F4A7C15ull;
+    st = t;
+    have_t = true;
+  }
+  if (have_t)
+    chunk(t, m, t / W, p_len, cseed);
+  else
+    chunk(0, m, 0, p_len, cseed);
+  // 5. volume envelope (pipeline.py:545-549) and peak normalisation (:550-552)
+  if (o.volume_envelope != 1.0) {
+    const int n1 = rms_frame_count(n, 16000), n2 = rms_frame_count(written, c.scfg.sr);
+    float* rws = c.buf<float>("pl.rms", (size_t)(n1 + n2), s);
+    check(change_rms(filtered, n, 16000, out, written, c.scfg.sr, (float)o.volume_envelope, rws, s), "change_rms");
+  }
   unsigned* mx = c.buf<unsigned>("pl.max", 4, s);
-  check(peak_normalize(out, nout, mx, s), "peak_normalize");
-  return nout;
+  check(peak_normalize(out, written, mx, s), "peak_normalize");
+  return written;
+}
+
+rvcx_pipeline_opts default_pipeline_opts() {
+  rvcx_pipeline_opts o;
+  std::memset(&o, 0, sizeof(o));
+  o.version = 0;
+  o.protect = 0.33f;
+  o.rmvpe_threshold = 0.03f;
+  o.t_pad = 16000;
+  o.t_pad_tgt = 48000;
+  o.t_query = 16000 * 6;
+  o.t_center = 16000 * 38;
+  o.t_max = 16000 * 41;
+  o.f0_autotune_strength = 1.0;
+  o.proposed_pitch_threshold = 155.0;
+  o.volume_envelope = 1.0;
+  return o;
 }
 
 }  // namespace rvcx

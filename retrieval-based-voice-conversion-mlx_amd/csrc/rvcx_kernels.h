@@ -151,5 +151,12 @@ hipError_t filtfilt_pad(const double* x, long long n, const double* b, const dou
                         hipStream_t s);
 size_t filtfilt_ws_doubles(long long n, int order);
 hipError_t peak_normalize(float* x, long long n, unsigned* ws, hipStream_t s);
+// Pipeline.get_f0 / Pipeline.pipeline host DSP moved on device (aux_kernels.hip)
+hipError_t f0_autotune(double* f0, int F, double strength, int skip_unvoiced, hipStream_t s);
+hipError_t split_points(const double* x, long long n, int window, long long t_center, long long t_query,
+                        double* sum_ws, long long* ts, int nts, hipStream_t s);
+int rms_frame_count(long long n, int sr);
+hipError_t change_rms(const double* src, long long n_src, int sr_src, float* y, long long n_y, int sr_y, float rate,
+                      float* ws, hipStream_t s);
 
 }  // namespace rvcx

@@ -22,7 +22,8 @@ STATUS = {
 EXPORTS = [
     "rvcx_create", "rvcx_destroy", "rvcx_last_error", "rvcx_set_synth_config", "rvcx_upload", "rvcx_finalize",
     "rvcx_hubert", "rvcx_rmvpe", "rvcx_f0_post", "rvcx_synth_infer", "rvcx_dec_only", "rvcx_voice_conversion",
-    "rvcx_synth_upp", "rvcx_set_highpass", "rvcx_pipeline", "rvcx_profile", "rvcx_profile_read",
+    "rvcx_synth_upp", "rvcx_set_highpass", "rvcx_pipeline", "rvcx_pipeline_default_opts", "rvcx_pipeline_ex",
+    "rvcx_f0_autotune", "rvcx_rmvpe_decode", "rvcx_profile", "rvcx_profile_read",
 ]
 
 
@@ -46,6 +47,18 @@ class SynthDesc(ctypes.Structure):
         ("upsample_initial_channel", ctypes.c_int), ("upsample_kernel_sizes", ctypes.c_int * 8),
         ("spk_embed_dim", ctypes.c_int), ("gin_channels", ctypes.c_int), ("sr", ctypes.c_int),
         ("text_enc_hidden_dim", ctypes.c_int),
+    ]
+
+
+class PipelineOpts(ctypes.Structure):
+    """rvcx_pipeline_opts (include/rvcx.h)."""
+    _fields_ = [
+        ("sid", ctypes.c_int), ("version", ctypes.c_int), ("pitch", ctypes.c_double), ("protect", ctypes.c_float),
+        ("rmvpe_threshold", ctypes.c_float), ("t_pad", ctypes.c_int64), ("t_pad_tgt", ctypes.c_int64),
+        ("t_query", ctypes.c_int64), ("t_center", ctypes.c_int64), ("t_max", ctypes.c_int64),
+        ("f0_autotune", ctypes.c_int), ("f0_autotune_strength", ctypes.c_double), ("proposed_pitch", ctypes.c_int),
+        ("proposed_pitch_threshold", ctypes.c_double), ("volume_envelope", ctypes.c_double),
+        ("mlx_semantics", ctypes.c_int),
     ]
 
 
@@ -86,6 +99,10 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "rvcx_profile": (i32, [vp, i32]),
         "rvcx_profile_read": (i32, [vp, P(f64), P(f64), P(i64)]),
         "rvcx_pipeline": (i32, [vp, vp, i64, i32, f64, f32, i64, i64, vp, vp, u64, vp, i64, P(i64), vp, vp]),
+        "rvcx_pipeline_default_opts": (i32, [P(PipelineOpts)]),
+        "rvcx_pipeline_ex": (i32, [vp, vp, i64, P(PipelineOpts), vp, vp, u64, vp, i64, P(i64), vp, vp]),
+        "rvcx_f0_autotune": (i32, [vp, vp, i64, f64, i32, vp]),
+        "rvcx_rmvpe_decode": (i32, [vp, vp, i64, f32, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -142,6 +142,15 @@ class Engine:
                                         _ptr(hid), self.stream()), "rmvpe")
         return (f0, hid) if want_hidden else f0
 
+    def rmvpe_decode(self, hidden, thred: float = 0.03):
+        """RMVPE0Predictor.decode on device: salience [F, 360] -> f0 fp64 [F]."""
+        t = self.torch
+        h = self._dev(hidden, t.float32).reshape(-1, 360)
+        f0 = t.empty((h.shape[0],), dtype=t.float64, device=self.device)
+        self._check(self.lib.rvcx_rmvpe_decode(self.ctx, h.data_ptr(), h.shape[0], float(thred), f0.data_ptr(),
+                                               self.stream()), "rmvpe_decode")
+        return f0
+
     def f0_post(self, f0, semitones: float):
         """Pitch shift + coarse quantisation on device: (coarse int32, pitchf fp32, f0 fp64)."""
         t = self.torch
@@ -237,6 +246,47 @@ class Engine:
                                            ctypes.byref(no), _ptr(f0), self.stream()), "pipeline")
         res = out[: no.value]
         return (res, f0) if want_f0 else res
+
+    def pipeline_opts(self, **kw) -> "_lib.PipelineOpts":
+        """rvcx_pipeline_opts with the C defaults, overridden by keyword (field names of the struct)."""
+        o = _lib.PipelineOpts()
+        self.lib.rvcx_pipeline_default_opts(ctypes.byref(o))
+        names = {f[0] for f in _lib.PipelineOpts._fields_}
+        for k, v in kw.items():
+            if k not in names:
+                raise TypeError(f"unknown pipeline option {k!r}")
+            setattr(o, k, v)
+        return o
+
+    def pipeline_ex(self, audio, opts: "_lib.PipelineOpts", eps_z=None, eps_src=None, seed: int = 0, out=None,
+                    want_f0: bool = False):
+        """Pipeline.pipeline on device with long-input splitting, f0 adjustments and volume envelope.
+        audio: fp64 [n] @16 kHz. Returns fp32 [n_out] on device (and the adjusted f0 when want_f0)."""
+        t = self.torch
+        a = self._dev(audio, t.float64).reshape(-1)
+        n = a.numel()
+        m = n + 2 * int(opts.t_pad)
+        n_split = n // int(opts.t_center) if opts.t_max > 0 and opts.t_center > 0 else 0
+        cap = (m // 160 + n_split + 2) * self.upp
+        if out is None or out.numel() < cap:
+            out = t.empty((cap,), dtype=t.float32, device=self.device)
+        f0 = t.empty((1 + m // 160,), dtype=t.float64, device=self.device) if want_f0 else None
+        no = ctypes.c_int64(0)
+        ez = None if eps_z is None else self._dev(eps_z, t.float32)
+        es = None if eps_src is None else self._dev(eps_src, t.float32)
+        self._check(self.lib.rvcx_pipeline_ex(self.ctx, a.data_ptr(), n, ctypes.byref(opts), _ptr(ez), _ptr(es),
+                                              ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), out.data_ptr(), out.numel(),
+                                              ctypes.byref(no), _ptr(f0), self.stream()), "pipeline_ex")
+        res = out[: no.value]
+        return (res, f0) if want_f0 else res
+
+    def f0_autotune(self, f0, strength: float = 1.0, skip_unvoiced: bool = False):
+        """Autotune.autotune_f0 on device; returns a new fp64 tensor."""
+        t = self.torch
+        f = self._dev(f0, t.float64).reshape(-1).clone()
+        self._check(self.lib.rvcx_f0_autotune(self.ctx, f.data_ptr(), f.numel(), float(strength),
+                                              1 if skip_unvoiced else 0, self.stream()), "f0_autotune")
+        return f
 
     # ------------------------------------------------------------------ kernel timing
     def profile(self, enable: bool):

@@ -1,0 +1,163 @@
+"""PipelineMLX-compatible conversion pipeline on MI355X.
+
+Mirrors the plugin surface of rvc_mlx/infer/pipeline_mlx.py (PipelineMLX, :84-373) and the
+semantics of its PyTorch oracle rvc/infer/pipeline.py (Pipeline, :165-558): same constructor,
+same ``pipeline`` / ``get_f0`` / ``voice_conversion`` signatures, numpy in and out. The work
+runs in librvcx.so on the GPU (see include/rvcx.h); this module only converts arguments.
+
+Semantics: ``semantics="rvc"`` (default) follows rvc/infer/pipeline.py -- t_pad = x_pad * 16000,
+autotune replaces the pitch shift, long inputs are split at quiet points (x_query/x_center/x_max).
+``semantics="mlx"`` applies the two documented deltas of the MLX port that are pure pipeline
+policy: t_pad forced to 1600 samples (pipeline_mlx.py:318) and the MLX get_f0 order (autotune
+skips f0 <= 0, then the shift is applied; pipeline_mlx.py:142-147). Differences the reference
+marks as port bugs (zeroed flow noise, no opt_ts split) are not reproduced.
+
+Errors raise (the reference prints and continues, pipeline_mlx.py:280-281).
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import numpy as np
+
+from .models import HubertModel, RMVPE0Predictor, Synthesizer, _np
+
+
+class Config:
+    """rvc_mlx/configs/config.py:7-20 (x_pad, x_query, x_center, x_max in seconds)."""
+
+    def __init__(self, x_pad=1, x_query=6, x_center=38, x_max=41):
+        self.device = "rocm"
+        self.gpu_name = "AMD Instinct MI355X"
+        self.x_pad, self.x_query, self.x_center, self.x_max = x_pad, x_query, x_center, x_max
+        self.is_half = False
+
+    def device_config(self):
+        return self.x_pad, self.x_query, self.x_center, self.x_max
+
+
+class PipelineRVCX:
+    SUPPORTED_F0_METHODS = ("rmvpe",)
+
+    def __init__(self, tgt_sr, config, hubert_model: Optional[HubertModel] = None,
+                 rmvpe_model: Optional[RMVPE0Predictor] = None, f0_method: str = "rmvpe", semantics: str = "rvc"):
+        if semantics not in ("rvc", "mlx"):
+            raise ValueError("semantics must be 'rvc' or 'mlx'")
+        self.x_pad, self.x_query, self.x_center, self.x_max = config.x_pad, config.x_query, config.x_center, \
+            config.x_max
+        self.sample_rate = 16000
+        self.tgt_sr = int(tgt_sr)
+        self.window = 160
+        self.t_pad = int(self.sample_rate * self.x_pad)
+        self.t_pad_tgt = int(self.tgt_sr * self.x_pad)
+        self.t_pad2 = self.t_pad * 2
+        self.t_query = int(self.sample_rate * self.x_query)
+        self.t_center = int(self.sample_rate * self.x_center)
+        self.t_max = int(self.sample_rate * self.x_max)
+        self.time_step = self.window / self.sample_rate * 1000
+        self.f0_min, self.f0_max = 50, 1100
+        self.f0_mel_min = 1127 * np.log(1 + self.f0_min / 700)
+        self.f0_mel_max = 1127 * np.log(1 + self.f0_max / 700)
+        self.hubert_model = hubert_model
+        self.rmvpe_model = rmvpe_model
+        self.semantics = semantics
+        self._check_method(f0_method)
+        self._f0_method = f0_method
+        self.engine = (hubert_model or rmvpe_model).engine if (hubert_model or rmvpe_model) else None
+        self.last_f0 = None
+
+    # ------------------------------------------------------------------ helpers
+    def _check_method(self, m):
+        if m not in self.SUPPORTED_F0_METHODS:
+            raise ValueError(f"f0_method {m!r} is not supported on this path (supported: {self.SUPPORTED_F0_METHODS})")
+
+    def _engine(self, *models):
+        for mdl in models + (self.hubert_model, self.rmvpe_model):
+            if mdl is not None and getattr(mdl, "engine", None) is not None:
+                return mdl.engine
+        if self.engine is None:
+            raise RuntimeError("no rvcx Engine: pass models created by rvcx.infer (HubertModel/RMVPE0Predictor)")
+        return self.engine
+
+    def _ensure_highpass(self, eng):
+        if getattr(eng, "_hp", None) is None:
+            from scipy import signal
+
+            # pipeline.py:22-27: signal.butter(N=5, Wn=48, btype="high", fs=16000)
+            b, a = signal.butter(N=5, Wn=48, btype="high", fs=self.sample_rate)
+            eng.set_highpass(b, a, signal.lfilter_zi(b, a))
+
+    # ------------------------------------------------------------------ API (pipeline_mlx.py:135-373)
+    def get_f0(self, x, p_len, f0_method="rmvpe", pitch=0, f0_autotune=False, f0_autotune_strength=1.0,
+               proposed_pitch=False, proposed_pitch_threshold=155.0):
+        """-> (f0_coarse int64 [F], f0 float64 [F]) with F = 1 + len(x)//160 (pipeline.py:200-291)."""
+        self._check_method(f0_method)
+        eng = self._engine()
+        f0 = eng.rmvpe(np.asarray(x, dtype=np.float32).reshape(-1), 0.03)
+        shift = float(pitch)
+        if f0_autotune:
+            f0 = eng.f0_autotune(f0, f0_autotune_strength, skip_unvoiced=self.semantics == "mlx")
+            if self.semantics == "rvc":
+                shift = 0.0
+        elif proposed_pitch and self.semantics == "rvc":
+            shift += proposed_key(f0.cpu().numpy(), proposed_pitch_threshold)
+        coarse, _, fs = eng.f0_post(f0, shift)
+        return coarse.cpu().numpy().astype(np.int64), fs.cpu().numpy()
+
+    def voice_conversion(self, model, net_g, sid, audio0, pitch, pitchf, index=None, big_npy=None, index_rate=0.0,
+                         version="v2", protect=0.33, eps_z=None, eps_src=None, seed: int = 0):
+        """One padded chunk: HuBERT -> x2 -> protect -> Synthesizer.infer. -> float32 [p_len * upp]."""
+        if index is not None and index_rate > 0:
+            raise NotImplementedError("feature index retrieval (index_rate > 0) is not available in this build")
+        if pitch is None or pitchf is None:
+            raise NotImplementedError("models without pitch guidance (f0 = 0) are not supported")
+        eng = self._engine(model)
+        out = eng.voice_conversion(np.asarray(audio0, dtype=np.float32).reshape(-1), _np(pitch).reshape(-1),
+                                   _np(pitchf).reshape(-1), int(_np(sid).reshape(-1)[0]), float(protect),
+                                   eps_z=eps_z, eps_src=eps_src, seed=seed)
+        return out.cpu().numpy()
+
+    def pipeline(self, model, net_g, sid, audio, pitch=0, f0_method="rmvpe", file_index=None, index_rate=0.0,
+                 pitch_guidance=True, volume_envelope=1.0, version="v2", protect=0.33, f0_autotune=False,
+                 f0_autotune_strength=1.0, proposed_pitch=False, proposed_pitch_threshold=155.0, eps_z=None,
+                 eps_src=None, seed: int = 0):
+        """Whole utterance -> float32 [N_out] @tgt_sr (pipeline.py:390-558)."""
+        self._check_method(f0_method)
+        if file_index and index_rate > 0:
+            if not os.path.exists(file_index):
+                raise FileNotFoundError(file_index)
+            raise NotImplementedError("feature index retrieval (index_rate > 0) is not available in this build")
+        if not pitch_guidance:
+            raise NotImplementedError("models without pitch guidance (f0 = 0) are not supported")
+        eng = self._engine(model)
+        self._ensure_highpass(eng)
+        mlx = self.semantics == "mlx"
+        t_pad = 1600 if mlx else self.t_pad
+        t_pad_tgt = int(t_pad * self.tgt_sr / self.sample_rate) if mlx else self.t_pad_tgt
+        opts = eng.pipeline_opts(
+            sid=int(_np(sid).reshape(-1)[0]), version={"v1": 1, "v2": 2}.get(version, 0), pitch=float(pitch),
+            protect=float(protect), t_pad=t_pad, t_pad_tgt=t_pad_tgt, t_query=self.t_query,
+            t_center=self.t_center, t_max=0 if mlx else self.t_max, f0_autotune=int(bool(f0_autotune)),
+            f0_autotune_strength=float(f0_autotune_strength),
+            proposed_pitch=int(bool(proposed_pitch) and not mlx),
+            proposed_pitch_threshold=float(proposed_pitch_threshold), volume_envelope=float(volume_envelope),
+            mlx_semantics=int(mlx))
+        y, f0 = eng.pipeline_ex(np.asarray(audio, dtype=np.float64).reshape(-1), opts, eps_z=eps_z,
+                                eps_src=eps_src, seed=seed, want_f0=True)
+        self.last_f0 = f0
+        return y.cpu().numpy()
+
+
+PipelineMLX = PipelineRVCX
+
+
+def proposed_key(f0: np.ndarray, threshold: float, limit: int = 12) -> int:
+    """Key offset of proposed_pitch (rvc/infer/pipeline.py:250-277)."""
+    valid = np.where(f0 > 0)[0]
+    if len(valid) < 2:
+        return 0
+    med = float(np.median(np.interp(np.arange(len(f0)), valid, f0[valid])))
+    if med <= 0 or np.isnan(med):
+        return 0
+    return max(-limit, min(limit, int(np.round(12 * np.log2(threshold / med)))))

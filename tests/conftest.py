@@ -45,3 +45,17 @@ def rmvpe_w():
     from rvcx.weights import normalize_state
 
     return normalize_state(synthetic.rmvpe_state(5))
+
+
+@pytest.fixture(scope="session")
+def engine(synth_w, hubert_w, rmvpe_w):
+    """One device context with the seeded synthetic weights (GPU tests only)."""
+    from rvcx.config import SYNTH_48K_V2
+    from rvcx.engine import Engine
+
+    e = Engine(0)
+    e.load_synth(synth_w, SYNTH_48K_V2)
+    e.load_hubert(hubert_w)
+    e.load_rmvpe(rmvpe_w)
+    yield e
+    e.close()
