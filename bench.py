@@ -37,6 +37,9 @@ def parse():
     ap.add_argument("--samples", type=int, default=C2_SAMPLES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-sec", type=float, default=2.0)
+    ap.add_argument("--roofline-pass", choices=["inline", "after"], default="after",
+                    help="inline: HIP events around every conv launch of the timed steps; after: the timed steps "
+                         "run without events and an identical K-step pass right after carries them")
     return ap.parse_args()
 
 
@@ -109,7 +112,7 @@ def main():
         step(i)
     torch.cuda.synchronize(dev)
     eng.profile_read()  # drop anything recorded so far
-    eng.profile(True)
+    eng.profile(args.roofline_pass == "inline")
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -121,15 +124,20 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     eng.profile(False)
+    if args.roofline_pass == "after":
+        eng.profile(True)
+        for i in range(args.steps):
+            step(args.warmup + i)
+        eng.profile(False)
     k_ms, k_flops, k_launches = eng.profile_read()
-    elapsed = t1 - t0
-    if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-    ms_per_step = elapsed / args.steps * 1000.0
+    from rvcx.sharding import reduce_throughput
+
     audio_sec = n / SR_IN
-    value = world * args.steps * audio_sec / elapsed
+    # whole job: audio-seconds summed over ranks / wall time maxed over ranks
+    tot = reduce_throughput(dist, args.steps * audio_sec, t1 - t0, device=dev)
+    elapsed = tot["elapsed"]
+    ms_per_step = elapsed / args.steps * 1000.0
+    value = tot["value"]
     assert y.numel() > 0 and bool(torch.isfinite(y).all())
 
     achieved_tflops = k_flops / (k_ms / 1000.0) / 1e12 if k_ms > 0 else 0.0

@@ -334,17 +334,33 @@ hipError_t upsample2_protect(const float* feats, int L, int D, float* out, int T
 // ------------------------------------------------------------------ NSF harmonic source (SineGen, harmonic_num=0)
 // generators/hifigan.py:156-228 + hifigan_nsf.py:48-52. Phase carry: rem[l] = fmod(f0[l]/sr*upp + .5, 1) - .5,
 // cumsum accumulated in fp64 and rounded per element (torch CPU cumsum acc_type<float> = double), then fmod 1.
-__global__ void k_sine_cum(const float* f0, int B, int L, int upp, float sr, double* cum) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
+// SineGen phase prefix (generators/hifigan.py:156-228): rem[l] = fmod(f0[l]/sr*upp + 0.5, 1) - 0.5,
+// cum = fmod(cumsum(rem), 1) with the cumsum accumulated in double (torch CPU acc type), sequentially
+// like torch. One block per batch row: the block computes a tile of rem into LDS in parallel, one
+// thread runs the dependent double chain over LDS, the block writes the tile back.
+__global__ void k_sine_cum(const float* __restrict__ f0, int B, int L, int upp, float sr, double* __restrict__ cum) {
+  constexpr int TILE = 4096;
+  __shared__ float rem[TILE];
+  const int b = blockIdx.x;
   const float* fb = f0 + (long long)b * L;
   float* cf = reinterpret_cast<float*>(cum + (long long)b * L);
   double acc = 0.0;
-  for (int l = 0; l < L - 1; ++l) {
-    const float inc = (fb[l] / sr) * (float)upp;
-    const float rem = fmodf(inc + 0.5f, 1.0f) - 0.5f;
-    acc += (double)rem;
-    cf[l] = fmodf((float)acc, 1.0f);
+  for (int t0 = 0; t0 < L - 1; t0 += TILE) {
+    const int n = min(TILE, L - 1 - t0);
+    for (int j = threadIdx.x; j < n; j += blockDim.x) {
+      const float inc = (fb[t0 + j] / sr) * (float)upp;
+      rem[j] = fmodf(inc + 0.5f, 1.0f) - 0.5f;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int j = 0; j < n; ++j) {
+        acc += (double)rem[j];
+        rem[j] = fmodf((float)acc, 1.0f);
+      }
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < n; j += blockDim.x) cf[t0 + j] = rem[j];
+    __syncthreads();
   }
 }
 __global__ void k_sine(const float* f0, int B, int L, int upp, float sr, const double* cum, const float* eps,
@@ -369,7 +385,7 @@ __global__ void k_sine(const float* f0, int B, int L, int upp, float sr, const d
 }
 hipError_t sine_source(const float* f0, int B, int L, int upp, float sr, const float* eps, uint64_t seed,
                        float lin_w, float lin_b, double* cum_ws, float* har, hipStream_t s) {
-  hipLaunchKernelGGL(k_sine_cum, dim3((B + 63) / 64), dim3(64), 0, s, f0, B, L, upp, sr, cum_ws);
+  hipLaunchKernelGGL(k_sine_cum, dim3(B), dim3(256), 0, s, f0, B, L, upp, sr, cum_ws);
   hipLaunchKernelGGL(k_sine, dim3(nblocks((long long)B * L * upp)), dim3(TB), 0, s, f0, B, L, upp, sr, cum_ws, eps,
                      seed, lin_w, lin_b, har);
   return hipGetLastError();

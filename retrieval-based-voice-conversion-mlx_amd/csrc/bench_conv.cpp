@@ -72,7 +72,7 @@ int main(int argc, char** argv) {
     std::vector<float> ref((size_t)T * N), out((size_t)T * N);
     CK_(hipMemcpy(ref.data(), yr, ref.size() * 4, hipMemcpyDeviceToHost));
     for (int cfg = 0; cfg < 6; ++cfg)
-      for (int pipe = 0; pipe < 2; ++pipe) {
+      for (int pipe : {-1, 1}) {
         ConvArgs a;
         a.x = x; a.ldx = C; a.T_in = T; a.C_in = C;
         a.w = w; a.ldw = C; a.w_ts = (long long)N * C; a.taps = taps; a.dil = dil; a.pad = pad;
@@ -109,25 +109,30 @@ int main(int argc, char** argv) {
     CK_(hipMemcpy(b, hb.data(), N * 4, hipMemcpyHostToDevice));
     hipLaunchKernelGGL(naive_conv1d, dim3((T * N + 255) / 256), dim3(256), 0, 0, x, w, b, yr, T, C, T, N, taps, dil,
                        pad, 1);
-    ConvArgs a;
-    a.x = x; a.ldx = C; a.T_in = T; a.C_in = C;
-    a.w = w; a.ldw = C; a.w_ts = (long long)N * C; a.taps = taps; a.dil = dil; a.pad = pad;
-    a.y = y; a.ldy = N; a.T_out = T; a.N = N; a.bias = b;
-    a.pre_act = ACT_LRELU; a.pre_slope = 0.1f;
-    const long long need = conv_plan_splitk(a, false);
-    CK_(hipMalloc(&ws, (need > 0 ? need : 1) * 4));
-    a.ws = ws;
-    CK_(conv1d(a, 0));
-    CK_(hipDeviceSynchronize());
     std::vector<float> ref((size_t)T * N), out((size_t)T * N);
     CK_(hipMemcpy(ref.data(), yr, ref.size() * 4, hipMemcpyDeviceToHost));
-    CK_(hipMemcpy(out.data(), y, out.size() * 4, hipMemcpyDeviceToHost));
-    double md = 0, mr = 0;
-    for (size_t i = 0; i < out.size(); ++i) {
-      md = std::max(md, (double)fabsf(out[i] - ref[i]));
-      mr = std::max(mr, (double)fabsf(ref[i]));
+    for (int pipe : {-1, 1}) {
+      ConvArgs a;
+      a.x = x; a.ldx = C; a.T_in = T; a.C_in = C;
+      a.w = w; a.ldw = C; a.w_ts = (long long)N * C; a.taps = taps; a.dil = dil; a.pad = pad;
+      a.y = y; a.ldy = N; a.T_out = T; a.N = N; a.bias = b;
+      a.pre_act = ACT_LRELU; a.pre_slope = 0.1f; a.pipe = pipe;
+      const long long need = conv_plan_splitk(a, false);
+      CK_(hipMalloc(&ws, (need > 0 ? need : 1) * 4));
+      a.ws = ws;
+      CK_(hipMemset(y, 0, (size_t)T * N * 4));
+      CK_(conv1d(a, 0));
+      CK_(hipDeviceSynchronize());
+      CK_(hipMemcpy(out.data(), y, out.size() * 4, hipMemcpyDeviceToHost));
+      double md = 0, mr = 0;
+      for (size_t i = 0; i < out.size(); ++i) {
+        md = std::max(md, (double)fabsf(out[i] - ref[i]));
+        mr = std::max(mr, (double)fabsf(ref[i]));
+      }
+      printf("check splitk ksplit=%d pipe=%d max|diff|/max|ref| = %.3e %s\n", a.ksplit, pipe, md / mr,
+             md / mr < 1e-5 ? "OK" : "FAIL");
+      (void)hipFree(ws);
     }
-    printf("check splitk ksplit=%d max|diff|/max|ref| = %.3e %s\n", a.ksplit, md / mr, md / mr < 1e-5 ? "OK" : "FAIL");
   }
   // timing
   std::vector<Case> cases = {
@@ -154,7 +159,7 @@ int main(int argc, char** argv) {
     CK_(hipMemset(b, 0, cs.N * 4));
     const double flops = 2.0 * cs.T * cs.N * (double)cs.Cin * cs.taps;
     for (int cfg : {-1, 1, 3})
-      for (int pipe = 0; pipe < 1; ++pipe) {
+      for (int pipe : {-1, 1}) {
         ConvArgs a;
         a.x = x; a.ldx = cs.Cin; a.T_in = cs.T; a.C_in = cs.Cin;
         a.w = w; a.ldw = cs.Cin; a.w_ts = (long long)cs.N * cs.Cin; a.taps = cs.taps; a.dil = cs.dil;
@@ -168,6 +173,7 @@ int main(int argc, char** argv) {
           if (need > 0) { CK_(hipMalloc(&wsp, need * 4)); a.ws = wsp; }
         }
         if (conv1d(a, 0) != hipSuccess) { (void)hipGetLastError(); continue; }
+        for (int i = 0; i < 5; ++i) CK_(conv1d(a, 0));
         CK_(hipDeviceSynchronize());
         hipEvent_t e0, e1;
         CK_(hipEventCreate(&e0));

@@ -1,5 +1,7 @@
 // extern "C" boundary (include/rvcx.h). Every entry point converts C++ exceptions into an
 // rvcx_status and stores the message for rvcx_last_error.
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "runtime.h"
@@ -53,7 +55,8 @@ void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double
     }
     return e;
   };
-  Ctx::ProfRec r{get_ev(), get_ev(), flops};
+  Ctx::ProfRec r{get_ev(), get_ev(), flops, two_d ? 1 : 0, two_d ? a.T_out * a.W_out : a.T_out, a.N, a.C_in,
+                 a.taps, a.batch * a.batch_inner, a.ksplit};
   RVCX_HIP(hipEventRecord(r.a, s));
   check(two_d ? conv2d(a, s) : conv1d(a, s), two_d ? "conv2d" : "conv1d");
   RVCX_HIP(hipEventRecord(r.b, s));
@@ -300,15 +303,21 @@ int rvcx_profile_read(rvcx_ctx* ctx, double* total_ms, double* total_flops, int6
   return guard(ctx, [&] {
     set_device(ctx);
     double ms = 0.0, fl = 0.0;
+    const char* dump = std::getenv("RVCX_PROF_DUMP");  // append one CSV line per conv launch
+    FILE* fd = dump ? std::fopen(dump, "a") : nullptr;
     for (auto& r : ctx->prof_recs) {
       RVCX_HIP(hipEventSynchronize(r.b));
       float t = 0.f;
       RVCX_HIP(hipEventElapsedTime(&t, r.a, r.b));
+      if (fd)
+        std::fprintf(fd, "%d,%d,%d,%d,%d,%d,%d,%.6f,%.0f\n", r.two_d, r.M, r.N, r.C_in, r.taps, r.batch, r.ksplit, t,
+                     r.flops);
       ms += t;
       fl += r.flops;
       ctx->prof_pool.push_back(r.a);
       ctx->prof_pool.push_back(r.b);
     }
+    if (fd) std::fclose(fd);
     if (total_ms) *total_ms = ms;
     if (total_flops) *total_flops = fl;
     if (launches) *launches = (int64_t)ctx->prof_recs.size();

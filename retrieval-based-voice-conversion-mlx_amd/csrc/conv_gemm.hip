@@ -15,6 +15,7 @@
 // ds_read_b128 per operand feeds 4 MFMAs (the k-pair of MFMA j is channels {8kk+j, 8kk+4+j}).
 // fp32 in / fp32 accumulate MFMA is a bit-exact fp32 fma chain at the FP32 vector peak rate.
 #include <algorithm>
+#include <cstdlib>
 
 #include "rvcx_kernels.h"
 
@@ -26,6 +27,8 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int CK = 32;   // contraction channels per LDS chunk
 constexpr int CKP = 36;  // padded LDS row: rows i..i+15 land on distinct 16-B bank slots
 constexpr int NTHREADS = 256;
+constexpr int TGMAX = 4;  // (chunk, tap) iterations staged per barrier pair
+constexpr int AVMAX = 7;  // pipelined A staging: up to 7 float4 per thread (nrows_a <= 224)
 
 __device__ __noinline__ float act_fn_slow(float v, int act, float slope) {
   switch (act) {
@@ -77,8 +80,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
   static_assert(WM * WN == 4, "4 waves per block");
   static_assert(TM >= 1 && TN >= 1, "tile too small");
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* As = smem;
-  float* Bs0 = smem + nrows_a * CKP;        // PIPE: two B buffers [2][BN][CKP]
+  float* As = smem;                                       // PIPE: two A buffers [2][nrows_a][CKP]
+  // non-PIPE: A slots [taps == 1 ? TGMAX : 1][nrows_a][CKP], then TGMAX B slots [BN][CKP]
+  float* Bs0 = smem + (PIPE ? 2 : (a.taps == 1 ? TGMAX : 1)) * nrows_a * CKP;  // PIPE: two B buffers
   float* Bs1 = Bs0 + BN * CKP;
 
   const int tid = threadIdx.x;
@@ -179,54 +183,71 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
       }
     }
   };
-  // A tile: nrows_a x 32 channels of chunk c0 -> LDS, pre-activation applied, zero outside the input
-  auto stage_a = [&](int c0) {
-    for (int idx = tid; idx < nrows_a * (CK / 4); idx += NTHREADS) {
-      const int r = idx >> 3;
-      const int c4 = (idx & 7) << 2;
-      const int c = c0 + c4;
-      long long grow;
-      bool valid;
-      if (!TWO_D) {
-        const int g = row0 + r;
-        valid = (g >= 0) && (g < a.T_in);
-        grow = g;
+  // A tile: nrows_a x 32 channels of chunk c0, pre-activation and row mask applied, zero outside the input
+  auto load_a4 = [&](int idx, int c0) -> f32x4 {
+    const int r = idx >> 3;
+    const int c = c0 + ((idx & 7) << 2);
+    long long grow;
+    bool valid;
+    if (!TWO_D) {
+      const int g = row0 + r;
+      valid = (g >= 0) && (g < a.T_in);
+      grow = g;
+    } else {
+      const int ah = r / aw, awi = r - ah * aw;
+      const int gh = h0 - a.padh + ah, gw = w0 - a.padw + awi;
+      valid = (gh >= 0) && (gh < a.T_in) && (gw >= 0) && (gw < a.W_in);
+      grow = (long long)gh * a.W_in + gw;
+    }
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (valid && c < a.C_in) {
+      const float* src = X + grow * a.ldx + c;
+      if (vec_a && c + 4 <= a.C_in) {
+        v = *reinterpret_cast<const f32x4*>(src);
       } else {
-        const int ah = r / aw, awi = r - ah * aw;
-        const int gh = h0 - a.padh + ah, gw = w0 - a.padw + awi;
-        valid = (gh >= 0) && (gh < a.T_in) && (gw >= 0) && (gw < a.W_in);
-        grow = (long long)gh * a.W_in + gw;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = (c + j < a.C_in) ? src[j] : 0.f;
       }
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (valid && c < a.C_in) {
-        const float* src = X + grow * a.ldx + c;
-        if (vec_a && c + 4 <= a.C_in) {
-          v = *reinterpret_cast<const f32x4*>(src);
-        } else {
+      if (a.pre_act != ACT_NONE) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = (c + j < a.C_in) ? src[j] : 0.f;
-        }
-        if (a.pre_act != ACT_NONE) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = act_fn(v[j], a.pre_act, a.pre_slope);
-        }
-        if (PM) {
-          const float mk = PM[grow];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] *= mk;
-        }
+        for (int j = 0; j < 4; ++j) v[j] = act_fn(v[j], a.pre_act, a.pre_slope);
       }
-      *reinterpret_cast<f32x4*>(&As[r * CKP + c4]) = v;
+      if (PM) {
+        const float mk = PM[grow];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] *= mk;
+      }
+    }
+    return v;
+  };
+  auto stage_a = [&](float* Ad, int c0) {
+    for (int idx = tid; idx < nrows_a * (CK / 4); idx += NTHREADS)
+      *reinterpret_cast<f32x4*>(&Ad[(idx >> 3) * CKP + ((idx & 7) << 2)]) = load_a4(idx, c0);
+  };
+  // register-staged A for the pipelined loop (host guarantees nrows_a * 8 <= AVMAX * NTHREADS)
+  constexpr int AV = PIPE ? AVMAX : 1;
+  auto load_a = [&](int c0, f32x4 (&reg)[AV]) {
+#pragma unroll
+    for (int v = 0; v < AV; ++v) {
+      const int idx = tid + v * NTHREADS;
+      if (idx < nrows_a * (CK / 4)) reg[v] = load_a4(idx, c0);
     }
   };
-  auto compute = [&](const float* Bs, int tap) {
+  auto store_a = [&](float* Ad, const f32x4 (&reg)[AV]) {
+#pragma unroll
+    for (int v = 0; v < AV; ++v) {
+      const int idx = tid + v * NTHREADS;
+      if (idx < nrows_a * (CK / 4)) *reinterpret_cast<f32x4*>(&Ad[(idx >> 3) * CKP + ((idx & 7) << 2)]) = reg[v];
+    }
+  };
+  auto compute = [&](const float* Ac, const float* Bs, int tap) {
     const int toff = TWO_D ? (tap / a.KW) * aw + (tap % a.KW) : tap * a.dil;
 #pragma unroll
     for (int kk = 0; kk < CK; kk += 8) {
       float av[TM][4], bv[TN][4];
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm) {
-        const f32x4 t = *reinterpret_cast<const f32x4*>(&As[(base[tm] + toff) * CKP + kk + hk * 4]);
+        const f32x4 t = *reinterpret_cast<const f32x4*>(&Ac[(base[tm] + toff) * CKP + kk + hk * 4]);
         av[tm][0] = t[0]; av[tm][1] = t[1]; av[tm][2] = t[2]; av[tm][3] = t[3];
       }
 #pragma unroll
@@ -245,51 +266,78 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
   };
 
   const int nchunks = (a.C_in + CK - 1) / CK;
+  const int total = nchunks * a.taps;
+  const int per = (total + ksplit - 1) / ksplit;
+  const int it0 = zsplit * per, it1 = min(total, it0 + per);
   if (!PIPE) {
-    f32x4 breg[BV];
-    const int total = nchunks * a.taps;
-    const int per = (total + ksplit - 1) / ksplit;
-    const int it0 = zsplit * per, it1 = min(total, it0 + per);
+    // Grouped staging: up to TG consecutive (chunk, tap) iterations are staged per barrier pair.
+    // Taps of one chunk share its A halo tile; with taps == 1 (plain GEMM) a group spans TG
+    // chunks, each with its own A slot. Groups never cross a chunk boundary when taps > 1.
+    const int tg = a.taps == 1 ? TGMAX : min(a.taps, TGMAX);
     int it = it0;
     while (it < it1) {
-      const int ch = it / a.taps;
-      __syncthreads();
-      stage_a(ch * CK);
-      for (int tap = it - ch * a.taps; tap < a.taps && it < it1; ++tap, ++it) {
-        if (it > it0 && tap != it0 - ch * a.taps) __syncthreads();
-        load_b(tap, ch * CK, breg);
-        store_b(Bs0, breg);
-        __syncthreads();
-        compute(Bs0, tap);
+      int cnt;
+      if (a.taps == 1) {
+        cnt = min(tg, it1 - it);
+      } else {
+        const int ch = it / a.taps;
+        cnt = min(tg, min(it1 - it, (ch + 1) * a.taps - it));
       }
+      __syncthreads();  // every wave is done with the previous group's tiles
+      f32x4 breg[TGMAX][BV];
+#pragma unroll
+      for (int j = 0; j < TGMAX; ++j) {
+        if (j < cnt) {
+          const int itj = it + j, ch = itj / a.taps;
+          load_b(itj - ch * a.taps, ch * CK, breg[j]);
+        }
+      }
+      if (a.taps == 1) {
+        for (int j = 0; j < cnt; ++j) stage_a(As + j * nrows_a * CKP, (it + j) * CK);
+      } else if (it == it0 || (it % a.taps) == 0) {
+        stage_a(As, (it / a.taps) * CK);
+      }
+#pragma unroll
+      for (int j = 0; j < TGMAX; ++j)
+        if (j < cnt) store_b(Bs0 + j * BN * CKP, breg[j]);
+      __syncthreads();
+      for (int j = 0; j < cnt; ++j) {
+        const int itj = it + j, ch = itj / a.taps;
+        compute(a.taps == 1 ? As + j * nrows_a * CKP : As, Bs0 + j * BN * CKP, itj - ch * a.taps);
+      }
+      it += cnt;
     }
-  } else {
-    // software pipeline over the (chunk, tap) sequence: the next B tile is fetched into registers
-    // while the MFMAs consume the current one from LDS; one barrier per tap (two at chunk change).
+  } else if (it0 < it1) {
+    // Software pipeline over the (chunk, tap) sequence. While the MFMAs consume iteration k from
+    // LDS buffers (A[chunk & 1], B[k & 1]), the global loads of iteration k+1 (its B tile and, at a
+    // chunk change, its A tile) are in flight in registers; they land in the other buffers after
+    // the MFMAs. One barrier per iteration: the writes of k+1 only touch buffers last read at k-1.
+    float* Abuf[2] = {As, As + nrows_a * CKP};
+    float* Bbuf[2] = {Bs0, Bs1};
     f32x4 breg[BV];
-    stage_a(0);
-    load_b(0, 0, breg);
-    store_b(Bs0, breg);
+    f32x4 areg[AV];
+    int ch = it0 / a.taps, tap = it0 - ch * a.taps;
+    load_a(ch * CK, areg);
+    load_b(tap, ch * CK, breg);
+    store_a(Abuf[ch & 1], areg);
+    store_b(Bbuf[0], breg);
     __syncthreads();
-    const int total = nchunks * a.taps;
-    int ch = 0, tap = 0;
-    for (int it = 0; it < total; ++it) {
-      float* Bcur = (it & 1) ? Bs1 : Bs0;
-      float* Bnxt = (it & 1) ? Bs0 : Bs1;
+    for (int it = it0, k = 0; it < it1; ++it, ++k) {
       int nch = ch, ntap = tap + 1;
       if (ntap == a.taps) {
         ntap = 0;
         ++nch;
       }
-      const bool more = it + 1 < total;
-      if (more) load_b(ntap, nch * CK, breg);
-      compute(Bcur, tap);
+      const bool more = it + 1 < it1;
+      const bool new_chunk = more && nch != ch;
       if (more) {
-        if (ntap == 0) {
-          __syncthreads();  // every wave is done with this chunk's A tile
-          stage_a(nch * CK);
-        }
-        store_b(Bnxt, breg);
+        load_b(ntap, nch * CK, breg);
+        if (new_chunk) load_a(nch * CK, areg);
+      }
+      compute(Abuf[ch & 1], Bbuf[k & 1], tap);
+      if (more) {
+        store_b(Bbuf[(k + 1) & 1], breg);
+        if (new_chunk) store_a(Abuf[nch & 1], areg);
       }
       __syncthreads();
       ch = nch;
@@ -383,7 +431,11 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
     mtiles = ((a.T_out + rh - 1) / rh) * tiles_w;
     nrows_a = (rh + a.KH - 1) * (rw + a.KW - 1);
   }
-  const size_t smem = (size_t)(nrows_a + (PIPE ? 2 : 1) * BN) * CKP * sizeof(float);
+  if constexpr (PIPE) {
+    if (nrows_a * (CK / 4) > AVMAX * NTHREADS) return launch_cfg<BM, BN, WM, WN, TWO_D, false>(a, s);
+  }
+  const size_t smem = PIPE ? (size_t)(2 * (nrows_a + BN)) * CKP * sizeof(float)
+                           : (size_t)((a.taps == 1 ? TGMAX : 1) * nrows_a + TGMAX * BN) * CKP * sizeof(float);
   if (smem > 160 * 1024) return hipErrorInvalidValue;
   const int vec_a = ((a.ldx & 3) == 0) && ((reinterpret_cast<uintptr_t>(a.x) & 15) == 0) &&
                     ((a.x_bs & 3) == 0) && ((a.x_bs2 & 3) == 0);
@@ -391,7 +443,7 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
                     ((a.w_bs & 3) == 0) && ((a.w_bs2 & 3) == 0) && ((a.w_ts & 3) == 0);
   if (a.batch_inner < 1) return hipErrorInvalidValue;
   int ksplit = 1;
-  if (!PIPE && a.ws && a.ksplit > 1) ksplit = a.ksplit;
+  if (a.ws && a.ksplit > 1) ksplit = a.ksplit;
   dim3 grid(mtiles, (a.N + BN - 1) / BN, a.batch * a.batch_inner * ksplit);
   auto kern = conv_gemm_kernel<BM, BN, WM, WN, TWO_D, PIPE>;
   if (smem > 64 * 1024) {
@@ -437,6 +489,15 @@ inline void cfg_tile(int cfg, int& BM, int& BN) {
   BN = t[cfg][1];
 }
 
+// RVCX_CONV_PIPE=0/1 overrides the default loop variant (measurement aid)
+inline bool default_pipe() {
+  static const int v = [] {
+    const char* e = std::getenv("RVCX_CONV_PIPE");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v != 0;
+}
+
 template <bool TWO_D>
 hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
   if (a.N <= 0 || a.T_out <= 0 || a.batch <= 0) return hipSuccess;
@@ -444,7 +505,7 @@ hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
   const int cfg = pick_cfg<TWO_D>(a);
   ConvArgs b = a;
   b.force_cfg = cfg;
-  if (a.pipe && a.force_cfg >= 0) return launch_forced<TWO_D, true>(b, s);
+  if (a.pipe > 0 || (a.pipe == 0 && default_pipe())) return launch_forced<TWO_D, true>(b, s);
   return launch_forced<TWO_D, false>(b, s);
 }
 

@@ -88,6 +88,7 @@ struct Ctx {
   struct ProfRec {
     hipEvent_t a, b;
     double flops;
+    int two_d, M, N, C_in, taps, batch, ksplit;  // shape, for RVCX_PROF_DUMP
   };
   std::vector<ProfRec> prof_recs;
   std::vector<hipEvent_t> prof_pool;

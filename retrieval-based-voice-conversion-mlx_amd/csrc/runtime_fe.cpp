@@ -138,7 +138,7 @@ int64_t hubert_forward(Ctx& c, const float* audio, int64_t n, int version, float
   if (L > cap) throw Error(RVCX_E_CAPACITY, "hubert: output needs " + std::to_string(L) + " rows");
   float* a = c.buf<float>("hb.a", (size_t)T[1] * HCONV, s);
   float* b = c.buf<float>("hb.b", (size_t)T[2] * HCONV, s);
-  double* gnws = c.buf<double>("hb.gnws", 64 * HCONV * 2, s);
+  double* gnws = c.buf<double>("hb.gnws", groupnorm_ws_doubles(HCONV), s);
   {  // conv0 over 5-sample rows (2 taps)
     ConvArgs a0 = lin(audio, 5, (int)(n / 5), 5, c.W("hb.conv0"), HCONV, nullptr, a, HCONV);
     a0.taps = 2;

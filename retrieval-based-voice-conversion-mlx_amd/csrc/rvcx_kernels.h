@@ -128,6 +128,9 @@ hipError_t conv_post_tanh(const float* x, int B, int T, int C, const float* w, i
 hipError_t randn(float* y, long long n, uint64_t seed, uint64_t offset, hipStream_t s);
 hipError_t zp_sample(const float* stats, int B, int T, int I, const float* eps, uint64_t seed, const float* mask,
                      float* zp, hipStream_t s);
+// ws: groupnorm_ws_doubles(C) doubles
+constexpr int GN_CHUNKS = 256;
+inline size_t groupnorm_ws_doubles(int C) { return (size_t)GN_CHUNKS * C * 2 + C; }
 hipError_t groupnorm_time_gelu(float* x, int T, int C, const float* gamma, const float* beta, float eps,
                                double* ws, hipStream_t s);
 hipError_t act_inplace(float* x, long long n, int act, float slope, hipStream_t s);
