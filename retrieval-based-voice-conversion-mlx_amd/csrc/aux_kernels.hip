@@ -11,6 +11,7 @@ namespace rvcx {
 namespace {
 
 constexpr int TB = 256;
+typedef float f32x4v __attribute__((ext_vector_type(4)));
 
 inline unsigned nblocks(long long n, int per = TB) {
   long long b = (n + per - 1) / per;
@@ -364,7 +365,7 @@ __global__ void k_sine_cum(const float* __restrict__ f0, int B, int L, int upp, 
   }
 }
 __global__ void k_sine(const float* f0, int B, int L, int upp, float sr, const double* cum, const float* eps,
-                       uint64_t seed, float lin_w, float lin_b, float* har) {
+                       uint64_t seed, float lin_w, float lin_b, float* har, long long har_ld) {
   const long long n = (long long)B * L * upp;
   const float two_pi = 6.283185307179586f;
   const float amp_unv = (float)(0.1 / 3.0);
@@ -380,51 +381,18 @@ __global__ void k_sine(const float* f0, int B, int L, int upp, float sr, const d
     const float amp = uv * 0.003f + (1.f - uv) * amp_unv;
     const float e = eps ? eps[i] : normal_at(seed, (uint64_t)i);
     const float merged = sine * uv + amp * e;
-    har[i] = tanhf(merged * lin_w + lin_b);
+    har[(long long)b * har_ld + (long long)l * upp + u] = tanhf(merged * lin_w + lin_b);
   }
 }
 hipError_t sine_source(const float* f0, int B, int L, int upp, float sr, const float* eps, uint64_t seed,
-                       float lin_w, float lin_b, double* cum_ws, float* har, hipStream_t s) {
+                       float lin_w, float lin_b, double* cum_ws, float* har, long long har_ld, hipStream_t s) {
   hipLaunchKernelGGL(k_sine_cum, dim3(B), dim3(256), 0, s, f0, B, L, upp, sr, cum_ws);
   hipLaunchKernelGGL(k_sine, dim3(nblocks((long long)B * L * upp)), dim3(TB), 0, s, f0, B, L, upp, sr, cum_ws, eps,
-                     seed, lin_w, lin_b, har);
+                     seed, lin_w, lin_b, har, har_ld);
   return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ noise_convs: y[b][t][c] += b[c] + sum_k har[t*s-p+k] w[c][k]
-__global__ void k_noise_conv(const float* har, int Nh, float* y, int T, int C, long long y_bs, const float* w,
-                             const float* bias, int K, int stride, int pad) {
-  extern __shared__ float seg[];
-  const int b = blockIdx.y;
-  const int t0 = blockIdx.x * 32;
-  const int span = 31 * stride + K;
-  const float* hb = har + (long long)b * Nh;
-  for (int k = threadIdx.x; k < span; k += blockDim.x) {
-    const long long g = (long long)t0 * stride - pad + k;
-    seg[k] = (g >= 0 && g < Nh) ? hb[g] : 0.f;
-  }
-  __syncthreads();
-  float* yb = y + (long long)b * y_bs;
-  for (int idx = threadIdx.x; idx < 32 * C; idx += blockDim.x) {
-    const int tt = idx / C, c = idx % C;
-    const int t = t0 + tt;
-    if (t >= T) continue;
-    const float* wc = w + (long long)c * K;
-    const float* sg = seg + tt * stride;
-    float acc = 0.f;
-    for (int k = 0; k < K; ++k) acc = fmaf(sg[k], wc[k], acc);
-    float* dst = yb + (long long)t * C + c;
-    *dst = *dst + (acc + bias[c]);
-  }
-}
-hipError_t noise_conv_add(const float* har, int Nh, float* y, int B, int T, int C, long long y_bs, const float* w,
-                          const float* b, int K, int stride, int pad, hipStream_t s) {
-  const int span = 31 * stride + K;
-  hipLaunchKernelGGL(k_noise_conv, dim3((T + 31) / 32, B), dim3(256), span * sizeof(float), s, har, Nh, y, T, C,
-                     y_bs, w, b, K, stride, pad);
-  return hipGetLastError();
-}
-
 // ------------------------------------------------------------------ conv_post: tanh(conv1d(lrelu(x, 0.01), w[1][C][K], pad K/2)), no bias
 __global__ void k_conv_post(const float* x, int T, int C, const float* w, int K, float slope, float* y) {
   extern __shared__ float tile[];  // [(256+K-1)][C+1]
@@ -507,31 +475,48 @@ __global__ void k_gn_stats(const float* x, int T, int C, int chunk, double* ws) 
     ws[((long long)blockIdx.y * C + c) * 2 + 1] = q;
   }
 }
-__global__ void k_gn_apply(float* x, int T, int C, int nchunks, const double* ws, const float* gamma,
-                           const float* beta, float eps) {
-  const long long n = (long long)T * C;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    double s = 0.0, q = 0.0;
-    for (int k = 0; k < nchunks; ++k) {
-      s += ws[((long long)k * C + c) * 2];
-      q += ws[((long long)k * C + c) * 2 + 1];
+// per-channel statistics -> affine form y = x * scale + shift (torch GroupNorm's ApplyScaleBias:
+// scale = rstd * gamma, shift = beta - mean * scale), once per channel instead of per element
+__global__ void k_gn_finalize(const double* ws, int nchunks, int T, int C, const float* gamma, const float* beta,
+                              float eps, float* ss) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int k = 0; k < nchunks; ++k) {
+    s += ws[((long long)k * C + c) * 2];
+    q += ws[((long long)k * C + c) * 2 + 1];
+  }
+  const double mean = s / T;
+  double var = q / T - mean * mean;
+  if (var < 0) var = 0;
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float scale = rstd * gamma[c];
+  ss[c] = scale;
+  ss[C + c] = beta[c] - (float)mean * scale;
+}
+__global__ void k_gn_apply(float* __restrict__ x, long long n4, int C4, const float* __restrict__ ss, int C) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4) * 4;
+    f32x4v v = reinterpret_cast<f32x4v*>(x)[i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float t = v[j] * ss[c + j] + ss[C + c + j];
+      v[j] = 0.5f * t * (1.f + erff(t * 0.70710678118654752440f));
     }
-    const double mean = s / T;
-    double var = q / T - mean * mean;
-    if (var < 0) var = 0;
-    const float rstd = (float)(1.0 / sqrt(var + (double)eps));
-    float v = (x[i] - (float)mean) * rstd * gamma[c] + beta[c];
-    x[i] = 0.5f * v * (1.f + erff(v * 0.70710678118654752440f));
+    reinterpret_cast<f32x4v*>(x)[i] = v;
   }
 }
 hipError_t groupnorm_time_gelu(float* x, int T, int C, const float* gamma, const float* beta, float eps, double* ws,
                                hipStream_t s) {
-  const int nchunks = 64;
+  // ws: GN_CHUNKS * C * 2 doubles of partial sums, then 2 * C floats of scale/shift
+  const int nchunks = GN_CHUNKS;
   const int chunk = (T + nchunks - 1) / nchunks;
+  if (C % 4) return hipErrorInvalidValue;
+  float* ss = reinterpret_cast<float*>(ws + (size_t)nchunks * C * 2);
   hipLaunchKernelGGL(k_gn_stats, dim3((C + 63) / 64, nchunks), dim3(256), 0, s, x, T, C, chunk, ws);
-  hipLaunchKernelGGL(k_gn_apply, dim3(nblocks((long long)T * C)), dim3(TB), 0, s, x, T, C, nchunks, ws, gamma, beta,
-                     eps);
+  hipLaunchKernelGGL(k_gn_finalize, dim3((C + 255) / 256), dim3(256), 0, s, ws, nchunks, T, C, gamma, beta, eps, ss);
+  const long long n4 = (long long)T * C / 4;
+  hipLaunchKernelGGL(k_gn_apply, dim3(nblocks(n4)), dim3(TB), 0, s, x, n4, C / 4, ss, C);
   return hipGetLastError();
 }
 

@@ -71,8 +71,8 @@ int main(int argc, char** argv) {
                        pad, 1);
     std::vector<float> ref((size_t)T * N), out((size_t)T * N);
     CK_(hipMemcpy(ref.data(), yr, ref.size() * 4, hipMemcpyDeviceToHost));
-    for (int cfg = 0; cfg < 6; ++cfg)
-      for (int pipe : {-1, 1}) {
+    for (int cfg = 0; cfg < 7; ++cfg)
+      for (int pipe : {-1}) {
         ConvArgs a;
         a.x = x; a.ldx = C; a.T_in = T; a.C_in = C;
         a.w = w; a.ldw = C; a.w_ts = (long long)N * C; a.taps = taps; a.dil = dil; a.pad = pad;
@@ -158,8 +158,11 @@ int main(int argc, char** argv) {
     CK_(hipMemcpy(w, hw.data(), nw * 4, hipMemcpyHostToDevice));
     CK_(hipMemset(b, 0, cs.N * 4));
     const double flops = 2.0 * cs.T * cs.N * (double)cs.Cin * cs.taps;
-    for (int cfg : {-1, 1, 3})
-      for (int pipe : {-1, 1}) {
+    double best[8] = {0};
+    int ksp[8] = {0};
+    for (int round = 0; round < 3; ++round)
+    for (int cfg : {-1, 0, 1, 2, 3, 4, 5, 6})
+      for (int pipe : {-1}) {
         ConvArgs a;
         a.x = x; a.ldx = cs.Cin; a.T_in = cs.T; a.C_in = cs.Cin;
         a.w = w; a.ldw = cs.Cin; a.w_ts = (long long)cs.N * cs.Cin; a.taps = cs.taps; a.dil = cs.dil;
@@ -173,7 +176,7 @@ int main(int argc, char** argv) {
           if (need > 0) { CK_(hipMalloc(&wsp, need * 4)); a.ws = wsp; }
         }
         if (conv1d(a, 0) != hipSuccess) { (void)hipGetLastError(); continue; }
-        for (int i = 0; i < 5; ++i) CK_(conv1d(a, 0));
+        for (int i = 0; i < 3; ++i) CK_(conv1d(a, 0));
         CK_(hipDeviceSynchronize());
         hipEvent_t e0, e1;
         CK_(hipEventCreate(&e0));
@@ -185,9 +188,14 @@ int main(int argc, char** argv) {
         float ms = 0;
         CK_(hipEventElapsedTime(&ms, e0, e1));
         ms /= iters;
-        printf("%-28s cfg=%2d pipe=%d ks=%2d %8.3f ms  %7.2f TFLOP/s\n", cs.name, cfg, pipe, a.ksplit, ms, flops / ms / 1e9);
+        const double tf = flops / ms / 1e9;
+        if (tf > best[cfg + 1]) best[cfg + 1] = tf;
+        ksp[cfg + 1] = a.ksplit;
         if (wsp) (void)hipFree(wsp);
       }
+    printf("%-28s", cs.name);
+    for (int c = 0; c < 8; ++c) printf(" %2d:%6.1f%s", c - 1, best[c], ksp[c] > 1 ? "*" : " ");
+    printf("\n");
     (void)hipFree(x); (void)hipFree(w); (void)hipFree(b); (void)hipFree(y);
   }
   return 0;

@@ -27,8 +27,6 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int CK = 32;   // contraction channels per LDS chunk
 constexpr int CKP = 36;  // padded LDS row: rows i..i+15 land on distinct 16-B bank slots
 constexpr int NTHREADS = 256;
-constexpr int TGMAX = 4;  // (chunk, tap) iterations staged per barrier pair
-constexpr int AVMAX = 7;  // pipelined A staging: up to 7 float4 per thread (nrows_a <= 224)
 
 __device__ __noinline__ float act_fn_slow(float v, int act, float slope) {
   switch (act) {
@@ -80,9 +78,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
   static_assert(WM * WN == 4, "4 waves per block");
   static_assert(TM >= 1 && TN >= 1, "tile too small");
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* As = smem;                                       // PIPE: two A buffers [2][nrows_a][CKP]
-  // non-PIPE: A slots [taps == 1 ? TGMAX : 1][nrows_a][CKP], then TGMAX B slots [BN][CKP]
-  float* Bs0 = smem + (PIPE ? 2 : (a.taps == 1 ? TGMAX : 1)) * nrows_a * CKP;  // PIPE: two B buffers
+  float* As = smem;
+  float* Bs0 = smem + nrows_a * CKP;        // PIPE: two B buffers [2][BN][CKP]
   float* Bs1 = Bs0 + BN * CKP;
 
   const int tid = threadIdx.x;
@@ -183,71 +180,54 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
       }
     }
   };
-  // A tile: nrows_a x 32 channels of chunk c0, pre-activation and row mask applied, zero outside the input
-  auto load_a4 = [&](int idx, int c0) -> f32x4 {
-    const int r = idx >> 3;
-    const int c = c0 + ((idx & 7) << 2);
-    long long grow;
-    bool valid;
-    if (!TWO_D) {
-      const int g = row0 + r;
-      valid = (g >= 0) && (g < a.T_in);
-      grow = g;
-    } else {
-      const int ah = r / aw, awi = r - ah * aw;
-      const int gh = h0 - a.padh + ah, gw = w0 - a.padw + awi;
-      valid = (gh >= 0) && (gh < a.T_in) && (gw >= 0) && (gw < a.W_in);
-      grow = (long long)gh * a.W_in + gw;
-    }
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (valid && c < a.C_in) {
-      const float* src = X + grow * a.ldx + c;
-      if (vec_a && c + 4 <= a.C_in) {
-        v = *reinterpret_cast<const f32x4*>(src);
+  // A tile: nrows_a x 32 channels of chunk c0 -> LDS, pre-activation applied, zero outside the input
+  auto stage_a = [&](int c0) {
+    for (int idx = tid; idx < nrows_a * (CK / 4); idx += NTHREADS) {
+      const int r = idx >> 3;
+      const int c4 = (idx & 7) << 2;
+      const int c = c0 + c4;
+      long long grow;
+      bool valid;
+      if (!TWO_D) {
+        const int g = row0 + r;
+        valid = (g >= 0) && (g < a.T_in);
+        grow = g;
       } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = (c + j < a.C_in) ? src[j] : 0.f;
+        const int ah = r / aw, awi = r - ah * aw;
+        const int gh = h0 - a.padh + ah, gw = w0 - a.padw + awi;
+        valid = (gh >= 0) && (gh < a.T_in) && (gw >= 0) && (gw < a.W_in);
+        grow = (long long)gh * a.W_in + gw;
       }
-      if (a.pre_act != ACT_NONE) {
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (valid && c < a.C_in) {
+        const float* src = X + grow * a.ldx + c;
+        if (vec_a && c + 4 <= a.C_in) {
+          v = *reinterpret_cast<const f32x4*>(src);
+        } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = act_fn(v[j], a.pre_act, a.pre_slope);
+          for (int j = 0; j < 4; ++j) v[j] = (c + j < a.C_in) ? src[j] : 0.f;
+        }
+        if (a.pre_act != ACT_NONE) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = act_fn(v[j], a.pre_act, a.pre_slope);
+        }
+        if (PM) {
+          const float mk = PM[grow];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] *= mk;
+        }
       }
-      if (PM) {
-        const float mk = PM[grow];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] *= mk;
-      }
-    }
-    return v;
-  };
-  auto stage_a = [&](float* Ad, int c0) {
-    for (int idx = tid; idx < nrows_a * (CK / 4); idx += NTHREADS)
-      *reinterpret_cast<f32x4*>(&Ad[(idx >> 3) * CKP + ((idx & 7) << 2)]) = load_a4(idx, c0);
-  };
-  // register-staged A for the pipelined loop (host guarantees nrows_a * 8 <= AVMAX * NTHREADS)
-  constexpr int AV = PIPE ? AVMAX : 1;
-  auto load_a = [&](int c0, f32x4 (&reg)[AV]) {
-#pragma unroll
-    for (int v = 0; v < AV; ++v) {
-      const int idx = tid + v * NTHREADS;
-      if (idx < nrows_a * (CK / 4)) reg[v] = load_a4(idx, c0);
-    }
-  };
-  auto store_a = [&](float* Ad, const f32x4 (&reg)[AV]) {
-#pragma unroll
-    for (int v = 0; v < AV; ++v) {
-      const int idx = tid + v * NTHREADS;
-      if (idx < nrows_a * (CK / 4)) *reinterpret_cast<f32x4*>(&Ad[(idx >> 3) * CKP + ((idx & 7) << 2)]) = reg[v];
+      *reinterpret_cast<f32x4*>(&As[r * CKP + c4]) = v;
     }
   };
-  auto compute = [&](const float* Ac, const float* Bs, int tap) {
+  auto compute = [&](const float* Bs, int tap) {
     const int toff = TWO_D ? (tap / a.KW) * aw + (tap % a.KW) : tap * a.dil;
 #pragma unroll
     for (int kk = 0; kk < CK; kk += 8) {
       float av[TM][4], bv[TN][4];
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm) {
-        const f32x4 t = *reinterpret_cast<const f32x4*>(&Ac[(base[tm] + toff) * CKP + kk + hk * 4]);
+        const f32x4 t = *reinterpret_cast<const f32x4*>(&As[(base[tm] + toff) * CKP + kk + hk * 4]);
         av[tm][0] = t[0]; av[tm][1] = t[1]; av[tm][2] = t[2]; av[tm][3] = t[3];
       }
 #pragma unroll
@@ -266,78 +246,51 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
   };
 
   const int nchunks = (a.C_in + CK - 1) / CK;
-  const int total = nchunks * a.taps;
-  const int per = (total + ksplit - 1) / ksplit;
-  const int it0 = zsplit * per, it1 = min(total, it0 + per);
   if (!PIPE) {
-    // Grouped staging: up to TG consecutive (chunk, tap) iterations are staged per barrier pair.
-    // Taps of one chunk share its A halo tile; with taps == 1 (plain GEMM) a group spans TG
-    // chunks, each with its own A slot. Groups never cross a chunk boundary when taps > 1.
-    const int tg = a.taps == 1 ? TGMAX : min(a.taps, TGMAX);
+    f32x4 breg[BV];
+    const int total = nchunks * a.taps;
+    const int per = (total + ksplit - 1) / ksplit;
+    const int it0 = zsplit * per, it1 = min(total, it0 + per);
     int it = it0;
     while (it < it1) {
-      int cnt;
-      if (a.taps == 1) {
-        cnt = min(tg, it1 - it);
-      } else {
-        const int ch = it / a.taps;
-        cnt = min(tg, min(it1 - it, (ch + 1) * a.taps - it));
-      }
-      __syncthreads();  // every wave is done with the previous group's tiles
-      f32x4 breg[TGMAX][BV];
-#pragma unroll
-      for (int j = 0; j < TGMAX; ++j) {
-        if (j < cnt) {
-          const int itj = it + j, ch = itj / a.taps;
-          load_b(itj - ch * a.taps, ch * CK, breg[j]);
-        }
-      }
-      if (a.taps == 1) {
-        for (int j = 0; j < cnt; ++j) stage_a(As + j * nrows_a * CKP, (it + j) * CK);
-      } else if (it == it0 || (it % a.taps) == 0) {
-        stage_a(As, (it / a.taps) * CK);
-      }
-#pragma unroll
-      for (int j = 0; j < TGMAX; ++j)
-        if (j < cnt) store_b(Bs0 + j * BN * CKP, breg[j]);
+      const int ch = it / a.taps;
       __syncthreads();
-      for (int j = 0; j < cnt; ++j) {
-        const int itj = it + j, ch = itj / a.taps;
-        compute(a.taps == 1 ? As + j * nrows_a * CKP : As, Bs0 + j * BN * CKP, itj - ch * a.taps);
+      stage_a(ch * CK);
+      for (int tap = it - ch * a.taps; tap < a.taps && it < it1; ++tap, ++it) {
+        if (it > it0 && tap != it0 - ch * a.taps) __syncthreads();
+        load_b(tap, ch * CK, breg);
+        store_b(Bs0, breg);
+        __syncthreads();
+        compute(Bs0, tap);
       }
-      it += cnt;
     }
-  } else if (it0 < it1) {
-    // Software pipeline over the (chunk, tap) sequence. While the MFMAs consume iteration k from
-    // LDS buffers (A[chunk & 1], B[k & 1]), the global loads of iteration k+1 (its B tile and, at a
-    // chunk change, its A tile) are in flight in registers; they land in the other buffers after
-    // the MFMAs. One barrier per iteration: the writes of k+1 only touch buffers last read at k-1.
-    float* Abuf[2] = {As, As + nrows_a * CKP};
-    float* Bbuf[2] = {Bs0, Bs1};
+  } else {
+    // software pipeline over the (chunk, tap) sequence: the next B tile is fetched into registers
+    // while the MFMAs consume the current one from LDS; one barrier per tap (two at chunk change).
     f32x4 breg[BV];
-    f32x4 areg[AV];
-    int ch = it0 / a.taps, tap = it0 - ch * a.taps;
-    load_a(ch * CK, areg);
-    load_b(tap, ch * CK, breg);
-    store_a(Abuf[ch & 1], areg);
-    store_b(Bbuf[0], breg);
+    stage_a(0);
+    load_b(0, 0, breg);
+    store_b(Bs0, breg);
     __syncthreads();
-    for (int it = it0, k = 0; it < it1; ++it, ++k) {
+    const int total = nchunks * a.taps;
+    int ch = 0, tap = 0;
+    for (int it = 0; it < total; ++it) {
+      float* Bcur = (it & 1) ? Bs1 : Bs0;
+      float* Bnxt = (it & 1) ? Bs0 : Bs1;
       int nch = ch, ntap = tap + 1;
       if (ntap == a.taps) {
         ntap = 0;
         ++nch;
       }
-      const bool more = it + 1 < it1;
-      const bool new_chunk = more && nch != ch;
+      const bool more = it + 1 < total;
+      if (more) load_b(ntap, nch * CK, breg);
+      compute(Bcur, tap);
       if (more) {
-        load_b(ntap, nch * CK, breg);
-        if (new_chunk) load_a(nch * CK, areg);
-      }
-      compute(Abuf[ch & 1], Bbuf[k & 1], tap);
-      if (more) {
-        store_b(Bbuf[(k + 1) & 1], breg);
-        if (new_chunk) store_a(Abuf[nch & 1], areg);
+        if (ntap == 0) {
+          __syncthreads();  // every wave is done with this chunk's A tile
+          stage_a(nch * CK);
+        }
+        store_b(Bnxt, breg);
       }
       __syncthreads();
       ch = nch;
@@ -350,35 +303,59 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
   const float* R = a.res ? a.res + (long long)b * a.res_bs + (long long)bi * a.res_bs2 : nullptr;
   const float* MK = a.mask ? a.mask + (long long)b * a.mask_bs : nullptr;
   float* Y = a.y + (long long)b * a.y_bs + (long long)bi * a.y_bs2;
+  auto emit = [&](float v, int ml, int n, bool n_ok, float bn) {
+    long long m;
+    int oh = 0, ow = 0;
+    bool ok;
+    if (!TWO_D) {
+      m = m0 + ml;
+      ok = n_ok && (m < a.T_out);
+    } else {
+      oh = h0 + ml / rw;
+      ow = w0 + ml % rw;
+      ok = n_ok && (ml < rh * rw) && (oh < a.T_out) && (ow < a.W_out);
+      m = (long long)oh * a.W_out + ow;
+    }
+    if (ok) {
+      if (ksplit > 1) {
+        a.ws[(((long long)zb * ksplit + zsplit) * a.ws_rows + m) * a.N + n] = v;
+      } else {
+        epilogue_store(a, v, bn, m, n, oh, ow, R, MK, Y);
+      }
+    }
+  };
+  if constexpr (TM * TN == 1) {
+    // one accumulator per wave: straight from registers (fully unrolled, 16 values per lane)
+    const int n = n0 + wn * 32 + li;
+    const bool n_ok = n < a.N;
+    const float bn = (bias && n_ok) ? bias[n] : 0.f;
 #pragma unroll
-  for (int tm = 0; tm < TM; ++tm) {
+    for (int r = 0; r < 16; ++r) emit(acc[0][0][r], wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hk, n, n_ok, bn);
+  } else {
+    // several accumulators per wave: stage one 32x32 tile at a time through the wave's own LDS slot
+    // (32 x 33 floats) and emit rows 2i + hk, column li; accumulator registers are only indexed with
+    // compile-time constants, so the large wave tiles keep them out of scratch
+    __syncthreads();  // every wave is done with the A/B tiles: their LDS becomes the staging area
+    float* Cs = smem + wave * (32 * 33);
 #pragma unroll
-    for (int tn = 0; tn < TN; ++tn) {
-      const int n = n0 + wn * TN * 32 + tn * 32 + li;
-      const bool n_ok = n < a.N;
-      const float bn = (bias && n_ok) ? bias[n] : 0.f;
+    for (int tm = 0; tm < TM; ++tm) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ml = wm * TM * 32 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hk;
-        long long m;
-        int oh = 0, ow = 0;
-        bool ok;
-        if (!TWO_D) {
-          m = m0 + ml;
-          ok = n_ok && (m < a.T_out);
-        } else {
-          oh = h0 + ml / rw;
-          ow = w0 + ml % rw;
-          ok = n_ok && (ml < rh * rw) && (oh < a.T_out) && (ow < a.W_out);
-          m = (long long)oh * a.W_out + ow;
+      for (int tn = 0; tn < TN; ++tn) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) Cs[((r & 3) + 8 * (r >> 2) + 4 * hk) * 33 + li] = acc[tm][tn][r];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int n = n0 + wn * TN * 32 + tn * 32 + li;
+        const bool n_ok = n < a.N;
+        const float bn = (bias && n_ok) ? bias[n] : 0.f;
+        for (int i = 0; i < 16; ++i) {
+          const int rr = 2 * i + hk;
+          emit(Cs[rr * 33 + li], wm * TM * 32 + tm * 32 + rr, n, n_ok, bn);
         }
-        if (ok) {
-          if (ksplit > 1) {
-            a.ws[(((long long)zb * ksplit + zsplit) * a.ws_rows + m) * a.N + n] = acc[tm][tn][r];
-          } else {
-            epilogue_store(a, acc[tm][tn][r], bn, m, n, oh, ow, R, MK, Y);
-          }
-        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
     }
   }
@@ -431,11 +408,8 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
     mtiles = ((a.T_out + rh - 1) / rh) * tiles_w;
     nrows_a = (rh + a.KH - 1) * (rw + a.KW - 1);
   }
-  if constexpr (PIPE) {
-    if (nrows_a * (CK / 4) > AVMAX * NTHREADS) return launch_cfg<BM, BN, WM, WN, TWO_D, false>(a, s);
-  }
-  const size_t smem = PIPE ? (size_t)(2 * (nrows_a + BN)) * CKP * sizeof(float)
-                           : (size_t)((a.taps == 1 ? TGMAX : 1) * nrows_a + TGMAX * BN) * CKP * sizeof(float);
+  size_t smem = (size_t)(nrows_a + (PIPE ? 2 : 1) * BN) * CKP * sizeof(float);
+  smem = std::max(smem, (size_t)4 * 32 * 33 * sizeof(float));  // epilogue staging slots (2x2-per-wave tiles)
   if (smem > 160 * 1024) return hipErrorInvalidValue;
   const int vec_a = ((a.ldx & 3) == 0) && ((reinterpret_cast<uintptr_t>(a.x) & 15) == 0) &&
                     ((a.x_bs & 3) == 0) && ((a.x_bs2 & 3) == 0);
@@ -443,7 +417,7 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
                     ((a.w_bs & 3) == 0) && ((a.w_bs2 & 3) == 0) && ((a.w_ts & 3) == 0);
   if (a.batch_inner < 1) return hipErrorInvalidValue;
   int ksplit = 1;
-  if (a.ws && a.ksplit > 1) ksplit = a.ksplit;
+  if (!PIPE && a.ws && a.ksplit > 1) ksplit = a.ksplit;
   dim3 grid(mtiles, (a.N + BN - 1) / BN, a.batch * a.batch_inner * ksplit);
   auto kern = conv_gemm_kernel<BM, BN, WM, WN, TWO_D, PIPE>;
   if (smem > 64 * 1024) {
@@ -470,32 +444,34 @@ hipError_t launch_forced(const ConvArgs& a, hipStream_t s) {
     case 3: return launch_cfg<64, 64, 2, 2, TWO_D, PIPE>(a, s);
     case 4: return launch_cfg<128, 128, 2, 2, TWO_D, PIPE>(a, s);
     case 5: return launch_cfg<64, 128, 2, 2, TWO_D, PIPE>(a, s);
+    case 6: return launch_cfg<256, 64, 4, 1, TWO_D, PIPE>(a, s);
     default: return hipErrorInvalidValue;
   }
 }
 
-// Tile choice measured on MI355X (build/bench_conv): one 32x32 accumulator per wave with 4 waves
-// per block (128x32 or 64x64 tiles) beats larger per-wave tiles on every RVC shape (more resident
-// waves hide the LDS/staging latency); split-K when the output-tile grid cannot fill 256 CUs.
+// Tile per shape class, measured on MI355X (same-box A/B of the whole pipeline, tools/ab_policy.sh):
+// one 32x32 accumulator per wave with 4 waves per block (128x32 for N <= 32, 64x64 otherwise) beats
+// the larger per-wave tiles in the pipeline; split-K when the output grid cannot fill 256 CUs.
+// RVCX_CFG_LONG / RVCX_CFG_SHORT / RVCX_CFG_NARROW override a class (measurement aid).
+inline int env_cfg(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
 template <bool TWO_D>
 int pick_cfg(const ConvArgs& a) {
   if (a.force_cfg >= 0) return a.force_cfg;
-  return a.N <= 32 ? 1 : 3;
+  static const int c_long = env_cfg("RVCX_CFG_LONG", 3);      // 1-D, taps >= 5, N > 32
+  static const int c_short = env_cfg("RVCX_CFG_SHORT", 3);    // everything else with N > 32
+  static const int c_narrow = env_cfg("RVCX_CFG_NARROW", 1);  // N <= 32
+  if (a.N <= 32) return c_narrow;
+  if (!TWO_D && a.taps >= 5) return c_long;
+  return c_short;
 }
 
 inline void cfg_tile(int cfg, int& BM, int& BN) {
-  static const int t[6][2] = {{256, 32}, {128, 32}, {128, 64}, {64, 64}, {128, 128}, {64, 128}};
+  static const int t[7][2] = {{256, 32}, {128, 32}, {128, 64}, {64, 64}, {128, 128}, {64, 128}, {256, 64}};
   BM = t[cfg][0];
   BN = t[cfg][1];
-}
-
-// RVCX_CONV_PIPE=0/1 overrides the default loop variant (measurement aid)
-inline bool default_pipe() {
-  static const int v = [] {
-    const char* e = std::getenv("RVCX_CONV_PIPE");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v != 0;
 }
 
 template <bool TWO_D>
@@ -505,8 +481,18 @@ hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
   const int cfg = pick_cfg<TWO_D>(a);
   ConvArgs b = a;
   b.force_cfg = cfg;
-  if (a.pipe > 0 || (a.pipe == 0 && default_pipe())) return launch_forced<TWO_D, true>(b, s);
-  return launch_forced<TWO_D, false>(b, s);
+  const bool pipe = a.pipe > 0 && a.force_cfg >= 0;
+  hipError_t e = pipe ? launch_forced<TWO_D, true>(b, s) : launch_forced<TWO_D, false>(b, s);
+  if (e == hipErrorInvalidValue && a.force_cfg < 0) {
+    // the chosen tile's halo does not fit in LDS (long strided taps): fall back to smaller tiles
+    for (int alt : {3, 1}) {
+      if (alt == cfg) continue;
+      b.force_cfg = alt;
+      e = launch_forced<TWO_D, false>(b, s);
+      if (e != hipErrorInvalidValue) break;
+    }
+  }
+  return e;
 }
 
 }  // namespace

@@ -10,6 +10,7 @@
 namespace rvcx {
 
 namespace {
+constexpr long long HAR_PAD = 64;  // >= max(noise-conv pad, stride - pad) of every stage
 
 uint64_t splitmix(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
@@ -236,7 +237,19 @@ void finalize_synth(Ctx& c) {
     for (int j = i + 1; j < nu; ++j) stride *= g.ups[j];
     const int kern = stride == 1 ? 1 : stride * 2 - stride % 2;
     const std::string nn = "dec.noise_convs." + std::to_string(i);
-    c.alloc_weight(nn + ".w", get(c, M, nn + ".weight", {cout, 1, kern}).v);
+    // framed form for the implicit GEMM: the source is read as rows of `stride` samples, so the
+    // kern = 2*stride conv becomes 2 taps x stride channels: wf[tap][co][ci] = w[co][0][tap*stride + ci]
+    // (kern = 1 when stride = 1: one tap, one channel)
+    const HostTensor& wn = get(c, M, nn + ".weight", {cout, 1, kern});
+    const int ntap = kern == 1 ? 1 : 2;
+    std::vector<float> wf((size_t)ntap * cout * stride, 0.f);
+    for (int tp = 0; tp < ntap; ++tp)
+      for (int co = 0; co < cout; ++co)
+        for (int ci = 0; ci < stride; ++ci) {
+          const int kk = tp * stride + ci;
+          if (kk < kern) wf[((size_t)tp * cout + co) * stride + ci] = wn.v[(size_t)co * kern + kk];
+        }
+    c.alloc_weight(nn + ".wf", wf);
     c.alloc_weight(nn + ".b", get(c, M, nn + ".bias", {cout}).v);
   }
   const int nk = (int)g.rb_k.size();
@@ -266,11 +279,14 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
   const int I = cf.I, C0 = cf.C0, upp = cf.upp();
   const long long Nh = (long long)T * upp;
   // NSF source (SineGen + l_linear + tanh)
-  float* har = c.buf<float>("dec.har", (size_t)B * Nh, s);
+  // har rows carry HAR_PAD zeros on both sides so every framed noise-conv read stays in its row
+  const long long har_ld = Nh + 2 * HAR_PAD;
+  float* har = c.buf<float>("dec.har", (size_t)(B * har_ld), s);
+  RVCX_HIP(hipMemsetAsync(har, 0, sizeof(float) * (size_t)(B * har_ld), s));
   double* cum = c.buf<double>("dec.cum", (size_t)B * T, s);
   const auto& lin_wb = c.host[0].at("__src_lin__").v;
   check(sine_source(f0, B, T, upp, (float)cf.sr, eps_src, splitmix(seed ^ 0x5352434e4f495345ull), lin_wb[0],
-                    lin_wb[1], cum, har, s),
+                    lin_wb[1], cum, har + HAR_PAD, har_ld, s),
         "sine_source");
   // conv_pre + cond(g)
   float* cv = c.buf<float>("dec.cvec", (size_t)B * C0, s);
@@ -309,15 +325,22 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
     a.pre_act = ACT_LRELU;
     a.pre_slope = 0.1f;
     run(c, a, s, 2.0 * B * curT * (double)Cin * C * L.k);
-    // + noise_convs[i](har)
-    int stride = 1;
-    for (size_t j = i + 1; j < cf.ups.size(); ++j) stride *= cf.ups[j];
-    const int kern = stride == 1 ? 1 : stride * 2 - stride % 2;
-    const int npad = stride == 1 ? 0 : (kern - stride) / 2;
-    const std::string nn = "dec.noise_convs." + std::to_string(i);
-    check(noise_conv_add(har, (int)Nh, y, B, Ti, C, (long long)Ti * C, c.W(nn + ".w"), c.W(nn + ".b"), kern, stride,
-                         npad, s),
-          "noise_conv_add");
+    // + noise_convs[i](har) (hifigan_nsf.py:196-199): framed implicit GEMM, accumulated into y
+    {
+      int stride = 1;
+      for (size_t j = i + 1; j < cf.ups.size(); ++j) stride *= cf.ups[j];
+      const int kern = stride == 1 ? 1 : stride * 2 - stride % 2;
+      const int npad = stride == 1 ? 0 : (kern - stride) / 2;
+      const int ntap = kern == 1 ? 1 : 2;
+      if (npad > HAR_PAD || ntap * stride - npad > HAR_PAD + stride)
+        throw Error(RVCX_E_SHAPE, "noise conv stride too large for the source padding");
+      const std::string nn = "dec.noise_convs." + std::to_string(i);
+      ConvArgs an = conv(har + HAR_PAD - npad, stride, Ti + ntap - 1, stride, c.W(nn + ".wf"), C, ntap, 1, 0,
+                         c.W(nn + ".b"), y, C, Ti, B);
+      an.x_bs = har_ld;
+      an.acc_mode = ACC_ADD;
+      run(c, an, s, 2.0 * B * (double)Ti * C * kern);
+    }
     // mean of the ResBlocks (residuals.py:71-80) accumulated into S. `cur` (= xin) is dead once the
     // ConvTranspose above has consumed it, so S reuses it and becomes the next stage's input.
     float* S = xin;

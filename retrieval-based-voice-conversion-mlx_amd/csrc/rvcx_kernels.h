@@ -120,9 +120,7 @@ hipError_t softmax_rows(float* scores, int rows, int cols, hipStream_t s);
 hipError_t upsample2_protect(const float* feats, int L, int D, float* out, int T, const float* pitchf, float protect,
                              hipStream_t s);
 hipError_t sine_source(const float* f0, int B, int L, int upp, float sr, const float* eps, uint64_t seed,
-                       float lin_w, float lin_b, double* cum_ws, float* har, hipStream_t s);
-hipError_t noise_conv_add(const float* har, int Nh, float* y, int B, int T, int C, long long y_bs,
-                          const float* w, const float* b, int K, int stride, int pad, hipStream_t s);
+                       float lin_w, float lin_b, double* cum_ws, float* har, long long har_ld, hipStream_t s);
 hipError_t conv_post_tanh(const float* x, int B, int T, int C, const float* w, int K, float slope, float* y,
                           hipStream_t s);
 hipError_t randn(float* y, long long n, uint64_t seed, uint64_t offset, hipStream_t s);

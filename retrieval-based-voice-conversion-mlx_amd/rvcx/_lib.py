@@ -105,6 +105,8 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "rvcx_rmvpe_decode": (i32, [vp, vp, i64, f32, vp, vp]),
     }
     for name, (res, args) in sig.items():
+        if not hasattr(lib, name):  # reported by exported_symbols(); an older build lacks newer entry points
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
