@@ -51,6 +51,10 @@ struct Case {
 
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 20;
+  // bench_conv ITERS CASE CFG: time one case with one forced config, no checks (for PMC passes)
+  const int only_case = argc > 3 ? atoi(argv[2]) : -1;
+  const int only_cfg = argc > 3 ? atoi(argv[3]) : -2;
+  if (only_case < 0) {
   // correctness on a small shape for every forced config x pipe
   {
     const int T = 1000, C = 128, N = 128, taps = 7, dil = 3, pad = (taps * dil - dil) / 2;
@@ -134,6 +138,7 @@ int main(int argc, char** argv) {
       (void)hipFree(ws);
     }
   }
+  }
   // timing
   std::vector<Case> cases = {
       {"gen.s1 C256 k11 d5", 18600, 256, 256, 11, 5}, {"gen.s2 C128 k3 d1", 186000, 128, 128, 3, 1},
@@ -144,7 +149,9 @@ int main(int argc, char** argv) {
       {"hubert ffn2 775x3072->768", 775, 3072, 768, 1, 1}, {"te ffn1 1550 k3 192->768", 1550, 192, 768, 3, 1},
       {"te qkv 1550x192->576", 1550, 192, 576, 1, 1}, {"flow in 1550 k5 192->384", 1550, 192, 384, 5, 1},
   };
-  for (auto& cs : cases) {
+  for (size_t ci = 0; ci < cases.size(); ++ci) {
+    if (only_case >= 0 && (int)ci != only_case) continue;
+    auto& cs = cases[ci];
     const size_t nx = (size_t)cs.T * cs.Cin, nw = (size_t)cs.taps * cs.N * cs.Cin, ny = (size_t)cs.T * cs.N;
     float *x, *w, *b, *y;
     CK_(hipMalloc(&x, nx * 4));
@@ -158,18 +165,20 @@ int main(int argc, char** argv) {
     CK_(hipMemcpy(w, hw.data(), nw * 4, hipMemcpyHostToDevice));
     CK_(hipMemset(b, 0, cs.N * 4));
     const double flops = 2.0 * cs.T * cs.N * (double)cs.Cin * cs.taps;
-    double best[8] = {0};
+    double best[2][8] = {{0}};
     int ksp[8] = {0};
-    for (int round = 0; round < 3; ++round)
+    for (int round = 0; round < (only_case >= 0 ? 1 : 3); ++round)
     for (int cfg : {-1, 0, 1, 2, 3, 4, 5, 6})
-      for (int pipe : {-1}) {
+      for (int asb : {1, 4}) {
+        const int pipe = -1;
+        if (only_case >= 0 && (cfg != only_cfg % 10 || asb != (only_cfg >= 10 ? 4 : 1))) continue;
         ConvArgs a;
         a.x = x; a.ldx = cs.Cin; a.T_in = cs.T; a.C_in = cs.Cin;
         a.w = w; a.ldw = cs.Cin; a.w_ts = (long long)cs.N * cs.Cin; a.taps = cs.taps; a.dil = cs.dil;
         a.pad = (cs.taps * cs.dil - cs.dil) / 2;
         a.y = y; a.ldy = cs.N; a.T_out = cs.T; a.N = cs.N; a.bias = b;
         a.pre_act = ACT_LRELU; a.pre_slope = 0.1f; a.act = ACT_LRELU; a.slope = 0.1f;
-        a.force_cfg = cfg; a.pipe = pipe;
+        a.force_cfg = cfg; a.pipe = pipe; a.astage = asb;
         float* wsp = nullptr;
         if (cfg < 0) {
           const long long need = conv_plan_splitk(a, false);
@@ -189,13 +198,15 @@ int main(int argc, char** argv) {
         CK_(hipEventElapsedTime(&ms, e0, e1));
         ms /= iters;
         const double tf = flops / ms / 1e9;
-        if (tf > best[cfg + 1]) best[cfg + 1] = tf;
+        if (tf > best[asb == 4][cfg + 1]) best[asb == 4][cfg + 1] = tf;
         ksp[cfg + 1] = a.ksplit;
         if (wsp) (void)hipFree(wsp);
       }
-    printf("%-28s", cs.name);
-    for (int c = 0; c < 8; ++c) printf(" %2d:%6.1f%s", c - 1, best[c], ksp[c] > 1 ? "*" : " ");
-    printf("\n");
+    for (int v = 0; v < 2; ++v) {
+      printf("%-24s asb%d", cs.name, v ? 4 : 1);
+      for (int c = 0; c < 8; ++c) printf(" %2d:%6.1f%s", c - 1, best[v][c], ksp[c] > 1 ? "*" : " ");
+      printf("\n");
+    }
     (void)hipFree(x); (void)hipFree(w); (void)hipFree(b); (void)hipFree(y);
   }
   return 0;

@@ -69,7 +69,7 @@ __device__ __forceinline__ void epilogue_store(const ConvArgs& a, float v, float
   *dst = v;
 }
 
-template <int BM, int BN, int WM, int WN, bool TWO_D, bool PIPE>
+template <int BM, int BN, int WM, int WN, bool TWO_D, bool PIPE, int ASB>
 __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a, const int nrows_a, const int rw,
                                                              const int rh, const int tiles_w, const int vec_a,
                                                              const int vec_b, const int ksplit) {
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
     }
   };
   // A tile: nrows_a x 32 channels of chunk c0 -> LDS, pre-activation applied, zero outside the input
-  auto stage_a = [&](int c0) {
+  auto stage_a_serial = [&](int c0) {
     for (int idx = tid; idx < nrows_a * (CK / 4); idx += NTHREADS) {
       const int r = idx >> 3;
       const int c4 = (idx & 7) << 2;
@@ -218,6 +218,70 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
         }
       }
       *reinterpret_cast<f32x4*>(&As[r * CKP + c4]) = v;
+    }
+  };
+  // batched staging: ASB float4 loads per thread in flight before the first wait, then the transform
+  auto stage_a = [&](int c0) {
+    if constexpr (ASB <= 1) {
+      stage_a_serial(c0);
+    } else {
+      const int total = nrows_a * (CK / 4);
+      for (int base = 0; base < total; base += ASB * NTHREADS) {
+        f32x4 rv[ASB];
+        float mk[ASB];
+#pragma unroll
+        for (int q = 0; q < ASB; ++q) {
+          const int idx = base + tid + q * NTHREADS;
+          rv[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+          mk[q] = 0.f;
+          if (idx < total) {
+            const int r = idx >> 3;
+            const int c = c0 + ((idx & 7) << 2);
+            long long grow;
+            bool valid;
+            if (!TWO_D) {
+              const int g = row0 + r;
+              valid = (g >= 0) && (g < a.T_in);
+              grow = g;
+            } else {
+              const int ah = r / aw, awi = r - ah * aw;
+              const int gh = h0 - a.padh + ah, gw = w0 - a.padw + awi;
+              valid = (gh >= 0) && (gh < a.T_in) && (gw >= 0) && (gw < a.W_in);
+              grow = (long long)gh * a.W_in + gw;
+            }
+            if (valid && c < a.C_in) {
+              mk[q] = PM ? PM[grow] : 1.f;
+              const float* src = X + grow * a.ldx + c;
+              if (vec_a && c + 4 <= a.C_in) {
+                rv[q] = *reinterpret_cast<const f32x4*>(src);
+              } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) rv[q][j] = (c + j < a.C_in) ? src[j] : 0.f;
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < ASB; ++q) {
+          const int idx = base + tid + q * NTHREADS;
+          if (idx < total) {
+            f32x4 v = rv[q];
+            if (mk[q] != 0.f) {
+              if (a.pre_act != ACT_NONE) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = act_fn(v[j], a.pre_act, a.pre_slope);
+              }
+              if (PM) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] *= mk[q];
+              }
+            } else {
+              v = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+            *reinterpret_cast<f32x4*>(&As[(idx >> 3) * CKP + ((idx & 7) << 2)]) = v;
+          }
+        }
+      }
     }
   };
   auto compute = [&](const float* Bs, int tap) {
@@ -395,7 +459,7 @@ struct TileCfg {
   int BM, BN;
 };
 
-template <int BM, int BN, int WM, int WN, bool TWO_D, bool PIPE = false>
+template <int BM, int BN, int WM, int WN, bool TWO_D, bool PIPE = false, int ASB = 1>
 hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
   int nrows_a, rw = 0, rh = 0, tiles_w = 1, mtiles;
   if (!TWO_D) {
@@ -419,7 +483,7 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
   int ksplit = 1;
   if (!PIPE && a.ws && a.ksplit > 1) ksplit = a.ksplit;
   dim3 grid(mtiles, (a.N + BN - 1) / BN, a.batch * a.batch_inner * ksplit);
-  auto kern = conv_gemm_kernel<BM, BN, WM, WN, TWO_D, PIPE>;
+  auto kern = conv_gemm_kernel<BM, BN, WM, WN, TWO_D, PIPE, ASB>;
   if (smem > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
@@ -435,18 +499,34 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <bool TWO_D, bool PIPE>
-hipError_t launch_forced(const ConvArgs& a, hipStream_t s) {
+template <bool TWO_D, bool PIPE, int ASB>
+hipError_t launch_forced_asb(const ConvArgs& a, hipStream_t s) {
   switch (a.force_cfg) {
-    case 0: return launch_cfg<256, 32, 4, 1, TWO_D, PIPE>(a, s);
-    case 1: return launch_cfg<128, 32, 4, 1, TWO_D, PIPE>(a, s);
-    case 2: return launch_cfg<128, 64, 2, 2, TWO_D, PIPE>(a, s);
-    case 3: return launch_cfg<64, 64, 2, 2, TWO_D, PIPE>(a, s);
-    case 4: return launch_cfg<128, 128, 2, 2, TWO_D, PIPE>(a, s);
-    case 5: return launch_cfg<64, 128, 2, 2, TWO_D, PIPE>(a, s);
-    case 6: return launch_cfg<256, 64, 4, 1, TWO_D, PIPE>(a, s);
+    case 0: return launch_cfg<256, 32, 4, 1, TWO_D, PIPE, ASB>(a, s);
+    case 1: return launch_cfg<128, 32, 4, 1, TWO_D, PIPE, ASB>(a, s);
+    case 2: return launch_cfg<128, 64, 2, 2, TWO_D, PIPE, ASB>(a, s);
+    case 3: return launch_cfg<64, 64, 2, 2, TWO_D, PIPE, ASB>(a, s);
+    case 4: return launch_cfg<128, 128, 2, 2, TWO_D, PIPE, ASB>(a, s);
+    case 5: return launch_cfg<64, 128, 2, 2, TWO_D, PIPE, ASB>(a, s);
+    case 6: return launch_cfg<256, 64, 4, 1, TWO_D, PIPE, ASB>(a, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+// A-tile staging: serial (1) or 4 loads in flight per thread (4); RVCX_CONV_ASB overrides the default
+inline int default_asb() {
+  static const int v = [] {
+    const char* e = std::getenv("RVCX_CONV_ASB");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+
+template <bool TWO_D, bool PIPE>
+hipError_t launch_forced(const ConvArgs& a, hipStream_t s) {
+  const int asb = a.astage > 0 ? a.astage : default_asb();
+  if (!PIPE && asb >= 4) return launch_forced_asb<TWO_D, false, 4>(a, s);
+  return launch_forced_asb<TWO_D, PIPE, 1>(a, s);
 }
 
 // Tile per shape class, measured on MI355X (same-box A/B of the whole pipeline, tools/ab_policy.sh):

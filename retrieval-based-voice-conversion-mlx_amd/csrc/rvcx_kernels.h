@@ -90,6 +90,7 @@ struct ConvArgs {
   // tuning / benchmarking: force a tile configuration (0..5) and the software pipeline on/off
   int force_cfg = -1;
   int pipe = 0;
+  int astage = 0;  // A-tile staging batch: 0 = default (RVCX_CONV_ASB or 1), 1 = serial, 4 = 4 loads in flight
   // split-K: set by conv_plan_splitk; ws holds ksplit partial [rows][N] tiles per batch entry
   int ksplit = 1;
   int no_splitk = 0;
