@@ -107,13 +107,15 @@ int rvcx_synth_infer(rvcx_ctx* ctx, int B, int T, const float* d_phone, const in
 int rvcx_dec_only(rvcx_ctx* ctx, int B, int T, const float* d_z, const float* d_f0, const int32_t* d_sid,
                   const float* d_eps_src, uint64_t seed, float* d_out, void* stream);
 
-/* Pipeline.voice_conversion on one padded chunk (rvc/infer/pipeline.py:293-376 with index_rate = 0;
- * rvc_mlx/infer/pipeline_mlx.py:166-261): HuBERT -> x2 nearest upsample -> protect blend ->
- * Synthesizer.infer, all on device. d_audio [n] @16 kHz (already filtered and padded);
- * d_pitch/d_pitchf [>= n/160]. Output out [p_len*upp], p_len = min(n/160, 2L). */
+/* Pipeline.voice_conversion on one padded chunk (rvc/infer/pipeline.py:293-376;
+ * rvc_mlx/infer/pipeline_mlx.py:166-261): HuBERT -> [speaker-embedding retrieval from the loaded
+ * feature index when index_rate > 0] -> x2 nearest upsample -> protect blend -> Synthesizer.infer,
+ * all on device. d_audio [n] @16 kHz (already filtered and padded); d_pitch/d_pitchf [>= n/160].
+ * Output out [p_len*upp], p_len = min(n/160, 2L). */
 int rvcx_voice_conversion(rvcx_ctx* ctx, const float* d_audio, int64_t n, const int32_t* d_pitch,
-                          const float* d_pitchf, int sid, float protect, const float* d_eps_z, const float* d_eps_src,
-                          uint64_t seed, float* d_out, int64_t cap, int64_t* n_out, void* stream);
+                          const float* d_pitchf, int sid, float protect, double index_rate, const float* d_eps_z,
+                          const float* d_eps_src, uint64_t seed, float* d_out, int64_t cap, int64_t* n_out,
+                          void* stream);
 
 /* Pipeline high-pass (rvc/infer/pipeline.py:22-27: signal.butter(5, 48, 'high', fs=16000)) as
  * transfer-function coefficients b[order+1], a[order+1] and lfilter_zi(b, a) zi[order]; used by
@@ -138,6 +140,8 @@ typedef struct {
   double volume_envelope;           /* AudioProcessor.change_rms rate; 1 = off (pipeline.py:545-549) */
   int mlx_semantics;                /* 1: f0 adjustments as rvc_mlx PipelineMLX.get_f0 (pipeline_mlx.py:135-164):
                                        autotune skips f0 <= 0 and the pitch shift is applied after it */
+  double index_rate;                /* speaker-embedding retrieval blend (pipeline.py:338-342, :378-388); 0 = off;
+                                       > 0 needs rvcx_index_load */
 } rvcx_pipeline_opts;
 
 /* Defaults of the rvc/ Config (x_pad 1, x_query 6, x_center 38, x_max 41; rvc/configs/config.py) at
@@ -168,6 +172,29 @@ int rvcx_pipeline(rvcx_ctx* ctx, const double* d_audio, int64_t n, int sid, doub
  * summed ALGORITHMIC FLOPs of those launches and the launch count, then clears the record. */
 int rvcx_profile(rvcx_ctx* ctx, int enable);
 int rvcx_profile_read(rvcx_ctx* ctx, double* total_ms, double* total_flops, int64_t* launches);
+
+/* ---------------------------------------------------------------- feature index (FAISS IndexIVFFlat)
+ * The bytes of a faiss .index file (IndexIVFFlat over IndexFlatL2, METRIC_L2, ArrayInvertedLists;
+ * faiss 1.7.4 write_index layout). Replaces faiss.read_index + index.reconstruct_n(0, ntotal) at
+ * rvc/infer/pipeline.py:430-434 (rvc_mlx/infer/pipeline_mlx.py:267-278). The lists, centroids and ids
+ * are kept in HBM; nprobe comes from the file. ids must be a permutation of 0..ntotal-1 (RVC indexes). */
+int rvcx_index_load(rvcx_ctx* ctx, const void* bytes, int64_t nbytes);
+int rvcx_index_unload(rvcx_ctx* ctx);
+/* RVCX_E_STATE when no index is loaded. */
+int rvcx_index_info(const rvcx_ctx* ctx, int64_t* d, int64_t* ntotal, int64_t* nlist, int64_t* nprobe);
+/* faiss.extract_index_ivf(index).nprobe = nprobe (clamped to nlist). */
+int rvcx_index_set_nprobe(rvcx_ctx* ctx, int64_t nprobe);
+/* index.search(x, k) (IndexIVF::search, L2; used at pipeline.py:380 with k = 8): d_x [n][d] fp32 ->
+ * d_dist [n][k] fp32 squared L2, d_ids [n][k] int64, ordered by (distance, id), (+inf, -1) padding. k <= 16. */
+int rvcx_index_search(rvcx_ctx* ctx, const float* d_x, int64_t n, int k, float* d_dist, int64_t* d_ids,
+                      void* stream);
+/* index.reconstruct_n(i0, ni) -> d_out [ni][d] (big_npy rows, pipeline.py:434). */
+int rvcx_index_reconstruct_n(rvcx_ctx* ctx, int64_t i0, int64_t ni, float* d_out, void* stream);
+/* Pipeline._retrieve_speaker_embeddings (pipeline.py:378-388): d_feats [L][d] -> d_out [L][d] =
+ * index_rate * sum_j w_j big_npy[ix_j] + (1 - index_rate) * feats, w = (1/dist)^2 normalised, k = 8,
+ * with numpy/torch float32 rounding. */
+int rvcx_index_retrieve(rvcx_ctx* ctx, const float* d_feats, int64_t L, int d, double index_rate, float* d_out,
+                        void* stream);
 
 /* Upsampling factor of the loaded synthesizer (prod(upsample_rates); net_g.dec.upp). */
 int rvcx_synth_upp(const rvcx_ctx* ctx);

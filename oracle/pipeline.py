@@ -99,12 +99,21 @@ class OraclePipeline:
         self.last["f0_raw"], self.last["hidden"] = f0.copy(), hidden
         return post_f0(f0, pitch, f0_autotune, f0_autotune_strength, proposed_pitch, proposed_pitch_threshold)
 
-    def voice_conversion(self, sid, audio0, pitch, pitchf, protect, version="v2"):
-        """pipeline.py:293-376 (index retrieval off: index_rate == 0)."""
+    def voice_conversion(self, sid, audio0, pitch, pitchf, protect, version="v2", index=None, index_rate=0.0):
+        """pipeline.py:293-376; ``index`` is an oracle.ivf.IvfFlat (faiss restatement), used when index_rate > 0."""
         with torch.no_grad():
             feats = torch.from_numpy(audio0).float().view(1, -1)
             feats = ohubert.hubert_forward(self.hw, self.hc, feats, version)
             feats0 = feats.clone()
+            if index is not None and index_rate > 0:  # pipeline.py:338-342, :378-388
+                from oracle import ivf
+
+                big_npy = ivf.reconstruct_n(index, 0, index.ntotal)
+                npy = feats[0].numpy()
+                score, ix = ivf.search(index, npy, 8)
+                self.last.setdefault("index_search", []).append((score, ix))
+                feats = torch.from_numpy(ivf.retrieve_speaker_embeddings(npy, score, ix, big_npy,
+                                                                         index_rate)).unsqueeze(0)
             feats = F.interpolate(feats.permute(0, 2, 1), scale_factor=2).permute(0, 2, 1)
             p_len = min(audio0.shape[0] // self.window, feats.shape[1])
             feats0 = F.interpolate(feats0.permute(0, 2, 1), scale_factor=2).permute(0, 2, 1)
@@ -123,8 +132,10 @@ class OraclePipeline:
             return o[0, 0].float().numpy()
 
     def pipeline(self, sid, audio, pitch=0, protect=0.33, volume_envelope=1.0, f0_autotune=False,
-                 f0_autotune_strength=1.0, proposed_pitch=False, proposed_pitch_threshold=155.0):
-        """pipeline.py:390-558 with pitch_guidance=True, file_index unset."""
+                 f0_autotune_strength=1.0, proposed_pitch=False, proposed_pitch_threshold=155.0, index=None,
+                 index_rate=0.0):
+        """pipeline.py:390-558 with pitch_guidance=True; ``index`` = the parsed file_index (oracle.ivf)."""
+        vc_kw = dict(index=index, index_rate=index_rate)
         audio = signal.filtfilt(BH, AH, audio)
         audio_pad = np.pad(audio, (self.window // 2, self.window // 2), mode="reflect")
         opt_ts = []
@@ -152,12 +163,14 @@ class OraclePipeline:
             audio_opt.append(self.voice_conversion(
                 sid_t, audio_pad[s:t + self.t_pad2 + self.window],
                 pitch_t[:, s // self.window:(t + self.t_pad2) // self.window],
-                pitchf_t[:, s // self.window:(t + self.t_pad2) // self.window], protect)[self.t_pad_tgt:-self.t_pad_tgt])
+                pitchf_t[:, s // self.window:(t + self.t_pad2) // self.window], protect,
+                **vc_kw)[self.t_pad_tgt:-self.t_pad_tgt])
             s = t
         audio_opt.append(self.voice_conversion(
             sid_t, audio_pad[t:] if t is not None else audio_pad,
             pitch_t[:, t // self.window:] if t is not None else pitch_t,
-            pitchf_t[:, t // self.window:] if t is not None else pitchf_t, protect)[self.t_pad_tgt:-self.t_pad_tgt])
+            pitchf_t[:, t // self.window:] if t is not None else pitchf_t, protect,
+            **vc_kw)[self.t_pad_tgt:-self.t_pad_tgt])
         audio_opt = np.concatenate(audio_opt)
         if volume_envelope != 1:
             audio_opt = change_rms(audio, self.sample_rate, audio_opt, self.tgt_sr, volume_envelope)

@@ -311,7 +311,11 @@ hipError_t softmax_rows(float* scores, int rows, int cols, hipStream_t s) {
 // ------------------------------------------------------------------ feature x2 upsample + protect blend
 // pipeline.py:344-362: feats = interpolate(x2, nearest); pitchff = 1 if pitchf > 0 else protect;
 // feats = feats * pitchff + feats0 * (1 - pitchff)   (feats0 == feats without index retrieval).
-__global__ void k_up2(const float* feats, int L, int D, float* out, int T, const float* pitchf, float protect) {
+// x2 nearest upsample + protect blend (pipeline.py:344-362): feats = retrieved (or raw) features,
+// feats0 = raw features; v = feats * p + feats0 * (1 - p) with each product and the sum rounded (torch).
+#pragma clang fp contract(off)
+__global__ void k_up2(const float* feats, const float* feats0, int L, int D, float* out, int T, const float* pitchf,
+                      float protect) {
   const long long n = (long long)T * D;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     const int t = (int)(i / D), c = (int)(i % D);
@@ -321,14 +325,16 @@ __global__ void k_up2(const float* feats, int L, int D, float* out, int T, const
     if (pitchf) {
       const float pf = pitchf[t];
       const float p = pf > 0.f ? 1.f : (pf < 1.f ? protect : pf);
-      v = f * p + f * (1.f - p);
+      v = f * p + feats0[(long long)src * D + c] * (1.f - p);
     }
     out[i] = v;
   }
 }
-hipError_t upsample2_protect(const float* feats, int L, int D, float* out, int T, const float* pitchf, float protect,
-                             hipStream_t s) {
-  hipLaunchKernelGGL(k_up2, dim3(nblocks((long long)T * D)), dim3(TB), 0, s, feats, L, D, out, T, pitchf, protect);
+#pragma clang fp contract(on)
+hipError_t upsample2_protect(const float* feats, const float* feats0, int L, int D, float* out, int T,
+                             const float* pitchf, float protect, hipStream_t s) {
+  hipLaunchKernelGGL(k_up2, dim3(nblocks((long long)T * D)), dim3(TB), 0, s, feats, feats0, L, D, out, T, pitchf,
+                     protect);
   return hipGetLastError();
 }
 

@@ -244,14 +244,16 @@ int rvcx_dec_only(rvcx_ctx* ctx, int B, int T, const float* d_z, const float* d_
 }
 
 int rvcx_voice_conversion(rvcx_ctx* ctx, const float* d_audio, int64_t n, const int32_t* d_pitch,
-                          const float* d_pitchf, int sid, float protect, const float* d_eps_z, const float* d_eps_src,
-                          uint64_t seed, float* d_out, int64_t cap, int64_t* n_out, void* stream) {
+                          const float* d_pitchf, int sid, float protect, double index_rate, const float* d_eps_z,
+                          const float* d_eps_src, uint64_t seed, float* d_out, int64_t cap, int64_t* n_out,
+                          void* stream) {
   return guard(ctx, [&] {
     if (!ctx->ready[0] || !ctx->ready[1]) throw Error(RVCX_E_STATE, "synthesizer/hubert not finalized");
     if (!d_audio || !d_pitch || !d_pitchf || !d_out || n <= 0) throw Error(RVCX_E_INVALID, "bad arguments");
     set_device(ctx);
-    const int64_t no = vc_forward(*ctx, d_audio, n, d_pitch, d_pitchf, n / 160, sid, protect, d_eps_z, d_eps_src,
-                                  seed, d_out, cap, static_cast<hipStream_t>(stream));
+    if (index_rate > 0 && !ctx->ivf) throw Error(RVCX_E_STATE, "index_rate > 0 but no feature index loaded");
+    const int64_t no = vc_forward(*ctx, d_audio, n, d_pitch, d_pitchf, n / 160, sid, protect, index_rate, d_eps_z,
+                                  d_eps_src, seed, d_out, cap, static_cast<hipStream_t>(stream));
     if (n_out) *n_out = no;
   });
 }
@@ -326,3 +328,65 @@ int rvcx_profile_read(rvcx_ctx* ctx, double* total_ms, double* total_flops, int6
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------ feature index (FAISS IVFFlat)
+int rvcx_index_load(rvcx_ctx* ctx, const void* bytes, int64_t nbytes) {
+  return guard(ctx, [&] {
+    if (!bytes || nbytes <= 0) throw Error(RVCX_E_INVALID, "index_load: empty buffer");
+    set_device(ctx);
+    index_load(*ctx, static_cast<const uint8_t*>(bytes), nbytes);
+  });
+}
+
+int rvcx_index_unload(rvcx_ctx* ctx) {
+  return guard(ctx, [&] {
+    set_device(ctx);
+    RVCX_HIP(hipDeviceSynchronize());
+    ctx->ivf.reset();
+  });
+}
+
+int rvcx_index_info(const rvcx_ctx* ctx, int64_t* d, int64_t* ntotal, int64_t* nlist, int64_t* nprobe) {
+  if (!ctx) return RVCX_E_INVALID;
+  if (!ctx->ivf) return RVCX_E_STATE;
+  const IvfView& v = ctx->ivf->view;
+  if (d) *d = v.d;
+  if (ntotal) *ntotal = v.ntotal;
+  if (nlist) *nlist = v.nlist;
+  if (nprobe) *nprobe = v.nprobe;
+  return RVCX_OK;
+}
+
+int rvcx_index_set_nprobe(rvcx_ctx* ctx, int64_t nprobe) {
+  return guard(ctx, [&] {
+    if (!ctx->ivf) throw Error(RVCX_E_STATE, "no feature index loaded");
+    if (nprobe < 1) throw Error(RVCX_E_INVALID, "nprobe must be >= 1");
+    ctx->ivf->view.nprobe = (int)std::min<int64_t>(nprobe, ctx->ivf->view.nlist);
+  });
+}
+
+int rvcx_index_search(rvcx_ctx* ctx, const float* d_x, int64_t n, int k, float* d_dist, int64_t* d_ids,
+                      void* stream) {
+  return guard(ctx, [&] {
+    if ((!d_x && n > 0) || !d_dist || !d_ids || n < 0) throw Error(RVCX_E_INVALID, "index_search: bad arguments");
+    set_device(ctx);
+    index_search(*ctx, d_x, n, k, d_dist, d_ids, static_cast<hipStream_t>(stream));
+  });
+}
+
+int rvcx_index_reconstruct_n(rvcx_ctx* ctx, int64_t i0, int64_t ni, float* d_out, void* stream) {
+  return guard(ctx, [&] {
+    if (!d_out && ni > 0) throw Error(RVCX_E_INVALID, "reconstruct_n: null output");
+    set_device(ctx);
+    index_reconstruct_n(*ctx, i0, ni, d_out, static_cast<hipStream_t>(stream));
+  });
+}
+
+int rvcx_index_retrieve(rvcx_ctx* ctx, const float* d_feats, int64_t L, int d, double index_rate, float* d_out,
+                        void* stream) {
+  return guard(ctx, [&] {
+    if ((!d_feats || !d_out) && L > 0) throw Error(RVCX_E_INVALID, "index_retrieve: bad arguments");
+    set_device(ctx);
+    index_retrieve(*ctx, d_feats, L, d, index_rate, d_out, static_cast<hipStream_t>(stream));
+  });
+}

@@ -68,6 +68,12 @@ struct UpsLayer {
   float* b = nullptr;     // [u*cout]
 };
 
+// FAISS IndexIVFFlat resident in HBM (index_ivf.cpp; layout in ivf.hip)
+struct IvfIndex {
+  IvfView view;
+  DevBuf cent, vecs, off, ids, slot_of_id;
+};
+
 struct Ctx {
   int device = 0;
   std::string err;
@@ -92,6 +98,7 @@ struct Ctx {
   };
   std::vector<ProfRec> prof_recs;
   std::vector<hipEvent_t> prof_pool;
+  std::unique_ptr<IvfIndex> ivf;  // speaker-embedding index (optional)
 
   float* W(const std::string& name) const;
   float* alloc_weight(const std::string& name, const std::vector<float>& data);
@@ -134,8 +141,13 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
 void set_highpass(Ctx& c, const double* b, const double* a, const double* zi, int order);
 int hubert_version_for(const Ctx& c);
 int64_t vc_forward(Ctx& c, const float* audio, int64_t n, const int32_t* pitch, const float* pitchf,
-                   int64_t pitch_len, int sid, float protect, const float* eps_z, const float* eps_src, uint64_t seed,
-                   float* out, int64_t cap, hipStream_t s);
+                   int64_t pitch_len, int sid, float protect, double index_rate, const float* eps_z,
+                   const float* eps_src, uint64_t seed, float* out, int64_t cap, hipStream_t s);
+// index (index_ivf.cpp)
+void index_load(Ctx& c, const uint8_t* bytes, int64_t nbytes);
+void index_search(Ctx& c, const float* x, int64_t n, int k, float* dist, int64_t* ids, hipStream_t s);
+void index_retrieve(Ctx& c, const float* feats, int64_t L, int d, double index_rate, float* out, hipStream_t s);
+void index_reconstruct_n(Ctx& c, int64_t i0, int64_t ni, float* out, hipStream_t s);
 int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_pipeline_opts& o,
                             const float* eps_z, const float* eps_src, uint64_t seed, float* out, int64_t cap,
                             double* f0_out, hipStream_t s);

@@ -29,8 +29,8 @@ void set_highpass(Ctx& c, const double* b, const double* a, const double* zi, in
 int hubert_version_for(const Ctx& c) { return c.scfg.emb_dim == 256 ? 1 : 2; }
 
 int64_t vc_forward(Ctx& c, const float* audio, int64_t n, const int32_t* pitch, const float* pitchf,
-                   int64_t pitch_len, int sid, float protect, const float* eps_z, const float* eps_src, uint64_t seed,
-                   float* out, int64_t cap, hipStream_t s) {
+                   int64_t pitch_len, int sid, float protect, double index_rate, const float* eps_z,
+                   const float* eps_src, uint64_t seed, float* out, int64_t cap, hipStream_t s) {
   if (sid < 0 || sid >= c.scfg.n_spk) throw Error(RVCX_E_INVALID, "sid out of range");
   const int E = c.scfg.emb_dim;
   const int64_t cap_rows = n / 320 + 8;  // HuBERT frames for n samples (upper bound n/320)
@@ -42,8 +42,16 @@ int64_t vc_forward(Ctx& c, const float* audio, int64_t n, const int32_t* pitch, 
   const int upp = c.scfg.upp();
   if ((int64_t)T * upp > cap)
     throw Error(RVCX_E_CAPACITY, "voice_conversion: output needs " + std::to_string((int64_t)T * upp) + " samples");
+  // speaker-embedding retrieval on the raw features (pipeline.py:338-342); feats0 stays raw for protect
+  const float* fx = feats;
+  if (index_rate > 0 && c.ivf) {
+    float* fr = c.buf<float>("vc.feats_idx", (size_t)L * E, s);
+    index_retrieve(c, feats, L, E, index_rate, fr, s);
+    fx = fr;
+  }
   float* phone = c.buf<float>("vc.phone", (size_t)T * E, s);
-  check(upsample2_protect(feats, (int)L, E, phone, T, protect < 0.5f ? pitchf : nullptr, protect, s), "upsample");
+  check(upsample2_protect(fx, feats, (int)L, E, phone, T, protect < 0.5f ? pitchf : nullptr, protect, s),
+        "upsample");
   int32_t* lens = c.buf<int32_t>("vc.len", 4, s);
   set_i32(lens, T, s);
   set_i32(lens + 1, sid, s);
@@ -90,6 +98,9 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
                             double* f0_out, hipStream_t s) {
   if (c.hp_order == 0) throw Error(RVCX_E_STATE, "pipeline: high-pass filter not configured");
   if (o.t_pad < 0 || o.t_pad_tgt < 0 || o.t_pad >= n) throw Error(RVCX_E_INVALID, "pipeline: bad t_pad");
+  if (o.index_rate > 0 && !c.ivf) throw Error(RVCX_E_STATE, "pipeline: index_rate > 0 but no feature index loaded");
+  if (o.index_rate > 0 && c.ivf->view.d != c.scfg.emb_dim)
+    throw Error(RVCX_E_SHAPE, "pipeline: feature index dimension does not match the model's feature width");
   if (o.version != 0 && o.version != hubert_version_for(c))
     throw Error(RVCX_E_INVALID, "pipeline: version does not match the synthesizer's embedding width");
   const int64_t W = 160;  // Pipeline.window
@@ -146,7 +157,7 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
     float* vc = c.buf<float>("pl.vc", (size_t)std::max<int64_t>(cap_vc, 1), s);
     // pitch[:, f_lo:f_hi], then [:p_len] inside voice_conversion with p_len = min(len/160, 2L)
     const int64_t nvc = vc_forward(c, pad32 + a0, len, pitch + f_lo, pitchf + f_lo, f_hi - f_lo, o.sid, o.protect,
-                                   eps_z ? eps_z + ez_off : nullptr, eps_src ? eps_src + es_off : nullptr, cseed, vc,
+                                   o.index_rate, eps_z ? eps_z + ez_off : nullptr, eps_src ? eps_src + es_off : nullptr, cseed, vc,
                                    cap_vc, s);
     const int64_t T = nvc / upp;
     ez_off += (int64_t)I * T;

@@ -118,7 +118,8 @@ hipError_t gate_tanh_sigmoid(const float* xin, int ldx, const float* g, long lon
 hipError_t softmax_rel(float* scores, int T, int n_heads, int B, const float* rel, int window,
                        const float* mask, float* pband, int rows_scaled_by_band, hipStream_t s);
 hipError_t softmax_rows(float* scores, int rows, int cols, hipStream_t s);
-hipError_t upsample2_protect(const float* feats, int L, int D, float* out, int T, const float* pitchf, float protect,
+hipError_t upsample2_protect(const float* feats, const float* feats0, int L, int D, float* out, int T, const float* pitchf,
+                             float protect,
                              hipStream_t s);
 hipError_t sine_source(const float* f0, int B, int L, int upp, float sr, const float* eps, uint64_t seed,
                        float lin_w, float lin_b, double* cum_ws, float* har, long long har_ld, hipStream_t s);
@@ -160,5 +161,21 @@ hipError_t split_points(const double* x, long long n, int window, long long t_ce
 int rms_frame_count(long long n, int sr);
 hipError_t change_rms(const double* src, long long n_src, int sr_src, float* y, long long n_y, int sr_y, float rate,
                       float* ws, hipStream_t s);
+
+// FAISS IndexIVFFlat on device (ivf.hip): search + the retrieval blend of pipeline.py:378-388
+struct IvfView {
+  int d = 0, nprobe = 1;
+  long long nlist = 0, ntotal = 0;
+  const float* cent = nullptr;       // [nlist][d]
+  const float* vecs = nullptr;       // [ntotal][d], list order
+  const long long* off = nullptr;    // [nlist + 1]
+  const long long* ids = nullptr;    // [ntotal], list order
+  const int* slot_of_id = nullptr;   // [ntotal]
+};
+constexpr int IVF_MAX_K = 16;
+size_t ivf_ws_floats(long long n, long long nlist, int nprobe);
+// dist_out/ids_out [n][k] (optional); out [n][d] = retrieval blend (optional)
+hipError_t ivf_search(const IvfView& v, const float* x, long long n, int k, float* dist_out, long long* ids_out,
+                      float rate, float one_minus_rate, float* out, float* ws, hipStream_t s);
 
 }  // namespace rvcx

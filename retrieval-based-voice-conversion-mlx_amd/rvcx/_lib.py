@@ -23,7 +23,9 @@ EXPORTS = [
     "rvcx_create", "rvcx_destroy", "rvcx_last_error", "rvcx_set_synth_config", "rvcx_upload", "rvcx_finalize",
     "rvcx_hubert", "rvcx_rmvpe", "rvcx_f0_post", "rvcx_synth_infer", "rvcx_dec_only", "rvcx_voice_conversion",
     "rvcx_synth_upp", "rvcx_set_highpass", "rvcx_pipeline", "rvcx_pipeline_default_opts", "rvcx_pipeline_ex",
-    "rvcx_f0_autotune", "rvcx_rmvpe_decode", "rvcx_profile", "rvcx_profile_read",
+    "rvcx_f0_autotune", "rvcx_rmvpe_decode", "rvcx_profile", "rvcx_profile_read", "rvcx_index_load",
+    "rvcx_index_unload", "rvcx_index_info", "rvcx_index_set_nprobe", "rvcx_index_search", "rvcx_index_reconstruct_n",
+    "rvcx_index_retrieve",
 ]
 
 
@@ -58,7 +60,7 @@ class PipelineOpts(ctypes.Structure):
         ("t_query", ctypes.c_int64), ("t_center", ctypes.c_int64), ("t_max", ctypes.c_int64),
         ("f0_autotune", ctypes.c_int), ("f0_autotune_strength", ctypes.c_double), ("proposed_pitch", ctypes.c_int),
         ("proposed_pitch_threshold", ctypes.c_double), ("volume_envelope", ctypes.c_double),
-        ("mlx_semantics", ctypes.c_int),
+        ("mlx_semantics", ctypes.c_int), ("index_rate", ctypes.c_double),
     ]
 
 
@@ -93,7 +95,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "rvcx_f0_post": (i32, [vp, vp, i64, f64, vp, vp, vp, vp]),
         "rvcx_synth_infer": (i32, [vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, u64, vp, vp, vp, vp]),
         "rvcx_dec_only": (i32, [vp, i32, i32, vp, vp, vp, vp, u64, vp, vp]),
-        "rvcx_voice_conversion": (i32, [vp, vp, i64, vp, vp, i32, f32, vp, vp, u64, vp, i64, P(i64), vp]),
+        "rvcx_voice_conversion": (i32, [vp, vp, i64, vp, vp, i32, f32, f64, vp, vp, u64, vp, i64, P(i64), vp]),
         "rvcx_synth_upp": (i32, [vp]),
         "rvcx_set_highpass": (i32, [vp, vp, vp, vp, i32]),
         "rvcx_profile": (i32, [vp, i32]),
@@ -103,6 +105,13 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "rvcx_pipeline_ex": (i32, [vp, vp, i64, P(PipelineOpts), vp, vp, u64, vp, i64, P(i64), vp, vp]),
         "rvcx_f0_autotune": (i32, [vp, vp, i64, f64, i32, vp]),
         "rvcx_rmvpe_decode": (i32, [vp, vp, i64, f32, vp, vp]),
+        "rvcx_index_load": (i32, [vp, vp, i64]),
+        "rvcx_index_unload": (i32, [vp]),
+        "rvcx_index_info": (i32, [vp, P(i64), P(i64), P(i64), P(i64)]),
+        "rvcx_index_set_nprobe": (i32, [vp, i64]),
+        "rvcx_index_search": (i32, [vp, vp, i64, i32, vp, vp, vp]),
+        "rvcx_index_reconstruct_n": (i32, [vp, i64, i64, vp, vp]),
+        "rvcx_index_retrieve": (i32, [vp, vp, i64, i32, f64, vp, vp]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(lib, name):  # reported by exported_symbols(); an older build lacks newer entry points

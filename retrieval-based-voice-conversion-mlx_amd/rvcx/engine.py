@@ -198,7 +198,7 @@ class Engine:
         return out
 
     def voice_conversion(self, audio_pad, pitch, pitchf, sid: int, protect: float, eps_z=None, eps_src=None,
-                         seed: int = 0):
+                         seed: int = 0, index_rate: float = 0.0):
         """HuBERT -> x2 upsample -> protect -> Synthesizer.infer on one padded chunk (device in/out)."""
         t = self.torch
         a = self._dev(audio_pad, t.float32).reshape(-1)
@@ -211,7 +211,7 @@ class Engine:
         ez = None if eps_z is None else self._dev(eps_z, t.float32)
         es = None if eps_src is None else self._dev(eps_src, t.float32)
         self._check(self.lib.rvcx_voice_conversion(self.ctx, a.data_ptr(), n, pc.data_ptr(), pf.data_ptr(), int(sid),
-                                                   float(protect), _ptr(ez), _ptr(es),
+                                                   float(protect), float(index_rate), _ptr(ez), _ptr(es),
                                                    ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), out.data_ptr(), cap,
                                                    ctypes.byref(no), self.stream()), "voice_conversion")
         return out[: no.value]
@@ -287,6 +287,59 @@ class Engine:
         self._check(self.lib.rvcx_f0_autotune(self.ctx, f.data_ptr(), f.numel(), float(strength),
                                               1 if skip_unvoiced else 0, self.stream()), "f0_autotune")
         return f
+
+    # ------------------------------------------------------------------ feature index (FAISS IVFFlat)
+    def index_load(self, data: bytes):
+        """Parse a faiss IndexIVFFlat file image and keep it in HBM (faiss.read_index, pipeline.py:430-434)."""
+        buf = ctypes.create_string_buffer(bytes(data), len(data))
+        self._check(self.lib.rvcx_index_load(self.ctx, buf, len(data)), "index_load")
+        self.index_info()
+
+    def index_unload(self):
+        self._check(self.lib.rvcx_index_unload(self.ctx), "index_unload")
+
+    def index_info(self):
+        """-> dict(d, ntotal, nlist, nprobe), or None when no index is loaded."""
+        v = [ctypes.c_int64(0) for _ in range(4)]
+        rc = self.lib.rvcx_index_info(self.ctx, *[ctypes.byref(x) for x in v])
+        if rc == -5:
+            return None
+        self._check(rc, "index_info")
+        return dict(zip(("d", "ntotal", "nlist", "nprobe"), (x.value for x in v)))
+
+    def index_set_nprobe(self, nprobe: int):
+        self._check(self.lib.rvcx_index_set_nprobe(self.ctx, int(nprobe)), "index_set_nprobe")
+
+    def index_search(self, x, k: int = 8):
+        """index.search(x, k) on device -> (dist fp32 [n, k], ids int64 [n, k]) device tensors."""
+        t = self.torch
+        xx = self._dev(x, t.float32)
+        xx = xx.reshape(-1, xx.shape[-1])
+        n = xx.shape[0]
+        dist = t.empty((n, k), dtype=t.float32, device=self.device)
+        ids = t.empty((n, k), dtype=t.int64, device=self.device)
+        self._check(self.lib.rvcx_index_search(self.ctx, xx.data_ptr(), n, int(k), dist.data_ptr(), ids.data_ptr(),
+                                               self.stream()), "index_search")
+        return dist, ids
+
+    def index_reconstruct_n(self, i0: int, ni: int):
+        info = self.index_info()
+        if info is None:
+            raise _lib.RvcxError(-5, "no feature index loaded")
+        out = self.torch.empty((int(ni), info["d"]), dtype=self.torch.float32, device=self.device)
+        self._check(self.lib.rvcx_index_reconstruct_n(self.ctx, int(i0), int(ni), out.data_ptr(), self.stream()),
+                    "index_reconstruct_n")
+        return out
+
+    def index_retrieve(self, feats, index_rate: float):
+        """Pipeline._retrieve_speaker_embeddings on device: feats [L, d] -> blended [L, d]."""
+        t = self.torch
+        f = self._dev(feats, t.float32)
+        f = f.reshape(-1, f.shape[-1])
+        out = t.empty_like(f)
+        self._check(self.lib.rvcx_index_retrieve(self.ctx, f.data_ptr(), f.shape[0], f.shape[1], float(index_rate),
+                                                 out.data_ptr(), self.stream()), "index_retrieve")
+        return out
 
     # ------------------------------------------------------------------ kernel timing
     def profile(self, enable: bool):

@@ -88,6 +88,18 @@ class PipelineRVCX:
             b, a = signal.butter(N=5, Wn=48, btype="high", fs=self.sample_rate)
             eng.set_highpass(b, a, signal.lfilter_zi(b, a))
 
+    def load_index(self, file_index: str, eng=None):
+        """faiss.read_index + reconstruct_n (pipeline.py:430-434), cached per (path, mtime, size)."""
+        from .index import IndexIVFFlat
+
+        eng = eng or self._engine()
+        st = os.stat(file_index)
+        key = (os.path.abspath(file_index), st.st_mtime_ns, st.st_size, id(eng))
+        if getattr(self, "_index_key", None) != key or eng.index_info() is None:
+            self.index = IndexIVFFlat(eng, path=file_index)
+            self._index_key = key
+        return self.index
+
     # ------------------------------------------------------------------ API (pipeline_mlx.py:135-373)
     def get_f0(self, x, p_len, f0_method="rmvpe", pitch=0, f0_autotune=False, f0_autotune_strength=1.0,
                proposed_pitch=False, proposed_pitch_threshold=155.0):
@@ -108,14 +120,18 @@ class PipelineRVCX:
     def voice_conversion(self, model, net_g, sid, audio0, pitch, pitchf, index=None, big_npy=None, index_rate=0.0,
                          version="v2", protect=0.33, eps_z=None, eps_src=None, seed: int = 0):
         """One padded chunk: HuBERT -> x2 -> protect -> Synthesizer.infer. -> float32 [p_len * upp]."""
-        if index is not None and index_rate > 0:
-            raise NotImplementedError("feature index retrieval (index_rate > 0) is not available in this build")
         if pitch is None or pitchf is None:
             raise NotImplementedError("models without pitch guidance (f0 = 0) are not supported")
         eng = self._engine(model)
+        rate = 0.0
+        if index is not None and index_rate > 0:  # pipeline.py:338-342 (big_npy is the index's own rows)
+            if getattr(index, "engine", None) is not eng:
+                raise TypeError("index must be an rvcx IndexIVFFlat loaded on this pipeline's engine (read_index)")
+            index._bound()
+            rate = float(index_rate)
         out = eng.voice_conversion(np.asarray(audio0, dtype=np.float32).reshape(-1), _np(pitch).reshape(-1),
                                    _np(pitchf).reshape(-1), int(_np(sid).reshape(-1)[0]), float(protect),
-                                   eps_z=eps_z, eps_src=eps_src, seed=seed)
+                                   eps_z=eps_z, eps_src=eps_src, seed=seed, index_rate=rate)
         return out.cpu().numpy()
 
     def pipeline(self, model, net_g, sid, audio, pitch=0, f0_method="rmvpe", file_index=None, index_rate=0.0,
@@ -124,13 +140,15 @@ class PipelineRVCX:
                  eps_src=None, seed: int = 0):
         """Whole utterance -> float32 [N_out] @tgt_sr (pipeline.py:390-558)."""
         self._check_method(f0_method)
-        if file_index and index_rate > 0:
-            if not os.path.exists(file_index):
-                raise FileNotFoundError(file_index)
-            raise NotImplementedError("feature index retrieval (index_rate > 0) is not available in this build")
         if not pitch_guidance:
             raise NotImplementedError("models without pitch guidance (f0 = 0) are not supported")
         eng = self._engine(model)
+        # pipeline.py:430-436: the index is used only when the file exists and index_rate > 0 (a missing
+        # file means no retrieval, as in the reference); a file that does not parse raises here.
+        rate = 0.0
+        if file_index and os.path.exists(file_index) and index_rate > 0:
+            self.load_index(file_index, eng)
+            rate = float(index_rate)
         self._ensure_highpass(eng)
         mlx = self.semantics == "mlx"
         t_pad = 1600 if mlx else self.t_pad
@@ -142,7 +160,7 @@ class PipelineRVCX:
             f0_autotune_strength=float(f0_autotune_strength),
             proposed_pitch=int(bool(proposed_pitch) and not mlx),
             proposed_pitch_threshold=float(proposed_pitch_threshold), volume_envelope=float(volume_envelope),
-            mlx_semantics=int(mlx))
+            mlx_semantics=int(mlx), index_rate=rate)
         y, f0 = eng.pipeline_ex(np.asarray(audio, dtype=np.float64).reshape(-1), opts, eps_z=eps_z,
                                 eps_src=eps_src, seed=seed, want_f0=True)
         self.last_f0 = f0
