@@ -196,6 +196,51 @@ int rvcx_index_reconstruct_n(rvcx_ctx* ctx, int64_t i0, int64_t ni, float* d_out
 int rvcx_index_retrieve(rvcx_ctx* ctx, const float* d_feats, int64_t L, int d, double index_rate, float* d_out,
                         void* stream);
 
+/* ---------------------------------------------------------------- streaming (config C5)
+ * A group of n_streams concurrent realtime streams of one buffer geometry, converted together per hop.
+ * Replaces VoiceChanger / Realtime / Realtime_Pipeline of rvc/realtime/core.py:329-484 and
+ * rvc/realtime/pipeline.py:99-334 (the MLX port of this path, rvc_mlx/realtime, is not functional).
+ * Geometry follows VoiceChanger.__init__ + Realtime.realloc (core.py:165-216, :351-374): block =
+ * read_chunk_size * 128 samples @48 kHz; convert buffer = block + sola (10 ms) + extra + crossfade
+ * @16 kHz rounded up to 10 ms; skip_head = extra / 10 ms; return_length = frames - skip_head. */
+typedef struct rvcx_rt rvcx_rt;
+
+typedef struct {
+  int n_streams;                  /* B streams per hop batch */
+  int read_chunk_size;            /* block = read_chunk_size * 128 samples @48 kHz (callbacks.py default 192) */
+  double cross_fade_overlap_size; /* seconds (default 0.1) */
+  double extra_convert_size;      /* seconds (default 0.5) */
+  double silent_threshold;        /* dB; hops with RMS below 10^(dB/20) output silence (core.py:58-59, :268-289) */
+} rvcx_rt_desc;
+
+typedef struct {                  /* per-hop options of VoiceChanger.on_request (core.py:453-484) */
+  double f0_up_key;
+  double index_rate;              /* > 0 needs rvcx_index_load; retrieval from skip_head // 2 */
+  float protect;                  /* active when < 0.5 */
+  double volume_envelope;         /* 1 = off */
+  int f0_autotune;
+  double f0_autotune_strength;
+  int proposed_pitch;             /* one host sync per hop */
+  double proposed_pitch_threshold;
+} rvcx_rt_opts;
+
+int rvcx_rt_default_desc(rvcx_rt_desc* desc);
+int rvcx_rt_default_opts(rvcx_rt_opts* opts);
+/* Needs the synthesizer, HuBERT and RMVPE finalized. State lives in HBM, zero-initialised. */
+int rvcx_rt_create(rvcx_ctx* ctx, const rvcx_rt_desc* desc, rvcx_rt** out);
+int rvcx_rt_destroy(rvcx_ctx* ctx, rvcx_rt* rt);
+/* geometry[12] = {n_streams, block48, block16, convert16, frames (p_len), skip_head, return_length,
+ *                 crossfade48, sola_search48, extra48, resampled_block16, silence_front} */
+int rvcx_rt_geometry(const rvcx_rt* rt, int64_t* geometry);
+int rvcx_rt_reset(rvcx_ctx* ctx, rvcx_rt* rt, void* stream);
+/* One hop for every stream: d_in [B][block48] fp32 @48 kHz -> d_out [B][block48] fp32 @48 kHz
+ * (VoiceChanger.process_audio). sids: host [B]. d_vol (optional, device [B]) receives each stream's
+ * input RMS (the `vol` of on_request); d_offs (optional, device int [B]) the SOLA offsets. Noise: d_eps_z
+ * [B][inter][frames] and d_eps_src [B][frames * upp] when injected, else Philox(seed). */
+int rvcx_rt_process(rvcx_ctx* ctx, rvcx_rt* rt, const float* d_in, const int32_t* sids, const rvcx_rt_opts* opts,
+                    const float* d_eps_z, const float* d_eps_src, uint64_t seed, float* d_out, float* d_vol,
+                    int32_t* d_offs, void* stream);
+
 /* Upsampling factor of the loaded synthesizer (prod(upsample_rates); net_g.dec.upp). */
 int rvcx_synth_upp(const rvcx_ctx* ctx);
 

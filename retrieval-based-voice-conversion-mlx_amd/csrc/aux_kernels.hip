@@ -324,7 +324,7 @@ __global__ void k_up2(const float* feats, const float* feats0, int L, int D, flo
     float v = f;
     if (pitchf) {
       const float pf = pitchf[t];
-      const float p = pf > 0.f ? 1.f : (pf < 1.f ? protect : pf);
+      const float p = pf < 1.f ? protect : (pf > 0.f ? 1.f : pf);
       v = f * p + feats0[(long long)src * D + c] * (1.f - p);
     }
     out[i] = v;
@@ -971,6 +971,16 @@ hipError_t change_rms(const double* src, long long n_src, int sr_src, float* y, 
                       float* ws, hipStream_t s) {
   const int n1 = rms_frame_count(n_src, sr_src), n2 = rms_frame_count(n_y, sr_y);
   hipLaunchKernelGGL(k_rms_frames<double>, dim3(n1), dim3(TB), 0, s, src, n_src, sr_src / 2 * 2, sr_src / 2, ws);
+  hipLaunchKernelGGL(k_rms_frames<float>, dim3(n2), dim3(TB), 0, s, (const float*)y, n_y, sr_y / 2 * 2, sr_y / 2,
+                     ws + n1);
+  hipLaunchKernelGGL(k_apply_rms, dim3(nblocks(n_y)), dim3(TB), 0, s, y, n_y, ws, n1, ws + n1, n2, rate);
+  return hipGetLastError();
+}
+// change_rms with a float32 source (the streaming path's 16 kHz convert buffer, rvc/realtime/pipeline.py:303-310)
+hipError_t change_rms_f32src(const float* src, long long n_src, int sr_src, float* y, long long n_y, int sr_y,
+                             float rate, float* ws, hipStream_t s) {
+  const int n1 = rms_frame_count(n_src, sr_src), n2 = rms_frame_count(n_y, sr_y);
+  hipLaunchKernelGGL(k_rms_frames<float>, dim3(n1), dim3(TB), 0, s, src, n_src, sr_src / 2 * 2, sr_src / 2, ws);
   hipLaunchKernelGGL(k_rms_frames<float>, dim3(n2), dim3(TB), 0, s, (const float*)y, n_y, sr_y / 2 * 2, sr_y / 2,
                      ws + n1);
   hipLaunchKernelGGL(k_apply_rms, dim3(nblocks(n_y)), dim3(TB), 0, s, y, n_y, ws, n1, ws + n1, n2, rate);

@@ -9,6 +9,9 @@
 using namespace rvcx;
 
 struct rvcx_ctx : public Ctx {};
+struct rvcx_rt {
+  RtState* s = nullptr;
+};
 
 namespace {
 
@@ -388,5 +391,77 @@ int rvcx_index_retrieve(rvcx_ctx* ctx, const float* d_feats, int64_t L, int d, d
     if ((!d_feats || !d_out) && L > 0) throw Error(RVCX_E_INVALID, "index_retrieve: bad arguments");
     set_device(ctx);
     index_retrieve(*ctx, d_feats, L, d, index_rate, d_out, static_cast<hipStream_t>(stream));
+  });
+}
+
+// ------------------------------------------------------------------ streaming (C5)
+int rvcx_rt_default_desc(rvcx_rt_desc* d) {
+  if (!d) return RVCX_E_INVALID;
+  d->n_streams = 1;
+  d->read_chunk_size = 192;  // rvc/realtime/callbacks.py:16-18
+  d->cross_fade_overlap_size = 0.1;
+  d->extra_convert_size = 0.5;
+  d->silent_threshold = -90.0;
+  return RVCX_OK;
+}
+
+int rvcx_rt_default_opts(rvcx_rt_opts* o) {
+  if (!o) return RVCX_E_INVALID;
+  std::memset(o, 0, sizeof(*o));
+  o->index_rate = 0.0;
+  o->protect = 0.5f;
+  o->volume_envelope = 1.0;
+  o->f0_autotune_strength = 1.0;
+  o->proposed_pitch_threshold = 155.0;
+  return RVCX_OK;
+}
+
+int rvcx_rt_create(rvcx_ctx* ctx, const rvcx_rt_desc* desc, rvcx_rt** out) {
+  return guard(ctx, [&] {
+    if (!desc || !out) throw Error(RVCX_E_INVALID, "rt_create: null argument");
+    set_device(ctx);
+    auto* h = new rvcx_rt();
+    try {
+      h->s = rt_create(*ctx, *desc);
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+int rvcx_rt_destroy(rvcx_ctx* ctx, rvcx_rt* rt) {
+  return guard(ctx, [&] {
+    if (!rt) return;
+    set_device(ctx);
+    RVCX_HIP(hipDeviceSynchronize());
+    rt_destroy(rt->s);
+    delete rt;
+  });
+}
+
+int rvcx_rt_geometry(const rvcx_rt* rt, int64_t* g) {
+  if (!rt || !rt->s || !g) return RVCX_E_INVALID;
+  rt_geometry(*rt->s, g);
+  return RVCX_OK;
+}
+
+int rvcx_rt_reset(rvcx_ctx* ctx, rvcx_rt* rt, void* stream) {
+  return guard(ctx, [&] {
+    if (!rt || !rt->s) throw Error(RVCX_E_INVALID, "rt_reset: null stream group");
+    set_device(ctx);
+    rt_reset(*ctx, *rt->s, static_cast<hipStream_t>(stream));
+  });
+}
+
+int rvcx_rt_process(rvcx_ctx* ctx, rvcx_rt* rt, const float* d_in, const int32_t* sids, const rvcx_rt_opts* opts,
+                    const float* d_eps_z, const float* d_eps_src, uint64_t seed, float* d_out, float* d_vol,
+                    int32_t* d_offs, void* stream) {
+  return guard(ctx, [&] {
+    if (!rt || !rt->s || !d_in || !sids || !opts || !d_out) throw Error(RVCX_E_INVALID, "rt_process: null argument");
+    set_device(ctx);
+    rt_process(*ctx, *rt->s, d_in, sids, *opts, d_eps_z, d_eps_src, seed, d_out, d_vol, d_offs,
+               static_cast<hipStream_t>(stream));
   });
 }

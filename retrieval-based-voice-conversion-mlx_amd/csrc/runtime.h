@@ -143,6 +143,15 @@ int hubert_version_for(const Ctx& c);
 int64_t vc_forward(Ctx& c, const float* audio, int64_t n, const int32_t* pitch, const float* pitchf,
                    int64_t pitch_len, int sid, float protect, double index_rate, const float* eps_z,
                    const float* eps_src, uint64_t seed, float* out, int64_t cap, hipStream_t s);
+// streaming (runtime_stream.cpp)
+struct RtState;
+RtState* rt_create(Ctx& c, const rvcx_rt_desc& d);
+void rt_destroy(RtState* s);
+void rt_geometry(const RtState& s, int64_t* g);
+void rt_reset(Ctx& c, RtState& s, hipStream_t st);
+void rt_process(Ctx& c, RtState& s, const float* in48, const int32_t* sids, const rvcx_rt_opts& o,
+                const float* eps_z, const float* eps_src, uint64_t seed, float* out48, float* vol_out, int* offs_out,
+                hipStream_t st);
 // index (index_ivf.cpp)
 void index_load(Ctx& c, const uint8_t* bytes, int64_t nbytes);
 void index_search(Ctx& c, const float* x, int64_t n, int k, float* dist, int64_t* ids, hipStream_t s);
@@ -152,6 +161,8 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
                             const float* eps_z, const float* eps_src, uint64_t seed, float* out, int64_t cap,
                             double* f0_out, hipStream_t s);
 rvcx_pipeline_opts default_pipeline_opts();
+int proposed_key(const std::vector<double>& f0, double threshold);
+int64_t hubert_frames(int64_t n);  // HuBERT output rows for n samples (0 when too short)
 void set_i32(int32_t* p, int32_t v, hipStream_t s);
 // launch one implicit-GEMM conv (1-D or 2-D) with optional event timing; flops = algorithmic FLOPs
 void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double flops = -1.0);

@@ -125,6 +125,15 @@ void finalize_hubert(Ctx& c) {
   }
 }
 
+int64_t hubert_frames(int64_t n) {
+  int64_t t = n;
+  for (int i = 0; i < 7; ++i) {
+    if (t < HK[i]) return 0;
+    t = (t - HK[i]) / HS[i] + 1;
+  }
+  return t;
+}
+
 int64_t hubert_forward(Ctx& c, const float* audio, int64_t n, int version, float* feats, int64_t cap,
                        hipStream_t s) {
   int64_t T[8];

@@ -59,8 +59,6 @@ int64_t vc_forward(Ctx& c, const float* audio, int64_t n, const int32_t* pitch, 
   return (int64_t)T * upp;
 }
 
-namespace {
-
 // key offset of proposed_pitch (pipeline.py:250-277): median of the voiced-interpolated track
 int proposed_key(const std::vector<double>& f0, double threshold) {
   std::vector<int64_t> valid;
@@ -90,8 +88,6 @@ int proposed_key(const std::vector<double>& f0, double threshold) {
   const double key = std::nearbyint(12.0 * std::log2(threshold / med));  // np.round: half to even
   return (int)std::max(-12.0, std::min(12.0, key));
 }
-
-}  // namespace
 
 int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_pipeline_opts& o,
                             const float* eps_z, const float* eps_src, uint64_t seed, float* out, int64_t cap,

@@ -178,4 +178,21 @@ size_t ivf_ws_floats(long long n, long long nlist, int nprobe);
 hipError_t ivf_search(const IvfView& v, const float* x, long long n, int k, float* dist_out, long long* ids_out,
                       float rate, float one_minus_rate, float* out, float* ws, hipStream_t s);
 
+// streaming (stream.hip): B streams of one geometry per launch
+hipError_t rt_resample(const float* x, long long ldx, int n_in, const float* ker, int K, int width, int orig, int nw,
+                       float* y, long long ldy, int n_out, const float* pre, int B, hipStream_t s);
+hipError_t rt_ingest(const float* in16, int n16, const float* abuf_old, float* abuf_new, int na, const float* cbuf_old,
+                     float* cbuf_new, int nc, double sensitivity, float* vol, float* volsq, int* gate, int B,
+                     hipStream_t s);
+hipError_t rt_pitch(const double* f0, int F, const double* factor, const int* pold, int* pnew, const float* fold,
+                    float* fnew, int nbuf, int B, hipStream_t s);
+hipError_t rt_up2(const float* feats, const float* feats0, int L, int D, float* phone, int T, const float* pitchf_buf,
+                  int nbuf, float pscale, float protect, int use_protect, int* pitch_out, const int* pitch_buf,
+                  float* pitchf_out, int B, hipStream_t s);
+hipError_t rt_clip(float* x, long long ld, int n, int B, hipStream_t s);
+hipError_t rt_sola(const float* audio, long long lda, const float* volsq, const int* gate, float* sola_buf, int cf,
+                   int search, const float* fade_in, float* out, int block, int* offs, int B, hipStream_t s);
+hipError_t change_rms_f32src(const float* src, long long n_src, int sr_src, float* y, long long n_y, int sr_y,
+                             float rate, float* ws, hipStream_t s);
+
 }  // namespace rvcx

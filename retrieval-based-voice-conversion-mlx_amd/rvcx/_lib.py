@@ -25,7 +25,8 @@ EXPORTS = [
     "rvcx_synth_upp", "rvcx_set_highpass", "rvcx_pipeline", "rvcx_pipeline_default_opts", "rvcx_pipeline_ex",
     "rvcx_f0_autotune", "rvcx_rmvpe_decode", "rvcx_profile", "rvcx_profile_read", "rvcx_index_load",
     "rvcx_index_unload", "rvcx_index_info", "rvcx_index_set_nprobe", "rvcx_index_search", "rvcx_index_reconstruct_n",
-    "rvcx_index_retrieve",
+    "rvcx_index_retrieve", "rvcx_rt_default_desc", "rvcx_rt_default_opts", "rvcx_rt_create", "rvcx_rt_destroy",
+    "rvcx_rt_geometry", "rvcx_rt_reset", "rvcx_rt_process",
 ]
 
 
@@ -62,6 +63,21 @@ class PipelineOpts(ctypes.Structure):
         ("proposed_pitch_threshold", ctypes.c_double), ("volume_envelope", ctypes.c_double),
         ("mlx_semantics", ctypes.c_int), ("index_rate", ctypes.c_double),
     ]
+
+
+class RtDesc(ctypes.Structure):
+    """rvcx_rt_desc (include/rvcx.h)."""
+    _fields_ = [("n_streams", ctypes.c_int), ("read_chunk_size", ctypes.c_int),
+                ("cross_fade_overlap_size", ctypes.c_double), ("extra_convert_size", ctypes.c_double),
+                ("silent_threshold", ctypes.c_double)]
+
+
+class RtOpts(ctypes.Structure):
+    """rvcx_rt_opts (include/rvcx.h)."""
+    _fields_ = [("f0_up_key", ctypes.c_double), ("index_rate", ctypes.c_double), ("protect", ctypes.c_float),
+                ("volume_envelope", ctypes.c_double), ("f0_autotune", ctypes.c_int),
+                ("f0_autotune_strength", ctypes.c_double), ("proposed_pitch", ctypes.c_int),
+                ("proposed_pitch_threshold", ctypes.c_double)]
 
 
 _lib: Optional[ctypes.CDLL] = None
@@ -112,6 +128,13 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "rvcx_index_search": (i32, [vp, vp, i64, i32, vp, vp, vp]),
         "rvcx_index_reconstruct_n": (i32, [vp, i64, i64, vp, vp]),
         "rvcx_index_retrieve": (i32, [vp, vp, i64, i32, f64, vp, vp]),
+        "rvcx_rt_default_desc": (i32, [P(RtDesc)]),
+        "rvcx_rt_default_opts": (i32, [P(RtOpts)]),
+        "rvcx_rt_create": (i32, [vp, P(RtDesc), P(vp)]),
+        "rvcx_rt_destroy": (i32, [vp, vp]),
+        "rvcx_rt_geometry": (i32, [vp, P(i64)]),
+        "rvcx_rt_reset": (i32, [vp, vp, vp]),
+        "rvcx_rt_process": (i32, [vp, vp, vp, P(ctypes.c_int32), P(RtOpts), vp, vp, u64, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(lib, name):  # reported by exported_symbols(); an older build lacks newer entry points
