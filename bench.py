@@ -37,6 +37,10 @@ def parse():
     ap.add_argument("--samples", type=int, default=C2_SAMPLES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-sec", type=float, default=2.0)
+    ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c2",
+                    help="c2 (default, the headline line): full pipeline, 13.5 s utterance per step; c3: HiFiGAN-NSF "
+                         "generator alone, B=32 x 400 frames per step; c5: 16 realtime streams, one 256 ms hop per step")
+    ap.add_argument("--streams", type=int, default=16, help="c5: concurrent streams")
     ap.add_argument("--roofline-pass", choices=["inline", "after"], default="after",
                     help="inline: HIP events around every conv launch of the timed steps; after: the timed steps "
                          "run without events and an identical K-step pass right after carries them")
@@ -71,6 +75,90 @@ def cpu_baseline(sample_sec: float):
                       f"speech-like clip, x_pad=1, median of 3 after 1 warm-up ({med:.2f} s/run)"}
 
 
+def _timed(step, args, dev, dist):
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def bench_c3(args, eng, dev, dist, rank, world):
+    """configs[2]: HiFiGAN-NSF generator alone, batch 32 x 400 frames of random z, f0 walk, sid 0."""
+    from rvcx import synthetic
+    from rvcx.sharding import reduce_throughput
+
+    B, T = 32, 400
+    rng = np.random.Generator(np.random.PCG64(3))
+    z = torch.as_tensor(rng.standard_normal((B, 192, T)).astype(np.float32), device=dev)
+    f0 = torch.as_tensor(synthetic.f0_walk(B, T, seed=3), dtype=torch.float32, device=dev)
+    sid = torch.zeros(B, dtype=torch.int32, device=dev)
+    eng.profile(True)
+    el = _timed(lambda i: eng.dec_only(z, f0, sid, seed=i), args, dev, dist)
+    eng.profile(False)
+    k_ms, k_flops, k_n = eng.profile_read()
+    audio_sec = B * T * eng.upp / 48000.0
+    tot = reduce_throughput(dist, args.steps * audio_sec, el, device=dev)
+    tf = k_flops / (k_ms / 1e3) / 1e12 if k_ms > 0 else 0.0
+    return {"metric": "audio-sec/sec HiFiGAN-NSF generator (C3)", "value": round(tot["value"], 3),
+            "unit": "audio-sec/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(tot["elapsed"] / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32", "data": "synthetic z ~ N(0,1), f0 random walk; random-init weights",
+            "config": {"workload": "C3: generator alone, B=32 x 400 frames (128 s of 48 kHz audio) per step",
+                       "parallelism": f"dp{world}"},
+            "roofline": {"bound": "mfma", "achieved": round(tf, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                         "kernel": "conv_gemm_kernel (events inline over the timed steps)",
+                         "alg_gflop_per_step": round(k_flops / (args.warmup + args.steps) / 1e9, 2)}}
+
+
+def bench_c5(args, eng, dev, dist, rank, world):
+    """configs[4]: S concurrent realtime streams, 256 ms hops (read_chunk_size 96), one hop per step;
+    latency = wall time of one hop for all streams (input and output in HBM)."""
+    from rvcx import synthetic
+    from rvcx.realtime import StreamGroup
+    from rvcx.sharding import reduce_throughput
+
+    S = args.streams
+    grp = StreamGroup(eng, S, read_chunk_size=96, cross_fade_overlap_size=0.1, extra_convert_size=0.5,
+                      silent_threshold=-90.0)
+    block = grp.block_frame
+    nh = args.warmup + args.steps
+    audio = np.stack([synthetic.speech_like(block * nh, seed=500 + 100 * rank + s, sr=48000).astype(np.float32)
+                      for s in range(S)])
+    x = torch.as_tensor(audio, device=dev)
+    opts = grp.opts(protect=0.5)
+    lat = []
+
+    def step(i):
+        t0 = time.perf_counter()
+        grp.process(x[:, i * block:(i + 1) * block], opts, seed=i)
+        torch.cuda.synchronize(dev)
+        lat.append(time.perf_counter() - t0)
+
+    el = _timed(step, args, dev, dist)
+    lat = np.array(lat[args.warmup:]) * 1e3
+    hop_sec = block / 48000.0
+    tot = reduce_throughput(dist, args.steps * S * hop_sec, el, device=dev)
+    grp.close()
+    return {"metric": "audio-sec/sec streaming VC (C5), hop latency p50/p99", "value": round(tot["value"], 3),
+            "unit": "audio-sec/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(tot["elapsed"] / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32", "data": "synthetic speech-like 48 kHz streams; random-init weights",
+            "config": {"workload": f"C5: {S} streams x 256 ms hop (block 12288 @48k, convert buffer 13920 @16k, "
+                                   "87 frames) per step", "streams": S, "parallelism": f"dp{world}"},
+            "latency_ms": {"p50": round(float(np.percentile(lat, 50)), 3),
+                           "p99": round(float(np.percentile(lat, 99)), 3), "budget": round(hop_sec * 1e3, 1)}}
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -97,6 +185,14 @@ def main():
     eng.load_rmvpe(normalize_state(synthetic.rmvpe_state(5)))
     b, a = signal.butter(N=5, Wn=48, btype="high", fs=SR_IN)
     eng.set_highpass(b, a, signal.lfilter_zi(b, a))
+    if args.config in ("c3", "c5"):
+        rec = (bench_c3 if args.config == "c3" else bench_c5)(args, eng, dev, dist, rank, world)
+        if rank == 0:
+            print(json.dumps(rec))
+        if dist:
+            dist.destroy_process_group()
+        eng.close()
+        return
 
     n = args.samples
     audio = torch.as_tensor(synthetic.speech_like(n, seed=1000 + rank), dtype=torch.float64, device=dev)

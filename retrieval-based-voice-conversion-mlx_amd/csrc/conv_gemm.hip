@@ -596,8 +596,11 @@ long long conv_plan_splitk(ConvArgs& a, bool two_d) {
   const double M = two_d ? (double)a.T_out * a.W_out : (double)a.T_out;
   const double flops = 2.0 * M * a.N * (double)a.C_in * a.taps * a.batch * a.batch_inner;
   // split only where the output grid leaves CUs idle AND the contraction is long enough to pay
-  // for the extra combine launch (~5-10 us)
-  if (tiles >= 384 || iters < 8 || flops < 1.0e8) return 0;
+  // for the extra combine launch (~5-10 us): a tile's (chunk, tap) steps are a serial chain of
+  // ~1.5-2 us each (global B load -> LDS -> barrier -> MFMA), so a handful of tiles walking >= 16 steps
+  // is latency-bound whatever the FLOP count (RMVPE's deepest levels at streaming sizes: 8 tiles x 144
+  // steps = 264 us unsplit)
+  if (tiles >= 384 || iters < 8 || (flops < 1.0e8 && iters < 16)) return 0;
   int ks = (int)((768 + tiles - 1) / tiles);
   ks = std::min(ks, iters / 2);
   ks = std::min(ks, 32);
