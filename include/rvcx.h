@@ -80,6 +80,14 @@ int rvcx_hubert(rvcx_ctx* ctx, const float* d_audio, int64_t n, int version, flo
 int rvcx_rmvpe(rvcx_ctx* ctx, const float* d_audio, int64_t n, float thred, double* d_f0, int64_t cap_frames,
                int64_t* frames_out, float* d_hidden, void* stream);
 
+/* Batched forms over B equal-length inputs (rows of stride lda floats; HuBERT needs lda % 5 == 0 when B > 1):
+ * feats [B][L][D] and f0 [B][F] (d_hidden [B][F][360]) back to back. Used by the streaming path (B streams
+ * per hop) and the batched offline mode; each sequence's result equals the unbatched call's. */
+int rvcx_hubert_batch(rvcx_ctx* ctx, const float* d_audio, int64_t n, int64_t lda, int B, int version, float* d_feats,
+                      int64_t cap_rows, int64_t* rows_out, void* stream);
+int rvcx_rmvpe_batch(rvcx_ctx* ctx, const float* d_audio, int64_t n, int64_t lda, int B, float thred, double* d_f0,
+                     int64_t cap_frames, int64_t* frames_out, float* d_hidden, void* stream);
+
 /* RMVPE0Predictor.decode (rvc/lib/predictors/RMVPE.py:515-540; rvc_mlx/lib/mlx/rmvpe.py:357-406):
  * salience [F][360] fp32 -> f0 [F] fp64 (argmax, +-4-bin weighted cents, threshold, 10 * 2^(c/1200), 10 -> 0). */
 int rvcx_rmvpe_decode(rvcx_ctx* ctx, const float* d_hidden, int64_t F, float thred, double* d_f0, void* stream);

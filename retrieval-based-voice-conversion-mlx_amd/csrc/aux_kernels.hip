@@ -457,11 +457,13 @@ hipError_t zp_sample(const float* stats, int B, int T, int I, const float* eps, 
 
 // ------------------------------------------------------------------ GroupNorm(C groups of 1 channel) over time + GELU (HuBERT conv0)
 __global__ void k_gn_stats(const float* x, int T, int C, int chunk, double* ws) {
-  // grid (C/64, nchunks); block 256 = 64 channels x 4 row lanes
+  // grid (C/64, nchunks, B); block 256 = 64 channels x 4 row lanes
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int rl = threadIdx.x >> 6;
   const int t0 = blockIdx.y * chunk;
   const int t1 = min(T, t0 + chunk);
+  x += (long long)blockIdx.z * T * C;
+  ws += (long long)blockIdx.z * gridDim.y * C * 2;
   double s = 0.0, q = 0.0;
   if (c < C) {
     for (int t = t0 + rl; t < t1; t += 4) {
@@ -482,11 +484,14 @@ __global__ void k_gn_stats(const float* x, int T, int C, int chunk, double* ws) 
   }
 }
 // per-channel statistics -> affine form y = x * scale + shift (torch GroupNorm's ApplyScaleBias:
-// scale = rstd * gamma, shift = beta - mean * scale), once per channel instead of per element
+// scale = rstd * gamma, shift = beta - mean * scale), once per channel instead of per element.
+// grid (C/256, B): sequence b's partials at ws + b*nchunks*C*2, its scale/shift at ss + b*2C
 __global__ void k_gn_finalize(const double* ws, int nchunks, int T, int C, const float* gamma, const float* beta,
                               float eps, float* ss) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
+  ws += (long long)blockIdx.y * nchunks * C * 2;
+  ss += (long long)blockIdx.y * 2 * C;
   double s = 0.0, q = 0.0;
   for (int k = 0; k < nchunks; ++k) {
     s += ws[((long long)k * C + c) * 2];
@@ -500,35 +505,42 @@ __global__ void k_gn_finalize(const double* ws, int nchunks, int T, int C, const
   ss[c] = scale;
   ss[C + c] = beta[c] - (float)mean * scale;
 }
-__global__ void k_gn_apply(float* __restrict__ x, long long n4, int C4, const float* __restrict__ ss, int C) {
+// x: B sequences of T rows back to back; n4_per = T*C/4 float4 per sequence
+__global__ void k_gn_apply(float* __restrict__ x, long long n4, long long n4_per, int C4, const float* __restrict__ ss,
+                           int C) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(i % C4) * 4;
+    const float* sb = ss + (i / n4_per) * 2 * C;
     f32x4v v = reinterpret_cast<f32x4v*>(x)[i];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float t = v[j] * ss[c + j] + ss[C + c + j];
+      const float t = v[j] * sb[c + j] + sb[C + c + j];
       v[j] = 0.5f * t * (1.f + erff(t * 0.70710678118654752440f));
     }
     reinterpret_cast<f32x4v*>(x)[i] = v;
   }
 }
 hipError_t groupnorm_time_gelu(float* x, int T, int C, const float* gamma, const float* beta, float eps, double* ws,
-                               hipStream_t s) {
-  // ws: GN_CHUNKS * C * 2 doubles of partial sums, then 2 * C floats of scale/shift
+                               hipStream_t s, int B) {
+  // ws (groupnorm_ws_doubles(C, B)): B * GN_CHUNKS * C * 2 doubles of partial sums, then B * 2C floats
   const int nchunks = GN_CHUNKS;
   const int chunk = (T + nchunks - 1) / nchunks;
-  if (C % 4) return hipErrorInvalidValue;
-  float* ss = reinterpret_cast<float*>(ws + (size_t)nchunks * C * 2);
-  hipLaunchKernelGGL(k_gn_stats, dim3((C + 63) / 64, nchunks), dim3(256), 0, s, x, T, C, chunk, ws);
-  hipLaunchKernelGGL(k_gn_finalize, dim3((C + 255) / 256), dim3(256), 0, s, ws, nchunks, T, C, gamma, beta, eps, ss);
-  const long long n4 = (long long)T * C / 4;
-  hipLaunchKernelGGL(k_gn_apply, dim3(nblocks(n4)), dim3(TB), 0, s, x, n4, C / 4, ss, C);
+  if (C % 4 || B < 1) return hipErrorInvalidValue;
+  float* ss = reinterpret_cast<float*>(ws + (size_t)B * nchunks * C * 2);
+  hipLaunchKernelGGL(k_gn_stats, dim3((C + 63) / 64, nchunks, B), dim3(256), 0, s, x, T, C, chunk, ws);
+  hipLaunchKernelGGL(k_gn_finalize, dim3((C + 255) / 256, B), dim3(256), 0, s, ws, nchunks, T, C, gamma, beta, eps,
+                     ss);
+  const long long n4p = (long long)T * C / 4;
+  hipLaunchKernelGGL(k_gn_apply, dim3(nblocks(n4p * B)), dim3(TB), 0, s, x, n4p * B, n4p, C / 4, ss, C);
   return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ RMVPE front end
-__global__ void k_reflect1d(const float* x, int n, int pl, int pr, float* y) {
+// grid.y = sequence: x rows of stride ldx, y rows of stride ldy
+__global__ void k_reflect1d(const float* x, int n, int pl, int pr, float* y, long long ldx, long long ldy) {
   const int m = n + pl + pr;
+  x += blockIdx.y * ldx;
+  y += blockIdx.y * ldy;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
     int j = i - pl;
     if (j < 0) j = -j;
@@ -536,23 +548,28 @@ __global__ void k_reflect1d(const float* x, int n, int pl, int pr, float* y) {
     y[i] = x[j];
   }
 }
-hipError_t reflect_pad_1d(const float* x, int n, int pad_l, int pad_r, float* y, hipStream_t s) {
+hipError_t reflect_pad_1d(const float* x, int n, int pad_l, int pad_r, float* y, hipStream_t s, int B, long long ldx,
+                          long long ldy) {
   if (pad_l >= n || pad_r >= n) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_reflect1d, dim3(nblocks(n + pad_l + pad_r)), dim3(TB), 0, s, x, n, pad_l, pad_r, y);
+  hipLaunchKernelGGL(k_reflect1d, dim3(std::min(nblocks(n + pad_l + pad_r), 2048u), B), dim3(TB), 0, s, x, n, pad_l,
+                     pad_r, y, ldx, ldy);
   return hipGetLastError();
 }
+// grid.y = image: x [B][rows][C] -> y [B][rows + pr][C]
 __global__ void k_reflect_rows(const float* x, int rows, int C, int pr, float* y) {
   const long long n = (long long)(rows + pr) * C;
+  x += (long long)blockIdx.y * rows * C;
+  y += (long long)blockIdx.y * n;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     const int r = (int)(i / C), c = (int)(i % C);
     const int src = r < rows ? r : 2 * (rows - 1) - r;
     y[i] = x[(long long)src * C + c];
   }
 }
-hipError_t reflect_pad_rows(const float* x, int rows, int C, int pad_r, float* y, hipStream_t s) {
+hipError_t reflect_pad_rows(const float* x, int rows, int C, int pad_r, float* y, hipStream_t s, int B) {
   if (pad_r >= rows) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_reflect_rows, dim3(nblocks((long long)(rows + pad_r) * C)), dim3(TB), 0, s, x, rows, C, pad_r,
-                     y);
+  hipLaunchKernelGGL(k_reflect_rows, dim3(std::min(nblocks((long long)(rows + pad_r) * C), 2048u), B), dim3(TB), 0,
+                     s, x, rows, C, pad_r, y);
   return hipGetLastError();
 }
 __global__ void k_stftmag(const float* spec, int F, int nb, float* mag, int ldm) {
@@ -601,12 +618,14 @@ hipError_t nhwc_to_hcw(const float* x, int H, int W, int C, float* y, hipStream_
 }
 
 // ------------------------------------------------------------------ RMVPE decode (RMVPE.py:484-540), fp64 like numpy
-__global__ void k_decode(const float* sal, int F, int ncls, float thred, double* f0) {
+// rows of B sequences: frame f of sequence b reads sal[(b*Fs + f)][.] and writes f0[b*F + f]
+__global__ void k_decode(const float* sal, int F, int Fs, int nrows, int ncls, float thred, double* f0) {
 #pragma clang fp contract(off)  // numpy rounds every product and sum separately
-  const int f = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (f >= F) return;
-  const float* s = sal + (long long)f * ncls;
+  if (row >= nrows) return;
+  const int f = row;
+  const float* s = sal + ((long long)(row / F) * Fs + row % F) * ncls;
   float best = -INFINITY;
   int bi = 0x7fffffff;
   for (int k = lane; k < ncls; k += 64) {
@@ -648,8 +667,10 @@ __global__ void k_decode(const float* sal, int F, int ncls, float thred, double*
     f0[f] = v;
   }
 }
-hipError_t rmvpe_decode(const float* sal, int F, int ncls, float thred, double* f0, hipStream_t s) {
-  hipLaunchKernelGGL(k_decode, dim3((F + 3) / 4), dim3(256), 0, s, sal, F, ncls, thred, f0);
+hipError_t rmvpe_decode(const float* sal, int F, int ncls, float thred, double* f0, hipStream_t s, int B, int Fs) {
+  if (Fs <= 0) Fs = F;
+  const int nrows = B * F;
+  hipLaunchKernelGGL(k_decode, dim3((nrows + 3) / 4), dim3(256), 0, s, sal, F, Fs, nrows, ncls, thred, f0);
   return hipGetLastError();
 }
 

@@ -188,6 +188,30 @@ int rvcx_rmvpe(rvcx_ctx* ctx, const float* d_audio, int64_t n, float thred, doub
   });
 }
 
+int rvcx_hubert_batch(rvcx_ctx* ctx, const float* d_audio, int64_t n, int64_t lda, int B, int version, float* d_feats,
+                      int64_t cap_rows, int64_t* rows_out, void* stream) {
+  return guard(ctx, [&] {
+    if (!ctx->ready[1]) throw Error(RVCX_E_STATE, "hubert weights not finalized");
+    if (!d_audio || !d_feats || n <= 0 || B < 1 || lda < n) throw Error(RVCX_E_INVALID, "rvcx_hubert_batch: bad arguments");
+    set_device(ctx);
+    const int64_t L = hubert_forward_b(*ctx, d_audio, n, lda, B, version == 1 ? 1 : 2, d_feats, cap_rows,
+                                       static_cast<hipStream_t>(stream));
+    if (rows_out) *rows_out = L;
+  });
+}
+
+int rvcx_rmvpe_batch(rvcx_ctx* ctx, const float* d_audio, int64_t n, int64_t lda, int B, float thred, double* d_f0,
+                     int64_t cap_frames, int64_t* frames_out, float* d_hidden, void* stream) {
+  return guard(ctx, [&] {
+    if (!ctx->ready[2]) throw Error(RVCX_E_STATE, "rmvpe weights not finalized");
+    if (!d_audio || !d_f0 || n <= 0 || B < 1 || lda < n) throw Error(RVCX_E_INVALID, "rvcx_rmvpe_batch: bad arguments");
+    set_device(ctx);
+    const int64_t F = rmvpe_forward_b(*ctx, d_audio, n, lda, B, thred, d_f0, cap_frames, d_hidden,
+                                      static_cast<hipStream_t>(stream));
+    if (frames_out) *frames_out = F;
+  });
+}
+
 int rvcx_rmvpe_decode(rvcx_ctx* ctx, const float* d_hidden, int64_t F, float thred, double* d_f0, void* stream) {
   return guard(ctx, [&] {
     if (!d_hidden || !d_f0 || F < 0) throw Error(RVCX_E_INVALID, "rvcx_rmvpe_decode: bad arguments");

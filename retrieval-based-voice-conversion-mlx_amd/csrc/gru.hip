@@ -45,6 +45,10 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ g
 
   const int d = blockIdx.x >> 1;  // direction
   const int q = blockIdx.x & 1;   // half
+  // blockIdx.y = independent sequence (batched streams / utterances of one length)
+  gi += (long long)blockIdx.y * T * 6 * H;
+  out += (long long)blockIdx.y * T * 2 * H;
+  xchg += (long long)blockIdx.y * 4 * 2 * UNITS;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int grp = tid / ROWS;     // 0: own columns, 1: partner columns (wave-uniform: ROWS % 64 == 0)
@@ -154,10 +158,12 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ g
 
 hipError_t gru_bidir(const float* gi, const float* whh_f, const float* bhh_f, const float* whh_b,
                      const float* bhh_b, int T, float* out, unsigned long long* xchg, unsigned* status,
-                     hipStream_t s) {
-  hipError_t e = hipMemsetAsync(xchg, 0, sizeof(unsigned long long) * 4 * 2 * UNITS, s);
+                     hipStream_t s, int B) {
+  // the two halves of a direction spin on each other: all 4B workgroups (1 per CU) must be co-resident
+  if (B < 1 || 4 * B > 256) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(xchg, 0, sizeof(unsigned long long) * gru_xchg_words(B), s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_gru_bidir, dim3(4), dim3(NT), 0, s, gi, whh_f, bhh_f, whh_b, bhh_b, T, out, xchg, status);
+  hipLaunchKernelGGL(k_gru_bidir, dim3(4, B), dim3(NT), 0, s, gi, whh_f, bhh_f, whh_b, bhh_b, T, out, xchg, status);
   return hipGetLastError();
 }
 

@@ -132,6 +132,11 @@ int64_t hubert_forward(Ctx& c, const float* audio, int64_t n, int version, float
                        hipStream_t s);
 int64_t rmvpe_forward(Ctx& c, const float* audio, int64_t n, float thred, double* f0, int64_t cap, float* hidden,
                       hipStream_t s);
+// batched over B equal-length inputs (rows of stride lda); outputs back to back per sequence
+int64_t hubert_forward_b(Ctx& c, const float* audio, int64_t n, int64_t lda, int B, int version, float* feats,
+                         int64_t cap, hipStream_t s);
+int64_t rmvpe_forward_b(Ctx& c, const float* audio, int64_t n, int64_t lda, int B, float thred, double* f0,
+                        int64_t cap, float* hidden, hipStream_t s);
 void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* lengths, const int32_t* pitch,
                    const float* pitchf, const int32_t* sid, const float* eps_z, const float* eps_src, uint64_t seed,
                    float* out, float* zp_out, float* z_out, hipStream_t s);

@@ -134,8 +134,13 @@ int64_t hubert_frames(int64_t n) {
   return t;
 }
 
-int64_t hubert_forward(Ctx& c, const float* audio, int64_t n, int version, float* feats, int64_t cap,
-                       hipStream_t s) {
+// B equal-length sequences: audio row b at audio + b*lda; feats row block b at feats + b*L*outD.
+// Row-wise ops (LayerNorm, Linear, FFN) run over all B*L rows at once; convolutions, GroupNorm and
+// attention take the sequence as their batch index.
+int64_t hubert_forward_b(Ctx& c, const float* audio, int64_t n, int64_t lda, int B, int version, float* feats,
+                         int64_t cap, hipStream_t s) {
+  if (B < 1) throw Error(RVCX_E_INVALID, "hubert: batch < 1");
+  if (B > 1 && lda % 5) throw Error(RVCX_E_INVALID, "hubert: batched audio stride must be a multiple of 5");
   int64_t T[8];
   T[0] = n;
   for (int i = 0; i < 7; ++i) {
@@ -143,20 +148,24 @@ int64_t hubert_forward(Ctx& c, const float* audio, int64_t n, int version, float
     T[i + 1] = (T[i] - HK[i]) / HS[i] + 1;
   }
   const int L = (int)T[7];
+  const int BL = B * L;
   const int outD = version == 1 ? 256 : HD;
   if (L > cap) throw Error(RVCX_E_CAPACITY, "hubert: output needs " + std::to_string(L) + " rows");
-  float* a = c.buf<float>("hb.a", (size_t)T[1] * HCONV, s);
-  float* b = c.buf<float>("hb.b", (size_t)T[2] * HCONV, s);
-  double* gnws = c.buf<double>("hb.gnws", groupnorm_ws_doubles(HCONV), s);
+  float* a = c.buf<float>("hb.a", (size_t)B * T[1] * HCONV, s);
+  float* b = c.buf<float>("hb.b", (size_t)B * T[2] * HCONV, s);
+  double* gnws = c.buf<double>("hb.gnws", groupnorm_ws_doubles(HCONV, B), s);
   {  // conv0 over 5-sample rows (2 taps)
     ConvArgs a0 = lin(audio, 5, (int)(n / 5), 5, c.W("hb.conv0"), HCONV, nullptr, a, HCONV);
     a0.taps = 2;
     a0.w_ts = (long long)HCONV * 5;
     a0.ldw = 5;
     a0.T_out = (int)T[1];
+    a0.batch = B;
+    a0.x_bs = lda;
+    a0.y_bs = T[1] * HCONV;
     run1(c, a0, s);
   }
-  check(groupnorm_time_gelu(a, (int)T[1], HCONV, c.W("hb.gn.g"), c.W("hb.gn.b"), 1e-5f, gnws, s), "groupnorm");
+  check(groupnorm_time_gelu(a, (int)T[1], HCONV, c.W("hb.gn.g"), c.W("hb.gn.b"), 1e-5f, gnws, s, B), "groupnorm");
   float* cur = a;
   float* nxt = b;
   for (int i = 1; i < 7; ++i) {
@@ -166,15 +175,19 @@ int64_t hubert_forward(Ctx& c, const float* audio, int64_t n, int version, float
     ci.w_ts = (long long)HCONV * HCONV;
     ci.T_out = (int)T[i + 1];
     ci.act = ACT_GELU;
+    ci.batch = B;
+    ci.x_bs = T[i] * HCONV;
+    ci.y_bs = T[i + 1] * HCONV;
     run1(c, ci, s);
     std::swap(cur, nxt);
   }
   // feature projection: LayerNorm(512) -> Linear(512, 768)
-  float* hs = c.buf<float>("hb.hs", (size_t)L * HD, s);
-  float* hs2 = c.buf<float>("hb.hs2", (size_t)L * HD, s);
-  check(layernorm_rows(cur, nullptr, nxt, c.W("hb.fp.ln.g"), c.W("hb.fp.ln.b"), L, HCONV, 1e-5f, nullptr, s), "fp_ln");
-  run1(c, lin(nxt, HCONV, L, HCONV, c.W("hb.fp.w"), HD, c.W("hb.fp.b"), hs, HD), s);
-  {  // hs + gelu(pos_conv(hs)) (groups as inner batch), then encoder LayerNorm
+  float* hs = c.buf<float>("hb.hs", (size_t)BL * HD, s);
+  float* hs2 = c.buf<float>("hb.hs2", (size_t)BL * HD, s);
+  check(layernorm_rows(cur, nullptr, nxt, c.W("hb.fp.ln.g"), c.W("hb.fp.ln.b"), BL, HCONV, 1e-5f, nullptr, s),
+        "fp_ln");
+  run1(c, lin(nxt, HCONV, BL, HCONV, c.W("hb.fp.w"), HD, c.W("hb.fp.b"), hs, HD), s);
+  {  // hs + gelu(pos_conv(hs)) (groups as inner batch, sequences as outer batch), then encoder LayerNorm
     const int cg = HD / POS_G;
     ConvArgs p = lin(hs, HD, L, cg, c.W("hb.pos.w"), cg, c.W("hb.pos.b"), hs2, HD);
     p.taps = POS_K;
@@ -191,18 +204,20 @@ int64_t hubert_forward(Ctx& c, const float* audio, int64_t n, int version, float
     p.ldr = HD;
     p.res_bs2 = cg;
     p.res_mode = RES_ADD_POST;
+    p.batch = B;
+    p.x_bs = p.y_bs = p.res_bs = (long long)L * HD;
     run1(c, p, s);
-    check(layernorm_rows(hs2, nullptr, hs, c.W("hb.enc.ln.g"), c.W("hb.enc.ln.b"), L, HD, 1e-5f, nullptr, s),
+    check(layernorm_rows(hs2, nullptr, hs, c.W("hb.enc.ln.g"), c.W("hb.enc.ln.b"), BL, HD, 1e-5f, nullptr, s),
           "enc_ln");
   }
-  float* qkv = c.buf<float>("hb.qkv", (size_t)L * 3 * HD, s);
-  float* sc = c.buf<float>("hb.scores", (size_t)HHEADS * L * L, s);
-  float* att = c.buf<float>("hb.att", (size_t)L * HD, s);
-  float* ff = c.buf<float>("hb.ff", (size_t)L * HFF, s);
+  float* qkv = c.buf<float>("hb.qkv", (size_t)BL * 3 * HD, s);
+  float* sc = c.buf<float>("hb.scores", (size_t)B * HHEADS * L * L, s);
+  float* att = c.buf<float>("hb.att", (size_t)BL * HD, s);
+  float* ff = c.buf<float>("hb.ff", (size_t)BL * HFF, s);
   const int hd = HD / HHEADS;
   for (int i = 0; i < 12; ++i) {
     const std::string q = "hb." + std::to_string(i);
-    run1(c, lin(hs, HD, L, HD, c.W(q + ".qkv.w"), 3 * HD, c.W(q + ".qkv.b"), qkv, 3 * HD), s);
+    run1(c, lin(hs, HD, BL, HD, c.W(q + ".qkv.w"), 3 * HD, c.W(q + ".qkv.b"), qkv, 3 * HD), s);
     {
       ConvArgs a1 = lin(qkv, 3 * HD, L, hd, qkv + HD, L, nullptr, sc, L);
       a1.ldw = 3 * HD;
@@ -211,9 +226,12 @@ int64_t hubert_forward(Ctx& c, const float* audio, int64_t n, int version, float
       a1.x_bs2 = hd;
       a1.w_bs2 = hd;
       a1.y_bs2 = (long long)L * L;
+      a1.batch = B;
+      a1.x_bs = a1.w_bs = (long long)L * 3 * HD;
+      a1.y_bs = (long long)HHEADS * L * L;
       run1(c, a1, s);
     }
-    check(softmax_rows(sc, HHEADS * L, L, s), "softmax");
+    check(softmax_rows(sc, B * HHEADS * L, L, s), "softmax");
     {
       ConvArgs a2 = lin(sc, L, L, L, qkv + 2 * HD, hd, nullptr, att, HD);
       a2.ldw = 3 * HD;
@@ -222,35 +240,44 @@ int64_t hubert_forward(Ctx& c, const float* audio, int64_t n, int version, float
       a2.x_bs2 = (long long)L * L;
       a2.w_bs2 = hd;
       a2.y_bs2 = hd;
+      a2.batch = B;
+      a2.x_bs = (long long)HHEADS * L * L;
+      a2.w_bs = (long long)L * 3 * HD;
+      a2.y_bs = (long long)L * HD;
       run1(c, a2, s);
     }
     {
-      ConvArgs a3 = lin(att, HD, L, HD, c.W(q + ".o.w"), HD, c.W(q + ".o.b"), hs2, HD);
+      ConvArgs a3 = lin(att, HD, BL, HD, c.W(q + ".o.w"), HD, c.W(q + ".o.b"), hs2, HD);
       a3.res = hs;
       a3.ldr = HD;
       a3.res_mode = RES_ADD_POST;
       run1(c, a3, s);
     }
-    check(layernorm_rows(hs2, nullptr, hs, c.W(q + ".ln1.g"), c.W(q + ".ln1.b"), L, HD, 1e-5f, nullptr, s), "ln1");
+    check(layernorm_rows(hs2, nullptr, hs, c.W(q + ".ln1.g"), c.W(q + ".ln1.b"), BL, HD, 1e-5f, nullptr, s), "ln1");
     {
-      ConvArgs f1 = lin(hs, HD, L, HD, c.W(q + ".ff1.w"), HFF, c.W(q + ".ff1.b"), ff, HFF);
+      ConvArgs f1 = lin(hs, HD, BL, HD, c.W(q + ".ff1.w"), HFF, c.W(q + ".ff1.b"), ff, HFF);
       f1.act = ACT_GELU;
       run1(c, f1, s);
-      ConvArgs f2 = lin(ff, HFF, L, HFF, c.W(q + ".ff2.w"), HD, c.W(q + ".ff2.b"), hs2, HD);
+      ConvArgs f2 = lin(ff, HFF, BL, HFF, c.W(q + ".ff2.w"), HD, c.W(q + ".ff2.b"), hs2, HD);
       f2.res = hs;
       f2.ldr = HD;
       f2.res_mode = RES_ADD_POST;
       run1(c, f2, s);
     }
-    check(layernorm_rows(hs2, nullptr, hs, c.W(q + ".ln2.g"), c.W(q + ".ln2.b"), L, HD, 1e-5f, nullptr, s), "ln2");
+    check(layernorm_rows(hs2, nullptr, hs, c.W(q + ".ln2.g"), c.W(q + ".ln2.b"), BL, HD, 1e-5f, nullptr, s), "ln2");
   }
   if (version == 1) {
     if (!c.dev.count("hb.final_proj.w")) throw Error(RVCX_E_STATE, "hubert: v1 needs final_proj weights");
-    run1(c, lin(hs, HD, L, HD, c.W("hb.final_proj.w"), 256, c.W("hb.final_proj.b"), feats, 256), s);
+    run1(c, lin(hs, HD, BL, HD, c.W("hb.final_proj.w"), 256, c.W("hb.final_proj.b"), feats, 256), s);
   } else {
-    RVCX_HIP(hipMemcpyAsync(feats, hs, (size_t)L * outD * sizeof(float), hipMemcpyDeviceToDevice, s));
+    RVCX_HIP(hipMemcpyAsync(feats, hs, (size_t)BL * outD * sizeof(float), hipMemcpyDeviceToDevice, s));
   }
   return L;
+}
+
+int64_t hubert_forward(Ctx& c, const float* audio, int64_t n, int version, float* feats, int64_t cap,
+                       hipStream_t s) {
+  return hubert_forward_b(c, audio, n, n, 1, version, feats, cap, s);
 }
 
 // ================================================================== RMVPE
@@ -343,8 +370,11 @@ void block_weights(Ctx& c, const std::string& p, const std::string& q, int cin, 
 }
 
 ConvArgs c2d(const float* x, int ldx, int H, int W, int Cin, const float* w, int N, const float* bias, float* y,
-             int ldy) {
+             int ldy, int B = 1) {
   ConvArgs a;
+  a.batch = B;  // B images of H x W pixels back to back
+  a.x_bs = (long long)H * W * ldx;
+  a.y_bs = (long long)H * W * ldy;
   a.x = x;
   a.ldx = ldx;
   a.T_in = H;
@@ -368,25 +398,27 @@ ConvArgs c2d(const float* x, int ldx, int H, int W, int Cin, const float* w, int
 }
 
 // ConvBlockRes (RMVPE.py:13-57): relu(bn(conv)) x2 + shortcut(x) (or x)
+// B images back to back (NHWC, row stride ldx / ldy per pixel)
 void conv_block(Ctx& c, const std::string& q, const float* x, int ldx, int H, int W, int cin, int cout, float* y,
-                int ldy, hipStream_t s) {
+                int ldy, hipStream_t s, int B = 1) {
   const size_t P = (size_t)H * W;
-  float* t = c.buf<float>("rm.blk.t", P * cout, s);
-  ConvArgs a = c2d(x, ldx, H, W, cin, c.W(q + ".c1.w"), cout, c.W(q + ".c1.b"), t, cout);
+  float* t = c.buf<float>("rm.blk.t", (size_t)B * P * cout, s);
+  ConvArgs a = c2d(x, ldx, H, W, cin, c.W(q + ".c1.w"), cout, c.W(q + ".c1.b"), t, cout, B);
   a.act = ACT_RELU;
   run2(c, a, s);
   const float* res = x;
   int ldr = ldx;
   if (cin != cout) {
-    float* sc = c.buf<float>("rm.blk.sc", P * cout, s);
-    run1(c, lin(x, ldx, (int)P, cin, c.W(q + ".sc.w"), cout, c.W(q + ".sc.b"), sc, cout), s);
+    float* sc = c.buf<float>("rm.blk.sc", (size_t)B * P * cout, s);
+    run1(c, lin(x, ldx, (int)(B * P), cin, c.W(q + ".sc.w"), cout, c.W(q + ".sc.b"), sc, cout), s);
     res = sc;
     ldr = cout;
   }
-  ConvArgs b = c2d(t, cout, H, W, cout, c.W(q + ".c2.w"), cout, c.W(q + ".c2.b"), y, ldy);
+  ConvArgs b = c2d(t, cout, H, W, cout, c.W(q + ".c2.w"), cout, c.W(q + ".c2.b"), y, ldy, B);
   b.act = ACT_RELU;
   b.res = res;
   b.ldr = ldr;
+  b.res_bs = (long long)P * ldr;
   b.res_mode = RES_ADD_POST;
   run2(c, b, s);
 }
@@ -479,8 +511,10 @@ void finalize_rmvpe(Ctx& c) {
   c.alloc_weight("rm.fc.b", getw(c, 2, "fc.1.bias", {NCLS}).v);
 }
 
-// E2E on a mel chunk image [Fc][128] (already padded to a multiple of 32 frames) -> sal [Fc][360]
-static void e2e_chunk(Ctx& c, float* img, int Fc, float* sal, hipStream_t s) {
+// E2E on B mel chunk images [B][Fc][128] (already padded to a multiple of 32 frames) -> sal [B][Fc][360].
+// Pooling and the per-row transforms run on the B images stacked along time (every level's height is
+// even, so no 2x2 window straddles two images); convolutions take the image as their batch index.
+static void e2e_chunk(Ctx& c, float* img, int Fc, float* sal, hipStream_t s, int B = 1) {
   int H = Fc, W = NMEL;
   // encoder: level outputs go to the second half of the decoder concat buffers
   float* catb[LEVELS];
@@ -488,22 +522,22 @@ static void e2e_chunk(Ctx& c, float* img, int Fc, float* sal, hipStream_t s) {
   const float* x = img;
   int ldx = 1;
   for (int i = 0; i < LEVELS; ++i) {
-    catb[i] = c.buf<float>("rm.cat" + std::to_string(i), (size_t)H * W * 2 * cout, s);
-    float* pa = c.buf<float>("rm.pa", (size_t)Fc * NMEL * C_BASE * 2, s);
-    float* pb = c.buf<float>("rm.pb", (size_t)Fc * NMEL * C_BASE * 2, s);
+    catb[i] = c.buf<float>("rm.cat" + std::to_string(i), (size_t)B * H * W * 2 * cout, s);
+    float* pa = c.buf<float>("rm.pa", (size_t)B * Fc * NMEL * C_BASE * 2, s);
+    float* pb = c.buf<float>("rm.pb", (size_t)B * Fc * NMEL * C_BASE * 2, s);
     const float* in = x;
     int ldi = ldx, ci = cin;
     for (int b = 0; b < NBLK; ++b) {
       const bool last = b == NBLK - 1;
       float* out = last ? catb[i] + cout : (b % 2 == 0 ? pa : pb);
       conv_block(c, "rm.enc" + std::to_string(i) + "." + std::to_string(b), in, ldi, H, W, ci, cout, out,
-                 last ? 2 * cout : cout, s);
+                 last ? 2 * cout : cout, s, B);
       in = out;
       ldi = last ? 2 * cout : cout;
       ci = cout;
     }
-    float* pooled = c.buf<float>("rm.pool" + std::to_string(i), (size_t)(H / 2) * (W / 2) * cout, s);
-    check(avgpool2(catb[i] + cout, H, W, cout, 2 * cout, pooled, s), "avgpool");
+    float* pooled = c.buf<float>("rm.pool" + std::to_string(i), (size_t)B * (H / 2) * (W / 2) * cout, s);
+    check(avgpool2(catb[i] + cout, B * H, W, cout, 2 * cout, pooled, s), "avgpool");
     x = pooled;
     ldx = cout;
     H /= 2;
@@ -514,14 +548,15 @@ static void e2e_chunk(Ctx& c, float* img, int Fc, float* sal, hipStream_t s) {
   // intermediate (4 x ResEncoderBlock without pooling)
   const int top = C_BASE << LEVELS;
   {
-    float* ia = c.buf<float>("rm.ia", (size_t)H * W * top, s);
-    float* ib = c.buf<float>("rm.ib", (size_t)H * W * top, s);
+    float* ia = c.buf<float>("rm.ia", (size_t)B * H * W * top, s);
+    float* ib = c.buf<float>("rm.ib", (size_t)B * H * W * top, s);
     const float* in = x;
     int ci = cin, ldi = ldx, k = 0;
     for (int i = 0; i < INTER; ++i)
       for (int b = 0; b < NBLK; ++b, ++k) {
         float* out = (k % 2 == 0) ? ia : ib;
-        conv_block(c, "rm.int" + std::to_string(i) + "." + std::to_string(b), in, ldi, H, W, ci, top, out, top, s);
+        conv_block(c, "rm.int" + std::to_string(i) + "." + std::to_string(b), in, ldi, H, W, ci, top, out, top, s,
+                   B);
         in = out;
         ci = top;
         ldi = top;
@@ -557,17 +592,20 @@ static void e2e_chunk(Ctx& c, float* img, int Fc, float* sal, hipStream_t s) {
       a.out_cv = co;
       a.bias = c.W(q + ".up.b");
       a.act = ACT_RELU;
-      run2(c, a, s, 2.0 * H * W * (double)C * co * 9);
+      a.batch = B;
+      a.x_bs = (long long)H * W * ldx;
+      a.y_bs = (long long)(2 * H) * (2 * W) * 2 * co;
+      run2(c, a, s, 2.0 * B * H * W * (double)C * co * 9);
     }
     H *= 2;
     W *= 2;
-    float* da = c.buf<float>("rm.da", (size_t)Fc * NMEL * C_BASE, s);
-    float* db = c.buf<float>("rm.db", (size_t)Fc * NMEL * C_BASE, s);
+    float* da = c.buf<float>("rm.da", (size_t)B * Fc * NMEL * C_BASE, s);
+    float* db = c.buf<float>("rm.db", (size_t)B * Fc * NMEL * C_BASE, s);
     const float* in = cb;
     int ci = 2 * co, ldi = 2 * co;
     for (int b = 0; b < NBLK; ++b) {
       float* out = (b % 2 == 0) ? da : db;
-      conv_block(c, q + "." + std::to_string(b), in, ldi, H, W, ci, co, out, co, s);
+      conv_block(c, q + "." + std::to_string(b), in, ldi, H, W, ci, co, out, co, s, B);
       in = out;
       ci = co;
       ldi = co;
@@ -577,73 +615,94 @@ static void e2e_chunk(Ctx& c, float* img, int Fc, float* sal, hipStream_t s) {
     C = co;
   }
   // cnn (16 -> 3, 3x3, bias) -> [Fc][3*128] (index c*128 + w) -> BiGRU -> Linear + sigmoid
-  float* cn = c.buf<float>("rm.cnn", (size_t)Fc * NMEL * 3, s);
-  run2(c, c2d(x, ldx, H, W, C_BASE, c.W("rm.cnn.w"), 3, c.W("rm.cnn.b"), cn, 3), s);
-  float* feat = c.buf<float>("rm.feat", (size_t)Fc * 3 * NMEL, s);
-  check(nhwc_to_hcw(cn, Fc, NMEL, 3, feat, s), "nhwc_to_hcw");
-  float* gi = c.buf<float>("rm.gi", (size_t)Fc * 6 * GRU_H, s);
-  run1(c, lin(feat, 3 * NMEL, Fc, 3 * NMEL, c.W("rm.gru.wih"), 6 * GRU_H, c.W("rm.gru.bih"), gi, 6 * GRU_H), s);
-  float* go = c.buf<float>("rm.gruout", (size_t)Fc * 2 * GRU_H, s);
-  unsigned long long* xchg = c.buf<unsigned long long>("rm.xchg", 4 * 2 * 128, s);
+  float* cn = c.buf<float>("rm.cnn", (size_t)B * Fc * NMEL * 3, s);
+  run2(c, c2d(x, ldx, H, W, C_BASE, c.W("rm.cnn.w"), 3, c.W("rm.cnn.b"), cn, 3, B), s);
+  float* feat = c.buf<float>("rm.feat", (size_t)B * Fc * 3 * NMEL, s);
+  check(nhwc_to_hcw(cn, B * Fc, NMEL, 3, feat, s), "nhwc_to_hcw");
+  float* gi = c.buf<float>("rm.gi", (size_t)B * Fc * 6 * GRU_H, s);
+  run1(c, lin(feat, 3 * NMEL, B * Fc, 3 * NMEL, c.W("rm.gru.wih"), 6 * GRU_H, c.W("rm.gru.bih"), gi, 6 * GRU_H), s);
+  float* go = c.buf<float>("rm.gruout", (size_t)B * Fc * 2 * GRU_H, s);
+  unsigned long long* xchg = c.buf<unsigned long long>("rm.xchg", gru_xchg_words(B), s);
   unsigned* status = c.buf<unsigned>("rm.status", 4, s);
   RVCX_HIP(hipMemsetAsync(status, 0, sizeof(unsigned), s));
   check(gru_bidir(gi, c.W("rm.gru.whh_f"), c.W("rm.gru.bhh_f"), c.W("rm.gru.whh_b"), c.W("rm.gru.bhh_b"), Fc, go,
-                  xchg, status, s),
+                  xchg, status, s, B),
         "gru");
-  ConvArgs f = lin(go, 2 * GRU_H, Fc, 2 * GRU_H, c.W("rm.fc.w"), NCLS, c.W("rm.fc.b"), sal, NCLS);
+  ConvArgs f = lin(go, 2 * GRU_H, B * Fc, 2 * GRU_H, c.W("rm.fc.w"), NCLS, c.W("rm.fc.b"), sal, NCLS);
   f.act = ACT_SIGMOID;
   run1(c, f, s);
 }
 
-int64_t rmvpe_forward(Ctx& c, const float* audio, int64_t n, float thred, double* f0, int64_t cap, float* hidden,
-                      hipStream_t s) {
+// B equal-length sequences: audio row b at audio + b*lda; f0 row b at f0 + b*F; hidden row b at hidden + b*F*360.
+int64_t rmvpe_forward_b(Ctx& c, const float* audio, int64_t n, int64_t lda, int B, float thred, double* f0,
+                        int64_t cap, float* hidden, hipStream_t s) {
+  if (B < 1) throw Error(RVCX_E_INVALID, "rmvpe: batch < 1");
   if (n < NFFT / 2 + 1) throw Error(RVCX_E_SHAPE, "rmvpe: input shorter than 513 samples");
   const int F = (int)(1 + n / HOP);
   if (F > cap) throw Error(RVCX_E_CAPACITY, "rmvpe: output needs " + std::to_string(F) + " frames");
   // MelSpectrogram (RMVPE.py:388-417): reflect pad 512, |STFT| (Hann 1024, hop 160), mel, log(clamp(1e-5))
   const int64_t np = n + NFFT;
   const int64_t rows = (np + 31) / 32;
-  float* xp = c.buf<float>("rm.xp", (size_t)rows * 32, s);
-  RVCX_HIP(hipMemsetAsync(xp + np, 0, (size_t)(rows * 32 - np) * sizeof(float), s));
-  check(reflect_pad_1d(audio, (int)n, NFFT / 2, NFFT / 2, xp, s), "reflect_pad");
-  float* spec = c.buf<float>("rm.spec", (size_t)F * 2 * NBIN, s);
+  float* xp = c.buf<float>("rm.xp", (size_t)B * rows * 32, s);
+  if (rows * 32 > np) RVCX_HIP(hipMemsetAsync(xp, 0, (size_t)B * rows * 32 * sizeof(float), s));
+  check(reflect_pad_1d(audio, (int)n, NFFT / 2, NFFT / 2, xp, s, B, lda, rows * 32), "reflect_pad");
+  float* spec = c.buf<float>("rm.spec", (size_t)B * F * 2 * NBIN, s);
   {
     ConvArgs a = lin(xp, 32, (int)rows, 32, c.W("rm.stft"), 2 * NBIN, nullptr, spec, 2 * NBIN);
     a.taps = 32;
     a.stride = 5;
     a.w_ts = (long long)2 * NBIN * 32;
     a.T_out = F;
+    a.batch = B;
+    a.x_bs = rows * 32;
+    a.y_bs = (long long)F * 2 * NBIN;
     run1(c, a, s, 0.0);
   }
   const int ldm = 516;
-  float* mag = c.buf<float>("rm.mag", (size_t)F * ldm, s);
-  check(stft_magnitude(spec, F, NBIN, mag, ldm, s), "stft_mag");
-  float* mel = c.buf<float>("rm.melout", (size_t)F * NMEL, s);
+  float* mag = c.buf<float>("rm.mag", (size_t)B * F * ldm, s);
+  check(stft_magnitude(spec, B * F, NBIN, mag, ldm, s), "stft_mag");
+  float* mel = c.buf<float>("rm.melout", (size_t)B * F * NMEL, s);
   {
-    ConvArgs a = lin(mag, ldm, F, NBIN, c.W("rm.mel"), NMEL, nullptr, mel, NMEL);
+    ConvArgs a = lin(mag, ldm, B * F, NBIN, c.W("rm.mel"), NMEL, nullptr, mel, NMEL);
     a.act = ACT_LOGCLAMP;
     a.slope = 1e-5f;
     run1(c, a, s);
   }
   // mel2hidden (RMVPE.py:445-482): reflect-pad frames to a multiple of 32, E2E per 32000-frame chunk
   const int Fp = 32 * ((F - 1) / 32 + 1);
-  float* img = c.buf<float>("rm.img", (size_t)Fp * NMEL, s);
+  float* img = c.buf<float>("rm.img", (size_t)B * Fp * NMEL, s);
   if (Fp > F) {
-    check(reflect_pad_rows(mel, F, NMEL, Fp - F, img, s), "pad_frames");
+    check(reflect_pad_rows(mel, F, NMEL, Fp - F, img, s, B), "pad_frames");
   } else {
-    RVCX_HIP(hipMemcpyAsync(img, mel, (size_t)F * NMEL * sizeof(float), hipMemcpyDeviceToDevice, s));
+    RVCX_HIP(hipMemcpyAsync(img, mel, (size_t)B * F * NMEL * sizeof(float), hipMemcpyDeviceToDevice, s));
   }
   const auto& bn0 = c.host[2].at("__bn0__").v;
-  check(affine_inplace(img, (long long)Fp * NMEL, bn0[0], bn0[1], s), "bn0");
-  float* sal = c.buf<float>("rm.sal", (size_t)Fp * NCLS, s);
+  check(affine_inplace(img, (long long)B * Fp * NMEL, bn0[0], bn0[1], s), "bn0");
+  float* sal = c.buf<float>("rm.sal", (size_t)B * Fp * NCLS, s);
   const int chunk = 32000;
-  for (int st = 0; st < Fp; st += chunk) {
-    const int Fc = std::min(chunk, Fp - st);
-    e2e_chunk(c, img + (size_t)st * NMEL, Fc, sal + (size_t)st * NCLS, s);
+  if (Fp <= chunk) {
+    for (int b0 = 0; b0 < B; b0 += 64) {  // the BiGRU keeps 4 co-resident workgroups per sequence
+      const int nb = std::min(64, B - b0);
+      e2e_chunk(c, img + (size_t)b0 * Fp * NMEL, Fp, sal + (size_t)b0 * Fp * NCLS, s, nb);
+    }
+  } else {
+    for (int b = 0; b < B; ++b)
+      for (int st = 0; st < Fp; st += chunk) {
+        const int Fc = std::min(chunk, Fp - st);
+        e2e_chunk(c, img + ((size_t)b * Fp + st) * NMEL, Fc, sal + ((size_t)b * Fp + st) * NCLS, s);
+      }
   }
-  if (hidden) RVCX_HIP(hipMemcpyAsync(hidden, sal, (size_t)F * NCLS * sizeof(float), hipMemcpyDeviceToDevice, s));
-  check(rmvpe_decode(sal, F, NCLS, thred, f0, s), "decode");
+  if (hidden)
+    for (int b = 0; b < B; ++b)
+      RVCX_HIP(hipMemcpyAsync(hidden + (size_t)b * F * NCLS, sal + (size_t)b * Fp * NCLS, (size_t)F * NCLS * sizeof(float),
+                              hipMemcpyDeviceToDevice, s));
+  check(rmvpe_decode(sal, F, NCLS, thred, f0, s, B, Fp), "decode");
   return F;
+}
+
+int64_t rmvpe_forward(Ctx& c, const float* audio, int64_t n, float thred, double* f0, int64_t cap, float* hidden,
+                      hipStream_t s) {
+  return rmvpe_forward_b(c, audio, n, n, 1, thred, f0, cap, hidden, s);
 }
 
 }  // namespace rvcx

@@ -220,8 +220,7 @@ void rt_process(Ctx& c, RtState& s, const float* in48, const int32_t* sids, cons
   const int F = 1 + nf / 160;
   if (F > s.pbuf_n) throw Error(RVCX_E_SHAPE, "stream: f0 track longer than the pitch buffer");
   double* f0 = c.buf<double>("rt.f0", (size_t)B * F, st);
-  for (int b = 0; b < B; ++b)
-    rmvpe_forward(c, conv + (size_t)b * s.conv16 + s.silence_front, nf, 0.03f, f0 + (size_t)b * F, F, nullptr, st);
+  rmvpe_forward_b(c, conv + s.silence_front, nf, s.conv16, B, 0.03f, f0, F, nullptr, st);
   std::vector<double> fac(B, std::pow(2.0, o.f0_up_key / 12.0));
   if (o.f0_autotune) {
     check(f0_autotune(f0, B * F, o.f0_autotune_strength, 0, st), "f0_autotune");
@@ -240,11 +239,10 @@ void rt_process(Ctx& c, RtState& s, const float* in48, const int32_t* sids, cons
                  static_cast<int*>(s.pbuf[nxt].p), static_cast<const float*>(s.fbuf[s.cur].p),
                  static_cast<float*>(s.fbuf[nxt].p), s.pbuf_n, B, st),
         "rt_pitch");
-  // 3. HuBERT per stream (pipeline.py:248-254), rows [B][L][E]
+  // 3. HuBERT over the B convert buffers (pipeline.py:248-254), rows [B][L][E]
   const int64_t L = hubert_frames(s.conv16);
   float* feats = c.buf<float>("rt.feats", (size_t)B * L * E, st);
-  for (int b = 0; b < B; ++b)
-    hubert_forward(c, conv + (size_t)b * s.conv16, s.conv16, hubert_version_for(c), feats + (size_t)b * L * E, L, st);
+  hubert_forward_b(c, conv, s.conv16, s.conv16, B, hubert_version_for(c), feats, L, st);
   // 4. index retrieval of rows skip_head // 2 .. (pipeline.py:264-268, :336-352)
   const float* fx = feats;
   if (o.index_rate > 0) {

@@ -128,22 +128,27 @@ hipError_t conv_post_tanh(const float* x, int B, int T, int C, const float* w, i
 hipError_t randn(float* y, long long n, uint64_t seed, uint64_t offset, hipStream_t s);
 hipError_t zp_sample(const float* stats, int B, int T, int I, const float* eps, uint64_t seed, const float* mask,
                      float* zp, hipStream_t s);
-// ws: groupnorm_ws_doubles(C) doubles
+// ws: groupnorm_ws_doubles(C, B) doubles; x = B sequences of T rows back to back
 constexpr int GN_CHUNKS = 256;
-inline size_t groupnorm_ws_doubles(int C) { return (size_t)GN_CHUNKS * C * 2 + C; }
+inline size_t groupnorm_ws_doubles(int C, int B = 1) { return (size_t)B * (GN_CHUNKS * C * 2 + C); }
 hipError_t groupnorm_time_gelu(float* x, int T, int C, const float* gamma, const float* beta, float eps,
-                               double* ws, hipStream_t s);
+                               double* ws, hipStream_t s, int B = 1);
 hipError_t act_inplace(float* x, long long n, int act, float slope, hipStream_t s);
-hipError_t reflect_pad_1d(const float* x, int n, int pad_l, int pad_r, float* y, hipStream_t s);
-hipError_t reflect_pad_rows(const float* x, int rows, int C, int pad_r, float* y, hipStream_t s);
+hipError_t reflect_pad_1d(const float* x, int n, int pad_l, int pad_r, float* y, hipStream_t s, int B = 1,
+                          long long ldx = 0, long long ldy = 0);
+hipError_t reflect_pad_rows(const float* x, int rows, int C, int pad_r, float* y, hipStream_t s, int B = 1);
 hipError_t stft_magnitude(const float* spec, int F, int nbins, float* mag, int ldm, hipStream_t s);
 hipError_t affine_inplace(float* x, long long n, float a, float b, hipStream_t s);
 hipError_t avgpool2(const float* x, int H, int W, int C, int ldx, float* y, hipStream_t s);
 hipError_t nhwc_to_hcw(const float* x, int H, int W, int C, float* y, hipStream_t s);
+// B independent sequences (gi [B][T][1536], out [B][T][512], xchg gru_xchg_words(B) words)
 hipError_t gru_bidir(const float* gi, const float* whh_f, const float* bhh_f, const float* whh_b,
                      const float* bhh_b, int T, float* out, unsigned long long* xchg, unsigned* status,
-                     hipStream_t s);
-hipError_t rmvpe_decode(const float* sal, int F, int ncls, float thred, double* f0, hipStream_t s);
+                     hipStream_t s, int B = 1);
+inline size_t gru_xchg_words(int B) { return (size_t)B * 4 * 2 * 128; }
+// B sequences: sal rows of sequence b start at b*Fs (Fs = F when 0), f0 [B][F]
+hipError_t rmvpe_decode(const float* sal, int F, int ncls, float thred, double* f0, hipStream_t s, int B = 1,
+                        int Fs = 0);
 hipError_t f0_post(const double* f0, int F, double shift, int32_t* coarse, float* pitchf, double* f0_out,
                    hipStream_t s);
 

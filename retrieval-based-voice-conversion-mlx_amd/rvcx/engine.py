@@ -142,6 +142,33 @@ class Engine:
                                         _ptr(hid), self.stream()), "rmvpe")
         return (f0, hid) if want_hidden else f0
 
+    def hubert_batch(self, audio, version: str = "v2"):
+        """audio [B, N] (16 kHz, equal lengths) -> feats [B, L, D] on device in one batched pass."""
+        t = self.torch
+        a = self._dev(audio, t.float32)
+        B, n = int(a.shape[0]), int(a.shape[1])
+        D = 256 if version == "v1" else 768
+        cap = n // 320 + 8
+        out = t.empty((B, cap, D), dtype=t.float32, device=self.device)
+        rows = ctypes.c_int64(0)
+        self._check(self.lib.rvcx_hubert_batch(self.ctx, a.data_ptr(), n, n, B, 1 if version == "v1" else 2,
+                                               out.data_ptr(), cap, ctypes.byref(rows), self.stream()), "hubert_batch")
+        L = rows.value
+        return out.reshape(-1)[: B * L * D].reshape(B, L, D)
+
+    def rmvpe_batch(self, audio, thred: float = 0.03, want_hidden: bool = False):
+        """audio [B, N] (16 kHz, equal lengths) -> f0 fp64 [B, 1 + N//160] (and salience [B, F, 360])."""
+        t = self.torch
+        a = self._dev(audio, t.float32)
+        B, n = int(a.shape[0]), int(a.shape[1])
+        F = 1 + n // 160
+        f0 = t.empty((B, F), dtype=t.float64, device=self.device)
+        hid = t.empty((B, F, 360), dtype=t.float32, device=self.device) if want_hidden else None
+        fo = ctypes.c_int64(0)
+        self._check(self.lib.rvcx_rmvpe_batch(self.ctx, a.data_ptr(), n, n, B, float(thred), f0.data_ptr(), F,
+                                              ctypes.byref(fo), _ptr(hid), self.stream()), "rmvpe_batch")
+        return (f0, hid) if want_hidden else f0
+
     def rmvpe_decode(self, hidden, thred: float = 0.03):
         """RMVPE0Predictor.decode on device: salience [F, 360] -> f0 fp64 [F]."""
         t = self.torch

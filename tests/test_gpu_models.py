@@ -101,3 +101,23 @@ def test_pipeline_vs_reference(engine):
     assert out.shape == ref.shape
     assert spectrogram_correlation(out, ref) > 0.995
     assert rel_err(out, ref) < 5e-2, rel_err(out, ref)
+
+
+def test_batched_frontends_match_single(engine):
+    """rvcx_hubert_batch / rvcx_rmvpe_batch (B equal-length inputs in one pass) == the per-input calls
+    up to split-K summation order."""
+    from oracle.metrics import cents_agreement
+    from rvcx import synthetic
+
+    B, n = 3, 20000
+    audio = np.stack([synthetic.speech_like(n, seed=70 + b) for b in range(B)]).astype(np.float32)
+    fb = engine.hubert_batch(audio).cpu().numpy()
+    f0b, hb = engine.rmvpe_batch(audio, want_hidden=True)
+    f0b, hb = f0b.cpu().numpy(), hb.cpu().numpy()
+    for b in range(B):
+        f1 = engine.hubert(audio[b]).cpu().numpy()
+        assert fb[b].shape == f1.shape and rel_err(fb[b], f1) < 1e-4, rel_err(fb[b], f1)
+        f01, h1 = engine.rmvpe(audio[b], want_hidden=True)
+        assert rel_err(hb[b], h1.cpu().numpy()) < 1e-4
+        acc, vuv = cents_agreement(f0b[b], f01.cpu().numpy(), 50.0)
+        assert acc >= 0.99 and vuv >= 0.99, (acc, vuv)
