@@ -37,10 +37,11 @@ def parse():
     ap.add_argument("--samples", type=int, default=C2_SAMPLES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-sec", type=float, default=2.0)
-    ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c2",
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
                     help="c2 (default, the headline line): full pipeline, 13.5 s utterance per step; c3: HiFiGAN-NSF "
                          "generator alone, B=32 x 400 frames per step; c5: 16 realtime streams, one 256 ms hop per step")
     ap.add_argument("--streams", type=int, default=16, help="c5: concurrent streams")
+    ap.add_argument("--batch", type=int, default=8, help="c4: 30 s utterances per batched pipeline pass")
     ap.add_argument("--roofline-pass", choices=["inline", "after"], default="after",
                     help="inline: HIP events around every conv launch of the timed steps; after: the timed steps "
                          "run without events and an identical K-step pass right after carries them")
@@ -120,6 +121,35 @@ def bench_c3(args, eng, dev, dist, rank, world):
                          "alg_gflop_per_step": round(k_flops / (args.warmup + args.steps) / 1e9, 2)}}
 
 
+def bench_c4(args, eng, dev, dist, rank, world):
+    """configs[3]: batched offline VC of 30 s utterances; each rank converts its own shard (utterance
+    i goes to rank i % world, extract.py:101-117 style) in batched passes of --batch utterances; one step =
+    one pass. 512 utterances over 8 GPUs = 8 steps of 8 per rank."""
+    from rvcx import synthetic
+    from rvcx.sharding import reduce_throughput
+
+    B, n = args.batch, 480000
+    nb = args.warmup + args.steps
+    utt = [synthetic.speech_like(n, seed=1000 + (i * world + rank)) for i in range(min(nb * B, 64))]
+    audio = torch.as_tensor(np.stack(utt), dtype=torch.float64, device=dev)
+    opts = eng.pipeline_opts(protect=0.33)
+    out = torch.empty((B, ((n + 32000) // 160) * eng.upp), dtype=torch.float32, device=dev)
+
+    def step(i):
+        j = (i * B) % (audio.shape[0] - B + 1)
+        eng.pipeline_batch(audio[j:j + B], opts, sids=0, seed=i, out=out)
+
+    el = _timed(step, args, dev, dist)
+    audio_sec = B * n / SR_IN
+    tot = reduce_throughput(dist, args.steps * audio_sec, el, device=dev)
+    return {"metric": "audio-sec/sec batched offline VC (C4)", "value": round(tot["value"], 3),
+            "unit": "audio-sec/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(tot["elapsed"] / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32", "data": "synthetic speech-like 30 s utterances; random-init weights",
+            "config": {"workload": f"C4: batched pipeline passes of {B} x 30 s utterances per step per GPU",
+                       "batch": B, "parallelism": f"dp{world}"}}
+
+
 def bench_c5(args, eng, dev, dist, rank, world):
     """configs[4]: S concurrent realtime streams, 256 ms hops (read_chunk_size 96), one hop per step;
     latency = wall time of one hop for all streams (input and output in HBM)."""
@@ -185,8 +215,8 @@ def main():
     eng.load_rmvpe(normalize_state(synthetic.rmvpe_state(5)))
     b, a = signal.butter(N=5, Wn=48, btype="high", fs=SR_IN)
     eng.set_highpass(b, a, signal.lfilter_zi(b, a))
-    if args.config in ("c3", "c5"):
-        rec = (bench_c3 if args.config == "c3" else bench_c5)(args, eng, dev, dist, rank, world)
+    if args.config in ("c3", "c4", "c5"):
+        rec = {"c3": bench_c3, "c4": bench_c4, "c5": bench_c5}[args.config](args, eng, dev, dist, rank, world)
         if rank == 0:
             print(json.dumps(rec))
         if dist:

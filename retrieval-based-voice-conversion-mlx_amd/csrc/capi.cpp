@@ -489,3 +489,19 @@ int rvcx_rt_process(rvcx_ctx* ctx, rvcx_rt* rt, const float* d_in, const int32_t
                static_cast<hipStream_t>(stream));
   });
 }
+
+// ------------------------------------------------------------------ batched offline conversion (C4)
+int rvcx_pipeline_batch(rvcx_ctx* ctx, const double* d_audio, int64_t n, int64_t lda, int B,
+                        const rvcx_pipeline_opts* opts, const int32_t* sids, const float* d_eps_z,
+                        const float* d_eps_src, uint64_t seed, float* d_out, int64_t ldo, int64_t* n_out,
+                        void* stream) {
+  return guard(ctx, [&] {
+    if (!ctx->ready[0] || !ctx->ready[1] || !ctx->ready[2]) throw Error(RVCX_E_STATE, "models not finalized");
+    if (!d_audio || !opts || !sids || !d_out || n <= 0 || B < 1 || lda < n)
+      throw Error(RVCX_E_INVALID, "rvcx_pipeline_batch: bad arguments");
+    set_device(ctx);
+    const int64_t no = pipeline_forward_batch(*ctx, d_audio, n, lda, B, *opts, sids, d_eps_z, d_eps_src, seed, d_out,
+                                              ldo, static_cast<hipStream_t>(stream));
+    if (n_out) *n_out = no;
+  });
+}

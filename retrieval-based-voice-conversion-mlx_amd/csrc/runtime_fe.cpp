@@ -140,7 +140,6 @@ int64_t hubert_frames(int64_t n) {
 int64_t hubert_forward_b(Ctx& c, const float* audio, int64_t n, int64_t lda, int B, int version, float* feats,
                          int64_t cap, hipStream_t s) {
   if (B < 1) throw Error(RVCX_E_INVALID, "hubert: batch < 1");
-  if (B > 1 && lda % 5) throw Error(RVCX_E_INVALID, "hubert: batched audio stride must be a multiple of 5");
   int64_t T[8];
   T[0] = n;
   for (int i = 0; i < 7; ++i) {

@@ -192,6 +192,114 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
   return written;
 }
 
+// Batched offline conversion (config C4): B equal-length utterances, each no longer than t_max (one chunk
+// each, pipeline.py:486-512 with opt_ts empty), through one batched RMVPE, one batched HuBERT and one
+// batched Synthesizer.infer. Per utterance the result is Pipeline.pipeline's; the batch only widens
+// every GEMM (B x rows). audio row b at audio + b*lda (fp64); out row b at out + b*ldo, n_out samples each.
+int64_t pipeline_forward_batch(Ctx& c, const double* audio, int64_t n, int64_t lda, int B, const rvcx_pipeline_opts& o,
+                               const int32_t* sids, const float* eps_z, const float* eps_src, uint64_t seed,
+                               float* out, int64_t ldo, hipStream_t s) {
+  if (B < 1) throw Error(RVCX_E_INVALID, "pipeline_batch: B < 1");
+  if (c.hp_order == 0) throw Error(RVCX_E_STATE, "pipeline: high-pass filter not configured");
+  if (o.t_pad < 0 || o.t_pad_tgt < 0 || o.t_pad >= n) throw Error(RVCX_E_INVALID, "pipeline: bad t_pad");
+  if (o.t_max > 0 && n + 160 > o.t_max)
+    throw Error(RVCX_E_INVALID, "pipeline_batch: utterances longer than t_max take the single-utterance path");
+  if (o.index_rate > 0 && !c.ivf) throw Error(RVCX_E_STATE, "pipeline: index_rate > 0 but no feature index loaded");
+  if (o.version != 0 && o.version != hubert_version_for(c))
+    throw Error(RVCX_E_INVALID, "pipeline: version does not match the synthesizer's embedding width");
+  for (int b = 0; b < B; ++b)
+    if (sids[b] < 0 || sids[b] >= c.scfg.n_spk) throw Error(RVCX_E_INVALID, "pipeline_batch: sid out of range");
+  const int64_t W = 160;
+  const int64_t m = n + 2 * o.t_pad;
+  const int64_t ldm = (m + 7) & ~int64_t(7);
+  const int E = c.scfg.emb_dim, upp = c.scfg.upp();
+  // 1. zero-phase high-pass + reflect pad per utterance (pipeline.py:439, :459)
+  float* pad32 = c.buf<float>("pb.pad32", (size_t)B * ldm, s);
+  double* pad64 = c.buf<double>("pb.pad64", (size_t)B * m, s);
+  double* ws = c.buf<double>("pl.iirws", filtfilt_ws_doubles(n, c.hp_order), s);
+  for (int b = 0; b < B; ++b)
+    check(filtfilt_pad(audio + (size_t)b * lda, n, c.hp_b.data(), c.hp_a.data(), c.hp_zi.data(), nullptr, c.hp_order,
+                       o.t_pad, ws, pad64 + (size_t)b * m, pad32 + (size_t)b * ldm, s),
+          "filtfilt_pad");
+  // 2. f0 (batched RMVPE) + get_f0 adjustments per utterance (pipeline.py:462-472, :248-291)
+  const int64_t F = 1 + m / W, T = m / W;
+  double* f0 = c.buf<double>("pb.f0", (size_t)B * F, s);
+  rmvpe_forward_b(c, pad32, m, ldm, B, o.rmvpe_threshold > 0 ? o.rmvpe_threshold : 0.03f, f0, F, nullptr, s);
+  std::vector<double> shift(B, o.pitch);
+  if (o.f0_autotune) {
+    check(f0_autotune(f0, (int)(B * F), o.f0_autotune_strength, o.mlx_semantics ? 1 : 0, s), "f0_autotune");
+    if (!o.mlx_semantics) std::fill(shift.begin(), shift.end(), 0.0);
+  } else if (o.proposed_pitch) {
+    std::vector<double> h((size_t)B * F);
+    RVCX_HIP(hipMemcpyAsync(h.data(), f0, sizeof(double) * h.size(), hipMemcpyDeviceToHost, s));
+    RVCX_HIP(hipStreamSynchronize(s));
+    for (int b = 0; b < B; ++b) {
+      std::vector<double> one(h.begin() + (size_t)b * F, h.begin() + (size_t)(b + 1) * F);
+      shift[b] = o.pitch + proposed_key(one, o.proposed_pitch_threshold);
+    }
+  }
+  int32_t* pitch = c.buf<int32_t>("pb.pitch", (size_t)B * F, s);
+  float* pitchf = c.buf<float>("pb.pitchf", (size_t)B * F, s);
+  for (int b = 0; b < B; ++b)
+    check(f0_post(f0 + (size_t)b * F, (int)F, std::pow(2.0, shift[b] / 12.0), pitch + (size_t)b * F,
+                  pitchf + (size_t)b * F, nullptr, s),
+          "f0_post");
+  // 3. batched HuBERT, retrieval, x2 upsample + protect (pipeline.py:327-362)
+  const int64_t L = hubert_frames(m);
+  const int64_t Tv = std::min<int64_t>(T, 2 * L);
+  if (Tv <= 0) throw Error(RVCX_E_SHAPE, "pipeline_batch: input shorter than one frame");
+  float* feats = c.buf<float>("pb.feats", (size_t)B * L * E, s);
+  hubert_forward_b(c, pad32, m, ldm, B, hubert_version_for(c), feats, L, s);
+  const float* fx = feats;
+  if (o.index_rate > 0) {
+    if (c.ivf->view.d != E) throw Error(RVCX_E_SHAPE, "pipeline: feature index dimension mismatch");
+    float* fr = c.buf<float>("pb.feats_idx", (size_t)B * L * E, s);
+    index_retrieve(c, feats, B * L, E, o.index_rate, fr, s);  // row-wise: the B sequences stack
+    fx = fr;
+  }
+  float* phone = c.buf<float>("pb.phone", (size_t)B * Tv * E, s);
+  int32_t* pc = c.buf<int32_t>("pb.pc", (size_t)B * Tv, s);
+  float* pf = c.buf<float>("pb.pf", (size_t)B * Tv, s);
+  RVCX_HIP(hipMemcpy2DAsync(pc, Tv * sizeof(int32_t), pitch, F * sizeof(int32_t), Tv * sizeof(int32_t), B,
+                            hipMemcpyDeviceToDevice, s));
+  RVCX_HIP(hipMemcpy2DAsync(pf, Tv * sizeof(float), pitchf, F * sizeof(float), Tv * sizeof(float), B,
+                            hipMemcpyDeviceToDevice, s));
+  for (int b = 0; b < B; ++b)
+    check(upsample2_protect(fx + (size_t)b * L * E, feats + (size_t)b * L * E, (int)L, E, phone + (size_t)b * Tv * E,
+                            (int)Tv, o.protect < 0.5f ? pf + (size_t)b * Tv : nullptr, o.protect, s),
+          "upsample");
+  // 4. one batched Synthesizer.infer (pipeline.py:365-372)
+  int32_t* meta = c.buf<int32_t>("pb.meta", 2 * (size_t)B, s);
+  std::vector<int32_t> hm(2 * (size_t)B);
+  for (int b = 0; b < B; ++b) {
+    hm[b] = (int32_t)Tv;
+    hm[B + b] = sids[b];
+  }
+  RVCX_HIP(hipMemcpyAsync(meta, hm.data(), sizeof(int32_t) * hm.size(), hipMemcpyHostToDevice, s));
+  const int64_t nvc = Tv * upp;
+  float* vc = c.buf<float>("pb.vc", (size_t)B * nvc, s);
+  synth_forward(c, B, (int)Tv, phone, meta, pc, pf, meta + B, eps_z, eps_src, seed, vc, nullptr, nullptr, s);
+  // 5. trim, volume envelope, peak normalisation per utterance (pipeline.py:545-552)
+  const int64_t keep = nvc - 2 * o.t_pad_tgt;
+  if (keep <= 0) throw Error(RVCX_E_SHAPE, "pipeline_batch: utterance too short for the padding");
+  if (keep > ldo) throw Error(RVCX_E_CAPACITY, "pipeline_batch: output rows need " + std::to_string(keep));
+  RVCX_HIP(hipMemcpy2DAsync(out, ldo * sizeof(float), vc + o.t_pad_tgt, nvc * sizeof(float), keep * sizeof(float), B,
+                            hipMemcpyDeviceToDevice, s));
+  unsigned* mx = c.buf<unsigned>("pb.max", 4, s);
+  for (int b = 0; b < B; ++b) {
+    float* ob = out + (size_t)b * ldo;
+    if (o.volume_envelope != 1.0) {
+      const int n1 = rms_frame_count(n, 16000), n2 = rms_frame_count(keep, c.scfg.sr);
+      float* rws = c.buf<float>("pl.rms", (size_t)(n1 + n2), s);
+      check(change_rms(pad64 + (size_t)b * m + o.t_pad, n, 16000, ob, keep, c.scfg.sr, (float)o.volume_envelope, rws,
+                       s),
+            "change_rms");
+    }
+    check(peak_normalize(ob, keep, mx, s), "peak_normalize");
+  }
+  return keep;
+}
+
 rvcx_pipeline_opts default_pipeline_opts() {
   rvcx_pipeline_opts o;
   std::memset(&o, 0, sizeof(o));

@@ -307,6 +307,28 @@ class Engine:
         res = out[: no.value]
         return (res, f0) if want_f0 else res
 
+    def pipeline_batch(self, audio, opts: "_lib.PipelineOpts", sids=0, eps_z=None, eps_src=None, seed: int = 0,
+                       out=None):
+        """B equal-length utterances (fp64 [B, n] @16 kHz, each within t_max) through one batched pass.
+        Returns fp32 [B, n_out] on device (row b = Pipeline.pipeline of utterance b)."""
+        t = self.torch
+        a = self._dev(audio, t.float64)
+        B, n = int(a.shape[0]), int(a.shape[1])
+        m = n + 2 * int(opts.t_pad)
+        ldo = (m // 160) * self.upp
+        if out is None or out.numel() < B * ldo:
+            out = t.empty((B, ldo), dtype=t.float32, device=self.device)
+        sid = np.broadcast_to(np.asarray(sids, dtype=np.int32), (B,))
+        sarr = (ctypes.c_int32 * B)(*[int(v) for v in sid])
+        no = ctypes.c_int64(0)
+        ez = None if eps_z is None else self._dev(eps_z, t.float32)
+        es = None if eps_src is None else self._dev(eps_src, t.float32)
+        self._check(self.lib.rvcx_pipeline_batch(self.ctx, a.data_ptr(), n, n, B, ctypes.byref(opts), sarr, _ptr(ez),
+                                                 _ptr(es), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF),
+                                                 out.data_ptr(), ldo, ctypes.byref(no), self.stream()),
+                    "pipeline_batch")
+        return out.reshape(-1)[: B * ldo].reshape(B, ldo)[:, : no.value]
+
     def f0_autotune(self, f0, strength: float = 1.0, skip_unvoiced: bool = False):
         """Autotune.autotune_f0 on device; returns a new fp64 tensor."""
         t = self.torch

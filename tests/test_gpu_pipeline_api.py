@@ -154,3 +154,33 @@ def test_unsupported_options_raise(api):
     with pytest.raises(NotImplementedError):
         pipe.pipeline(hub, net_g, 0, np.zeros(32000), 0, "rmvpe", None, 0.0, False, 1.0, "v2", 0.33, False, 1.0,
                       False, 155.0)
+
+
+def test_pipeline_batch_matches_single(engine):
+    """rvcx_pipeline_batch (C4: B equal-length utterances in one batched pass) == rvcx_pipeline_ex per
+    utterance with the same noise (up to split-K summation order), per-utterance sid and pitch shift."""
+    from oracle.metrics import spectrogram_correlation
+    from rvcx import synthetic
+
+    from scipy import signal
+
+    b_, a_ = signal.butter(N=5, Wn=48, btype="high", fs=16000)
+    engine.set_highpass(b_, a_, signal.lfilter_zi(b_, a_))
+    B, n = 3, 40000
+    audio = np.stack([synthetic.speech_like(n, seed=90 + b) for b in range(B)])
+    opts = engine.pipeline_opts(pitch=2.0, protect=0.33)
+    upp = engine.upp
+    sids = [0, 3, 7]
+    n_out = engine.pipeline_batch(audio, opts, sids=sids).shape[1]
+    T = (n_out + 2 * 48000) // upp  # p_len = min(len // 160, 2L): the synthesizer's frame count
+    assert T <= (n + 2 * 16000) // 160 and T * upp == n_out + 2 * 48000
+    rng = np.random.default_rng(3)
+    ez = rng.standard_normal((B, 192, T)).astype(np.float32)
+    es = rng.standard_normal((B, T * upp)).astype(np.float32)
+    yb = engine.pipeline_batch(audio, opts, sids=sids, eps_z=ez, eps_src=es).cpu().numpy()
+    for b in range(B):
+        o1 = engine.pipeline_opts(pitch=2.0, protect=0.33, sid=sids[b])
+        y1 = engine.pipeline_ex(audio[b], o1, eps_z=ez[b], eps_src=es[b]).cpu().numpy()
+        assert y1.shape == yb[b].shape
+        assert spectrogram_correlation(yb[b], y1) > 0.999
+        assert float(np.abs(yb[b] - y1).max()) < 5e-3 * max(float(np.abs(y1).max()), 1e-6)
