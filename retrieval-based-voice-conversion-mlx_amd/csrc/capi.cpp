@@ -36,10 +36,48 @@ void set_device(rvcx_ctx* c) { RVCX_HIP(hipSetDevice(c->device)); }
 }  // namespace
 
 namespace rvcx {
+hipStream_t Ctx::aux_stream() {
+  if (!aux) {
+    RVCX_HIP(hipSetDevice(device));
+    RVCX_HIP(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
+    RVCX_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+    RVCX_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+  }
+  return aux;
+}
+
+Ctx::~Ctx() {
+  if (aux) {
+    (void)hipStreamSynchronize(aux);
+    (void)hipEventDestroy(ev_fork);
+    (void)hipEventDestroy(ev_join);
+    (void)hipStreamDestroy(aux);
+  }
+}
+
+hipStream_t fork_aux(Ctx& c, hipStream_t s) {
+  static const bool no_overlap = [] {
+    const char* e = std::getenv("RVCX_NO_OVERLAP");
+    return e && std::atoi(e) != 0;
+  }();
+  if (c.prof || no_overlap) return s;
+  hipStream_t ax = c.aux_stream();
+  RVCX_HIP(hipEventRecord(c.ev_fork, s));
+  RVCX_HIP(hipStreamWaitEvent(ax, c.ev_fork, 0));
+  return ax;
+}
+
+void join_aux(Ctx& c, hipStream_t s, hipStream_t ax) {
+  if (ax == s) return;
+  RVCX_HIP(hipEventRecord(c.ev_join, ax));
+  RVCX_HIP(hipStreamWaitEvent(s, c.ev_join, 0));
+}
+
 void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double flops) {
   ConvArgs a = a_in;
   const long long need = conv_plan_splitk(a, two_d);
-  if (need > 0) a.ws = c.buf<float>("conv.splitk", (size_t)need, s);
+  // split-K slabs are per stream: the aux stream's convs run concurrently with the caller's
+  if (need > 0) a.ws = c.buf<float>(c.aux && s == c.aux ? "conv.splitk.aux" : "conv.splitk", (size_t)need, s);
   if (flops < 0) {
     const double M = two_d ? (double)a.T_out * a.W_out : (double)a.T_out;
     flops = 2.0 * M * a.N * (double)a.C_in * a.taps * a.batch * a.batch_inner;

@@ -99,6 +99,11 @@ struct Ctx {
   std::vector<ProfRec> prof_recs;
   std::vector<hipEvent_t> prof_pool;
   std::unique_ptr<IvfIndex> ivf;  // speaker-embedding index (optional)
+  // second stream for work independent of the caller's stream (HuBERT beside RMVPE), created lazily
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipStream_t aux_stream();
+  ~Ctx();
 
   float* W(const std::string& name) const;
   float* alloc_weight(const std::string& name, const std::vector<float>& data);
@@ -145,9 +150,11 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
 
 void set_highpass(Ctx& c, const double* b, const double* a, const double* zi, int order);
 int hubert_version_for(const Ctx& c);
+// feats_pre (optional): HuBERT rows of this chunk computed ahead (e.g. on the aux stream), L_pre rows
 int64_t vc_forward(Ctx& c, const float* audio, int64_t n, const int32_t* pitch, const float* pitchf,
                    int64_t pitch_len, int sid, float protect, double index_rate, const float* eps_z,
-                   const float* eps_src, uint64_t seed, float* out, int64_t cap, hipStream_t s);
+                   const float* eps_src, uint64_t seed, float* out, int64_t cap, hipStream_t s,
+                   const float* feats_pre = nullptr, int64_t L_pre = 0);
 // streaming (runtime_stream.cpp)
 struct RtState;
 RtState* rt_create(Ctx& c, const rvcx_rt_desc& d);
@@ -172,6 +179,11 @@ rvcx_pipeline_opts default_pipeline_opts();
 int proposed_key(const std::vector<double>& f0, double threshold);
 int64_t hubert_frames(int64_t n);  // HuBERT output rows for n samples (0 when too short)
 void set_i32(int32_t* p, int32_t v, hipStream_t s);
+// Overlap of independent stages: fork_aux returns the aux stream, ordered after everything queued on s so
+// far (or s itself when overlap is off: kernel timing on, or RVCX_NO_OVERLAP=1); join_aux makes s wait for
+// everything queued on the aux stream so far.
+hipStream_t fork_aux(Ctx& c, hipStream_t s);
+void join_aux(Ctx& c, hipStream_t s, hipStream_t ax);
 // launch one implicit-GEMM conv (1-D or 2-D) with optional event timing; flops = algorithmic FLOPs
 void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double flops = -1.0);
 

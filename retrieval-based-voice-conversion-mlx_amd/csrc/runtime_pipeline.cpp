@@ -8,6 +8,7 @@
 // sets the key offset (pipeline.py:250-277) -- both are a few KB and need one stream sync each.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "runtime.h"
@@ -30,12 +31,18 @@ int hubert_version_for(const Ctx& c) { return c.scfg.emb_dim == 256 ? 1 : 2; }
 
 int64_t vc_forward(Ctx& c, const float* audio, int64_t n, const int32_t* pitch, const float* pitchf,
                    int64_t pitch_len, int sid, float protect, double index_rate, const float* eps_z,
-                   const float* eps_src, uint64_t seed, float* out, int64_t cap, hipStream_t s) {
+                   const float* eps_src, uint64_t seed, float* out, int64_t cap, hipStream_t s,
+                   const float* feats_pre, int64_t L_pre) {
   if (sid < 0 || sid >= c.scfg.n_spk) throw Error(RVCX_E_INVALID, "sid out of range");
   const int E = c.scfg.emb_dim;
-  const int64_t cap_rows = n / 320 + 8;  // HuBERT frames for n samples (upper bound n/320)
-  float* feats = c.buf<float>("vc.feats", (size_t)cap_rows * E, s);
-  const int64_t L = hubert_forward(c, audio, n, hubert_version_for(c), feats, cap_rows, s);
+  const float* feats = feats_pre;
+  int64_t L = L_pre;
+  if (!feats) {
+    const int64_t cap_rows = n / 320 + 8;  // HuBERT frames for n samples (upper bound n/320)
+    float* fb = c.buf<float>("vc.feats", (size_t)cap_rows * E, s);
+    L = hubert_forward(c, audio, n, hubert_version_for(c), fb, cap_rows, s);
+    feats = fb;
+  }
   const int T = (int)std::min<int64_t>(n / 160, 2 * L);
   if (T <= 0) throw Error(RVCX_E_SHAPE, "voice_conversion: input shorter than one frame");
   if (T > pitch_len) throw Error(RVCX_E_SHAPE, "voice_conversion: pitch track shorter than the features");
@@ -124,9 +131,40 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
       RVCX_HIP(hipStreamSynchronize(s));
     }
   }
-  // 3. f0 over the whole padded input (pipeline.py:462-472) + get_f0 adjustments (:248-291)
+  // 3. chunk plan (pipeline.py:486-512): [a0, a1) samples and [f_lo, f_hi) pitch frames per chunk
+  struct Chunk {
+    int64_t a0, a1, f_lo, f_hi;
+  };
+  std::vector<Chunk> chunks;
+  {
+    const int64_t t_pad2 = 2 * o.t_pad;
+    int64_t st = 0, t = 0;
+    bool have_t = false;
+    for (int64_t t_raw : opt_ts) {
+      t = t_raw / W * W;
+      chunks.push_back({st, std::min(m, t + t_pad2 + W), st / W, (t + t_pad2) / W});
+      st = t;
+      have_t = true;
+    }
+    chunks.push_back(have_t ? Chunk{t, m, t / W, m / W} : Chunk{0, m, 0, m / W});
+  }
+  // 4. HuBERT of every chunk on the aux stream, beside RMVPE on the caller's stream (they only share
+  //    the padded input); the chunk loop waits for it before the upsample. Kernel timing (rvcx_profile)
+  //    and RVCX_NO_OVERLAP=1 keep it on the caller's stream so per-kernel durations are not shared.
+  const int E = c.scfg.emb_dim;
+  std::vector<float*> cfeats(chunks.size());
+  std::vector<int64_t> cL(chunks.size());
+  hipStream_t ax = fork_aux(c, s);
+  {
+    for (size_t i = 0; i < chunks.size(); ++i) {
+      const int64_t len = chunks[i].a1 - chunks[i].a0;
+      const int64_t cap_rows = len / 320 + 8;
+      cfeats[i] = c.buf<float>("pl.hb" + std::to_string(i), (size_t)cap_rows * E, ax);
+      cL[i] = hubert_forward(c, pad32 + chunks[i].a0, len, hubert_version_for(c), cfeats[i], cap_rows, ax);
+    }
+  }
+  // 5. f0 over the whole padded input (pipeline.py:462-472) + get_f0 adjustments (:248-291)
   const int64_t F = 1 + m / W;
-  const int64_t p_len = m / W;
   double* f0 = c.buf<double>("pl.f0", (size_t)F, s);
   rmvpe_forward(c, pad32, m, o.rmvpe_threshold > 0 ? o.rmvpe_threshold : 0.03f, f0, F, nullptr, s);
   double shift_semitones = o.pitch;
@@ -142,19 +180,21 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
   int32_t* pitch = c.buf<int32_t>("pl.pitch", (size_t)F, s);
   float* pitchf = c.buf<float>("pl.pitchf", (size_t)F, s);
   check(f0_post(f0, (int)F, std::pow(2.0, shift_semitones / 12.0), pitch, pitchf, f0_out, s), "f0_post");
-  // 4. voice conversion per chunk (pipeline.py:486-512), outputs trimmed t_pad_tgt per side
+  join_aux(c, s, ax);
+  // 6. voice conversion per chunk (pipeline.py:486-512), outputs trimmed t_pad_tgt per side
   const int upp = c.scfg.upp();
   const int I = c.scfg.I;
   int64_t written = 0, ez_off = 0, es_off = 0;
-  int64_t st = 0;
-  auto chunk = [&](int64_t a0, int64_t a1, int64_t f_lo, int64_t f_hi, uint64_t cseed) {
-    const int64_t len = a1 - a0;
+  uint64_t cseed = seed;
+  for (size_t i = 0; i < chunks.size(); ++i) {
+    const Chunk& ch = chunks[i];
+    const int64_t len = ch.a1 - ch.a0;
     const int64_t cap_vc = (len / W) * upp;
     float* vc = c.buf<float>("pl.vc", (size_t)std::max<int64_t>(cap_vc, 1), s);
     // pitch[:, f_lo:f_hi], then [:p_len] inside voice_conversion with p_len = min(len/160, 2L)
-    const int64_t nvc = vc_forward(c, pad32 + a0, len, pitch + f_lo, pitchf + f_lo, f_hi - f_lo, o.sid, o.protect,
-                                   o.index_rate, eps_z ? eps_z + ez_off : nullptr, eps_src ? eps_src + es_off : nullptr, cseed, vc,
-                                   cap_vc, s);
+    const int64_t nvc = vc_forward(c, pad32 + ch.a0, len, pitch + ch.f_lo, pitchf + ch.f_lo, ch.f_hi - ch.f_lo, o.sid,
+                                   o.protect, o.index_rate, eps_z ? eps_z + ez_off : nullptr,
+                                   eps_src ? eps_src + es_off : nullptr, cseed, vc, cap_vc, s, cfeats[i], cL[i]);
     const int64_t T = nvc / upp;
     ez_off += (int64_t)I * T;
     es_off += nvc;
@@ -165,23 +205,9 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
     RVCX_HIP(hipMemcpyAsync(out + written, vc + o.t_pad_tgt, (size_t)keep * sizeof(float), hipMemcpyDeviceToDevice,
                             s));
     written += keep;
-  };
-  uint64_t cseed = seed;
-  const int64_t t_pad2 = 2 * o.t_pad;
-  bool have_t = false;
-  int64_t t = 0;
-  for (int64_t t_raw : opt_ts) {
-    t = t_raw / W * W;
-    chunk(st, std::min(m, t + t_pad2 + W), st / W, (t + t_pad2) / W, cseed);
     cseed += 0x9E3779B97F4A7C15ull;
-    st = t;
-    have_t = true;
   }
-  if (have_t)
-    chunk(t, m, t / W, p_len, cseed);
-  else
-    chunk(0, m, 0, p_len, cseed);
-  // 5. volume envelope (pipeline.py:545-549) and peak normalisation (:550-552)
+  // 7. volume envelope (pipeline.py:545-549) and peak normalisation (:550-552)
   if (o.volume_envelope != 1.0) {
     const int n1 = rms_frame_count(n, 16000), n2 = rms_frame_count(written, c.scfg.sr);
     float* rws = c.buf<float>("pl.rms", (size_t)(n1 + n2), s);
@@ -224,6 +250,10 @@ int64_t pipeline_forward_batch(Ctx& c, const double* audio, int64_t n, int64_t l
   // 2. f0 (batched RMVPE) + get_f0 adjustments per utterance (pipeline.py:462-472, :248-291)
   const int64_t F = 1 + m / W, T = m / W;
   double* f0 = c.buf<double>("pb.f0", (size_t)B * F, s);
+  const int64_t L = hubert_frames(m);
+  float* feats = c.buf<float>("pb.feats", (size_t)B * L * E, s);
+  hipStream_t ax = fork_aux(c, s);  // batched HuBERT beside batched RMVPE
+  hubert_forward_b(c, pad32, m, ldm, B, hubert_version_for(c), feats, L, ax);
   rmvpe_forward_b(c, pad32, m, ldm, B, o.rmvpe_threshold > 0 ? o.rmvpe_threshold : 0.03f, f0, F, nullptr, s);
   std::vector<double> shift(B, o.pitch);
   if (o.f0_autotune) {
@@ -245,11 +275,9 @@ int64_t pipeline_forward_batch(Ctx& c, const double* audio, int64_t n, int64_t l
                   pitchf + (size_t)b * F, nullptr, s),
           "f0_post");
   // 3. batched HuBERT, retrieval, x2 upsample + protect (pipeline.py:327-362)
-  const int64_t L = hubert_frames(m);
+  join_aux(c, s, ax);
   const int64_t Tv = std::min<int64_t>(T, 2 * L);
   if (Tv <= 0) throw Error(RVCX_E_SHAPE, "pipeline_batch: input shorter than one frame");
-  float* feats = c.buf<float>("pb.feats", (size_t)B * L * E, s);
-  hubert_forward_b(c, pad32, m, ldm, B, hubert_version_for(c), feats, L, s);
   const float* fx = feats;
   if (o.index_rate > 0) {
     if (c.ivf->view.d != E) throw Error(RVCX_E_SHAPE, "pipeline: feature index dimension mismatch");

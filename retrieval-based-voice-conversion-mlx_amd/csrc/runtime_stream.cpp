@@ -220,6 +220,10 @@ void rt_process(Ctx& c, RtState& s, const float* in48, const int32_t* sids, cons
   const int F = 1 + nf / 160;
   if (F > s.pbuf_n) throw Error(RVCX_E_SHAPE, "stream: f0 track longer than the pitch buffer");
   double* f0 = c.buf<double>("rt.f0", (size_t)B * F, st);
+  const int64_t L = hubert_frames(s.conv16);
+  float* feats = c.buf<float>("rt.feats", (size_t)B * L * E, st);
+  hipStream_t ax = fork_aux(c, st);  // batched HuBERT beside batched RMVPE (pipeline.py:233-254)
+  hubert_forward_b(c, conv, s.conv16, s.conv16, B, hubert_version_for(c), feats, L, ax);
   rmvpe_forward_b(c, conv + s.silence_front, nf, s.conv16, B, 0.03f, f0, F, nullptr, st);
   std::vector<double> fac(B, std::pow(2.0, o.f0_up_key / 12.0));
   if (o.f0_autotune) {
@@ -240,9 +244,7 @@ void rt_process(Ctx& c, RtState& s, const float* in48, const int32_t* sids, cons
                  static_cast<float*>(s.fbuf[nxt].p), s.pbuf_n, B, st),
         "rt_pitch");
   // 3. HuBERT over the B convert buffers (pipeline.py:248-254), rows [B][L][E]
-  const int64_t L = hubert_frames(s.conv16);
-  float* feats = c.buf<float>("rt.feats", (size_t)B * L * E, st);
-  hubert_forward_b(c, conv, s.conv16, s.conv16, B, hubert_version_for(c), feats, L, st);
+  join_aux(c, st, ax);
   // 4. index retrieval of rows skip_head // 2 .. (pipeline.py:264-268, :336-352)
   const float* fx = feats;
   if (o.index_rate > 0) {
