@@ -202,8 +202,6 @@ def main():
 
         dist.init_process_group("nccl", device_id=dev)
 
-    from scipy import signal
-
     from rvcx import synthetic
     from rvcx.config import SYNTH_48K_V2
     from rvcx.engine import Engine
@@ -213,8 +211,7 @@ def main():
     eng.load_synth(normalize_state(synthetic.synth_state(2)), SYNTH_48K_V2)
     eng.load_hubert(normalize_state(synthetic.hubert_state(4)))
     eng.load_rmvpe(normalize_state(synthetic.rmvpe_state(5)))
-    b, a = signal.butter(N=5, Wn=48, btype="high", fs=SR_IN)
-    eng.set_highpass(b, a, signal.lfilter_zi(b, a))
+    eng.set_pipeline_highpass(SR_IN)
     if args.config in ("c3", "c4", "c5"):
         rec = {"c3": bench_c3, "c4": bench_c4, "c5": bench_c5}[args.config](args, eng, dev, dist, rank, world)
         if rank == 0:

@@ -130,6 +130,16 @@ int rvcx_voice_conversion(rvcx_ctx* ctx, const float* d_audio, int64_t n, const 
  * rvcx_pipeline's zero-phase filtfilt (padtype 'odd', padlen 3*(order+1)). */
 int rvcx_set_highpass(rvcx_ctx* ctx, const double* b, const double* a, const double* zi, int order);
 
+/* The same high-pass as second-order sections sos[nsec][6] = (b0 b1 b2 a0 a1 a2) per section (scipy
+ * butter(5, 48, 'high', fs=16000, output='sos'): exact zpk sections). When set, filtfilt runs as a
+ * chunk-parallel scan over the sections (stable: each section's 2x2 state matrix is well conditioned, unlike
+ * the order-5 companion form). Call after rvcx_set_highpass (which sets the padding length). */
+int rvcx_set_highpass_sos(rvcx_ctx* ctx, const double* sos, int nsec);
+/* signal.filtfilt(bh, ah, audio) then np.pad(..., (t_pad, t_pad), 'reflect') (pipeline.py:439, :459):
+ * d_audio [n] fp64 -> d_pad64 (optional) / d_pad32 [n + 2 t_pad]. */
+int rvcx_highpass_pad(rvcx_ctx* ctx, const double* d_audio, int64_t n, int64_t t_pad, double* d_pad64, float* d_pad32,
+                      void* stream);
+
 /* Options of Pipeline.pipeline (rvc/infer/pipeline.py:390-408; rvc_mlx/infer/pipeline_mlx.py:263) that
  * reach the device path. Fill with rvcx_pipeline_default_opts, then override. Times are in samples. */
 typedef struct {

@@ -829,6 +829,30 @@ hipError_t filtfilt_pad(const double* x, long long n, const double* b, const dou
   return hipGetLastError();
 }
 
+hipError_t filtfilt_sos_pad(const SosPlan& p, int order, const double* x, long long n, long long t_pad, double* ws,
+                            double* pad64, float* pad32, hipStream_t s) {
+  const int padlen = 3 * (order + 1);
+  if (n <= padlen || t_pad >= n || p.nsec < 1) return hipErrorInvalidValue;
+  const long long ne = n + 2 * padlen;
+  double* ext = ws;
+  double* yf = ext + ne;
+  double* yb = yf + ne;
+  double* sw = yb + ne;
+  hipLaunchKernelGGL(k_odd_ext, dim3(nblocks(ne)), dim3(TB), 0, s, x, n, padlen, ext);
+  hipError_t e = sos_pass(p, ext, ne, 0, yf, sw, s);  // forward, x0 = ext[0]
+  if (e != hipSuccess) return e;
+  e = sos_pass(p, yf, ne, 1, yb, sw, s);  // backward over reversed yf, x0 = yf[ne - 1]
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_filt_pad, dim3(nblocks(n + 2 * t_pad)), dim3(TB), 0, s, yb, ne, padlen, n, t_pad, pad64,
+                     pad32);
+  return hipGetLastError();
+}
+
+size_t filtfilt_sos_ws_doubles(long long n, int order, int L) {
+  const long long ne = n + 2 * 3 * (order + 1);
+  return (size_t)(3 * ne) + sos_ws_doubles(ne, L);
+}
+
 size_t filtfilt_ws_doubles(long long n, int order) {
   const long long ne = n + 2 * 3 * (order + 1);
   return (size_t)(3 * ne);

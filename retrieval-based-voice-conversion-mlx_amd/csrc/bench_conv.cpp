@@ -75,7 +75,7 @@ int main(int argc, char** argv) {
                        pad, 1);
     std::vector<float> ref((size_t)T * N), out((size_t)T * N);
     CK_(hipMemcpy(ref.data(), yr, ref.size() * 4, hipMemcpyDeviceToHost));
-    for (int cfg = 0; cfg < 7; ++cfg)
+    for (int cfg = 0; cfg < 10; ++cfg)
       for (int pipe : {-1}) {
         ConvArgs a;
         a.x = x; a.ldx = C; a.T_in = T; a.C_in = C;
@@ -165,11 +165,11 @@ int main(int argc, char** argv) {
     CK_(hipMemcpy(w, hw.data(), nw * 4, hipMemcpyHostToDevice));
     CK_(hipMemset(b, 0, cs.N * 4));
     const double flops = 2.0 * cs.T * cs.N * (double)cs.Cin * cs.taps;
-    double best[2][8] = {{0}};
-    int ksp[8] = {0};
+    double best[2][11] = {{0}};
+    int ksp[11] = {0};
     for (int round = 0; round < (only_case >= 0 ? 1 : 3); ++round)
-    for (int cfg : {-1, 0, 1, 2, 3, 4, 5, 6})
-      for (int asb : {1, 4}) {
+    for (int cfg : {-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9})
+      for (int asb : {1}) {
         const int pipe = -1;
         if (only_case >= 0 && (cfg != only_cfg % 10 || asb != (only_cfg >= 10 ? 4 : 1))) continue;
         ConvArgs a;
@@ -202,9 +202,9 @@ int main(int argc, char** argv) {
         ksp[cfg + 1] = a.ksplit;
         if (wsp) (void)hipFree(wsp);
       }
-    for (int v = 0; v < 2; ++v) {
+    for (int v = 0; v < 1; ++v) {
       printf("%-24s asb%d", cs.name, v ? 4 : 1);
-      for (int c = 0; c < 8; ++c) printf(" %2d:%6.1f%s", c - 1, best[v][c], ksp[c] > 1 ? "*" : " ");
+      for (int c = 0; c < 11; ++c) printf(" %2d:%6.1f%s", c - 1, best[v][c], ksp[c] > 1 ? "*" : " ");
       printf("\n");
     }
     (void)hipFree(x); (void)hipFree(w); (void)hipFree(b); (void)hipFree(y);

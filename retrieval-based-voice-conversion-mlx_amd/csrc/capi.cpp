@@ -330,6 +330,24 @@ int rvcx_set_highpass(rvcx_ctx* ctx, const double* b, const double* a, const dou
   });
 }
 
+int rvcx_set_highpass_sos(rvcx_ctx* ctx, const double* sos, int nsec) {
+  return guard(ctx, [&] {
+    if (!sos) throw Error(RVCX_E_INVALID, "null sections");
+    if (ctx->hp_order == 0) throw Error(RVCX_E_STATE, "set the (b, a) form first (rvcx_set_highpass)");
+    set_device(ctx);
+    set_highpass_sos(*ctx, sos, nsec);
+  });
+}
+
+int rvcx_highpass_pad(rvcx_ctx* ctx, const double* d_audio, int64_t n, int64_t t_pad, double* d_pad64, float* d_pad32,
+                      void* stream) {
+  return guard(ctx, [&] {
+    if (!d_audio || !d_pad32 || n <= 0 || t_pad < 0) throw Error(RVCX_E_INVALID, "rvcx_highpass_pad: bad arguments");
+    set_device(ctx);
+    highpass_pad(*ctx, d_audio, n, t_pad, d_pad64, d_pad32, static_cast<hipStream_t>(stream));
+  });
+}
+
 int rvcx_pipeline(rvcx_ctx* ctx, const double* d_audio, int64_t n, int sid, double semitones, float protect,
                   int64_t t_pad, int64_t t_pad_tgt, const float* d_eps_z, const float* d_eps_src, uint64_t seed,
                   float* d_out, int64_t cap, int64_t* n_out, double* d_f0, void* stream) {

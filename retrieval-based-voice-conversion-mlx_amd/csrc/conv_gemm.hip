@@ -25,7 +25,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int CK = 32;   // contraction channels per LDS chunk
-constexpr int CKP = 36;  // padded LDS row: rows i..i+15 land on distinct 16-B bank slots
 constexpr int NTHREADS = 256;
 
 __device__ __noinline__ float act_fn_slow(float v, int act, float slope) {
@@ -69,10 +68,12 @@ __device__ __forceinline__ void epilogue_store(const ConvArgs& a, float v, float
   *dst = v;
 }
 
-template <int BM, int BN, int WM, int WN, bool TWO_D, bool PIPE, int ASB>
+template <int BM, int BN, int WM, int WN, bool TWO_D, bool PIPE, int ASB, int CKT = CK>
 __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a, const int nrows_a, const int rw,
                                                              const int rh, const int tiles_w, const int vec_a,
                                                              const int vec_b, const int ksplit) {
+  constexpr int CKP = CKT + 4;  // padded LDS row: rows i..i+15 land on distinct 16-B bank slots
+  constexpr int C4 = CKT / 4;   // float4 per LDS row
   constexpr int TM = BM / (WM * 32);
   constexpr int TN = BN / (WN * 32);
   static_assert(WM * WN == 4, "4 waves per block");
@@ -125,17 +126,17 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
       for (int r = 0; r < 16; ++r) acc[tm][tn][r] = 0.f;
 
   // B tile loader: global -> registers (BN x 32 floats of (tap, chunk)); NK or KN weight layout
-  constexpr int BV = (BN * (CK / 4) + NTHREADS - 1) / NTHREADS;  // float4 per thread
+  constexpr int BV = (BN * C4 + NTHREADS - 1) / NTHREADS;  // float4 per thread
   auto load_b = [&](int tap, int c0, f32x4 (&reg)[BV]) {
     const float* Wt = Wb + (long long)tap * a.w_ts;
 #pragma unroll
     for (int v = 0; v < BV; ++v) {
       const int idx = tid + v * NTHREADS;
       f32x4 val = {0.f, 0.f, 0.f, 0.f};
-      if (idx < BN * (CK / 4)) {
+      if (idx < BN * C4) {
         if (!a.b_kn) {
-          const int n = idx >> 3;
-          const int c = c0 + ((idx & 7) << 2);
+          const int n = idx / C4;
+          const int c = c0 + ((idx % C4) << 2);
           const int gn = n0 + n;
           if (gn < a.N && c < a.C_in) {
             const float* src = Wt + (long long)gn * a.ldw + c;
@@ -168,9 +169,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
 #pragma unroll
     for (int v = 0; v < BV; ++v) {
       const int idx = tid + v * NTHREADS;
-      if (idx < BN * (CK / 4)) {
+      if (idx < BN * C4) {
         if (!a.b_kn) {
-          *reinterpret_cast<f32x4*>(&Bs[(idx >> 3) * CKP + ((idx & 7) << 2)]) = reg[v];
+          *reinterpret_cast<f32x4*>(&Bs[(idx / C4) * CKP + ((idx % C4) << 2)]) = reg[v];
         } else {
           const int cc = idx / (BN / 4);
           const int n4 = (idx - cc * (BN / 4)) << 2;
@@ -182,9 +183,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
   };
   // A tile: nrows_a x 32 channels of chunk c0 -> LDS, pre-activation applied, zero outside the input
   auto stage_a_serial = [&](int c0) {
-    for (int idx = tid; idx < nrows_a * (CK / 4); idx += NTHREADS) {
-      const int r = idx >> 3;
-      const int c4 = (idx & 7) << 2;
+    for (int idx = tid; idx < nrows_a * C4; idx += NTHREADS) {
+      const int r = idx / C4;
+      const int c4 = (idx % C4) << 2;
       const int c = c0 + c4;
       long long grow;
       bool valid;
@@ -225,7 +226,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
     if constexpr (ASB <= 1) {
       stage_a_serial(c0);
     } else {
-      const int total = nrows_a * (CK / 4);
+      const int total = nrows_a * C4;
       for (int base = 0; base < total; base += ASB * NTHREADS) {
         f32x4 rv[ASB];
         float mk[ASB];
@@ -235,8 +236,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
           rv[q] = f32x4{0.f, 0.f, 0.f, 0.f};
           mk[q] = 0.f;
           if (idx < total) {
-            const int r = idx >> 3;
-            const int c = c0 + ((idx & 7) << 2);
+            const int r = idx / C4;
+            const int c = c0 + ((idx % C4) << 2);
             long long grow;
             bool valid;
             if (!TWO_D) {
@@ -278,7 +279,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
             } else {
               v = f32x4{0.f, 0.f, 0.f, 0.f};
             }
-            *reinterpret_cast<f32x4*>(&As[(idx >> 3) * CKP + ((idx & 7) << 2)]) = v;
+            *reinterpret_cast<f32x4*>(&As[(idx / C4) * CKP + ((idx % C4) << 2)]) = v;
           }
         }
       }
@@ -287,7 +288,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
   auto compute = [&](const float* Bs, int tap) {
     const int toff = TWO_D ? (tap / a.KW) * aw + (tap % a.KW) : tap * a.dil;
 #pragma unroll
-    for (int kk = 0; kk < CK; kk += 8) {
+    for (int kk = 0; kk < CKT; kk += 8) {
       float av[TM][4], bv[TN][4];
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm) {
@@ -309,7 +310,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
     }
   };
 
-  const int nchunks = (a.C_in + CK - 1) / CK;
+  const int nchunks = (a.C_in + CKT - 1) / CKT;
   if (!PIPE) {
     f32x4 breg[BV];
     const int total = nchunks * a.taps;
@@ -319,10 +320,10 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
     while (it < it1) {
       const int ch = it / a.taps;
       __syncthreads();
-      stage_a(ch * CK);
+      stage_a(ch * CKT);
       for (int tap = it - ch * a.taps; tap < a.taps && it < it1; ++tap, ++it) {
         if (it > it0 && tap != it0 - ch * a.taps) __syncthreads();
-        load_b(tap, ch * CK, breg);
+        load_b(tap, ch * CKT, breg);
         store_b(Bs0, breg);
         __syncthreads();
         compute(Bs0, tap);
@@ -347,12 +348,12 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
         ++nch;
       }
       const bool more = it + 1 < total;
-      if (more) load_b(ntap, nch * CK, breg);
+      if (more) load_b(ntap, nch * CKT, breg);
       compute(Bcur, tap);
       if (more) {
         if (ntap == 0) {
           __syncthreads();  // every wave is done with this chunk's A tile
-          stage_a(nch * CK);
+          stage_a(nch * CKT);
         }
         store_b(Bnxt, breg);
       }
@@ -459,8 +460,9 @@ struct TileCfg {
   int BM, BN;
 };
 
-template <int BM, int BN, int WM, int WN, bool TWO_D, bool PIPE = false, int ASB = 1>
+template <int BM, int BN, int WM, int WN, bool TWO_D, bool PIPE = false, int ASB = 1, int CKT = CK>
 hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
+  constexpr int CKP = CKT + 4;
   int nrows_a, rw = 0, rh = 0, tiles_w = 1, mtiles;
   if (!TWO_D) {
     nrows_a = (BM - 1) * a.stride + (a.taps - 1) * a.dil + 1;
@@ -483,7 +485,7 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
   int ksplit = 1;
   if (!PIPE && a.ws && a.ksplit > 1) ksplit = a.ksplit;
   dim3 grid(mtiles, (a.N + BN - 1) / BN, a.batch * a.batch_inner * ksplit);
-  auto kern = conv_gemm_kernel<BM, BN, WM, WN, TWO_D, PIPE, ASB>;
+  auto kern = conv_gemm_kernel<BM, BN, WM, WN, TWO_D, PIPE, ASB, CKT>;
   if (smem > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
@@ -509,6 +511,9 @@ hipError_t launch_forced_asb(const ConvArgs& a, hipStream_t s) {
     case 4: return launch_cfg<128, 128, 2, 2, TWO_D, PIPE, ASB>(a, s);
     case 5: return launch_cfg<64, 128, 2, 2, TWO_D, PIPE, ASB>(a, s);
     case 6: return launch_cfg<256, 64, 4, 1, TWO_D, PIPE, ASB>(a, s);
+    case 7: return launch_cfg<64, 64, 2, 2, TWO_D, PIPE, ASB, 64>(a, s);
+    case 8: return launch_cfg<128, 32, 4, 1, TWO_D, PIPE, ASB, 64>(a, s);
+    case 9: return launch_cfg<128, 128, 2, 2, TWO_D, PIPE, ASB, 64>(a, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -549,7 +554,8 @@ int pick_cfg(const ConvArgs& a) {
 }
 
 inline void cfg_tile(int cfg, int& BM, int& BN) {
-  static const int t[7][2] = {{256, 32}, {128, 32}, {128, 64}, {64, 64}, {128, 128}, {64, 128}, {256, 64}};
+  static const int t[10][2] = {{256, 32}, {128, 32}, {128, 64}, {64, 64}, {128, 128}, {64, 128}, {256, 64},
+                               {64, 64}, {128, 32}, {128, 128}};
   BM = t[cfg][0];
   BN = t[cfg][1];
 }

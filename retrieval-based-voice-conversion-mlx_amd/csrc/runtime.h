@@ -86,6 +86,9 @@ struct Ctx {
   // pipeline high-pass (rvc/infer/pipeline.py:22-27), normalised so a[0] = 1
   int hp_order = 0;
   std::vector<double> hp_b, hp_a, hp_zi;
+  // the same filter as second-order sections (rvcx_set_highpass_sos): chunk-parallel scan (iir_scan.hip)
+  SosPlan hp_sos;
+  DevBuf hp_sos_buf;
   // workspace pool
   std::map<std::string, std::unique_ptr<DevBuf>> ws;
   uint64_t call_counter = 0;
@@ -149,6 +152,9 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
                  const float* eps_src, uint64_t seed, float* out, hipStream_t s);
 
 void set_highpass(Ctx& c, const double* b, const double* a, const double* zi, int order);
+void set_highpass_sos(Ctx& c, const double* sos, int nsec);
+// filtfilt + reflect pad of one utterance with whichever high-pass form is configured
+void highpass_pad(Ctx& c, const double* audio, int64_t n, int64_t t_pad, double* pad64, float* pad32, hipStream_t s);
 int hubert_version_for(const Ctx& c);
 // feats_pre (optional): HuBERT rows of this chunk computed ahead (e.g. on the aux stream), L_pre rows
 int64_t vc_forward(Ctx& c, const float* audio, int64_t n, const int32_t* pitch, const float* pitchf,

@@ -19,12 +19,81 @@ void set_highpass(Ctx& c, const double* b, const double* a, const double* zi, in
   if (order < 1 || order > IIR_MAXO) throw Error(RVCX_E_INVALID, "highpass order out of range");
   if (!(a[0] != 0.0)) throw Error(RVCX_E_INVALID, "highpass a[0] == 0");
   c.hp_order = order;
+  c.hp_sos = SosPlan();  // a new (b, a) filter drops any section form set for the previous one
   c.hp_b.assign(b, b + order + 1);
   c.hp_a.assign(a, a + order + 1);
   c.hp_zi.assign(zi, zi + order);
   const double a0 = a[0];
   for (auto& v : c.hp_b) v /= a0;
   for (auto& v : c.hp_a) v /= a0;
+}
+
+// SOS plan (iir_scan.hip): per section the DF2T biquad, its steady state for a unit pass input (scipy
+// filtfilt's zi * x0: the whole cascade at rest on the constant x0, DC gains of the preceding sections
+// included), A^(L 2^s) for the carry scan and the rows C A^k of the chunk fix-up.
+void set_highpass_sos(Ctx& c, const double* sos, int nsec) {
+  if (nsec < 1 || nsec > IIR_MAXO) throw Error(RVCX_E_INVALID, "highpass: bad section count");
+  SosPlan p;
+  p.nsec = nsec;
+  p.L = 256;
+  std::vector<double> tab((size_t)nsec * p.stride(), 0.0);
+  double gain = 1.0;  // DC gain of the sections before j
+  for (int j = 0; j < nsec; ++j) {
+    const double* q = sos + 6 * j;
+    if (!(q[3] != 0.0)) throw Error(RVCX_E_INVALID, "highpass: section a0 == 0");
+    const double b0 = q[0] / q[3], b1 = q[1] / q[3], b2 = q[2] / q[3], a1 = q[4] / q[3], a2 = q[5] / q[3];
+    double* t = tab.data() + (size_t)j * p.stride();
+    t[0] = b0, t[1] = b1, t[2] = b2, t[3] = a1, t[4] = a2;
+    // steady state z = (I - A)^-1 B u with A = [[-a1, 1], [-a2, 0]], B = [b1 - a1 b0, b2 - a2 b0], u = gain
+    const double B0 = b1 - a1 * b0, B1 = b2 - a2 * b0;
+    const double det = (1.0 + a1) * 1.0 + a2;  // det(I - A) = (1 + a1) * 1 - (-1) * (a2)
+    if (!(std::fabs(det) > 1e-300)) throw Error(RVCX_E_INVALID, "highpass: section has a pole at z = 1");
+    // (I - A) = [[1 + a1, -1], [a2, 1]] -> inverse = [[1, 1], [-a2, 1 + a1]] / det
+    t[8] = (B0 + B1) / det * gain;
+    t[9] = (-a2 * B0 + (1.0 + a1) * B1) / det * gain;
+    gain *= (b0 + b1 + b2) / (1.0 + a1 + a2);
+    // A^L then squarings: pow[s] = A^(L 2^s), s = 0..10
+    double M[4] = {1, 0, 0, 1};
+    double* ca = t + 64;
+    for (int k = 0; k < p.L; ++k) {
+      ca[2 * k] = M[0];
+      ca[2 * k + 1] = M[1];
+      const double n0 = -a1 * M[0] + M[2], n1 = -a1 * M[1] + M[3], n2 = -a2 * M[0], n3 = -a2 * M[1];
+      M[0] = n0, M[1] = n1, M[2] = n2, M[3] = n3;  // M <- A M
+    }
+    for (int sidx = 0; sidx < 11; ++sidx) {
+      double* P = t + 16 + 4 * sidx;
+      P[0] = M[0], P[1] = M[1], P[2] = M[2], P[3] = M[3];
+      const double n0 = M[0] * M[0] + M[1] * M[2], n1 = M[0] * M[1] + M[1] * M[3];
+      const double n2 = M[2] * M[0] + M[3] * M[2], n3 = M[2] * M[1] + M[3] * M[3];
+      M[0] = n0, M[1] = n1, M[2] = n2, M[3] = n3;
+    }
+  }
+  RVCX_HIP(hipSetDevice(c.device));
+  c.hp_sos_buf.~DevBuf();
+  new (&c.hp_sos_buf) DevBuf();
+  const size_t bytes = tab.size() * sizeof(double);
+  if (hipMalloc(&c.hp_sos_buf.p, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    throw Error(RVCX_E_OOM, "highpass: device allocation failed");
+  }
+  c.hp_sos_buf.bytes = bytes;
+  RVCX_HIP(hipMemcpy(c.hp_sos_buf.p, tab.data(), bytes, hipMemcpyHostToDevice));
+  p.dev = static_cast<const double*>(c.hp_sos_buf.p);
+  c.hp_sos = p;
+}
+
+void highpass_pad(Ctx& c, const double* audio, int64_t n, int64_t t_pad, double* pad64, float* pad32, hipStream_t s) {
+  if (c.hp_order == 0) throw Error(RVCX_E_STATE, "pipeline: high-pass filter not configured");
+  if (c.hp_sos.nsec > 0) {
+    double* ws = c.buf<double>("pl.sosws", filtfilt_sos_ws_doubles(n, c.hp_order, c.hp_sos.L), s);
+    check(filtfilt_sos_pad(c.hp_sos, c.hp_order, audio, n, t_pad, ws, pad64, pad32, s), "filtfilt_sos");
+    return;
+  }
+  double* ws = c.buf<double>("pl.iirws", filtfilt_ws_doubles(n, c.hp_order), s);
+  check(filtfilt_pad(audio, n, c.hp_b.data(), c.hp_a.data(), c.hp_zi.data(), nullptr, c.hp_order, t_pad, ws, pad64,
+                     pad32, s),
+        "filtfilt_pad");
 }
 
 int hubert_version_for(const Ctx& c) { return c.scfg.emb_dim == 256 ? 1 : 2; }
@@ -112,10 +181,7 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
   //    search and the RMS envelope, fp32 copy feeds the models (torch.from_numpy(...).float()).
   float* pad32 = c.buf<float>("pl.pad32", (size_t)m, s);
   double* pad64 = c.buf<double>("pl.pad64", (size_t)m, s);
-  double* ws = c.buf<double>("pl.iirws", filtfilt_ws_doubles(n, c.hp_order), s);
-  check(filtfilt_pad(audio, n, c.hp_b.data(), c.hp_a.data(), c.hp_zi.data(), nullptr, c.hp_order, o.t_pad, ws, pad64,
-                     pad32, s),
-        "filtfilt_pad");
+  highpass_pad(c, audio, n, o.t_pad, pad64, pad32, s);
   const double* filtered = pad64 + o.t_pad;
   // 2. split points for inputs longer than t_max (pipeline.py:440-452)
   std::vector<int64_t> opt_ts;
@@ -242,11 +308,8 @@ int64_t pipeline_forward_batch(Ctx& c, const double* audio, int64_t n, int64_t l
   // 1. zero-phase high-pass + reflect pad per utterance (pipeline.py:439, :459)
   float* pad32 = c.buf<float>("pb.pad32", (size_t)B * ldm, s);
   double* pad64 = c.buf<double>("pb.pad64", (size_t)B * m, s);
-  double* ws = c.buf<double>("pl.iirws", filtfilt_ws_doubles(n, c.hp_order), s);
   for (int b = 0; b < B; ++b)
-    check(filtfilt_pad(audio + (size_t)b * lda, n, c.hp_b.data(), c.hp_a.data(), c.hp_zi.data(), nullptr, c.hp_order,
-                       o.t_pad, ws, pad64 + (size_t)b * m, pad32 + (size_t)b * ldm, s),
-          "filtfilt_pad");
+    highpass_pad(c, audio + (size_t)b * lda, n, o.t_pad, pad64 + (size_t)b * m, pad32 + (size_t)b * ldm, s);
   // 2. f0 (batched RMVPE) + get_f0 adjustments per utterance (pipeline.py:462-472, :248-291)
   const int64_t F = 1 + m / W, T = m / W;
   double* f0 = c.buf<double>("pb.f0", (size_t)B * F, s);

@@ -27,7 +27,7 @@ EXPORTS = [
     "rvcx_index_unload", "rvcx_index_info", "rvcx_index_set_nprobe", "rvcx_index_search", "rvcx_index_reconstruct_n",
     "rvcx_index_retrieve", "rvcx_rt_default_desc", "rvcx_rt_default_opts", "rvcx_rt_create", "rvcx_rt_destroy",
     "rvcx_rt_geometry", "rvcx_rt_reset", "rvcx_rt_process", "rvcx_hubert_batch", "rvcx_rmvpe_batch",
-    "rvcx_pipeline_batch",
+    "rvcx_pipeline_batch", "rvcx_set_highpass_sos", "rvcx_highpass_pad",
 ]
 
 
@@ -131,6 +131,8 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "rvcx_index_retrieve": (i32, [vp, vp, i64, i32, f64, vp, vp]),
         "rvcx_pipeline_batch": (i32, [vp, vp, i64, i64, i32, P(PipelineOpts), P(ctypes.c_int32), vp, vp, u64, vp, i64,
                                       P(i64), vp]),
+        "rvcx_set_highpass_sos": (i32, [vp, vp, i32]),
+        "rvcx_highpass_pad": (i32, [vp, vp, i64, i64, vp, vp, vp]),
         "rvcx_hubert_batch": (i32, [vp, vp, i64, i64, i32, i32, vp, i64, P(i64), vp]),
         "rvcx_rmvpe_batch": (i32, [vp, vp, i64, i64, i32, f32, vp, i64, P(i64), vp, vp]),
         "rvcx_rt_default_desc": (i32, [P(RtDesc)]),

@@ -244,13 +244,37 @@ class Engine:
         return out[: no.value]
 
     # ------------------------------------------------------------------ whole pipeline
-    def set_highpass(self, b, a, zi):
+    def set_highpass(self, b, a, zi, sos=None):
+        """The pipeline's high-pass (pipeline.py:22-27) as transfer function (+ lfilter_zi) and, when given,
+        as second-order sections (run as a chunk-parallel scan)."""
         b = np.ascontiguousarray(b, dtype=np.float64)
         a = np.ascontiguousarray(a, dtype=np.float64)
         zi = np.ascontiguousarray(zi, dtype=np.float64)
         self._check(self.lib.rvcx_set_highpass(self.ctx, b.ctypes.data, a.ctypes.data, zi.ctypes.data, len(a) - 1),
                     "set_highpass")
+        if sos is not None:
+            q = np.ascontiguousarray(sos, dtype=np.float64).reshape(-1, 6)
+            self._check(self.lib.rvcx_set_highpass_sos(self.ctx, q.ctypes.data, q.shape[0]), "set_highpass_sos")
         self._hp = (b, a, zi)
+
+    def set_pipeline_highpass(self, sr: int = 16000):
+        """signal.butter(N=5, Wn=48, btype='high', fs=16000) as rvc/infer/pipeline.py:22-27 designs it."""
+        from scipy import signal
+
+        b, a = signal.butter(N=5, Wn=48, btype="high", fs=sr)
+        sos = signal.butter(N=5, Wn=48, btype="high", fs=sr, output="sos")
+        self.set_highpass(b, a, signal.lfilter_zi(b, a), sos)
+
+    def highpass_pad(self, audio, t_pad: int):
+        """filtfilt + reflect pad on device: fp64 [n] -> (fp64, fp32) [n + 2 t_pad]."""
+        t = self.torch
+        a = self._dev(audio, t.float64).reshape(-1)
+        n = a.numel()
+        p64 = t.empty((n + 2 * t_pad,), dtype=t.float64, device=self.device)
+        p32 = t.empty((n + 2 * t_pad,), dtype=t.float32, device=self.device)
+        self._check(self.lib.rvcx_highpass_pad(self.ctx, a.data_ptr(), n, int(t_pad), p64.data_ptr(), p32.data_ptr(),
+                                               self.stream()), "highpass_pad")
+        return p64, p32
 
     def pipeline(self, audio, sid: int = 0, semitones: float = 0.0, protect: float = 0.33, t_pad: int = 16000,
                  t_pad_tgt: int = 48000, eps_z=None, eps_src=None, seed: int = 0, out=None, want_f0: bool = False):

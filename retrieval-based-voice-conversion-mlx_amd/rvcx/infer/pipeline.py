@@ -82,11 +82,7 @@ class PipelineRVCX:
 
     def _ensure_highpass(self, eng):
         if getattr(eng, "_hp", None) is None:
-            from scipy import signal
-
-            # pipeline.py:22-27: signal.butter(N=5, Wn=48, btype="high", fs=16000)
-            b, a = signal.butter(N=5, Wn=48, btype="high", fs=self.sample_rate)
-            eng.set_highpass(b, a, signal.lfilter_zi(b, a))
+            eng.set_pipeline_highpass(self.sample_rate)  # pipeline.py:22-27
 
     def load_index(self, file_index: str, eng=None):
         """faiss.read_index + reconstruct_n (pipeline.py:430-434), cached per (path, mtime, size)."""

@@ -88,13 +88,10 @@ def test_rmvpe_decode_kat_on_device(engine):
 def test_pipeline_vs_reference(engine):
     """Whole Pipeline.pipeline (filtfilt, pad, RMVPE, f0 post, HuBERT, synth, trim, normalise) on device
     vs the reference run on the same 2.5 s clip with the same noise draws."""
-    from scipy import signal
-
     from oracle.metrics import spectrogram_correlation
 
     g = golden("pipeline_2p5s.npz")
-    b, a = signal.butter(N=5, Wn=48, btype="high", fs=16000)
-    engine.set_highpass(b, a, signal.lfilter_zi(b, a))
+    engine.set_pipeline_highpass()
     out = engine.pipeline(g["audio"], sid=0, semitones=0, protect=0.33, t_pad=16000, t_pad_tgt=48000,
                           eps_z=g["eps_z"], eps_src=g["eps_src"]).cpu().numpy()
     ref = g["out"]
@@ -121,3 +118,29 @@ def test_batched_frontends_match_single(engine):
         assert rel_err(hb[b], h1.cpu().numpy()) < 1e-4
         acc, vuv = cents_agreement(f0b[b], f01.cpu().numpy(), 50.0)
         assert acc >= 0.99 and vuv >= 0.99, (acc, vuv)
+
+
+@pytest.mark.parametrize("form", ["sos", "tf"])
+@pytest.mark.parametrize("n", [1000, 216100, 960000])
+def test_highpass_pad_vs_scipy(engine, form, n):
+    """signal.filtfilt(bh, ah, x) + reflect pad (pipeline.py:22-27, :439, :459) on device, as the chunk-parallel
+    SOS scan and as the (b, a) warm-up form, vs scipy: max |diff| <= 1e-7 of the peak (scipy's own (b, a) form
+    differs from its exact-section sosfiltfilt by 5.7e-8 of the peak on speech)."""
+    from scipy import signal
+
+    from rvcx import synthetic
+
+    b, a = signal.butter(N=5, Wn=48, btype="high", fs=16000)
+    if form == "sos":
+        engine.set_pipeline_highpass()
+    else:
+        engine.set_highpass(b, a, signal.lfilter_zi(b, a))
+    x = synthetic.speech_like(n, seed=13)
+    t_pad = min(16000, n - 1)
+    p64, p32 = engine.highpass_pad(x, t_pad)
+    ref = np.pad(signal.filtfilt(b, a, x), (t_pad, t_pad), mode="reflect")
+    got = p64.cpu().numpy()
+    assert got.shape == ref.shape
+    assert np.abs(got - ref).max() <= 1e-7 * np.abs(ref).max(), np.abs(got - ref).max() / np.abs(ref).max()
+    assert np.array_equal(p32.cpu().numpy(), got.astype(np.float32))
+    engine.set_pipeline_highpass()

@@ -162,10 +162,7 @@ def test_pipeline_batch_matches_single(engine):
     from oracle.metrics import spectrogram_correlation
     from rvcx import synthetic
 
-    from scipy import signal
-
-    b_, a_ = signal.butter(N=5, Wn=48, btype="high", fs=16000)
-    engine.set_highpass(b_, a_, signal.lfilter_zi(b_, a_))
+    engine.set_pipeline_highpass()
     B, n = 3, 40000
     audio = np.stack([synthetic.speech_like(n, seed=90 + b) for b in range(B)])
     opts = engine.pipeline_opts(pitch=2.0, protect=0.33)
