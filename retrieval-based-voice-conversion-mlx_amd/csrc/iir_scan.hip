@@ -27,7 +27,11 @@ __device__ __forceinline__ double in_at(const double* x, long long n, int rev, l
 }
 }  // namespace
 
-// zero-state pass of section `sec` (coef: b0 b1 b2 a1 a2) over chunk c; input read reversed when rev
+// One lane per chunk; inputs are fetched NB at a time ahead of the recurrence (each lane's NB samples
+// are one 128-B line) so the load latency overlaps the dependent fp64 chain of the previous batch.
+constexpr int NB = 16;
+
+// zero-state pass of section (coef: b0 b1 b2 a1 a2) over chunk c; input read reversed when rev
 __global__ void k_sos_local(const double* __restrict__ x, long long n, int rev, const double* __restrict__ coef,
                             int L, double* __restrict__ y0, double* __restrict__ e) {
   const long long c = blockIdx.x * (long long)blockDim.x + threadIdx.x;
@@ -35,8 +39,30 @@ __global__ void k_sos_local(const double* __restrict__ x, long long n, int rev, 
   if (c >= nch) return;
   const double b0 = coef[0], b1 = coef[1], b2 = coef[2], a1 = coef[3], a2 = coef[4];
   double z0 = 0.0, z1 = 0.0;
-  const long long t1 = min(n, (c + 1) * L);
-  for (long long t = c * L; t < t1; ++t) {
+  const long long t0 = c * L, t1 = min(n, t0 + L);
+  long long t = t0;
+  double xb[NB];
+  if (t + NB <= t1) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) xb[i] = in_at(x, n, rev, t + i);
+  }
+  for (; t + NB <= t1; t += NB) {
+    double cur[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) cur[i] = xb[i];
+    if (t + 2 * NB <= t1) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) xb[i] = in_at(x, n, rev, t + NB + i);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const double y = b0 * cur[i] + z0;
+      z0 = b1 * cur[i] - a1 * y + z1;
+      z1 = b2 * cur[i] - a2 * y;
+      y0[t + i] = y;
+    }
+  }
+  for (; t < t1; ++t) {
     const double xv = in_at(x, n, rev, t);
     const double y = b0 * xv + z0;
     z0 = b1 * xv - a1 * y + z1;
@@ -119,25 +145,54 @@ __global__ void k_sos_fix(const double* __restrict__ y0, long long n, int L, con
   if (c >= nch) return;
   const double s0 = S[2 * c], s1 = S[2 * c + 1];
   const long long t0 = c * L, t1 = min(n, t0 + L);
-  if (!next_coef) {
-    for (long long t = t0; t < t1; ++t) {
-      const int k = (int)(t - t0);
-      out[t] = y0[t] + (CA[2 * k] * s0 + CA[2 * k + 1] * s1);
-    }
-    return;
-  }
-  const double b0 = next_coef[0], b1 = next_coef[1], b2 = next_coef[2], a1 = next_coef[3], a2 = next_coef[4];
+  double b0 = 0, b1 = 0, b2 = 0, a1 = 0, a2 = 0;
+  if (next_coef) b0 = next_coef[0], b1 = next_coef[1], b2 = next_coef[2], a1 = next_coef[3], a2 = next_coef[4];
+  double* dst = next_coef ? y0n : out;
   double z0 = 0.0, z1 = 0.0;
-  for (long long t = t0; t < t1; ++t) {
+  long long t = t0;
+  double xb[NB];
+  if (t + NB <= t1) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) xb[i] = y0[t + i];
+  }
+  for (; t + NB <= t1; t += NB) {
+    double cur[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) cur[i] = xb[i];
+    if (t + 2 * NB <= t1) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) xb[i] = y0[t + NB + i];
+    }
+    const int k0 = (int)(t - t0);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const double xv = cur[i] + (CA[2 * (k0 + i)] * s0 + CA[2 * (k0 + i) + 1] * s1);
+      if (next_coef) {
+        const double y = b0 * xv + z0;
+        z0 = b1 * xv - a1 * y + z1;
+        z1 = b2 * xv - a2 * y;
+        dst[t + i] = y;
+      } else {
+        dst[t + i] = xv;
+      }
+    }
+  }
+  for (; t < t1; ++t) {
     const int k = (int)(t - t0);
     const double xv = y0[t] + (CA[2 * k] * s0 + CA[2 * k + 1] * s1);
-    const double y = b0 * xv + z0;
-    z0 = b1 * xv - a1 * y + z1;
-    z1 = b2 * xv - a2 * y;
-    y0n[t] = y;
+    if (next_coef) {
+      const double y = b0 * xv + z0;
+      z0 = b1 * xv - a1 * y + z1;
+      z1 = b2 * xv - a2 * y;
+      dst[t] = y;
+    } else {
+      dst[t] = xv;
+    }
   }
-  en[2 * c] = z0;
-  en[2 * c + 1] = z1;
+  if (next_coef) {
+    en[2 * c] = z0;
+    en[2 * c + 1] = z1;
+  }
 }
 
 size_t sos_ws_doubles(long long n_ext, int L) {
