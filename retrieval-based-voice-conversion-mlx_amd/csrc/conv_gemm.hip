@@ -560,10 +560,20 @@ inline void cfg_tile(int cfg, int& BM, int& BN) {
   BN = t[cfg][1];
 }
 
+inline bool small2d_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("RVCX_NO_SMALL2D");
+    return !(e && std::atoi(e) != 0);
+  }();
+  return v;
+}
+
 template <bool TWO_D>
 hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
   if (a.N <= 0 || a.T_out <= 0 || a.batch <= 0) return hipSuccess;
   if (a.C_in <= 0 || a.taps <= 0) return hipErrorInvalidValue;
+  // 3x3 convs with 16/32 channels: 16x16x4 MFMA fragments (conv2d_small.hip)
+  if (TWO_D && a.force_cfg < 0 && small2d_enabled() && conv2d_small_fits(a)) return conv2d_small(a, s);
   const int cfg = pick_cfg<TWO_D>(a);
   ConvArgs b = a;
   b.force_cfg = cfg;
@@ -586,6 +596,7 @@ hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
 long long conv_plan_splitk(ConvArgs& a, bool two_d) {
   a.ksplit = 1;
   if (a.N <= 0 || a.T_out <= 0 || a.no_splitk) return 0;
+  if (two_d && a.force_cfg < 0 && small2d_enabled() && conv2d_small_fits(a)) return 0;
   const int cfg = two_d ? pick_cfg<true>(a) : pick_cfg<false>(a);
   int BM, BN;
   cfg_tile(cfg, BM, BN);

@@ -100,6 +100,10 @@ struct ConvArgs {
 
 hipError_t conv1d(const ConvArgs& a, hipStream_t s);
 hipError_t conv2d(const ConvArgs& a, hipStream_t s);
+// 3x3/pad-1 2-D convs with C_in, N in {16, 32} on 16x16x4 MFMA fragments (conv2d_small.hip); conv2d routes
+// the shapes conv2d_small_fits accepts there (RVCX_NO_SMALL2D=1 disables)
+bool conv2d_small_fits(const ConvArgs& a);
+hipError_t conv2d_small(const ConvArgs& a, hipStream_t s);
 // choose split-K for small output grids; returns the workspace floats needed (0 = no split)
 long long conv_plan_splitk(ConvArgs& a, bool two_d);
 
