@@ -535,8 +535,9 @@ hipError_t launch_forced(const ConvArgs& a, hipStream_t s) {
 }
 
 // Tile per shape class, measured on MI355X (same-box A/B of the whole pipeline, tools/ab_policy.sh):
-// one 32x32 accumulator per wave with 4 waves per block (128x32 for N <= 32, 64x64 otherwise) beats
-// the larger per-wave tiles in the pipeline; split-K when the output grid cannot fill 256 CUs.
+// one 32x32 accumulator per wave with 4 waves per block beats the larger per-wave tiles in the pipeline:
+// 128x32 for N <= 32 and for the long-tap 1-D convs (the generator's dilated ResBlock convs), 64x64
+// otherwise; split-K when the output grid cannot fill 256 CUs.
 // RVCX_CFG_LONG / RVCX_CFG_SHORT / RVCX_CFG_NARROW override a class (measurement aid).
 inline int env_cfg(const char* name, int dflt) {
   const char* e = std::getenv(name);
@@ -545,7 +546,7 @@ inline int env_cfg(const char* name, int dflt) {
 template <bool TWO_D>
 int pick_cfg(const ConvArgs& a) {
   if (a.force_cfg >= 0) return a.force_cfg;
-  static const int c_long = env_cfg("RVCX_CFG_LONG", 3);      // 1-D, taps >= 5, N > 32
+  static const int c_long = env_cfg("RVCX_CFG_LONG", 1);      // 1-D, taps >= 5, N > 32 (A/B: 32.8 vs 33.6 ms)
   static const int c_short = env_cfg("RVCX_CFG_SHORT", 3);    // everything else with N > 32
   static const int c_narrow = env_cfg("RVCX_CFG_NARROW", 1);  // N <= 32
   if (a.N <= 32) return c_narrow;
