@@ -97,7 +97,7 @@ int main(int argc, char** argv) {
   }
   // split-K correctness on a small-M shape
   {
-    const int T = 150, C = 512, N = 384, taps = 3, dil = 1, pad = 1;
+    const int T = 150, C = 512, N = 384, taps = 1, dil = 1, pad = 0;
     std::vector<float> hx((size_t)T * C), hw((size_t)taps * N * C), hb(N);
     fill_rand(hx, 11);
     fill_rand(hw, 12);
@@ -169,8 +169,9 @@ int main(int argc, char** argv) {
     int ksp[11] = {0};
     for (int round = 0; round < (only_case >= 0 ? 1 : 3); ++round)
     for (int cfg : {-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9})
-      for (int asb : {1}) {
-        const int pipe = -1;
+      for (int asb : {1, 4}) {
+        const int pipe = asb == 4 ? 1 : -1;  // column "asb4" = the double-buffered GEMM pipeline (taps 1)
+        if (pipe > 0 && cs.taps != 1) continue;
         if (only_case >= 0 && (cfg != only_cfg % 10 || asb != (only_cfg >= 10 ? 4 : 1))) continue;
         ConvArgs a;
         a.x = x; a.ldx = cs.Cin; a.T_in = cs.T; a.C_in = cs.Cin;
@@ -202,8 +203,8 @@ int main(int argc, char** argv) {
         ksp[cfg + 1] = a.ksplit;
         if (wsp) (void)hipFree(wsp);
       }
-    for (int v = 0; v < 1; ++v) {
-      printf("%-24s asb%d", cs.name, v ? 4 : 1);
+    for (int v = 0; v < (cs.taps == 1 ? 2 : 1); ++v) {
+      printf("%-24s %s", cs.name, v ? "pipe" : "sync");
       for (int c = 0; c < 11; ++c) printf(" %2d:%6.1f%s", c - 1, best[v][c], ksp[c] > 1 ? "*" : " ");
       printf("\n");
     }

@@ -80,8 +80,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
   static_assert(TM >= 1 && TN >= 1, "tile too small");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* As = smem;
-  float* Bs0 = smem + nrows_a * CKP;        // PIPE: two B buffers [2][BN][CKP]
-  float* Bs1 = Bs0 + BN * CKP;
+  float* Bs0 = smem + nrows_a * CKP;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -330,36 +329,86 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
       }
     }
   } else {
-    // software pipeline over the (chunk, tap) sequence: the next B tile is fetched into registers
-    // while the MFMAs consume the current one from LDS; one barrier per tap (two at chunk change).
+    // PIPE (1-D, taps == 1, stride 1: a plain GEMM over C_in): A and B both double-buffered in LDS; the next
+    // chunk's tiles are fetched into registers while the MFMAs consume the current ones, then written to
+    // the other buffers; one barrier per chunk. Small-M GEMMs (HuBERT at 775 rows, TextEncoder/flow at
+    // 1550) otherwise expose two dependent global-load latencies per 32-channel chunk.
+    constexpr int AV = (BM * C4 + NTHREADS - 1) / NTHREADS;
+    float* const A0 = smem;
+    float* const A1 = smem + BM * CKP;
+    float* const B0 = smem + 2 * BM * CKP;
+    float* const B1 = B0 + BN * CKP;
+    f32x4 areg[AV];
+    float amk[AV];
     f32x4 breg[BV];
-    stage_a(0);
-    load_b(0, 0, breg);
-    store_b(Bs0, breg);
-    __syncthreads();
-    const int total = nchunks * a.taps;
-    int ch = 0, tap = 0;
-    for (int it = 0; it < total; ++it) {
-      float* Bcur = (it & 1) ? Bs1 : Bs0;
-      float* Bnxt = (it & 1) ? Bs0 : Bs1;
-      int nch = ch, ntap = tap + 1;
-      if (ntap == a.taps) {
-        ntap = 0;
-        ++nch;
-      }
-      const bool more = it + 1 < total;
-      if (more) load_b(ntap, nch * CKT, breg);
-      compute(Bcur, tap);
-      if (more) {
-        if (ntap == 0) {
-          __syncthreads();  // every wave is done with this chunk's A tile
-          stage_a(nch * CKT);
+    auto load_a = [&](int c0) {
+#pragma unroll
+      for (int v = 0; v < AV; ++v) {
+        const int idx = tid + v * NTHREADS;
+        areg[v] = f32x4{0.f, 0.f, 0.f, 0.f};
+        amk[v] = 0.f;
+        if (idx < BM * C4) {
+          const int r = idx / C4;
+          const int c = c0 + ((idx % C4) << 2);
+          const int g = row0 + r;
+          if (g >= 0 && g < a.T_in && c < a.C_in) {
+            amk[v] = PM ? PM[g] : 1.f;
+            const float* src = X + (long long)g * a.ldx + c;
+            if (vec_a && c + 4 <= a.C_in) {
+              areg[v] = *reinterpret_cast<const f32x4*>(src);
+            } else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) areg[v][j] = (c + j < a.C_in) ? src[j] : 0.f;
+            }
+          }
         }
-        store_b(Bnxt, breg);
       }
+    };
+    auto store_a = [&](float* dst) {
+#pragma unroll
+      for (int v = 0; v < AV; ++v) {
+        const int idx = tid + v * NTHREADS;
+        if (idx < BM * C4) {
+          f32x4 val = areg[v];
+          if (amk[v] != 0.f) {
+            if (a.pre_act != ACT_NONE) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) val[j] = act_fn(val[j], a.pre_act, a.pre_slope);
+            }
+            if (PM) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) val[j] *= amk[v];
+            }
+          } else {
+            val = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+          *reinterpret_cast<f32x4*>(&dst[(idx / C4) * CKP + ((idx % C4) << 2)]) = val;
+        }
+      }
+    };
+    const int per = (nchunks + ksplit - 1) / ksplit;
+    const int it0 = zsplit * per, it1 = min(nchunks, it0 + per);
+    if (it0 < it1) {
+      load_a(it0 * CKT);
+      load_b(0, it0 * CKT, breg);
+      store_a(A0);
+      store_b(B0, breg);
       __syncthreads();
-      ch = nch;
-      tap = ntap;
+      for (int it = it0; it < it1; ++it) {
+        const bool odd = (it - it0) & 1;
+        const bool more = it + 1 < it1;
+        if (more) {
+          load_a((it + 1) * CKT);
+          load_b(0, (it + 1) * CKT, breg);
+        }
+        As = odd ? A1 : A0;
+        compute(odd ? B1 : B0, 0);
+        if (more) {
+          store_a(odd ? A0 : A1);
+          store_b(odd ? B0 : B1, breg);
+        }
+        __syncthreads();
+      }
     }
   }
 
@@ -474,7 +523,8 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
     mtiles = ((a.T_out + rh - 1) / rh) * tiles_w;
     nrows_a = (rh + a.KH - 1) * (rw + a.KW - 1);
   }
-  size_t smem = (size_t)(nrows_a + (PIPE ? 2 : 1) * BN) * CKP * sizeof(float);
+  if (PIPE && (TWO_D || a.taps != 1 || a.stride != 1)) return hipErrorInvalidValue;
+  size_t smem = (size_t)(PIPE ? 2 : 1) * (nrows_a + BN) * CKP * sizeof(float);
   smem = std::max(smem, (size_t)4 * 32 * 33 * sizeof(float));  // epilogue staging slots (2x2-per-wave tiles)
   if (smem > 160 * 1024) return hipErrorInvalidValue;
   const int vec_a = ((a.ldx & 3) == 0) && ((reinterpret_cast<uintptr_t>(a.x) & 15) == 0) &&
@@ -483,7 +533,7 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
                     ((a.w_bs & 3) == 0) && ((a.w_bs2 & 3) == 0) && ((a.w_ts & 3) == 0);
   if (a.batch_inner < 1) return hipErrorInvalidValue;
   int ksplit = 1;
-  if (!PIPE && a.ws && a.ksplit > 1) ksplit = a.ksplit;
+  if (a.ws && a.ksplit > 1) ksplit = a.ksplit;
   dim3 grid(mtiles, (a.N + BN - 1) / BN, a.batch * a.batch_inner * ksplit);
   auto kern = conv_gemm_kernel<BM, BN, WM, WN, TWO_D, PIPE, ASB, CKT>;
   if (smem > 64 * 1024) {
@@ -578,7 +628,14 @@ hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
   const int cfg = pick_cfg<TWO_D>(a);
   ConvArgs b = a;
   b.force_cfg = cfg;
-  const bool pipe = a.pipe > 0 && a.force_cfg >= 0;
+  // plain GEMMs (1-D, one tap, stride 1) take the double-buffered pipeline unless a.pipe < 0 or
+  // RVCX_NO_PIPE=1; a.pipe > 0 forces it (benchmarks)
+  static const bool pipe_env = [] {
+    const char* e = std::getenv("RVCX_NO_PIPE");
+    return !(e && std::atoi(e) != 0);
+  }();
+  const bool gemm = !TWO_D && a.taps == 1 && a.stride == 1;
+  const bool pipe = gemm && (a.pipe > 0 || (a.pipe == 0 && pipe_env));
   hipError_t e = pipe ? launch_forced<TWO_D, true>(b, s) : launch_forced<TWO_D, false>(b, s);
   if (e == hipErrorInvalidValue && a.force_cfg < 0) {
     // the chosen tile's halo does not fit in LDS (long strided taps): fall back to smaller tiles
