@@ -71,7 +71,7 @@ __device__ __forceinline__ void epilogue_store(const ConvArgs& a, float v, float
 template <int BM, int BN, int WM, int WN, bool TWO_D, bool PIPE, int ASB, int CKT = CK>
 __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a, const int nrows_a, const int rw,
                                                              const int rh, const int tiles_w, const int vec_a,
-                                                             const int vec_b, const int ksplit) {
+                                                             const int vec_b, const int ksplit, const int ntn) {
   constexpr int CKP = CKT + 4;  // padded LDS row: rows i..i+15 land on distinct 16-B bank slots
   constexpr int C4 = CKT / 4;   // float4 per LDS row
   constexpr int TM = BM / (WM * 32);
@@ -87,17 +87,32 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
   const int wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int li = lane & 31, hk = lane >> 5;
-  const int zsplit = blockIdx.z % ksplit;     // split-K slice
-  const int zb = blockIdx.z / ksplit;
-  const int b = zb / a.batch_inner;           // outer batch
-  const int bi = zb % a.batch_inner;          // inner batch (heads / groups)
-  const int n0 = blockIdx.y * BN;
+  // Tile order (ntn > 0): the grid is 1-D over (M tile, N tile) with N fastest, and the linear workgroup
+  // id is remapped so each XCD (workgroups are dealt to the 8 XCDs round-robin) owns one contiguous run of
+  // tiles: the N tiles of an M tile then share its A halo through one L2 instead of re-reading it from
+  // HBM/L3 (bijective remap, cdna_hip_programming.md T1). ntn = 0: the plain (x = M, y = N) grid.
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (ntn > 0) {
+    const int X = gridDim.x, total = X * gridDim.z;
+    const int orig = blockIdx.z * X + blockIdx.x;
+    const int xcd = orig & 7, q = total >> 3, r = total & 7;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+    bz = wg / X;
+    const int t = wg - bz * X;
+    bx = t / ntn;
+    by = t - bx * ntn;
+  }
+  const int zsplit = bz % ksplit;     // split-K slice
+  const int zb = bz / ksplit;
+  const int b = zb / a.batch_inner;   // outer batch
+  const int bi = zb % a.batch_inner;  // inner batch (heads / groups)
+  const int n0 = by * BN;
   int m0 = 0, h0 = 0, w0 = 0;
   if (!TWO_D) {
-    m0 = blockIdx.x * BM;
+    m0 = bx * BM;
   } else {
-    h0 = (blockIdx.x / tiles_w) * rh;
-    w0 = (blockIdx.x % tiles_w) * rw;
+    h0 = (bx / tiles_w) * rh;
+    w0 = (bx % tiles_w) * rw;
   }
   const float* X = a.x + (long long)b * a.x_bs + (long long)bi * a.x_bs2;
   const float* Wb = a.w + (long long)b * a.w_bs + (long long)bi * a.w_bs2;
@@ -534,14 +549,20 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
   if (a.batch_inner < 1) return hipErrorInvalidValue;
   int ksplit = 1;
   if (a.ws && a.ksplit > 1) ksplit = a.ksplit;
-  dim3 grid(mtiles, (a.N + BN - 1) / BN, a.batch * a.batch_inner * ksplit);
+  const int ntiles = (a.N + BN - 1) / BN;
+  static const bool xcd_env = [] {
+    const char* e = std::getenv("RVCX_NO_XCD");
+    return !(e && std::atoi(e) != 0);
+  }();
+  const int ntn = xcd_env ? ntiles : 0;
+  dim3 grid(ntn ? mtiles * ntiles : mtiles, ntn ? 1 : ntiles, a.batch * a.batch_inner * ksplit);
   auto kern = conv_gemm_kernel<BM, BN, WM, WN, TWO_D, PIPE, ASB, CKT>;
   if (smem > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(kern, grid, dim3(NTHREADS), smem, s, a, nrows_a, rw, rh, tiles_w, vec_a, vec_b, ksplit);
+  hipLaunchKernelGGL(kern, grid, dim3(NTHREADS), smem, s, a, nrows_a, rw, rh, tiles_w, vec_a, vec_b, ksplit, ntn);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || ksplit == 1) return e;
   const long long total = (long long)a.ws_rows * a.N * a.batch * a.batch_inner;

@@ -1,0 +1,46 @@
+"""HBM bytes per conv-GEMM launch from the two PMC passes of tools/pmc_traffic.sh.
+
+FETCH_SIZE and WRITE_SIZE are in KB per dispatch (rocprofv3 derived counters). On gfx950 FETCH_SIZE reports
+half the bytes of 16-B-per-lane streaming reads (MI355X_MICROARCH.md, HBM section), so it is doubled;
+WRITE_SIZE is taken as is. The bench runs warm-up + 1 timed step + 1 event pass (inline: the timed step
+carries the events), so each kernel of the step appears `steps` times; per-launch numbers are averages.
+usage: python tools/pmc_traffic.py gpurun_out [kernel-substring]
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def load(d, counter):
+    f = glob.glob(os.path.join(d, f"pmc_{counter}", "**", "*counter_collection.csv"), recursive=True)
+    rows = list(csv.DictReader(open(f[0])))
+    out = collections.defaultdict(list)
+    for r in rows:
+        if r["Counter_Name"] == counter:
+            out[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return out
+
+
+def main():
+    d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
+    key = sys.argv[2] if len(sys.argv) > 2 else "conv_gemm_kernel"
+    fe, wr = load(d, "FETCH_SIZE"), load(d, "WRITE_SIZE")
+    tot_f = sum(sum(v) for k, v in fe.items() if key in k)
+    tot_w = sum(sum(v) for k, v in wr.items() if key in k)
+    n = sum(len(v) for k, v in fe.items() if key in k)
+    fetch = 2.0 * tot_f * 1024 / max(1, n)
+    write = tot_w * 1024 / max(1, n)
+    rec = {"kernel": key, "launches": n, "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
+           "traffic_bytes_per_launch": fetch + write,
+           "note": "FETCH_SIZE doubled (gfx950 16-B/lane reads), WRITE_SIZE as is; KB counters x 1024"}
+    all_f = sum(sum(v) for v in fe.values()) * 2 * 1024
+    all_w = sum(sum(v) for v in wr.values()) * 1024
+    rec["all_kernels_bytes"] = all_f + all_w
+    print(json.dumps(rec))
+
+
+if __name__ == "__main__":
+    main()
