@@ -179,7 +179,7 @@ int main(int argc, char** argv) {
         a.pad = (cs.taps * cs.dil - cs.dil) / 2;
         a.y = y; a.ldy = cs.N; a.T_out = cs.T; a.N = cs.N; a.bias = b;
         a.pre_act = ACT_LRELU; a.pre_slope = 0.1f; a.act = ACT_LRELU; a.slope = 0.1f;
-        a.force_cfg = cfg; a.pipe = pipe; a.astage = asb;
+        a.force_cfg = cfg; a.pipe = pipe; a.astage = asb == 1 ? 0 : asb;
         float* wsp = nullptr;
         if (cfg < 0) {
           const long long need = conv_plan_splitk(a, false);
