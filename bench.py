@@ -76,6 +76,18 @@ def cpu_baseline(sample_sec: float):
                       f"speech-like clip, x_pad=1, median of 3 after 1 warm-up ({med:.2f} s/run)"}
 
 
+def _pmc_traffic():
+    """HBM bytes per conv-GEMM launch from the committed PMC passes (tools/pmc_traffic.sh: FETCH_SIZE and
+    WRITE_SIZE in separate rocprofv3 runs of this bench, FETCH_SIZE doubled per MI355X_MICROARCH.md);
+    None when the summary is absent. PMC counters cannot be read from inside the timed process."""
+    p = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    try:
+        with open(p) as f:
+            return round(json.load(f)["traffic_bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def _timed(step, args, dev, dist):
     for i in range(args.warmup):
         step(i)
@@ -265,7 +277,8 @@ def main():
 
     achieved_tflops = k_flops / (k_ms / 1000.0) / 1e12 if k_ms > 0 else 0.0
     roofline = {"bound": "mfma", "achieved": round(achieved_tflops, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4), "traffic": _pmc_traffic(),
+                "traffic_unit": "HBM bytes per launch (profiles/r01_pmc_traffic.json)",
                 "kernel": "conv_gemm_kernel (fp32 MFMA implicit-GEMM; all launches of the step)",
                 "launches_per_step": k_launches // max(1, args.steps),
                 "kernel_ms_per_step": round(k_ms / args.steps, 3),

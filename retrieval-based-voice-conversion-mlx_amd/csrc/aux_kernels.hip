@@ -342,32 +342,44 @@ hipError_t upsample2_protect(const float* feats, const float* feats0, int L, int
 // generators/hifigan.py:156-228 + hifigan_nsf.py:48-52. Phase carry: rem[l] = fmod(f0[l]/sr*upp + .5, 1) - .5,
 // cumsum accumulated in fp64 and rounded per element (torch CPU cumsum acc_type<float> = double), then fmod 1.
 // SineGen phase prefix (generators/hifigan.py:156-228): rem[l] = fmod(f0[l]/sr*upp + 0.5, 1) - 0.5,
-// cum = fmod(cumsum(rem), 1) with the cumsum accumulated in double (torch CPU acc type), sequentially
-// like torch. One block per batch row: the block computes a tile of rem into LDS in parallel, one
-// thread runs the dependent double chain over LDS, the block writes the tile back.
-__global__ void k_sine_cum(const float* __restrict__ f0, int B, int L, int upp, float sr, double* __restrict__ cum) {
-  constexpr int TILE = 4096;
-  __shared__ float rem[TILE];
+// cum = fmod(cumsum(rem), 1) with the cumsum accumulated in double (torch CPU acc type).
+// Parallel scan, bit-identical to torch's sequential double loop: for f0 >= 0, inc + 0.5 >= 0.5 so every
+// rem is a multiple of 2^-24 with |rem| <= 0.5, and any partial sum of fewer than 2^28 of them is a
+// multiple of 2^-24 below 2^27 in magnitude (51 significant bits): every double addition is exact and the
+// summation order cannot change a bit. One block per batch row: each thread sums a contiguous segment, a
+// block scan of the segment sums gives each segment's start, and the segment is re-walked to emit
+// fmod((float)acc, 1).
+constexpr int SINE_T = 1024;
+__global__ __launch_bounds__(SINE_T) void k_sine_cum(const float* __restrict__ f0, int B, int L, int upp, float sr,
+                                                     double* __restrict__ cum) {
+  __shared__ double wsum[SINE_T / 64];
   const int b = blockIdx.x;
   const float* fb = f0 + (long long)b * L;
   float* cf = reinterpret_cast<float*>(cum + (long long)b * L);
-  double acc = 0.0;
-  for (int t0 = 0; t0 < L - 1; t0 += TILE) {
-    const int n = min(TILE, L - 1 - t0);
-    for (int j = threadIdx.x; j < n; j += blockDim.x) {
-      const float inc = (fb[t0 + j] / sr) * (float)upp;
-      rem[j] = fmodf(inc + 0.5f, 1.0f) - 0.5f;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      for (int j = 0; j < n; ++j) {
-        acc += (double)rem[j];
-        rem[j] = fmodf((float)acc, 1.0f);
-      }
-    }
-    __syncthreads();
-    for (int j = threadIdx.x; j < n; j += blockDim.x) cf[t0 + j] = rem[j];
-    __syncthreads();
+  const int n = L - 1;
+  if (n <= 0) return;  // block-uniform
+  const int per = (n + SINE_T - 1) / SINE_T;
+  const int j0 = min(n, (int)threadIdx.x * per), j1 = min(n, j0 + per);
+  auto rem_at = [&](int j) {
+    const float inc = (fb[j] / sr) * (float)upp;
+    return fmodf(inc + 0.5f, 1.0f) - 0.5f;
+  };
+  double s = 0.0;
+  for (int j = j0; j < j1; ++j) s += (double)rem_at(j);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double v = s;  // inclusive scan over the wave
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const double u = __shfl_up(v, d);
+    if (lane >= d) v += u;
+  }
+  if (lane == 63) wsum[w] = v;
+  __syncthreads();
+  double acc = v - s;
+  for (int k = 0; k < w; ++k) acc += wsum[k];
+  for (int j = j0; j < j1; ++j) {
+    acc += (double)rem_at(j);
+    cf[j] = fmodf((float)acc, 1.0f);
   }
 }
 __global__ void k_sine(const float* f0, int B, int L, int upp, float sr, const double* cum, const float* eps,
@@ -392,7 +404,7 @@ __global__ void k_sine(const float* f0, int B, int L, int upp, float sr, const d
 }
 hipError_t sine_source(const float* f0, int B, int L, int upp, float sr, const float* eps, uint64_t seed,
                        float lin_w, float lin_b, double* cum_ws, float* har, long long har_ld, hipStream_t s) {
-  hipLaunchKernelGGL(k_sine_cum, dim3(B), dim3(256), 0, s, f0, B, L, upp, sr, cum_ws);
+  hipLaunchKernelGGL(k_sine_cum, dim3(B), dim3(SINE_T), 0, s, f0, B, L, upp, sr, cum_ws);
   hipLaunchKernelGGL(k_sine, dim3(nblocks((long long)B * L * upp)), dim3(TB), 0, s, f0, B, L, upp, sr, cum_ws, eps,
                      seed, lin_w, lin_b, har, har_ld);
   return hipGetLastError();
@@ -400,13 +412,18 @@ hipError_t sine_source(const float* f0, int B, int L, int upp, float sr, const f
 
 // ------------------------------------------------------------------ noise_convs: y[b][t][c] += b[c] + sum_k har[t*s-p+k] w[c][k]
 // ------------------------------------------------------------------ conv_post: tanh(conv1d(lrelu(x, 0.01), w[1][C][K], pad K/2)), no bias
-__global__ void k_conv_post(const float* x, int T, int C, const float* w, int K, float slope, float* y) {
-  extern __shared__ float tile[];  // [(256+K-1)][C+1]
+// The C*K weights sit in LDS too: read from global inside the FMA loop (uniform address, possibly
+// aliasing y) they were one dependent vector load per FMA (80 us at C2).
+__global__ void k_conv_post(const float* __restrict__ x, int T, int C, const float* __restrict__ wg, int K,
+                            float slope, float* __restrict__ y) {
+  extern __shared__ float tile[];  // [(256+K-1)][C+1], then w[C*K]
   const int b = blockIdx.y;
   const int t0 = blockIdx.x * 256;
   const int pad = K / 2;
   const int rows = 256 + K - 1;
   const int ldt = C + 1;
+  float* w = tile + rows * ldt;
+  for (int i = threadIdx.x; i < C * K; i += blockDim.x) w[i] = wg[i];
   const float* xb = x + (long long)b * T * C;
   for (int idx = threadIdx.x; idx < rows * C; idx += blockDim.x) {
     const int r = idx / C, c = idx % C;
@@ -428,7 +445,7 @@ __global__ void k_conv_post(const float* x, int T, int C, const float* w, int K,
 }
 hipError_t conv_post_tanh(const float* x, int B, int T, int C, const float* w, int K, float slope, float* y,
                           hipStream_t s) {
-  const size_t smem = (size_t)(256 + K - 1) * (C + 1) * sizeof(float);
+  const size_t smem = ((size_t)(256 + K - 1) * (C + 1) + (size_t)C * K) * sizeof(float);
   hipLaunchKernelGGL(k_conv_post, dim3((T + 255) / 256, B), dim3(256), smem, s, x, T, C, w, K, slope, y);
   return hipGetLastError();
 }
@@ -859,12 +876,19 @@ size_t filtfilt_ws_doubles(long long n, int order) {
 }
 
 // peak normalisation (pipeline.py:550-552): m = max|x| / 0.99 ; if m > 1: x /= m
+// block-reduced, one atomic per block (a per-wave atomic on one address serialised 4096 of them: 49 us)
 __global__ void k_absmax(const float* x, long long n, unsigned* out) {
+  __shared__ float wm[TB / 64];
   float m = 0.f;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
     m = fmaxf(m, fabsf(x[i]));
   m = warp_max(m);
-  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) m = fmaxf(m, wm[w]);
+    atomicMax(out, __float_as_uint(m));
+  }
 }
 __global__ void k_peak_scale(float* x, long long n, const unsigned* mx) {
   const float m = __uint_as_float(*mx) / 0.99f;
@@ -874,8 +898,8 @@ __global__ void k_peak_scale(float* x, long long n, const unsigned* mx) {
 }
 hipError_t peak_normalize(float* x, long long n, unsigned* ws, hipStream_t s) {
   hipError_t e = hipMemsetAsync(ws, 0, sizeof(unsigned), s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_absmax, dim3(std::min<long long>(1024, (n + TB - 1) / TB)), dim3(TB), 0, s, x, n, ws);
+  if (e != hipSuccess || n <= 0) return e;
+  hipLaunchKernelGGL(k_absmax, dim3(std::min<long long>(256, (n + TB - 1) / TB)), dim3(TB), 0, s, x, n, ws);
   hipLaunchKernelGGL(k_peak_scale, dim3(nblocks(n)), dim3(TB), 0, s, x, n, ws);
   return hipGetLastError();
 }

@@ -47,6 +47,7 @@ static void fill_rand(std::vector<float>& v, unsigned seed) {
 struct Case {
   const char* name;
   int T, Cin, N, taps, dil;
+  int res = 0;  // ResBlock convs2 epilogue: + residual (separate buffer), accumulated into y, no activation
 };
 
 int main(int argc, char** argv) {
@@ -95,7 +96,7 @@ int main(int argc, char** argv) {
         printf("check cfg=%d pipe=%d max|diff|/max|ref| = %.3e %s\n", cfg, pipe, md / mr, md / mr < 1e-5 ? "OK" : "FAIL");
       }
   }
-  // split-K correctness on a small-M shape
+  // split-K correctness on small-M shapes
   {
     const int T = 150, C = 512, N = 384, taps = 1, dil = 1, pad = 0;
     std::vector<float> hx((size_t)T * C), hw((size_t)taps * N * C), hb(N);
@@ -148,12 +149,19 @@ int main(int argc, char** argv) {
       {"hubert conv1 24808 k3 s2", 24808, 512, 512, 3, 1},
       {"hubert ffn2 775x3072->768", 775, 3072, 768, 1, 1}, {"te ffn1 1550 k3 192->768", 1550, 192, 768, 3, 1},
       {"te qkv 1550x192->576", 1550, 192, 576, 1, 1}, {"flow in 1550 k5 192->384", 1550, 192, 384, 5, 1},
+      {"gen.s4 C32 k3 d1", 744000, 32, 32, 3, 1},      {"gen.s4 C32 k3 d1 res", 744000, 32, 32, 3, 1, 1},
+      {"gen.s3 C64 k3 d1 res", 372000, 64, 64, 3, 1, 1}, {"gen.s4 C32 k7 d3 res", 744000, 32, 32, 7, 3, 1},
+      {"gen.s2 C128 k3 d1 res", 186000, 128, 128, 3, 1, 1},
   };
   for (size_t ci = 0; ci < cases.size(); ++ci) {
     if (only_case >= 0 && (int)ci != only_case) continue;
     auto& cs = cases[ci];
     const size_t nx = (size_t)cs.T * cs.Cin, nw = (size_t)cs.taps * cs.N * cs.Cin, ny = (size_t)cs.T * cs.N;
-    float *x, *w, *b, *y;
+    float *x, *w, *b, *y, *rb = nullptr;
+    if (cs.res) {
+      CK_(hipMalloc(&rb, ny * 4));
+      CK_(hipMemset(rb, 0, ny * 4));
+    }
     CK_(hipMalloc(&x, nx * 4));
     CK_(hipMalloc(&w, nw * 4));
     CK_(hipMalloc(&b, cs.N * 4));
@@ -179,6 +187,10 @@ int main(int argc, char** argv) {
         a.pad = (cs.taps * cs.dil - cs.dil) / 2;
         a.y = y; a.ldy = cs.N; a.T_out = cs.T; a.N = cs.N; a.bias = b;
         a.pre_act = ACT_LRELU; a.pre_slope = 0.1f; a.act = ACT_LRELU; a.slope = 0.1f;
+        if (cs.res) {
+          a.act = ACT_NONE;
+          a.res = rb; a.ldr = cs.N; a.res_mode = RES_ADD_POST; a.acc_mode = ACC_ADD;
+        }
         a.force_cfg = cfg; a.pipe = pipe; a.astage = asb == 1 ? 0 : asb;
         float* wsp = nullptr;
         if (cfg < 0) {
@@ -209,6 +221,7 @@ int main(int argc, char** argv) {
       printf("\n");
     }
     (void)hipFree(x); (void)hipFree(w); (void)hipFree(b); (void)hipFree(y);
+    if (rb) (void)hipFree(rb);
   }
   return 0;
 }

@@ -458,8 +458,48 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
     const int n = n0 + wn * 32 + li;
     const bool n_ok = n < a.N;
     const float bn = (bias && n_ok) ? bias[n] : 0.f;
+    if (!TWO_D && ksplit == 1 && a.out_map == OUT_ROWS) {
+      // 1-D gather first: the residual, accumulate and mask operands of the lane's 16 outputs are all loaded
+      // before the first store. The stores may alias them (an in-place residual reads the very element it
+      // writes), so the compiler cannot hoist the loads across the stores itself and would expose one load
+      // latency per output (16 per lane): the short-contraction convs (ResBlock k=3 at 32/64 channels) were
+      // latency-bound on exactly that. Each element is read and written by this lane only, so the reorder is
+      // exact.
+      const bool need_r = R && a.res_mode != RES_NONE;
+      const bool need_d = a.acc_mode != ACC_STORE;
+      auto out_row = [&](int r, long long& m) {  // output row of accumulator element r; false if outside
+        m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hk;
+        return n_ok && (m < a.T_out);
+      };
+      float rv[16], dv[16], mv[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) emit(acc[0][0][r], wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hk, n, n_ok, bn);
+      for (int r = 0; r < 16; ++r) {
+        long long m;
+        const bool ok = out_row(r, m);
+        rv[r] = (ok && need_r) ? R[m * a.ldr + n] : 0.f;
+        dv[r] = (ok && need_d) ? Y[m * a.ldy + n] : 0.f;
+        mv[r] = (ok && MK) ? MK[m] : 1.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        long long m;
+        if (!out_row(r, m)) continue;
+        float v = acc[0][0][r];
+        if (a.bias) v += bn;
+        if (a.res_mode == RES_ADD_PRE) v = v + rv[r];
+        if (a.alpha != 1.f) v *= a.alpha;
+        v = act_fn(v, a.act, a.slope);
+        if (a.res_mode == RES_ADD_POST) v = v + rv[r];
+        else if (a.res_mode == RES_RSUB_POST) v = rv[r] - v;
+        if (a.acc_mode == ACC_ADD) v = dv[r] + v;
+        else if (a.acc_mode == ACC_ADD_DIV) v = (dv[r] + v) / a.acc_div;
+        if (MK) v *= mv[r];
+        Y[m * a.ldy + n] = v;
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) emit(acc[0][0][r], wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hk, n, n_ok, bn);
+    }
   } else {
     // several accumulators per wave: stage one 32x32 tile at a time through the wave's own LDS slot
     // (32 x 33 floats) and emit rows 2i + hk, column li; accumulator registers are only indexed with
