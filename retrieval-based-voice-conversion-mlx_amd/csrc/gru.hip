@@ -6,14 +6,16 @@
 //
 // Design: one launch of 4 workgroups = 2 directions x 2 halves of the hidden units. A workgroup
 // owns 128 hidden units = 384 rows of W_hh (its units' r, z, n rows) and keeps ALL of them in
-// VGPRs: 768 threads, thread (g, r) holds row r's 128 columns of column-half g (128 floats).
-//   g = 0 : columns of the workgroup's OWN units  -> dot with h_own (known locally)
-//   g = 1 : columns of the PARTNER's units        -> dot with h_partner (received)
-// Per step the two column halves run concurrently in different waves, so the partner hand-off
-// latency overlaps the own-half dot products; the gate threads then add both halves.
+// VGPRs: 768 threads, thread (j, r) holds 128 columns of row r: columns [64j, 64j+64) of its OWN
+// half of h and the same 64 columns of the PARTNER's half, as packed pairs for v_pk_fma_f32.
+// Per step every wave first takes the dot with its own columns (h_own is local), then waits for
+// the 64 partner values it needs and takes the second dot: the partner-dependent work after the
+// hand-off is 64 packed FMAs spread over all 12 waves (3 per SIMD), not 128 FMAs on half of them.
+// The gate threads add both halves. Measured (build/gru/bench_gru, T = 1568): 1.37 us/step, from 2.18
+// for 128 columns per thread split own/partner by wave (the partner half on 6 waves, 2 on some SIMDs).
 // Hand-off: 8-byte {tag = step + 1, value} granules stored with agent-scope relaxed atomics (the
-// data IS the flag; MI355X_MICROARCH.md, hand-off "R2"), double-buffered by step parity; every
-// partner-half wave polls all 128 granules (2 per lane) with agent-scope relaxed loads (sc1,
+// data IS the flag; MI355X_MICROARCH.md, hand-off "R2"), double-buffered by step parity; each
+// wave polls the 64 granules its lanes need (one per lane) with agent-scope relaxed loads (sc1,
 // L1-bypassing). Spins are bounded: on timeout *status is set and the kernel exits (no hang).
 // The granule buffer is zeroed before every launch (hipMemsetAsync in gru_bidir).
 //
@@ -28,9 +30,14 @@ constexpr int H = 256;
 constexpr int UNITS = 128;  // hidden units per workgroup
 constexpr int ROWS = 3 * UNITS;
 constexpr int NT = 2 * ROWS;  // 768 threads
+constexpr int HALF = UNITS / 2;  // columns of each half a thread covers
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr unsigned SPIN_LIMIT = 1u << 22;
 
-__device__ __forceinline__ float sigm(float v) { return 1.f / (1.f + expf(-v)); }
+// gate activations on the hardware exp/rcp (v_exp_f32, v_rcp_f32): the libm expf/tanhf and IEEE divisions
+// were 0.14 us of every 1.5 us step; error <= ~2e-6 relative on sigmoid, ~1e-7 absolute on tanh
+__device__ __forceinline__ float sigm(float v) { return __frcp_rn(1.f + __expf(-v)); }
+__device__ __forceinline__ float tanh_g(float v) { return 1.f - 2.f * __frcp_rn(1.f + __expf(2.f * v)); }
 }  // namespace
 
 __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ gi, const float* whh_f,
@@ -38,7 +45,7 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ g
                                                      int T, float* out, unsigned long long* xchg,
                                                      unsigned* status) {
   __shared__ __attribute__((aligned(16))) float h_own[UNITS];
-  __shared__ __attribute__((aligned(16))) float h_par[NT / 64][UNITS];  // per-wave copy of the partner half
+  __shared__ __attribute__((aligned(16))) float h_pw[NT / 64][HALF];  // per-wave copy of its partner columns
   __shared__ float part[2][ROWS];
   __shared__ float bias_h[ROWS];
   __shared__ int abort_flag;
@@ -51,8 +58,8 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ g
   xchg += (long long)blockIdx.y * 4 * 2 * UNITS;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int grp = tid / ROWS;     // 0: own columns, 1: partner columns (wave-uniform: ROWS % 64 == 0)
-  const int r = tid - grp * ROWS; // local row: gate r / 128, unit r % 128
+  const int j = tid / ROWS;        // column quarter within each half (wave-uniform: ROWS % 64 == 0)
+  const int r = tid - j * ROWS;    // local row: gate r / 128, unit r % 128
   const float* whh = d ? whh_b : whh_f;
   const float* bhh = d ? bhh_b : bhh_f;
   unsigned long long* mine = xchg + ((long long)(d * 2 + q) * 2) * UNITS;          // [2][128]
@@ -60,77 +67,81 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ g
 
   const int gate = r / UNITS, unit = r % UNITS;
   const int grow = gate * H + q * UNITS + unit;
-  const int colbase = (grp == 0 ? q : 1 - q) * UNITS;
-  float w[UNITS];
+  // this thread's columns: HALF of the workgroup's own units and the same HALF of the partner's
+  const int own0 = q * UNITS + j * HALF, par0 = (1 - q) * UNITS + j * HALF;
+  f32x2 wo[HALF / 2], wp[HALF / 2];
 #pragma unroll
-  for (int k = 0; k < UNITS; k += 4) {
-    const float4 v = *reinterpret_cast<const float4*>(&whh[(long long)grow * H + colbase + k]);
-    w[k] = v.x;
-    w[k + 1] = v.y;
-    w[k + 2] = v.z;
-    w[k + 3] = v.w;
+  for (int k = 0; k < HALF; k += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(&whh[(long long)grow * H + own0 + k]);
+    wo[k / 2] = f32x2{v.x, v.y};
+    wo[k / 2 + 1] = f32x2{v.z, v.w};
+    const float4 u = *reinterpret_cast<const float4*>(&whh[(long long)grow * H + par0 + k]);
+    wp[k / 2] = f32x2{u.x, u.y};
+    wp[k / 2 + 1] = f32x2{u.z, u.w};
   }
   if (tid < UNITS) h_own[tid] = 0.f;
   if (tid == 0) abort_flag = 0;
   const int gunit = q * UNITS + tid;  // gate threads: tid < 128
   if (tid < ROWS) bias_h[tid] = bhh[(tid / UNITS) * H + q * UNITS + tid % UNITS];
-  float* hp = h_par[wave];
   __syncthreads();
 
+  // dot of HALF weights with HALF values in LDS (broadcast float4 reads), two packed-FMA chains
+#define RVCX_GRU_DOT(W, HV, OUT)                                                      \
+  do {                                                                               \
+    f32x2 a0_ = {0.f, 0.f}, a1_ = {0.f, 0.f};                                        \
+    _Pragma("unroll") for (int k = 0; k < HALF; k += 4) {                            \
+      const float4 x_ = *reinterpret_cast<const float4*>(&(HV)[k]);                  \
+      a0_ = __builtin_elementwise_fma(W[k / 2], f32x2{x_.x, x_.y}, a0_);             \
+      a1_ = __builtin_elementwise_fma(W[k / 2 + 1], f32x2{x_.z, x_.w}, a1_);         \
+    }                                                                                \
+    OUT = (a0_.x + a1_.x) + (a0_.y + a1_.y);                                         \
+  } while (0)
+
+  // input gates of step s: issued at the top of the step, consumed after the hand-off (a prefetch one step
+  // ahead measured slower: its registers pushed the kernel into scratch)
+  auto load_ig = [&](int s, float& ir, float& iz, float& in) {
+    const int t = d ? (T - 1 - s) : s;
+    const int o = t * (6 * H) + d * 3 * H + gunit;  // 32-bit offset from the uniform base (T * 1536 < 2^31)
+    ir = gi[o];
+    iz = gi[o + H];
+    in = gi[o + 2 * H];
+  };
+  float ig_r = 0.f, ig_z = 0.f, ig_n = 0.f;
   for (int s = 0; s < T; ++s) {
     const int t = d ? (T - 1 - s) : s;
-    // ---- phase A: half dot products (own half uses h_own(s-1); partner half waits for it)
-    const float* hv;
-    if (grp == 0) {
-      hv = h_own;
-    } else {
+    if (tid < UNITS) load_ig(s, ig_r, ig_z, ig_n);
+    // ---- phase A: own columns from h_own(s-1) right away, then each wave fetches the 64 partner values of
+    // h(s-1) it needs (one granule per lane) and takes its partner columns. (One polling wave + a barrier
+    // measured slower: 2.4 vs 1.9 us/step.)
+    float own, par;
+    RVCX_GRU_DOT(wo, h_own + j * HALF, own);
+    asm volatile("" : "+v"(own));  // finish the own-column dot before polling (else it is sunk past the spin)
+    {
+      float* hp = h_pw[wave];
       if (s > 0) {
-        const unsigned epoch = (unsigned)s;  // partner's h(s-1), published with tag s
-        const unsigned long long* slot = theirs + ((s - 1) & 1) * UNITS;
-#pragma unroll
-        for (int rep = 0; rep < 2; ++rep) {
-          const int jj = lane + rep * 64;
-          unsigned spins = 0;
-          unsigned long long gv;
-          while (true) {
-            gv = __hip_atomic_load(&slot[jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((unsigned)(gv >> 32) == epoch) break;
-            if (++spins > SPIN_LIMIT) {
-              abort_flag = 1;
-              break;
-            }
-            __builtin_amdgcn_s_sleep(1);
+        const unsigned epoch = (unsigned)s;
+        const unsigned long long* slot = theirs + ((s - 1) & 1) * UNITS + j * HALF;
+        unsigned long long gv = 0;
+#pragma nounroll
+        for (unsigned spins = 0;; ++spins) {
+          gv = __hip_atomic_load(&slot[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((unsigned)(gv >> 32) == epoch) break;
+          if (spins > SPIN_LIMIT) {
+            abort_flag = 1;
+            break;
           }
-          hp[jj] = __uint_as_float((unsigned)gv);
+          __builtin_amdgcn_s_sleep(1);
         }
+        hp[lane] = __uint_as_float((unsigned)gv);
       } else {
         hp[lane] = 0.f;
-        hp[lane + 64] = 0.f;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      hv = hp;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      RVCX_GRU_DOT(wp, hp, par);
     }
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-#pragma unroll
-    for (int k = 0; k < UNITS; k += 16) {
-      const float4 x0 = *reinterpret_cast<const float4*>(&hv[k]);
-      const float4 x1 = *reinterpret_cast<const float4*>(&hv[k + 4]);
-      const float4 x2 = *reinterpret_cast<const float4*>(&hv[k + 8]);
-      const float4 x3 = *reinterpret_cast<const float4*>(&hv[k + 12]);
-      a0 = fmaf(w[k], x0.x, a0); a0 = fmaf(w[k + 1], x0.y, a0); a0 = fmaf(w[k + 2], x0.z, a0); a0 = fmaf(w[k + 3], x0.w, a0);
-      a1 = fmaf(w[k + 4], x1.x, a1); a1 = fmaf(w[k + 5], x1.y, a1); a1 = fmaf(w[k + 6], x1.z, a1); a1 = fmaf(w[k + 7], x1.w, a1);
-      a2 = fmaf(w[k + 8], x2.x, a2); a2 = fmaf(w[k + 9], x2.y, a2); a2 = fmaf(w[k + 10], x2.z, a2); a2 = fmaf(w[k + 11], x2.w, a2);
-      a3 = fmaf(w[k + 12], x3.x, a3); a3 = fmaf(w[k + 13], x3.y, a3); a3 = fmaf(w[k + 14], x3.z, a3); a3 = fmaf(w[k + 15], x3.w, a3);
-    }
-    part[grp][r] = (a0 + a1) + (a2 + a3);
-    float ig_r = 0.f, ig_z = 0.f, ig_n = 0.f;
-    if (tid < UNITS) {  // input gates for this step (issued before the barrier)
-      const float* g = gi + (long long)t * (6 * H) + d * 3 * H;
-      ig_r = g[gunit];
-      ig_z = g[H + gunit];
-      ig_n = g[2 * H + gunit];
-    }
+    part[j][r] = own + par;
     __syncthreads();
     if (abort_flag) {
       if (tid == 0) atomicOr(status, 1u);
@@ -143,7 +154,7 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ g
       const float hn = (part[0][2 * UNITS + tid] + part[1][2 * UNITS + tid]) + bias_h[2 * UNITS + tid];
       const float rr = sigm(hr + ig_r);
       const float zz = sigm(hz + ig_z);
-      const float nn = tanhf(ig_n + hn * rr);
+      const float nn = tanh_g(ig_n + hn * rr);
       const float hprev = h_own[tid];
       const float hnew = (hprev - nn) * zz + nn;
       h_own[tid] = hnew;
@@ -154,6 +165,7 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ g
     }
     __syncthreads();
   }
+#undef RVCX_GRU_DOT
 }
 
 hipError_t gru_bidir(const float* gi, const float* whh_f, const float* bhh_f, const float* whh_b,
