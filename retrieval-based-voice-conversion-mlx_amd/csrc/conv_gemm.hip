@@ -141,6 +141,17 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
 
   // B tile loader: global -> registers (BN x 32 floats of (tap, chunk)); NK or KN weight layout
   constexpr int BV = (BN * C4 + NTHREADS - 1) / NTHREADS;  // float4 per thread
+  // NK layout: thread v-slot reads row n0 + idx / C4, channels c0 + 4 (idx % C4): the row offset is fixed for
+  // the whole kernel, so it is computed once (32-bit: one layer's weights are < 2^31 floats)
+  int b_row_off[BV];
+  bool b_row_ok[BV];
+#pragma unroll
+  for (int v = 0; v < BV; ++v) {
+    const int idx = tid + v * NTHREADS;
+    const int gn = n0 + idx / C4;
+    b_row_ok[v] = idx < BN * C4 && gn < a.N;
+    b_row_off[v] = gn * a.ldw + ((idx % C4) << 2);
+  }
   auto load_b = [&](int tap, int c0, f32x4 (&reg)[BV]) {
     const float* Wt = Wb + (long long)tap * a.w_ts;
 #pragma unroll
@@ -149,11 +160,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
       f32x4 val = {0.f, 0.f, 0.f, 0.f};
       if (idx < BN * C4) {
         if (!a.b_kn) {
-          const int n = idx / C4;
           const int c = c0 + ((idx % C4) << 2);
-          const int gn = n0 + n;
-          if (gn < a.N && c < a.C_in) {
-            const float* src = Wt + (long long)gn * a.ldw + c;
+          if (b_row_ok[v] && c < a.C_in) {
+            const float* src = Wt + c0 + b_row_off[v];
             if (vec_b && c + 4 <= a.C_in) {
               val = *reinterpret_cast<const f32x4*>(src);
             } else {
@@ -197,6 +206,41 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
   };
   // A tile: nrows_a x 32 channels of chunk c0 -> LDS, pre-activation applied, zero outside the input
   auto stage_a_serial = [&](int c0) {
+    if constexpr (!TWO_D) {
+      // 1-D: a thread keeps one 4-channel column and walks rows NTHREADS / C4 apart, so the source and LDS
+      // addresses advance by constants (no per-element 64-bit index math)
+      constexpr int RSTEP = NTHREADS / C4;
+      const int c4 = (tid % C4) << 2;
+      const int c = c0 + c4;
+      const bool c_ok = c < a.C_in;
+      const bool c_vec = vec_a && c + 4 <= a.C_in;
+      int r = tid / C4;
+      int g = row0 + r;
+      const float* src = X + (long long)g * a.ldx + c;
+      const long long src_step = (long long)RSTEP * a.ldx;
+      for (; r < nrows_a; r += RSTEP, g += RSTEP, src += src_step) {
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (c_ok && g >= 0 && g < a.T_in) {
+          if (c_vec) {
+            v = *reinterpret_cast<const f32x4*>(src);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = (c + j < a.C_in) ? src[j] : 0.f;
+          }
+          if (a.pre_act != ACT_NONE) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = act_fn(v[j], a.pre_act, a.pre_slope);
+          }
+          if (PM) {
+            const float mk = PM[g];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] *= mk;
+          }
+        }
+        *reinterpret_cast<f32x4*>(&As[r * CKP + c4]) = v;
+      }
+      return;
+    }
     for (int idx = tid; idx < nrows_a * C4; idx += NTHREADS) {
       const int r = idx / C4;
       const int c4 = (idx % C4) << 2;
@@ -467,23 +511,26 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
       // exact.
       const bool need_r = R && a.res_mode != RES_NONE;
       const bool need_d = a.acc_mode != ACC_STORE;
-      auto out_row = [&](int r, long long& m) {  // output row of accumulator element r; false if outside
-        m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hk;
-        return n_ok && (m < a.T_out);
-      };
+      // element r sits at row mb + (r&3) + 8(r>>2) of column n: per-lane base pointers, constant row offsets
+      const int mb = m0 + wm * 32 + 4 * hk;
+      const bool full = m0 + wm * 32 + 32 <= a.T_out;
+      const float* Rl = need_r ? R + (long long)mb * a.ldr + n : nullptr;
+      float* Yl = Y + (long long)mb * a.ldy + n;
+      const float* Ml = MK ? MK + mb : nullptr;
+      auto row_ok = [&](int r) { return n_ok && (full || mb + (r & 3) + 8 * (r >> 2) < a.T_out); };
       float rv[16], dv[16], mv[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        long long m;
-        const bool ok = out_row(r, m);
-        rv[r] = (ok && need_r) ? R[m * a.ldr + n] : 0.f;
-        dv[r] = (ok && need_d) ? Y[m * a.ldy + n] : 0.f;
-        mv[r] = (ok && MK) ? MK[m] : 1.f;
+        const int ro = (r & 3) + 8 * (r >> 2);
+        const bool ok = row_ok(r);
+        rv[r] = (ok && need_r) ? Rl[ro * a.ldr] : 0.f;
+        dv[r] = (ok && need_d) ? Yl[ro * a.ldy] : 0.f;
+        mv[r] = (ok && MK) ? Ml[ro] : 1.f;
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        long long m;
-        if (!out_row(r, m)) continue;
+        if (!row_ok(r)) continue;
+        const int ro = (r & 3) + 8 * (r >> 2);
         float v = acc[0][0][r];
         if (a.bias) v += bn;
         if (a.res_mode == RES_ADD_PRE) v = v + rv[r];
@@ -494,7 +541,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
         if (a.acc_mode == ACC_ADD) v = dv[r] + v;
         else if (a.acc_mode == ACC_ADD_DIV) v = (dv[r] + v) / a.acc_div;
         if (MK) v *= mv[r];
-        Y[m * a.ldy + n] = v;
+        Yl[ro * a.ldy] = v;
       }
     } else {
 #pragma unroll
