@@ -129,10 +129,12 @@ hipError_t launch_small(const ConvArgs& a, hipStream_t s) {
   const size_t lds = ((size_t)(RH + 2) * (W + 2) * (CIN + 4) + (size_t)9 * NOUT * (CIN + 4)) * sizeof(float);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   auto kern = k_conv2d_small<CIN, NOUT, PIX>;
-  if (lds > 64 * 1024) {
+  static size_t lds_set = 64 * 1024;  // per instantiation: raise the dynamic-LDS limit once, not per launch
+  if (lds > lds_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
+    lds_set = lds;
   }
   dim3 grid((a.T_out + RH - 1) / RH, 1, a.batch);
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a, RH);

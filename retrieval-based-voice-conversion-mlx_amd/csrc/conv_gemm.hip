@@ -644,10 +644,12 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
   const int ntn = xcd_env ? ntiles : 0;
   dim3 grid(ntn ? mtiles * ntiles : mtiles, ntn ? 1 : ntiles, a.batch * a.batch_inner * ksplit);
   auto kern = conv_gemm_kernel<BM, BN, WM, WN, TWO_D, PIPE, ASB, CKT>;
-  if (smem > 64 * 1024) {
+  static size_t smem_set = 64 * 1024;  // per instantiation: raise the dynamic-LDS limit once, not per launch
+  if (smem > smem_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
+    smem_set = smem;
   }
   hipLaunchKernelGGL(kern, grid, dim3(NTHREADS), smem, s, a, nrows_a, rw, rh, tiles_w, vec_a, vec_b, ksplit, ntn);
   hipError_t e = hipGetLastError();
