@@ -206,13 +206,20 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; ranks beyond the visible GPUs wrap around (rehearsing N > 1 on a 1-GPU box
+    # with RVCX_DIST_BACKEND=gloo) -- device_count() does not initialise the GPU
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("RVCX_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI on the MI355X node
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from rvcx import synthetic
     from rvcx.config import SYNTH_48K_V2

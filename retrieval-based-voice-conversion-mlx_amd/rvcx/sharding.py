@@ -30,6 +30,8 @@ def reduce_throughput(dist, audio_sec: float, elapsed: float, device=None) -> Di
 
     if dist is None or not dist.is_initialized():
         return {"audio_sec": audio_sec, "elapsed": elapsed, "value": audio_sec / elapsed if elapsed > 0 else 0.0}
+    if dist.get_backend() == "gloo":
+        device = "cpu"  # gloo reduces host tensors
     t = torch.tensor([audio_sec, elapsed], dtype=torch.float64, device=device)
     s = t.clone()
     dist.all_reduce(s[0:1], op=dist.ReduceOp.SUM)
