@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 #include <map>
 #include <memory>
 #include <stdexcept>
@@ -104,8 +105,10 @@ struct Ctx {
   std::unique_ptr<IvfIndex> ivf;  // speaker-embedding index (optional)
   // second stream for work independent of the caller's stream (HuBERT beside RMVPE), created lazily
   hipStream_t aux = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_gate = nullptr;
   hipStream_t aux_stream();
+  // issued by RMVPE's E2E right before the BiGRU launch (host callback, cleared when taken)
+  std::function<void(hipStream_t)> before_gru;
   ~Ctx();
 
   float* W(const std::string& name) const;
@@ -138,6 +141,17 @@ void finalize_hubert(Ctx& c);
 void finalize_rmvpe(Ctx& c);
 int64_t hubert_forward(Ctx& c, const float* audio, int64_t n, int version, float* feats, int64_t cap,
                        hipStream_t s);
+// HuBERT in three parts, so a caller can issue the encoder's last layers later on another stream:
+// front end (feature convs, projection, positional conv, encoder LN), layers [l0, l1), tail (v1 projection)
+constexpr int HUBERT_LAYERS = 12;
+struct HubertRun {
+  int B = 0, L = 0, version = 0;
+  float* feats = nullptr;
+};
+HubertRun hubert_front(Ctx& c, const float* audio, int64_t n, int64_t lda, int B, int version, float* feats,
+                       int64_t cap, hipStream_t s);
+void hubert_layers(Ctx& c, const HubertRun& run, int l0, int l1, hipStream_t s);
+int64_t hubert_tail(Ctx& c, const HubertRun& run, hipStream_t s);
 int64_t rmvpe_forward(Ctx& c, const float* audio, int64_t n, float thred, double* f0, int64_t cap, float* hidden,
                       hipStream_t s);
 // batched over B equal-length inputs (rows of stride lda); outputs back to back per sequence

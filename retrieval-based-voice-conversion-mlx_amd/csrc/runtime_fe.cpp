@@ -137,8 +137,8 @@ int64_t hubert_frames(int64_t n) {
 // B equal-length sequences: audio row b at audio + b*lda; feats row block b at feats + b*L*outD.
 // Row-wise ops (LayerNorm, Linear, FFN) run over all B*L rows at once; convolutions, GroupNorm and
 // attention take the sequence as their batch index.
-int64_t hubert_forward_b(Ctx& c, const float* audio, int64_t n, int64_t lda, int B, int version, float* feats,
-                         int64_t cap, hipStream_t s) {
+HubertRun hubert_front(Ctx& c, const float* audio, int64_t n, int64_t lda, int B, int version, float* feats,
+                       int64_t cap, hipStream_t s) {
   if (B < 1) throw Error(RVCX_E_INVALID, "hubert: batch < 1");
   int64_t T[8];
   T[0] = n;
@@ -148,7 +148,6 @@ int64_t hubert_forward_b(Ctx& c, const float* audio, int64_t n, int64_t lda, int
   }
   const int L = (int)T[7];
   const int BL = B * L;
-  const int outD = version == 1 ? 256 : HD;
   if (L > cap) throw Error(RVCX_E_CAPACITY, "hubert: output needs " + std::to_string(L) + " rows");
   float* a = c.buf<float>("hb.a", (size_t)B * T[1] * HCONV, s);
   float* b = c.buf<float>("hb.b", (size_t)B * T[2] * HCONV, s);
@@ -209,12 +208,26 @@ int64_t hubert_forward_b(Ctx& c, const float* audio, int64_t n, int64_t lda, int
     check(layernorm_rows(hs2, nullptr, hs, c.W("hb.enc.ln.g"), c.W("hb.enc.ln.b"), BL, HD, 1e-5f, nullptr, s),
           "enc_ln");
   }
+  HubertRun r;
+  r.B = B;
+  r.L = L;
+  r.version = version;
+  r.feats = feats;
+  return r;
+}
+
+// encoder layers [l0, l1) on the hidden states the front end left in "hb.hs" (modeling_hubert.py
+// HubertEncoderLayer: post-LN attention + FFN)
+void hubert_layers(Ctx& c, const HubertRun& run, int l0, int l1, hipStream_t s) {
+  const int B = run.B, L = run.L, BL = B * L;
+  float* hs = c.buf<float>("hb.hs", (size_t)BL * HD, s);
+  float* hs2 = c.buf<float>("hb.hs2", (size_t)BL * HD, s);
   float* qkv = c.buf<float>("hb.qkv", (size_t)BL * 3 * HD, s);
   float* sc = c.buf<float>("hb.scores", (size_t)B * HHEADS * L * L, s);
   float* att = c.buf<float>("hb.att", (size_t)BL * HD, s);
   float* ff = c.buf<float>("hb.ff", (size_t)BL * HFF, s);
   const int hd = HD / HHEADS;
-  for (int i = 0; i < 12; ++i) {
+  for (int i = l0; i < l1; ++i) {
     const std::string q = "hb." + std::to_string(i);
     run1(c, lin(hs, HD, BL, HD, c.W(q + ".qkv.w"), 3 * HD, c.W(q + ".qkv.b"), qkv, 3 * HD), s);
     {
@@ -265,13 +278,28 @@ int64_t hubert_forward_b(Ctx& c, const float* audio, int64_t n, int64_t lda, int
     }
     check(layernorm_rows(hs2, nullptr, hs, c.W(q + ".ln2.g"), c.W(q + ".ln2.b"), BL, HD, 1e-5f, nullptr, s), "ln2");
   }
+}
+
+// v2: last_hidden_state; v1: final_proj (pipeline.py:331-334)
+int64_t hubert_tail(Ctx& c, const HubertRun& run, hipStream_t s) {
+  const int BL = run.B * run.L;
+  const int version = run.version, outD = version == 1 ? 256 : HD;
+  float* hs = c.buf<float>("hb.hs", (size_t)BL * HD, s);
+  float* feats = run.feats;
   if (version == 1) {
     if (!c.dev.count("hb.final_proj.w")) throw Error(RVCX_E_STATE, "hubert: v1 needs final_proj weights");
     run1(c, lin(hs, HD, BL, HD, c.W("hb.final_proj.w"), 256, c.W("hb.final_proj.b"), feats, 256), s);
   } else {
     RVCX_HIP(hipMemcpyAsync(feats, hs, (size_t)BL * outD * sizeof(float), hipMemcpyDeviceToDevice, s));
   }
-  return L;
+  return run.L;
+}
+
+int64_t hubert_forward_b(Ctx& c, const float* audio, int64_t n, int64_t lda, int B, int version, float* feats,
+                         int64_t cap, hipStream_t s) {
+  const HubertRun r = hubert_front(c, audio, n, lda, B, version, feats, cap, s);
+  hubert_layers(c, r, 0, HUBERT_LAYERS, s);
+  return hubert_tail(c, r, s);
 }
 
 int64_t hubert_forward(Ctx& c, const float* audio, int64_t n, int version, float* feats, int64_t cap,
@@ -624,6 +652,11 @@ static void e2e_chunk(Ctx& c, float* img, int Fc, float* sal, hipStream_t s, int
   unsigned long long* xchg = c.buf<unsigned long long>("rm.xchg", gru_xchg_words(B), s);
   unsigned* status = c.buf<unsigned>("rm.status", 4, s);
   RVCX_HIP(hipMemsetAsync(status, 0, sizeof(unsigned), s));
+  if (c.before_gru) {  // work the caller wants issued beside the BiGRU (which occupies 4 CUs)
+    auto hook = std::move(c.before_gru);
+    c.before_gru = nullptr;
+    hook(s);
+  }
   check(gru_bidir(gi, c.W("rm.gru.whh_f"), c.W("rm.gru.bhh_f"), c.W("rm.gru.whh_b"), c.W("rm.gru.bhh_b"), Fc, go,
                   xchg, status, s, B),
         "gru");

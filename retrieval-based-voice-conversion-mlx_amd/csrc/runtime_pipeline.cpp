@@ -220,19 +220,51 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
   const int E = c.scfg.emb_dim;
   std::vector<float*> cfeats(chunks.size());
   std::vector<int64_t> cL(chunks.size());
+  //    The encoder's last layers are issued only when RMVPE reaches its BiGRU (which holds 4 CUs for ~2 ms):
+  //    the U-Net then shares the GPU with less of HuBERT and the rest of HuBERT fills the BiGRU's idle CUs.
   hipStream_t ax = fork_aux(c, s);
-  {
-    for (size_t i = 0; i < chunks.size(); ++i) {
-      const int64_t len = chunks[i].a1 - chunks[i].a0;
-      const int64_t cap_rows = len / 320 + 8;
-      cfeats[i] = c.buf<float>("pl.hb" + std::to_string(i), (size_t)cap_rows * E, ax);
-      cL[i] = hubert_forward(c, pad32 + chunks[i].a0, len, hubert_version_for(c), cfeats[i], cap_rows, ax);
+  static const int gate_layer = [] {
+    const char* e = std::getenv("RVCX_HUBERT_GATE");  // first layer issued beside the BiGRU (12: none)
+    const int v = e ? std::atoi(e) : 6;
+    return v < 0 ? 0 : (v > HUBERT_LAYERS ? HUBERT_LAYERS : v);
+  }();
+  const int split = ax != s ? gate_layer : HUBERT_LAYERS;
+  std::vector<HubertRun> hruns(chunks.size());
+  for (size_t i = 0; i < chunks.size(); ++i) {
+    const int64_t len = chunks[i].a1 - chunks[i].a0;
+    const int64_t cap_rows = len / 320 + 8;
+    cfeats[i] = c.buf<float>("pl.hb" + std::to_string(i), (size_t)cap_rows * E, ax);
+    hruns[i] = hubert_front(c, pad32 + chunks[i].a0, len, len, 1, hubert_version_for(c), cfeats[i], cap_rows, ax);
+    if (chunks.size() == 1) {
+      hubert_layers(c, hruns[i], 0, split, ax);
+    } else {  // several chunks share the HuBERT workspace: each runs to completion before the next
+      hubert_layers(c, hruns[i], 0, HUBERT_LAYERS, ax);
+      cL[i] = hubert_tail(c, hruns[i], ax);
     }
   }
+  auto hubert_rest = [&](hipStream_t main) {
+    if (chunks.size() != 1) return;
+    if (split < HUBERT_LAYERS && ax != main) {
+      RVCX_HIP(hipEventRecord(c.ev_gate, main));
+      RVCX_HIP(hipStreamWaitEvent(ax, c.ev_gate, 0));
+    }
+    hubert_layers(c, hruns[0], split, HUBERT_LAYERS, ax);
+    cL[0] = hubert_tail(c, hruns[0], ax);
+  };
+  struct HookScope {
+    Ctx& c;
+    ~HookScope() { c.before_gru = nullptr; }
+  } hook_scope{c};
+  c.before_gru = hubert_rest;
   // 5. f0 over the whole padded input (pipeline.py:462-472) + get_f0 adjustments (:248-291)
   const int64_t F = 1 + m / W;
   double* f0 = c.buf<double>("pl.f0", (size_t)F, s);
   rmvpe_forward(c, pad32, m, o.rmvpe_threshold > 0 ? o.rmvpe_threshold : 0.03f, f0, F, nullptr, s);
+  if (c.before_gru) {  // RMVPE did not reach a BiGRU launch (cannot happen for valid input): issue it now
+    auto rest = std::move(c.before_gru);
+    c.before_gru = nullptr;
+    rest(s);
+  }
   double shift_semitones = o.pitch;
   if (o.f0_autotune) {
     check(f0_autotune(f0, (int)F, o.f0_autotune_strength, o.mlx_semantics ? 1 : 0, s), "f0_autotune");
