@@ -518,30 +518,37 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
       float* Yl = Y + (long long)mb * a.ldy + n;
       const float* Ml = MK ? MK + mb : nullptr;
       auto row_ok = [&](int r) { return n_ok && (full || mb + (r & 3) + 8 * (r >> 2) < a.T_out); };
-      float rv[16], dv[16], mv[16];
+      // two halves of 8 elements: one exposed load latency each, 24 staging registers instead of 48 (the
+      // VGPR count sets the workgroups per CU of this latency-bound kernel)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ro = (r & 3) + 8 * (r >> 2);
-        const bool ok = row_ok(r);
-        rv[r] = (ok && need_r) ? Rl[ro * a.ldr] : 0.f;
-        dv[r] = (ok && need_d) ? Yl[ro * a.ldy] : 0.f;
-        mv[r] = (ok && MK) ? Ml[ro] : 1.f;
-      }
+      for (int h = 0; h < 2; ++h) {
+        float rv[8], dv[8], mv[8];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (!row_ok(r)) continue;
-        const int ro = (r & 3) + 8 * (r >> 2);
-        float v = acc[0][0][r];
-        if (a.bias) v += bn;
-        if (a.res_mode == RES_ADD_PRE) v = v + rv[r];
-        if (a.alpha != 1.f) v *= a.alpha;
-        v = act_fn(v, a.act, a.slope);
-        if (a.res_mode == RES_ADD_POST) v = v + rv[r];
-        else if (a.res_mode == RES_RSUB_POST) v = rv[r] - v;
-        if (a.acc_mode == ACC_ADD) v = dv[r] + v;
-        else if (a.acc_mode == ACC_ADD_DIV) v = (dv[r] + v) / a.acc_div;
-        if (MK) v *= mv[r];
-        Yl[ro * a.ldy] = v;
+        for (int i = 0; i < 8; ++i) {
+          const int r = 8 * h + i;
+          const int ro = (r & 3) + 8 * (r >> 2);
+          const bool ok = row_ok(r);
+          rv[i] = (ok && need_r) ? Rl[ro * a.ldr] : 0.f;
+          dv[i] = (ok && need_d) ? Yl[ro * a.ldy] : 0.f;
+          mv[i] = (ok && MK) ? Ml[ro] : 1.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int r = 8 * h + i;
+          if (!row_ok(r)) continue;
+          const int ro = (r & 3) + 8 * (r >> 2);
+          float v = acc[0][0][r];
+          if (a.bias) v += bn;
+          if (a.res_mode == RES_ADD_PRE) v = v + rv[i];
+          if (a.alpha != 1.f) v *= a.alpha;
+          v = act_fn(v, a.act, a.slope);
+          if (a.res_mode == RES_ADD_POST) v = v + rv[i];
+          else if (a.res_mode == RES_RSUB_POST) v = rv[i] - v;
+          if (a.acc_mode == ACC_ADD) v = dv[i] + v;
+          else if (a.acc_mode == ACC_ADD_DIV) v = (dv[i] + v) / a.acc_div;
+          if (MK) v *= mv[i];
+          Yl[ro * a.ldy] = v;
+        }
       }
     } else {
 #pragma unroll
