@@ -152,6 +152,8 @@ int main(int argc, char** argv) {
       {"gen.s4 C32 k3 d1", 744000, 32, 32, 3, 1},      {"gen.s4 C32 k3 d1 res", 744000, 32, 32, 3, 1, 1},
       {"gen.s3 C64 k3 d1 res", 372000, 64, 64, 3, 1, 1}, {"gen.s4 C32 k7 d3 res", 744000, 32, 32, 7, 3, 1},
       {"gen.s2 C128 k3 d1 res", 186000, 128, 128, 3, 1, 1},
+      {"gen.up1 1550 512->12x256 t2", 1550, 512, 3072, 2, 1}, {"gen.up2 18600 256->10x128 t2", 18600, 256, 1280, 2, 1},
+      {"gen.up3 186000 128->2x64 t2", 186000, 128, 128, 2, 1},
   };
   for (size_t ci = 0; ci < cases.size(); ++ci) {
     if (only_case >= 0 && (int)ci != only_case) continue;
