@@ -39,19 +39,7 @@ namespace rvcx {
 hipStream_t Ctx::aux_stream() {
   if (!aux) {
     RVCX_HIP(hipSetDevice(device));
-    // the aux stream carries work that runs beside the critical path (HuBERT beside RMVPE, whose U-Net
-    // and BiGRU gate everything after them): lowest priority, so the critical stream's workgroups are
-    // dispatched first and the aux work fills the CUs they leave (RVCX_AUX_PRIORITY=0: same priority)
-    static const bool low = [] {
-      const char* e = std::getenv("RVCX_AUX_PRIORITY");
-      return !(e && std::atoi(e) == 0);
-    }();
-    int least = 0, greatest = 0;
-    if (low && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && least != greatest) {
-      RVCX_HIP(hipStreamCreateWithPriority(&aux, hipStreamNonBlocking, least));
-    } else {
-      RVCX_HIP(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
-    }
+    RVCX_HIP(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
     RVCX_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     RVCX_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
     RVCX_HIP(hipEventCreateWithFlags(&ev_gate, hipEventDisableTiming));
