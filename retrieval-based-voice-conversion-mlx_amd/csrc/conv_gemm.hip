@@ -792,8 +792,10 @@ long long conv_plan_splitk(ConvArgs& a, bool two_d) {
   // ~1.5-2 us each (global B load -> LDS -> barrier -> MFMA), so a handful of tiles walking >= 16 steps
   // is latency-bound whatever the FLOP count (RMVPE's deepest levels at streaming sizes: 8 tiles x 144
   // steps = 264 us unsplit)
-  if (tiles >= 384 || iters < 8 || (flops < 1.0e8 && iters < 16)) return 0;
-  int ks = (int)((768 + tiles - 1) / tiles);
+  static const int target = env_cfg("RVCX_SPLITK_TARGET", 768);   // workgroups a split launch aims for
+  static const int min_tiles = env_cfg("RVCX_SPLITK_TILES", 384);  // grids with at least this many tiles stay unsplit
+  if (tiles >= min_tiles || iters < 8 || (flops < 1.0e8 && iters < 16)) return 0;
+  int ks = (int)((target + tiles - 1) / tiles);
   ks = std::min(ks, iters / 2);
   ks = std::min(ks, 32);
   if (ks < 2) return 0;
