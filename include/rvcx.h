@@ -198,6 +198,13 @@ int rvcx_pipeline(rvcx_ctx* ctx, const double* d_audio, int64_t n, int sid, doub
  * rvcx_profile_read synchronises those events and returns the summed kernel time (ms), the
  * summed ALGORITHMIC FLOPs of those launches and the launch count, then clears the record. */
 int rvcx_profile(rvcx_ctx* ctx, int enable);
+
+/* Synchronise `stream` (and the context's internal side stream) and report device-side faults raised by
+ * kernels of earlier calls: RVCX_E_HIP when, e.g., the RMVPE BiGRU's cross-workgroup hand-off timed out (its
+ * outputs are then invalid). The flags are cleared once reported. Every compute entry point also reports
+ * flags of already-completed calls on entry, and the pipeline checks them at its own synchronisation points.
+ * (Replaces nothing in the reference, whose computations cannot fail this way; it never prints and continues.) */
+int rvcx_device_status(rvcx_ctx* ctx, void* stream);
 int rvcx_profile_read(rvcx_ctx* ctx, double* total_ms, double* total_flops, int64_t* launches);
 
 /* ---------------------------------------------------------------- feature index (FAISS IndexIVFFlat)
@@ -207,6 +214,11 @@ int rvcx_profile_read(rvcx_ctx* ctx, double* total_ms, double* total_flops, int6
  * are kept in HBM; nprobe comes from the file. ids must be a permutation of 0..ntotal-1 (RVC indexes). */
 int rvcx_index_load(rvcx_ctx* ctx, const void* bytes, int64_t nbytes);
 int rvcx_index_unload(rvcx_ctx* ctx);
+/* Validate a faiss .index image on the host only (no context, no device): the same parser rvcx_index_load runs.
+ * Fills d/ntotal/nlist/nprobe (each optional); on failure writes the message to err (err_cap bytes). Every size
+ * in the file is untrusted: counts are checked against the bytes left and list sizes against ntotal. */
+int rvcx_index_parse(const void* bytes, int64_t nbytes, int64_t* d, int64_t* ntotal, int64_t* nlist, int64_t* nprobe,
+                     char* err, int64_t err_cap);
 /* RVCX_E_STATE when no index is loaded. */
 int rvcx_index_info(const rvcx_ctx* ctx, int64_t* d, int64_t* ntotal, int64_t* nlist, int64_t* nprobe);
 /* faiss.extract_index_ivf(index).nprobe = nprobe (clamped to nlist). */

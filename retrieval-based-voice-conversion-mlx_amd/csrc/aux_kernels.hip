@@ -4,6 +4,7 @@
 // contiguous (time-major rows) so a wave reads whole 128-B lines.
 #include <cmath>
 
+#include "dd_math.h"
 #include "rvcx_kernels.h"
 
 namespace rvcx {
@@ -697,9 +698,12 @@ __global__ void k_f0post(const double* f0, int F, double shift, int32_t* coarse,
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= F) return;
   const double f = f0[i] * shift;
-  const double mel_min = 1127.0 * log(1.0 + 50.0 / 700.0);
-  const double mel_max = 1127.0 * log(1.0 + 1100.0 / 700.0);
-  double m = 1127.0 * log(1.0 + f / 700.0);
+  // self.f0_mel_min / f0_mel_max = 1127 * np.log(1 + 50/700), 1127 * np.log(1 + 1100/700) (pipeline.py:195-196):
+  // numpy, glibc and the correctly rounded log agree on both
+  constexpr double mel_min = 0x1.370515d9beb10p+6;
+  constexpr double mel_max = 0x1.0a1a207dfdbe5p+10;
+  // log correctly rounded (dd_math.h): the coarse pitch is integer output; every other step is one IEEE op
+  double m = 1127.0 * dd::log_cr(1.0 + f / 700.0);
   if (m > 0) m = (m - mel_min) * 254.0 / (mel_max - mel_min) + 1.0;
   if (m <= 1) m = 1;
   if (m > 255) m = 255;

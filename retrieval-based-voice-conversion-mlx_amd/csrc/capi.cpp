@@ -31,7 +31,11 @@ int guard(rvcx_ctx* c, F&& f) {
   }
 }
 
-void set_device(rvcx_ctx* c) { RVCX_HIP(hipSetDevice(c->device)); }
+// every compute entry point: select the device and report device-side faults of earlier, completed calls
+void set_device(rvcx_ctx* c) {
+  RVCX_HIP(hipSetDevice(c->device));
+  c->check_device_status();
+}
 
 }  // namespace
 
@@ -47,7 +51,32 @@ hipStream_t Ctx::aux_stream() {
   return aux;
 }
 
+unsigned* Ctx::device_status() {
+  if (!status_host) {
+    RVCX_HIP(hipSetDevice(device));
+    void* h = nullptr;
+    RVCX_HIP(hipHostMalloc(&h, 64, hipHostMallocMapped));
+    std::memset(h, 0, 64);
+    status_host = static_cast<unsigned*>(h);
+    void* d = nullptr;
+    RVCX_HIP(hipHostGetDevicePointer(&d, h, 0));
+    status_dev = static_cast<unsigned*>(d);
+  }
+  return status_dev;
+}
+
+void Ctx::check_device_status() {
+  if (!status_host) return;
+  const unsigned v = __atomic_load_n(status_host, __ATOMIC_ACQUIRE);
+  if (v == 0) return;
+  __atomic_store_n(status_host, 0u, __ATOMIC_RELEASE);
+  std::string what;
+  if (v & 1u) what += "gru: partner hand-off timed out (the RMVPE BiGRU's workgroups were not co-resident); ";
+  throw Error(RVCX_E_HIP, what + "the outputs of the call that raised this flag are invalid");
+}
+
 Ctx::~Ctx() {
+  if (status_host) (void)hipHostFree(status_host);
   if (aux) {
     (void)hipStreamSynchronize(aux);
     (void)hipEventDestroy(ev_fork);
@@ -380,6 +409,35 @@ int rvcx_pipeline_ex(rvcx_ctx* ctx, const double* d_audio, int64_t n, const rvcx
                                            static_cast<hipStream_t>(stream));
     if (n_out) *n_out = no;
   });
+}
+
+int rvcx_device_status(rvcx_ctx* ctx, void* stream) {
+  return guard(ctx, [&] {
+    RVCX_HIP(hipSetDevice(ctx->device));
+    RVCX_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    if (ctx->aux) RVCX_HIP(hipStreamSynchronize(ctx->aux));
+    ctx->check_device_status();
+  });
+}
+
+int rvcx_index_parse(const void* bytes, int64_t nbytes, int64_t* d, int64_t* ntotal, int64_t* nlist,
+                     int64_t* nprobe, char* err, int64_t err_cap) {
+  try {
+    if (!bytes || nbytes <= 0) throw Error(RVCX_E_INVALID, "index_parse: empty buffer");
+    const ParsedIvf P = parse_ivf(static_cast<const uint8_t*>(bytes), nbytes);
+    if (d) *d = P.d;
+    if (ntotal) *ntotal = P.ntotal;
+    if (nlist) *nlist = P.nlist;
+    if (nprobe) *nprobe = P.nprobe;
+    if (err && err_cap > 0) err[0] = 0;
+    return RVCX_OK;
+  } catch (const Error& e) {
+    if (err && err_cap > 0) std::snprintf(err, (size_t)err_cap, "%s", e.what());
+    return e.code;
+  } catch (const std::exception& e) {
+    if (err && err_cap > 0) std::snprintf(err, (size_t)err_cap, "%s", e.what());
+    return RVCX_E_INVALID;
+  }
 }
 
 int rvcx_profile(rvcx_ctx* ctx, int enable) {

@@ -16,11 +16,14 @@
 // Hand-off: 8-byte {tag = step + 1, value} granules stored with agent-scope relaxed atomics (the
 // data IS the flag; MI355X_MICROARCH.md, hand-off "R2"), double-buffered by step parity; each
 // wave polls the 64 granules its lanes need (one per lane) with agent-scope relaxed loads (sc1,
-// L1-bypassing). Spins are bounded: on timeout *status is set and the kernel exits (no hang).
+// L1-bypassing). Spins are bounded: on timeout *status is set and the kernel exits (no hang); the
+// runtime reports it as an error (RVCX_E_HIP, "gru: partner hand-off timed out") at its next check.
 // The granule buffer is zeroed before every launch (hipMemsetAsync in gru_bidir).
 //
 // Cell arithmetic follows ATen GRUCell: r = sig(hg_r + ig_r), z = sig(hg_z + ig_z),
 // n = tanh(ig_n + hg_n * r), h' = (h - n) * z + n, with hg = W_hh h + b_hh.
+#include <cstdlib>
+
 #include "rvcx_kernels.h"
 
 namespace rvcx {
@@ -32,7 +35,7 @@ constexpr int ROWS = 3 * UNITS;
 constexpr int NT = 2 * ROWS;  // 768 threads
 constexpr int HALF = UNITS / 2;  // columns of each half a thread covers
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-constexpr unsigned SPIN_LIMIT = 1u << 22;
+constexpr unsigned SPIN_LIMIT = 1u << 22;  // default bound on the polls of one hand-off (RVCX_GRU_SPIN_LIMIT overrides)
 
 // gate activations on the hardware exp/rcp (v_exp_f32, v_rcp_f32): the libm expf/tanhf and IEEE divisions
 // were 0.14 us of every 1.5 us step; error <= ~2e-6 relative on sigmoid, ~1e-7 absolute on tanh
@@ -43,7 +46,7 @@ __device__ __forceinline__ float tanh_g(float v) { return 1.f - 2.f * __frcp_rn(
 __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ gi, const float* whh_f,
                                                      const float* bhh_f, const float* whh_b, const float* bhh_b,
                                                      int T, float* out, unsigned long long* xchg,
-                                                     unsigned* status) {
+                                                     unsigned* status, unsigned spin_limit) {
   __shared__ __attribute__((aligned(16))) float h_own[UNITS];
   __shared__ __attribute__((aligned(16))) float h_pw[NT / 64][HALF];  // per-wave copy of its partner columns
   __shared__ float part[2][ROWS];
@@ -126,7 +129,7 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ g
         for (unsigned spins = 0;; ++spins) {
           gv = __hip_atomic_load(&slot[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if ((unsigned)(gv >> 32) == epoch) break;
-          if (spins > SPIN_LIMIT) {
+          if (spins > spin_limit) {
             abort_flag = 1;
             break;
           }
@@ -144,7 +147,9 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ g
     part[j][r] = own + par;
     __syncthreads();
     if (abort_flag) {
-      if (tid == 0) atomicOr(status, 1u);
+      // status is host-mapped pinned memory (the context's device-status word): a plain system-scope store
+      // (idempotent: every aborting workgroup writes the same 1), read by the host after it synchronises
+      if (tid == 0) __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return;
     }
     // ---- phase B: gates for the 128 own units, publish h(s)
@@ -175,7 +180,10 @@ hipError_t gru_bidir(const float* gi, const float* whh_f, const float* bhh_f, co
   if (B < 1 || 4 * B > 256) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(xchg, 0, sizeof(unsigned long long) * gru_xchg_words(B), s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_gru_bidir, dim3(4, B), dim3(NT), 0, s, gi, whh_f, bhh_f, whh_b, bhh_b, T, out, xchg, status);
+  unsigned spin = SPIN_LIMIT;  // test hook: a tiny RVCX_GRU_SPIN_LIMIT forces the timeout path
+  if (const char* e = std::getenv("RVCX_GRU_SPIN_LIMIT")) spin = (unsigned)std::strtoul(e, nullptr, 10);
+  hipLaunchKernelGGL(k_gru_bidir, dim3(4, B), dim3(NT), 0, s, gi, whh_f, bhh_f, whh_b, bhh_b, T, out, xchg, status,
+                     spin);
   return hipGetLastError();
 }
 

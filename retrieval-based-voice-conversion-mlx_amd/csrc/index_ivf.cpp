@@ -40,6 +40,15 @@ struct Reader {
     at += k;
     return r;
   }
+  // `count` elements of `elem` bytes, with the byte count checked against the bytes left (no wrap-around:
+  // counts come from the file and are untrusted)
+  const uint8_t* take_n(uint64_t count, uint64_t elem) {
+    const uint64_t left = (uint64_t)(n - at);
+    if (elem == 0 || count > left / elem)
+      throw Error(RVCX_E_INVALID, "faiss index: truncated at byte " + std::to_string(at) + " (count " +
+                                      std::to_string(count) + " x " + std::to_string(elem) + " B)");
+    return take((int64_t)(count * elem));
+  }
 };
 
 struct Header {
@@ -74,7 +83,8 @@ void upload(DevBuf& b, const T* host, size_t count) {
 
 }  // namespace
 
-void index_load(Ctx& c, const uint8_t* bytes, int64_t nbytes) {
+ParsedIvf parse_ivf(const uint8_t* bytes, int64_t nbytes) {
+  ParsedIvf P;
   Reader r{bytes, nbytes};
   const std::string magic = r.fourcc();
   if (magic != "IwFl") throw Error(RVCX_E_INVALID, "faiss index: fourcc '" + magic + "' is not IndexIVFFlat (IwFl)");
@@ -93,12 +103,13 @@ void index_load(Ctx& c, const uint8_t* bytes, int64_t nbytes) {
   const uint64_t ncent = r.get<uint64_t>();
   if (qh.d != h.d || (uint64_t)qh.ntotal != nlist || ncent != nlist * (uint64_t)h.d)
     throw Error(RVCX_E_INVALID, "faiss index: quantizer shape does not match the IVF header");
-  const float* cent = reinterpret_cast<const float*>(r.take((int64_t)ncent * 4));
+  const float* cent = reinterpret_cast<const float*>(r.take_n(ncent, 4));
+  P.cent.assign(cent, cent + ncent);
   // direct map: type u8, array (u64 count + i64s), [hashtable pairs]
   const uint8_t dm_type = r.get<uint8_t>();
   const uint64_t dm_n = r.get<uint64_t>();
-  r.take((int64_t)dm_n * 8);
-  if (dm_type == 2) r.take((int64_t)r.get<uint64_t>() * 16);
+  r.take_n(dm_n, 8);
+  if (dm_type == 2) r.take_n(r.get<uint64_t>(), 16);
   // inverted lists: ArrayInvertedLists
   const std::string il = r.fourcc();
   if (il != "ilar") throw Error(RVCX_E_INVALID, "faiss index: inverted lists '" + il + "' are not ArrayInvertedLists");
@@ -106,10 +117,13 @@ void index_load(Ctx& c, const uint8_t* bytes, int64_t nbytes) {
   const uint64_t code_size = r.get<uint64_t>();
   if (il_n != nlist || code_size != 4 * (uint64_t)h.d)
     throw Error(RVCX_E_INVALID, "faiss index: inverted list header does not match the IVF header");
+  if (h.ntotal <= 0 || h.ntotal >= (int64_t(1) << 31))
+    throw Error(RVCX_E_INVALID, "faiss index: ntotal " + std::to_string(h.ntotal) + " out of range");
   const std::string kind = r.fourcc();
   const uint64_t cnt = r.get<uint64_t>();
+  const uint8_t* raw_bytes = r.take_n(cnt, 8);  // checked before anything is allocated from cnt
   std::vector<uint64_t> raw(cnt);
-  if (cnt) std::memcpy(raw.data(), r.take((int64_t)cnt * 8), cnt * 8);
+  if (cnt) std::memcpy(raw.data(), raw_bytes, cnt * 8);
   std::vector<uint64_t> sizes(nlist, 0);
   if (kind == "full") {
     if (cnt != nlist) throw Error(RVCX_E_INVALID, "faiss index: list size count mismatch");
@@ -123,40 +137,60 @@ void index_load(Ctx& c, const uint8_t* bytes, int64_t nbytes) {
   } else {
     throw Error(RVCX_E_INVALID, "faiss index: unknown list size encoding '" + kind + "'");
   }
-  std::vector<long long> off(nlist + 1, 0);
-  for (uint64_t l = 0; l < nlist; ++l) off[l + 1] = off[l] + (long long)sizes[l];
+  // list sizes are untrusted: bound each by ntotal and the running sum step by step (no wrap-around)
+  std::vector<long long>& off = P.off;
+  off.assign(nlist + 1, 0);
+  const uint64_t ntot_u = (uint64_t)h.ntotal;
+  uint64_t acc = 0;
+  for (uint64_t l = 0; l < nlist; ++l) {
+    if (sizes[l] > ntot_u || acc + sizes[l] > ntot_u)
+      throw Error(RVCX_E_INVALID, "faiss index: inverted list " + std::to_string(l) + " size exceeds ntotal");
+    acc += sizes[l];
+    off[l + 1] = (long long)acc;
+  }
   const long long ntotal = off[nlist];
   if (ntotal != h.ntotal) throw Error(RVCX_E_INVALID, "faiss index: ntotal does not match the inverted lists");
-  if (ntotal <= 0) throw Error(RVCX_E_INVALID, "faiss index: empty index");
-  std::vector<float> vecs((size_t)ntotal * h.d);
-  std::vector<long long> ids((size_t)ntotal);
+  std::vector<float>& vecs = P.vecs;
+  std::vector<long long>& ids = P.ids;
+  vecs.resize((size_t)ntotal * h.d);
+  ids.resize((size_t)ntotal);
   for (uint64_t l = 0; l < nlist; ++l) {
     const uint64_t s = sizes[l];
     if (!s) continue;
-    std::memcpy(vecs.data() + (size_t)off[l] * h.d, r.take((int64_t)(s * code_size)), s * code_size);
-    std::memcpy(ids.data() + off[l], r.take((int64_t)s * 8), s * 8);
+    std::memcpy(vecs.data() + (size_t)off[l] * h.d, r.take_n(s, code_size), s * code_size);
+    std::memcpy(ids.data() + off[l], r.take_n(s, 8), s * 8);
   }
   // reconstruct_n(0, ntotal) semantics: row id <- the stored vector with that id. RVC indexes hold ids
   // 0..ntotal-1 (sequential add, extract_index.py:66-68); anything else is refused.
-  std::vector<int> slot((size_t)ntotal, -1);
+  std::vector<int>& slot = P.slot;
+  slot.assign((size_t)ntotal, -1);
   for (long long i = 0; i < ntotal; ++i) {
     const long long id = ids[i];
     if (id < 0 || id >= ntotal || slot[id] >= 0)
       throw Error(RVCX_E_INVALID, "faiss index: ids are not a permutation of 0..ntotal-1");
     slot[id] = (int)i;
   }
+  P.d = h.d;
+  P.nlist = (long long)nlist;
+  P.ntotal = ntotal;
+  P.nprobe = (int)std::max<uint64_t>(1, std::min<uint64_t>(nprobe, nlist));
+  return P;
+}
+
+void index_load(Ctx& c, const uint8_t* bytes, int64_t nbytes) {
+  const ParsedIvf P = parse_ivf(bytes, nbytes);
   auto ix = std::make_unique<IvfIndex>();
   RVCX_HIP(hipSetDevice(c.device));
-  upload(ix->cent, cent, (size_t)ncent);
-  upload(ix->vecs, vecs.data(), vecs.size());
-  upload(ix->off, off.data(), off.size());
-  upload(ix->ids, ids.data(), ids.size());
-  upload(ix->slot_of_id, slot.data(), slot.size());
+  upload(ix->cent, P.cent.data(), P.cent.size());
+  upload(ix->vecs, P.vecs.data(), P.vecs.size());
+  upload(ix->off, P.off.data(), P.off.size());
+  upload(ix->ids, P.ids.data(), P.ids.size());
+  upload(ix->slot_of_id, P.slot.data(), P.slot.size());
   IvfView& v = ix->view;
-  v.d = h.d;
-  v.nlist = (long long)nlist;
-  v.ntotal = ntotal;
-  v.nprobe = (int)std::max<uint64_t>(1, std::min<uint64_t>(nprobe, nlist));
+  v.d = P.d;
+  v.nlist = P.nlist;
+  v.ntotal = P.ntotal;
+  v.nprobe = P.nprobe;
   v.cent = static_cast<const float*>(ix->cent.p);
   v.vecs = static_cast<const float*>(ix->vecs.p);
   v.off = static_cast<const long long*>(ix->off.p);

@@ -109,6 +109,14 @@ struct Ctx {
   hipStream_t aux_stream();
   // issued by RMVPE's E2E right before the BiGRU launch (host callback, cleared when taken)
   std::function<void(hipStream_t)> before_gru;
+  // device-side fault flags in pinned host-mapped memory (bit 0: a BiGRU partner hand-off timed out).
+  // Kernels store into it; the host reads it after a synchronisation: every compute entry point checks
+  // it on entry (faults of earlier, completed calls), the pipeline at its own sync points, and
+  // rvcx_device_status after synchronising the caller's stream.
+  unsigned* status_host = nullptr;
+  unsigned* status_dev = nullptr;
+  unsigned* device_status();
+  void check_device_status();  // throws Error(RVCX_E_HIP, ...) and clears the flags when any is set
   ~Ctx();
 
   float* W(const std::string& name) const;
@@ -185,6 +193,14 @@ void rt_process(Ctx& c, RtState& s, const float* in48, const int32_t* sids, cons
                 const float* eps_z, const float* eps_src, uint64_t seed, float* out48, float* vol_out, int* offs_out,
                 hipStream_t st);
 // index (index_ivf.cpp)
+struct ParsedIvf {  // a validated faiss IndexIVFFlat image on the host (lists in list order)
+  int d = 0, nprobe = 1;
+  long long nlist = 0, ntotal = 0;
+  std::vector<float> cent, vecs;
+  std::vector<long long> off, ids;
+  std::vector<int> slot;  // id -> slot
+};
+ParsedIvf parse_ivf(const uint8_t* bytes, int64_t nbytes);  // host only; throws Error(RVCX_E_INVALID)
 void index_load(Ctx& c, const uint8_t* bytes, int64_t nbytes);
 void index_search(Ctx& c, const float* x, int64_t n, int k, float* dist, int64_t* ids, hipStream_t s);
 void index_retrieve(Ctx& c, const float* feats, int64_t L, int d, double index_rate, float* out, hipStream_t s);

@@ -650,8 +650,7 @@ static void e2e_chunk(Ctx& c, float* img, int Fc, float* sal, hipStream_t s, int
   run1(c, lin(feat, 3 * NMEL, B * Fc, 3 * NMEL, c.W("rm.gru.wih"), 6 * GRU_H, c.W("rm.gru.bih"), gi, 6 * GRU_H), s);
   float* go = c.buf<float>("rm.gruout", (size_t)B * Fc * 2 * GRU_H, s);
   unsigned long long* xchg = c.buf<unsigned long long>("rm.xchg", gru_xchg_words(B), s);
-  unsigned* status = c.buf<unsigned>("rm.status", 4, s);
-  RVCX_HIP(hipMemsetAsync(status, 0, sizeof(unsigned), s));
+  unsigned* status = c.device_status();  // sticky until the host reads it (Ctx::check_device_status)
   if (c.before_gru) {  // work the caller wants issued beside the BiGRU (which occupies 4 CUs)
     auto hook = std::move(c.before_gru);
     c.before_gru = nullptr;

@@ -195,6 +195,7 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
     if (nts > 0) {
       RVCX_HIP(hipMemcpyAsync(opt_ts.data(), dts, sizeof(long long) * nts, hipMemcpyDeviceToHost, s));
       RVCX_HIP(hipStreamSynchronize(s));
+      c.check_device_status();
     }
   }
   // 3. chunk plan (pipeline.py:486-512): [a0, a1) samples and [f_lo, f_hi) pitch frames per chunk
@@ -273,6 +274,7 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
     std::vector<double> h(F);
     RVCX_HIP(hipMemcpyAsync(h.data(), f0, sizeof(double) * F, hipMemcpyDeviceToHost, s));
     RVCX_HIP(hipStreamSynchronize(s));
+    c.check_device_status();
     shift_semitones = o.pitch + proposed_key(h, o.proposed_pitch_threshold);
   }
   int32_t* pitch = c.buf<int32_t>("pl.pitch", (size_t)F, s);
@@ -358,6 +360,7 @@ int64_t pipeline_forward_batch(Ctx& c, const double* audio, int64_t n, int64_t l
     std::vector<double> h((size_t)B * F);
     RVCX_HIP(hipMemcpyAsync(h.data(), f0, sizeof(double) * h.size(), hipMemcpyDeviceToHost, s));
     RVCX_HIP(hipStreamSynchronize(s));
+    c.check_device_status();
     for (int b = 0; b < B; ++b) {
       std::vector<double> one(h.begin() + (size_t)b * F, h.begin() + (size_t)(b + 1) * F);
       shift[b] = o.pitch + proposed_key(one, o.proposed_pitch_threshold);

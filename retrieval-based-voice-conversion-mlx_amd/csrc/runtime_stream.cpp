@@ -233,6 +233,7 @@ void rt_process(Ctx& c, RtState& s, const float* in48, const int32_t* sids, cons
     std::vector<double> h((size_t)B * F);
     RVCX_HIP(hipMemcpyAsync(h.data(), f0, sizeof(double) * h.size(), hipMemcpyDeviceToHost, st));
     RVCX_HIP(hipStreamSynchronize(st));
+    c.check_device_status();
     for (int b = 0; b < B; ++b) {
       std::vector<double> one(h.begin() + (size_t)b * F, h.begin() + (size_t)(b + 1) * F);
       fac[b] = std::pow(2.0, (o.f0_up_key + proposed_key(one, o.proposed_pitch_threshold)) / 12.0);

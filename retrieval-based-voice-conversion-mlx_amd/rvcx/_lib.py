@@ -27,7 +27,7 @@ EXPORTS = [
     "rvcx_index_unload", "rvcx_index_info", "rvcx_index_set_nprobe", "rvcx_index_search", "rvcx_index_reconstruct_n",
     "rvcx_index_retrieve", "rvcx_rt_default_desc", "rvcx_rt_default_opts", "rvcx_rt_create", "rvcx_rt_destroy",
     "rvcx_rt_geometry", "rvcx_rt_reset", "rvcx_rt_process", "rvcx_hubert_batch", "rvcx_rmvpe_batch",
-    "rvcx_pipeline_batch", "rvcx_set_highpass_sos", "rvcx_highpass_pad",
+    "rvcx_pipeline_batch", "rvcx_set_highpass_sos", "rvcx_highpass_pad", "rvcx_device_status", "rvcx_index_parse",
 ]
 
 
@@ -142,6 +142,8 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "rvcx_rt_geometry": (i32, [vp, P(i64)]),
         "rvcx_rt_reset": (i32, [vp, vp, vp]),
         "rvcx_rt_process": (i32, [vp, vp, vp, P(ctypes.c_int32), P(RtOpts), vp, vp, u64, vp, vp, vp, vp]),
+        "rvcx_device_status": (i32, [vp, vp]),
+        "rvcx_index_parse": (i32, [vp, i64, P(i64), P(i64), P(i64), P(i64), ctypes.c_char_p, i64]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(lib, name):  # reported by exported_symbols(); an older build lacks newer entry points
@@ -158,3 +160,16 @@ def exported_symbols(path: Optional[str] = None):
     """Names of the C-ABI entry points that resolve in the library (no compute call)."""
     lib = load(path)
     return [n for n in EXPORTS if hasattr(lib, n)]
+
+
+def index_parse(data: bytes) -> dict:
+    """Validate a faiss IndexIVFFlat file image on the host (rvcx_index_parse; no context, no GPU).
+    Returns dict(d, ntotal, nlist, nprobe); raises RvcxError for anything the loader would refuse."""
+    lib = load()
+    buf = ctypes.create_string_buffer(bytes(data), len(data))
+    v = [ctypes.c_int64(0) for _ in range(4)]
+    err = ctypes.create_string_buffer(512)
+    rc = lib.rvcx_index_parse(buf, len(data), *[ctypes.byref(x) for x in v], err, 512)
+    if rc != 0:
+        raise RvcxError(rc, err.value.decode(errors="replace"))
+    return dict(zip(("d", "ntotal", "nlist", "nprobe"), (x.value for x in v)))

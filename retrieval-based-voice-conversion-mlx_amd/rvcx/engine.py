@@ -56,6 +56,11 @@ class Engine:
             msg = self.lib.rvcx_last_error(self.ctx)
             raise _lib.RvcxError(rc, f"{what}: {msg.decode() if msg else ''}")
 
+    def check_device_status(self):
+        """Synchronise the current stream and raise RvcxError(RVCX_E_HIP) if a kernel of an earlier call raised
+        a device-side fault flag (e.g. the RMVPE BiGRU hand-off timed out: that call's outputs are invalid)."""
+        self._check(self.lib.rvcx_device_status(self.ctx, self.stream()), "device status")
+
     def stream(self) -> int:
         return self.torch.cuda.current_stream(self.device).cuda_stream
 

@@ -59,3 +59,26 @@ def engine(synth_w, hubert_w, rmvpe_w):
     e.load_rmvpe(rmvpe_w)
     yield e
     e.close()
+
+
+def fixture_noise(g):
+    """The reference run's injected noise of a fixture that stores only its seed (make_golden.NoiseStream:
+    PCG64 standard normals as float32, eps_z then eps_src), flattened to the device layout ([192*T], [T*upp])."""
+    import numpy as np
+
+    rng = np.random.Generator(np.random.PCG64(int(g["noise_seed"])))
+    ez = rng.standard_normal(tuple(g["eps_z_shape"])).astype(np.float32)
+    es = rng.standard_normal(tuple(g["eps_src_shape"])).astype(np.float32)
+    s = g["eps_sum"]
+    assert abs(float(ez.astype(np.float64).sum()) - s[0]) < 1e-6 * max(1.0, abs(s[0]))
+    assert abs(float(es.astype(np.float64).sum()) - s[1]) < 1e-6 * max(1.0, abs(s[1]))
+    return ez.reshape(-1), es.reshape(-1)
+
+
+def c2_audio(name):
+    """The 13.5 s input of pipeline_c2_<name>.npz: the reference's ios_test_data clip or the bench clip."""
+    import numpy as np
+
+    if name == "ios":
+        return golden("ios_kat.npz")["input_audio"].astype(np.float64)
+    return golden("pipeline_c2_synth.npz")["audio32"].astype(np.float64)

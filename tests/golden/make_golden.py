@@ -1,6 +1,7 @@
 """Generate golden vectors by running the REFERENCE implementation (survey container only).
 
 Run:  python tests/golden/make_golden.py        (needs /root/reference; never on the GPU box)
+      python tests/golden/make_golden.py --only-c2   (only the full-size C2 pipeline fixtures)
 
 What it does (SURVEY.md Appendix C recipe):
   1. import transformers first, then stub the modules the reference imports but the
@@ -133,6 +134,74 @@ def build_rmvpe_state():
     return model.eval(), sd
 
 
+class Recorder(torch.nn.Module):
+    """HuBERT wrapper for the reference pipeline that keeps last_hidden_state of every call."""
+
+    def __init__(self, m):
+        super().__init__()
+        self.m = m
+        self.out = []
+
+    def forward(self, x):
+        r = self.m(x)
+        self.out.append(r["last_hidden_state"].detach().numpy().copy())
+        return r
+
+
+def c2_fixtures(hub, net, scratch):
+    """The headline config C2 at full size: the reference Pipeline.pipeline
+    (rvc/infer/pipeline.py:390-558, x_pad=1, one chunk) on the 13.5 s clips
+      * ios: the reference's own real-speech clip ios_test_data/input_audio.npy (216100 samples), and
+      * synth: the bench's C2 clip (rvcx.synthetic.speech_like(216100, seed=1000), rounded to float32
+        values so the fixture is exact and small),
+    with seeded noise. Saved per clip: the final output, the RMVPE f0 and get_f0's (pitch, pitchf), the
+    HuBERT features (fp16, for the staged test) and the noise seed; the noise itself is regenerated from
+    the seed (NoiseStream: PCG64 standard normals, eps_z [1,192,T] then eps_src [1,T*480,1])."""
+    import rvc.infer.pipeline as rpipe
+    from rvc.infer.pipeline import Pipeline
+
+    class Cfg:
+        x_pad, x_query, x_center, x_max, device = 1, 6, 38, 41, "cpu"
+
+    clips = {
+        "ios": np.load(os.path.join(REF, "ios_test_data", "input_audio.npy")).astype(np.float64),
+        "synth": synthetic.speech_like(216100, seed=1000).astype(np.float32).astype(np.float64),
+    }
+    for k, (name, audio) in enumerate(clips.items()):
+        pipe = Pipeline(48000, Cfg())
+        rec = Recorder(hub)
+        got = {}
+        orig_get_f0 = rpipe.Pipeline.get_f0
+
+        def get_f0(self, *a, **kw):
+            c, f = orig_get_f0(self, *a, **kw)
+            got["pitch"], got["pitchf"] = np.array(c), np.array(f)
+            return c, f
+
+        seed = SEEDS["noise"] + 100 + k
+        ns = NoiseStream(seed)
+        orig = torch.randn_like
+        torch.randn_like = ns
+        rpipe.Pipeline.get_f0 = get_f0
+        try:
+            outp = pipe.pipeline(rec, net, 0, audio.copy(), 0, "rmvpe", "", 0.0, True, 1.0, "v2", 0.33,
+                                 False, 1.0, False, 155.0)
+        finally:
+            torch.randn_like = orig
+            rpipe.Pipeline.get_f0 = orig_get_f0
+        assert len(rec.out) == 1 and len(ns.draws) == 2, "expected one chunk"
+        extra = {"audio32": audio.astype(np.float32)} if name == "synth" else {}
+        np.savez_compressed(
+            os.path.join(OUT, f"pipeline_c2_{name}.npz"), out=np.asarray(outp, np.float32),
+            f0_raw=got["pitchf"].astype(np.float64), pitch=got["pitch"].astype(np.int64),
+            feats16=rec.out[0][0].astype(np.float16), noise_seed=np.int64(seed),
+            eps_z_shape=np.array(ns.draws[0].shape), eps_src_shape=np.array(ns.draws[1].shape),
+            eps_sum=np.array([float(ns.draws[0].astype(np.float64).sum()), float(ns.draws[1].astype(np.float64).sum())]),
+            **extra)
+        print(f"pipeline_c2_{name}:", np.shape(outp), "voiced", int((got["pitchf"] > 0).sum()),
+              "feats", rec.out[0].shape)
+
+
 def main():
     install_stubs()
     sys.path.insert(0, REF)
@@ -144,8 +213,16 @@ def main():
     rng = np.random.Generator(np.random.PCG64(SEEDS["inputs"]))
     meta = {"seeds": SEEDS, "torch": torch.__version__, "transformers": transformers.__version__}
 
-    # ---------------- synthesizer at T=64 frames (module outputs) ----------------
+    only_c2 = "--only-c2" in sys.argv
     net = build_synth()
+    if only_c2:
+        hub = build_hubert()
+        e2e, rsd = build_rmvpe_state()
+        torch.save(rsd, os.path.join(scratch, "rvc", "models", "predictors", "rmvpe.pt"))
+        c2_fixtures(hub, net, scratch)
+        return
+
+    # ---------------- synthesizer at T=64 frames (module outputs) ----------------
     T = 64
     phone = rng.standard_normal((1, T, 768)).astype(np.float32)
     f0 = synthetic.f0_walk(1, T, seed=SEEDS["inputs"])

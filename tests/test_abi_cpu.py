@@ -39,3 +39,65 @@ def test_engine_refuses_without_gpu():
         pytest.skip("GPU present")
     with pytest.raises(RuntimeError):
         Engine(0)
+
+
+def _ivf_bytes(nlist=4, direct_map=0):
+    import numpy as np
+
+    from oracle import ivf
+
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((300, 64)).astype(np.float32)
+    return ivf.write_ivfflat(ivf.build_ivfflat(x, nlist=nlist, nprobe=2), sparse=False, direct_map=direct_map)
+
+
+def test_index_parse_accepts_a_valid_file():
+    """rvcx_index_parse (host only, the parser rvcx_index_load runs) on a well-formed IndexIVFFlat image."""
+    from rvcx import _lib
+
+    info = _lib.index_parse(_ivf_bytes())
+    assert info == {"d": 64, "ntotal": 300, "nlist": 4, "nprobe": 2}
+
+
+def test_index_parse_rejects_wrapping_list_sizes():
+    """List sizes are untrusted: sizes whose sum wraps around 2^64 to ntotal, and whose byte counts
+    (size * code_size) wrap to the true byte counts, must be refused (they would drive the device scan
+    over ~2^63 rows)."""
+    import struct
+
+    from rvcx import _lib
+
+    buf = bytearray(_ivf_bytes())
+    at = buf.index(b"full") + 4
+    (cnt,) = struct.unpack_from("<Q", buf, at)
+    sizes = list(struct.unpack_from(f"<{cnt}Q", buf, at + 8))
+    evil = list(sizes)
+    evil[0] = (sizes[0] + (1 << 63)) % (1 << 64)
+    evil[1] = (sizes[1] + (1 << 63)) % (1 << 64)
+    assert sum(evil) % (1 << 64) == sum(sizes)  # the wrapped total still matches ntotal
+    struct.pack_into(f"<{cnt}Q", buf, at + 8, *evil)
+    with pytest.raises(_lib.RvcxError) as e:
+        _lib.index_parse(bytes(buf))
+    assert e.value.code == -1 and "exceeds ntotal" in str(e.value)
+
+
+def test_index_parse_rejects_huge_counts():
+    """A direct-map or size-vector count whose byte size wraps (count * 8 == 0 mod 2^64) is refused before
+    anything is allocated from it."""
+    import struct
+
+    from rvcx import _lib
+
+    buf = bytearray(_ivf_bytes(direct_map=1))
+    # the direct map follows the quantizer: fourcc, header (33 B), centroid count u64, centroids [4][64] f32
+    at = buf.index(b"IxF2") + 4 + 33 + 8 + 4 * 64 * 4
+    assert buf[at] == 1 and struct.unpack_from("<Q", buf, at + 1)[0] == 300
+    struct.pack_into("<Q", buf, at + 1, 1 << 61)
+    with pytest.raises(_lib.RvcxError) as e:
+        _lib.index_parse(bytes(buf))
+    assert e.value.code == -1 and "truncated" in str(e.value)
+    buf = bytearray(_ivf_bytes())
+    at = buf.index(b"full") + 4
+    struct.pack_into("<Q", buf, at, (1 << 61) + 4)
+    with pytest.raises(_lib.RvcxError):
+        _lib.index_parse(bytes(buf))
