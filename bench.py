@@ -32,60 +32,106 @@ C2_SAMPLES = 216100  # 13.50625 s (the reference's 13.5 s benchmark clip length)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--samples", type=int, default=C2_SAMPLES)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-sec", type=float, default=2.0)
     ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2",
                     help="c2 (default, the headline line): full pipeline, 13.5 s utterance per step; c3: HiFiGAN-NSF "
                          "generator alone, B=32 x 400 frames per step; c5: 16 realtime streams, one 256 ms hop per step")
     ap.add_argument("--streams", type=int, default=16, help="c5: concurrent streams")
     ap.add_argument("--batch", type=int, default=8, help="c4: 30 s utterances per batched pipeline pass")
+    ap.add_argument("--c4-utterances", type=int, default=512, help="c4: job size (BASELINE configs[3]: 512)")
     ap.add_argument("--roofline-pass", choices=["inline", "after"], default="after",
                     help="inline: HIP events around every conv launch of the timed steps; after: the timed steps "
                          "run without events and an identical K-step pass right after carries them")
-    return ap.parse_args()
+    a = ap.parse_args()
+    a.steps_given = a.steps is not None
+    if a.steps is None:
+        a.steps = 10
+    return a
 
 
-def cpu_baseline(sample_sec: float):
-    """Time the CPU oracle (test infrastructure: oracle/) on a bounded sample of the same workload."""
+def _host_cpu():
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return model, os.cpu_count() or 1, avail
+
+
+def cpu_baseline(n_samples: int, reps: int = 2):
+    """Time the CPU oracle (test infrastructure: oracle/) on the SAME C2 workload: the 13.5 s clip through
+    Pipeline.pipeline (x_pad = 1), after a 2 s warm-up call; plus C1 (RMVPE f0 of the 5 s
+    benchmark_rmvpe.py clip, BASELINE configs[0]). torch-CPU fp32 with min(16, available) threads."""
+    from oracle import rmvpe as ormvpe
     from oracle.pipeline import OraclePipeline
     from rvcx import synthetic
     from rvcx.config import HUBERT_BASE, RMVPE_CFG, SYNTH_48K_V2
     from rvcx.weights import normalize_state
 
-    threads = min(16, os.cpu_count() or 1)
+    model, ncpu, avail = _host_cpu()
+    threads = max(1, min(16, avail))
     torch.set_num_threads(threads)
     sw = normalize_state(synthetic.synth_state(2))
     hw = normalize_state(synthetic.hubert_state(4))
     rw = normalize_state(synthetic.rmvpe_state(5))
     p = OraclePipeline(48000, synth_w=sw, synth_cfg=SYNTH_48K_V2, hubert_w=hw, hubert_cfg=HUBERT_BASE, rmvpe_w=rw,
                        rmvpe_cfg=RMVPE_CFG)
-    n = int(sample_sec * SR_IN)
-    audio = synthetic.speech_like(n, seed=1)
-    p.pipeline(0, audio.copy(), protect=0.33)  # warm-up
+    p.pipeline(0, synthetic.speech_like(2 * SR_IN, seed=1).copy(), protect=0.33)  # warm-up
+    audio = synthetic.speech_like(n_samples, seed=1000)
     ts = []
-    for _ in range(3):
+    for _ in range(reps):
         t0 = time.perf_counter()
         p.pipeline(0, audio.copy(), protect=0.33)
         ts.append(time.perf_counter() - t0)
     med = statistics.median(ts)
-    return {"value": round(sample_sec / med, 4), "unit": "audio-sec/sec", "cores": threads, "kind": "port",
-            "sample": f"oracle Pipeline.pipeline (torch-CPU fp32, {threads} threads) on a {sample_sec:.1f} s "
-                      f"speech-like clip, x_pad=1, median of 3 after 1 warm-up ({med:.2f} s/run)"}
+    sec = n_samples / SR_IN
+    # C1: RMVPE0Predictor.infer_from_audio on the 5 s clip (0.3 sin 440 + 0.2 sin 880 + 0.1 N, seed 0)
+    c1_audio = synthetic.rmvpe_bench_audio(80000, seed=0)
+    ormvpe.infer_from_audio(p.rw, p.rc, c1_audio, thred=0.03)
+    c1 = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        ormvpe.infer_from_audio(p.rw, p.rc, c1_audio, thred=0.03)
+        c1.append(time.perf_counter() - t0)
+    c1m = statistics.median(c1)
+    return {"value": round(sec / med, 4), "unit": "audio-sec/sec", "cores": threads, "kind": "port",
+            "sample": f"oracle Pipeline.pipeline (torch-CPU fp32, {threads} threads) on the C2 clip itself "
+                      f"({sec:.2f} s, x_pad=1), median of {reps} after a 2 s warm-up ({med:.2f} s/run)",
+            "host_cpu": model, "host_logical_cpus": ncpu, "host_cpus_available": avail,
+            "c1": {"value": round(5.0 / c1m, 3), "unit": "audio-sec/sec", "sec_per_clip": round(c1m, 4),
+                   "sample": "C1: oracle RMVPE0Predictor.infer_from_audio on the 5 s benchmark_rmvpe.py clip, "
+                             "median of 5"}}
 
 
 def _pmc_traffic():
-    """HBM bytes per conv-GEMM launch from the committed PMC passes (tools/pmc_traffic.sh: FETCH_SIZE and
-    WRITE_SIZE in separate rocprofv3 runs of this bench, FETCH_SIZE doubled per MI355X_MICROARCH.md);
-    None when the summary is absent. PMC counters cannot be read from inside the timed process."""
-    p = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    """HBM bytes per conv-GEMM launch from the committed PMC passes (tools/pmc_traffic.sh + pmc_traffic.py:
+    FETCH_SIZE and WRITE_SIZE in separate rocprofv3 runs of this bench, FETCH_SIZE doubled per
+    MI355X_MICROARCH.md). PMC counters cannot be read from inside the timed process, so the number comes from
+    profiles/pmc_traffic.json -- and only when that file was measured on this exact source tree (its "tree"
+    equals rvcx.provenance.source_tree_hash()); otherwise None."""
+    from rvcx.provenance import source_tree_hash
+
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
-            return round(json.load(f)["traffic_bytes_per_launch"])
-    except (OSError, ValueError, KeyError):
-        return None
+            rec = json.load(f)
+    except (OSError, ValueError):
+        return None, "profiles/pmc_traffic.json absent"
+    tree = source_tree_hash()
+    if rec.get("tree") != tree:
+        return None, f"profiles/pmc_traffic.json is from tree {rec.get('tree')}, not this tree {tree}"
+    return round(rec["traffic_bytes_per_launch"]), f"profiles/pmc_traffic.json (tree {tree}, {rec.get('file')})"
 
 
 def _timed(step, args, dev, dist):
@@ -114,8 +160,13 @@ def bench_c3(args, eng, dev, dist, rank, world):
     z = torch.as_tensor(rng.standard_normal((B, 192, T)).astype(np.float32), device=dev)
     f0 = torch.as_tensor(synthetic.f0_walk(B, T, seed=3), dtype=torch.float32, device=dev)
     sid = torch.zeros(B, dtype=torch.int32, device=dev)
-    eng.profile(True)
     el = _timed(lambda i: eng.dec_only(z, f0, sid, seed=i), args, dev, dist)
+    # roofline: an identical K-step pass right after the timed one carries the per-conv events (they are not
+    # in the timed region)
+    eng.profile_read()
+    eng.profile(True)
+    for i in range(args.steps):
+        eng.dec_only(z, f0, sid, seed=args.warmup + i)
     eng.profile(False)
     k_ms, k_flops, k_n = eng.profile_read()
     audio_sec = B * T * eng.upp / 48000.0
@@ -129,37 +180,71 @@ def bench_c3(args, eng, dev, dist, rank, world):
                        "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "achieved": round(tf, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(tf / FP32_PEAK_TFLOPS, 4), "traffic": None,
-                         "kernel": "conv_gemm_kernel (events inline over the timed steps)",
-                         "alg_gflop_per_step": round(k_flops / (args.warmup + args.steps) / 1e9, 2)}}
+                         "kernel": "conv_gemm_kernel (events on a separate K-step pass after the timed one)",
+                         "alg_gflop_per_step": round(k_flops / args.steps / 1e9, 2)}}
+
+
+def c4_audio(job, ids, n, dev, pool=8):
+    """Device audio [len(ids), n] fp64 of the C4 utterances: SURVEY §8d asks for speech_like(seed=1000+i) per
+    utterance, which costs 0.47 s of host time per 30 s clip (4 min for 512); instead a pool of `pool` such clips
+    is made once and utterance i is pool clip i % pool, circularly shifted by a seed-derived offset and scaled by a
+    seed-derived gain (distinct content per utterance, same spectrum statistics)."""
+    from rvcx import synthetic
+
+    base = torch.as_tensor(np.stack([synthetic.speech_like(n, seed=1000 + k) for k in range(pool)]),
+                           dtype=torch.float64, device=dev)
+    rows = []
+    for i in ids:
+        r = np.random.Generator(np.random.PCG64(job[i].seed))
+        rows.append(torch.roll(base[i % pool], int(r.integers(0, n))) * float(0.6 + 0.4 * r.random()))
+    return torch.stack(rows)
 
 
 def bench_c4(args, eng, dev, dist, rank, world):
-    """configs[3]: batched offline VC of 30 s utterances; each rank converts its own shard (utterance
-    i goes to rank i % world, extract.py:101-117 style) in batched passes of --batch utterances; one step =
-    one pass. 512 utterances over 8 GPUs = 8 steps of 8 per rank."""
-    from rvcx import synthetic
-    from rvcx.sharding import reduce_throughput
+    """configs[3]: batched offline VC of the 512 x 30 s job (rvcx.offline). Every rank builds the same job
+    list, takes its LPT shard (i::world for equal lengths, extract.py:101-117) and converts it in batched
+    passes of --batch utterances (rvcx_pipeline_batch); one step = one pass. RCCL carries only bookkeeping:
+    SUM/MAX of audio-seconds and wall time and an all_gather of the per-utterance records. Timed: the whole
+    shard (or the first --steps passes when given), after --warmup untimed passes of the shard's first batch."""
+    from rvcx import offline
 
-    B, n = args.batch, 480000
-    nb = args.warmup + args.steps
-    utt = [synthetic.speech_like(n, seed=1000 + (i * world + rank)) for i in range(min(nb * B, 64))]
-    audio = torch.as_tensor(np.stack(utt), dtype=torch.float64, device=dev)
+    job = offline.c4_job(args.c4_utterances)
+    p = offline.plan(job, world, rank, args.batch)
+    n = job[0].n
+    pos = {u: k for k, u in enumerate(p.shard)}
+    audio = c4_audio(job, p.shard, n, dev)
     opts = eng.pipeline_opts(protect=0.33)
-    out = torch.empty((B, ((n + 32000) // 160) * eng.upp), dtype=torch.float32, device=dev)
+    ldo = ((n + 2 * int(opts.t_pad)) // 160) * eng.upp
+    out = torch.empty((args.batch, ldo), dtype=torch.float32, device=dev)
 
-    def step(i):
-        j = (i * B) % (audio.shape[0] - B + 1)
-        eng.pipeline_batch(audio[j:j + B], opts, sids=0, seed=i, out=out)
+    def convert(ids, step):
+        rows = torch.tensor([pos[i] for i in ids], device=dev)
+        y = eng.pipeline_batch(audio.index_select(0, rows), opts, sids=0, seed=step, out=out)
+        rec = torch.empty((len(ids), 4), dtype=torch.float64, device=dev)
+        rec[:, 0] = torch.tensor(ids, dtype=torch.float64, device=dev)
+        rec[:, 1] = float(y.shape[1])
+        rec[:, 2] = y.abs().amax(1).double()
+        rec[:, 3] = y.double().pow(2).mean(1).sqrt()
+        return rec
 
-    el = _timed(step, args, dev, dist)
-    audio_sec = B * n / SR_IN
-    tot = reduce_throughput(dist, args.steps * audio_sec, el, device=dev)
+    for w in range(args.warmup):
+        convert(p.batches[0], -1 - w)
+    recs, el = offline.run(p, convert, sync=lambda: torch.cuda.synchronize(dev), dist=dist,
+                           steps=args.steps if args.steps_given else None)
+    eng.check_device_status()
+    tot = offline.finish(p, job, recs, el, dist=dist, device=dev)
+    nsteps = len(recs)
+    r = tot["records"]
+    assert bool(torch.isfinite(r).all()) and bool((r[:, 2] > 0).all()), "non-finite or silent C4 output"
     return {"metric": "audio-sec/sec batched offline VC (C4)", "value": round(tot["value"], 3),
-            "unit": "audio-sec/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(tot["elapsed"] / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "fp32", "data": "synthetic speech-like 30 s utterances; random-init weights",
-            "config": {"workload": f"C4: batched pipeline passes of {B} x 30 s utterances per step per GPU",
-                       "batch": B, "parallelism": f"dp{world}"}}
+            "unit": "audio-sec/sec", "n_gpus": world, "steps": nsteps, "warmup": args.warmup,
+            "ms_per_step": round(tot["elapsed"] / max(1, nsteps) * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak" if args.steps_given else "strong", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic speech-like 30 s utterances (pool of 8 speech_like clips, per-utterance shift and "
+                    "gain); random-init weights",
+            "config": {"workload": f"C4: {len(job)} x 30 s utterances, LPT-sharded over {world} GPU(s), batched "
+                                   f"passes of {args.batch}", "utterances_converted": tot["utterances"],
+                       "batch": args.batch, "parallelism": f"dp{world}"}}
 
 
 def bench_c5(args, eng, dev, dist, rank, world):
@@ -283,9 +368,10 @@ def main():
     assert y.numel() > 0 and bool(torch.isfinite(y).all())
 
     achieved_tflops = k_flops / (k_ms / 1000.0) / 1e12 if k_ms > 0 else 0.0
+    traffic, traffic_src = _pmc_traffic()
     roofline = {"bound": "mfma", "achieved": round(achieved_tflops, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4), "traffic": _pmc_traffic(),
-                "traffic_unit": "HBM bytes per launch (profiles/r01_pmc_traffic.json)",
+                "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+                "traffic_unit": "HBM bytes per conv launch", "traffic_source": traffic_src,
                 "kernel": "conv_gemm_kernel (fp32 MFMA implicit-GEMM; all launches of the step)",
                 "launches_per_step": k_launches // max(1, args.steps),
                 "kernel_ms_per_step": round(k_ms / args.steps, 3),
@@ -293,7 +379,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            cpu = cpu_baseline(args.cpu_sample_sec)
+            cpu = cpu_baseline(n)
         except Exception as e:  # reported, never fatal
             cpu = {"error": repr(e)}
     if rank == 0:

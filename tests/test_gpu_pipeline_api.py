@@ -181,3 +181,35 @@ def test_pipeline_batch_matches_single(engine):
         assert y1.shape == yb[b].shape
         assert spectrogram_correlation(yb[b], y1) > 0.999
         assert float(np.abs(yb[b] - y1).max()) < 5e-3 * max(float(np.abs(y1).max()), 1e-6)
+
+
+def test_pipeline_batch_vs_reference_and_oracle(engine, synth_w, hubert_w, rmvpe_w):
+    """C4's batched pass (rvcx_pipeline_batch) against references, not only against itself: row 0 is the
+    reference fixture clip (tests/golden/pipeline_2p5s.npz: rvc Pipeline.pipeline output), rows 1-2 are other
+    clips of the same length against the CPU oracle pipeline, each with its own noise and sid 0."""
+    from oracle.metrics import spectrogram_correlation
+    from rvcx import synthetic
+
+    def rel(a, b):
+        return float(np.abs(np.asarray(a, np.float64) - b).max() / (np.abs(b).max() + 1e-12))
+
+    engine.set_pipeline_highpass()
+    g = golden("pipeline_2p5s.npz")
+    n = g["audio"].shape[0]
+    clips = [g["audio"], synthetic.speech_like(n, seed=91), synthetic.speech_like(n, seed=92)]
+    refs, ez, es = [g["out"]], [g["eps_z"].reshape(-1)], [g["eps_src"].reshape(-1)]
+    for b in (1, 2):
+        noise = NoiseRecorder(40 + b)
+        orc = oracle_pipeline(synth_w, hubert_w, rmvpe_w, noise)
+        refs.append(orc.pipeline(0, clips[b].copy(), protect=0.33))
+        z, s = noise.cat()
+        ez.append(z)
+        es.append(s)
+    opts = engine.pipeline_opts(protect=0.33)
+    yb = engine.pipeline_batch(np.stack(clips), opts, sids=0, eps_z=np.stack(ez), eps_src=np.stack(es))
+    engine.check_device_status()
+    yb = yb.cpu().numpy()
+    for b in range(3):
+        assert yb[b].shape == refs[b].shape
+        assert spectrogram_correlation(yb[b], refs[b]) >= 0.999
+        assert rel(yb[b], refs[b]) <= 2e-3, (b, rel(yb[b], refs[b]))

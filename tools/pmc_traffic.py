@@ -4,7 +4,8 @@ FETCH_SIZE and WRITE_SIZE are in KB per dispatch (rocprofv3 derived counters). O
 half the bytes of 16-B-per-lane streaming reads (MI355X_MICROARCH.md, HBM section), so it is doubled;
 WRITE_SIZE is taken as is. The bench runs warm-up + 1 timed step + 1 event pass (inline: the timed step
 carries the events), so each kernel of the step appears `steps` times; per-launch numbers are averages.
-usage: python tools/pmc_traffic.py gpurun_out [kernel-substring]
+usage: python tools/pmc_traffic.py gpurun_out [kernel-substring] > profiles/pmc_traffic.json
+The record carries the source-tree hash (rvcx.provenance) so bench.py can tell whether it applies.
 """
 import collections
 import csv
@@ -12,6 +13,9 @@ import glob
 import json
 import os
 import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "retrieval-based-voice-conversion-mlx_amd"))
 
 
 def load(d, counter):
@@ -39,6 +43,10 @@ def main():
     all_f = sum(sum(v) for v in fe.values()) * 2 * 1024
     all_w = sum(sum(v) for v in wr.values()) * 1024
     rec["all_kernels_bytes"] = all_f + all_w
+    from rvcx.provenance import source_tree_hash
+
+    rec["tree"] = source_tree_hash()
+    rec["file"] = d
     print(json.dumps(rec))
 
 
