@@ -280,6 +280,20 @@ int rvcx_rt_process(rvcx_ctx* ctx, rvcx_rt* rt, const float* d_in, const int32_t
                     const float* d_eps_z, const float* d_eps_src, uint64_t seed, float* d_out, float* d_vol,
                     int32_t* d_offs, void* stream);
 
+/* Contraction arithmetic of every convolution / linear / attention matmul of this context (replaces nothing in
+ * the reference; torch's fp32 CPU conv is what both modes reproduce): 0 = default (2), 1 = fp32-input MFMA
+ * (v_mfma_f32_32x32x2_f32, an exact fp32 fma chain at 157 TF), 2 = fp32 through an exact 3-way bf16 split of both
+ * operands with the six significant plane products on bf16 MFMA (error below fp32's own rounding, 2.67x the
+ * MFMA rate). Env RVCX_CONV_MATH=f32 sets the process default to 1. */
+int rvcx_set_conv_math(rvcx_ctx* ctx, int mode);
+
+/* One Conv1d forward, time-major: d_x [T][C_in], d_w [taps][N][C_in] (torch weight [N][C_in][taps] permuted),
+ * d_bias [N] (optional), d_y [T_out][N]; y[t] = bias + sum_k W[k] x[t*stride - pad + k*dilation] (zero outside).
+ * The kernel family behind every contraction of the path, exposed for numerics tests; replaces
+ * torch.nn.Conv1d.forward as used throughout rvc/lib/algorithm (e.g. residuals.py:34-80). math as above. */
+int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const float* d_w, const float* d_bias, int N,
+                int taps, int dilation, int pad, int stride, int math, float* d_y, int64_t T_out, void* stream);
+
 /* Upsampling factor of the loaded synthesizer (prod(upsample_rates); net_g.dec.upp). */
 int rvcx_synth_upp(const rvcx_ctx* ctx);
 

@@ -52,7 +52,7 @@ struct Case {
 
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 20;
-  // bench_conv ITERS CASE CFG: time one case with one forced config, no checks (for PMC passes)
+  // bench_conv ITERS CASE CFG: time one case with one forced config (10.. = split kernel), no checks (PMC passes)
   const int only_case = argc > 3 ? atoi(argv[2]) : -1;
   const int only_cfg = argc > 3 ? atoi(argv[3]) : -2;
   if (only_case < 0) {
@@ -76,7 +76,7 @@ int main(int argc, char** argv) {
                        pad, 1);
     std::vector<float> ref((size_t)T * N), out((size_t)T * N);
     CK_(hipMemcpy(ref.data(), yr, ref.size() * 4, hipMemcpyDeviceToHost));
-    for (int cfg = 0; cfg < 10; ++cfg)
+    for (int cfg : {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16})
       for (int pipe : {-1}) {
         ConvArgs a;
         a.x = x; a.ldx = C; a.T_in = T; a.C_in = C;
@@ -93,7 +93,8 @@ int main(int argc, char** argv) {
           md = std::max(md, (double)fabsf(out[i] - ref[i]));
           mr = std::max(mr, (double)fabsf(ref[i]));
         }
-        printf("check cfg=%d pipe=%d max|diff|/max|ref| = %.3e %s\n", cfg, pipe, md / mr, md / mr < 1e-5 ? "OK" : "FAIL");
+        printf("check cfg=%d (%s) pipe=%d max|diff|/max|ref| = %.3e %s\n", cfg, cfg >= 10 ? "split" : "f32", pipe,
+               md / mr, md / mr < 1e-5 ? "OK" : "FAIL");
       }
   }
   // split-K correctness on small-M shapes
@@ -116,8 +117,10 @@ int main(int argc, char** argv) {
                        pad, 1);
     std::vector<float> ref((size_t)T * N), out((size_t)T * N);
     CK_(hipMemcpy(ref.data(), yr, ref.size() * 4, hipMemcpyDeviceToHost));
-    for (int pipe : {-1, 1}) {
+    for (int pipe : {-1, 1})
+    for (int math : {1, 2}) {
       ConvArgs a;
+      a.math = math;
       a.x = x; a.ldx = C; a.T_in = T; a.C_in = C;
       a.w = w; a.ldw = C; a.w_ts = (long long)N * C; a.taps = taps; a.dil = dil; a.pad = pad;
       a.y = y; a.ldy = N; a.T_out = T; a.N = N; a.bias = b;
@@ -134,7 +137,7 @@ int main(int argc, char** argv) {
         md = std::max(md, (double)fabsf(out[i] - ref[i]));
         mr = std::max(mr, (double)fabsf(ref[i]));
       }
-      printf("check splitk ksplit=%d pipe=%d max|diff|/max|ref| = %.3e %s\n", a.ksplit, pipe, md / mr,
+      printf("check splitk math=%d ksplit=%d pipe=%d max|diff|/max|ref| = %.3e %s\n", math, a.ksplit, pipe, md / mr,
              md / mr < 1e-5 ? "OK" : "FAIL");
       (void)hipFree(ws);
     }
@@ -175,14 +178,19 @@ int main(int argc, char** argv) {
     CK_(hipMemcpy(w, hw.data(), nw * 4, hipMemcpyHostToDevice));
     CK_(hipMemset(b, 0, cs.N * 4));
     const double flops = 2.0 * cs.T * cs.N * (double)cs.Cin * cs.taps;
-    double best[2][11] = {{0}};
-    int ksp[11] = {0};
-    for (int round = 0; round < (only_case >= 0 ? 1 : 3); ++round)
-    for (int cfg : {-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9})
-      for (int asb : {1, 4}) {
-        const int pipe = asb == 4 ? 1 : -1;  // column "asb4" = the double-buffered GEMM pipeline (taps 1)
-        if (pipe > 0 && cs.taps != 1) continue;
-        if (only_case >= 0 && (cfg != only_cfg % 10 || asb != (only_cfg >= 10 ? 4 : 1))) continue;
+    // variants: (cfg, math, pipe); cfg -1 = the library's policy for that math
+    struct V { int cfg, math, pipe; };
+    std::vector<V> vars = {{-1, 2, 0}, {10, 2, -1}, {11, 2, -1}, {12, 2, -1}, {13, 2, -1}, {14, 2, -1}, {15, 2, -1},
+                           {16, 2, -1}, {-1, 1, 0}, {1, 1, -1}, {3, 1, -1}};
+    if (cs.taps == 1)
+      for (int c : {10, 12, 13, 14, 15}) vars.push_back({c, 2, 1});
+    printf("%-28s", cs.name);
+    for (size_t vi = 0; vi < vars.size(); ++vi) {
+      const V& vv = vars[vi];
+      if (only_case >= 0 && (vv.cfg != only_cfg || vv.pipe > 0)) continue;
+      double best = 0;
+      int ksp = 1;
+      for (int round = 0; round < (only_case >= 0 ? 1 : 2); ++round) {
         ConvArgs a;
         a.x = x; a.ldx = cs.Cin; a.T_in = cs.T; a.C_in = cs.Cin;
         a.w = w; a.ldw = cs.Cin; a.w_ts = (long long)cs.N * cs.Cin; a.taps = cs.taps; a.dil = cs.dil;
@@ -193,13 +201,13 @@ int main(int argc, char** argv) {
           a.act = ACT_NONE;
           a.res = rb; a.ldr = cs.N; a.res_mode = RES_ADD_POST; a.acc_mode = ACC_ADD;
         }
-        a.force_cfg = cfg; a.pipe = pipe; a.astage = asb == 1 ? 0 : asb;
+        a.force_cfg = vv.cfg; a.pipe = vv.pipe; a.math = vv.math;
         float* wsp = nullptr;
-        if (cfg < 0) {
+        if (vv.cfg < 0) {
           const long long need = conv_plan_splitk(a, false);
           if (need > 0) { CK_(hipMalloc(&wsp, need * 4)); a.ws = wsp; }
         }
-        if (conv1d(a, 0) != hipSuccess) { (void)hipGetLastError(); continue; }
+        if (conv1d(a, 0) != hipSuccess) { (void)hipGetLastError(); if (wsp) (void)hipFree(wsp); break; }
         for (int i = 0; i < 3; ++i) CK_(conv1d(a, 0));
         CK_(hipDeviceSynchronize());
         hipEvent_t e0, e1;
@@ -212,16 +220,14 @@ int main(int argc, char** argv) {
         float ms = 0;
         CK_(hipEventElapsedTime(&ms, e0, e1));
         ms /= iters;
-        const double tf = flops / ms / 1e9;
-        if (tf > best[asb == 4][cfg + 1]) best[asb == 4][cfg + 1] = tf;
-        ksp[cfg + 1] = a.ksplit;
+        best = std::max(best, flops / ms / 1e9);
+        ksp = a.ksplit;
         if (wsp) (void)hipFree(wsp);
       }
-    for (int v = 0; v < (cs.taps == 1 ? 2 : 1); ++v) {
-      printf("%-24s %s", cs.name, v ? "pipe" : "sync");
-      for (int c = 0; c < 11; ++c) printf(" %2d:%6.1f%s", c - 1, best[v][c], ksp[c] > 1 ? "*" : " ");
-      printf("\n");
+      printf(" %s%d%s:%6.1f%s", vv.math == 2 ? "e" : "f", vv.cfg, vv.pipe > 0 ? "p" : "", best, ksp > 1 ? "*" : " ");
     }
+    printf("\n");
+    fflush(stdout);
     (void)hipFree(x); (void)hipFree(w); (void)hipFree(b); (void)hipFree(y);
     if (rb) (void)hipFree(rb);
   }

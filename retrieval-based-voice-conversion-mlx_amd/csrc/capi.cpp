@@ -106,6 +106,7 @@ void join_aux(Ctx& c, hipStream_t s, hipStream_t ax) {
 
 void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double flops) {
   ConvArgs a = a_in;
+  if (c.conv_math > 0 && a.math == 0) a.math = c.conv_math;
   const long long need = conv_plan_splitk(a, two_d);
   // split-K slabs are per stream: the aux stream's convs run concurrently with the caller's
   if (need > 0) a.ws = c.buf<float>(c.aux && s == c.aux ? "conv.splitk.aux" : "conv.splitk", (size_t)need, s);
@@ -438,6 +439,35 @@ int rvcx_index_parse(const void* bytes, int64_t nbytes, int64_t* d, int64_t* nto
     if (err && err_cap > 0) std::snprintf(err, (size_t)err_cap, "%s", e.what());
     return RVCX_E_INVALID;
   }
+}
+
+int rvcx_set_conv_math(rvcx_ctx* ctx, int mode) {
+  return guard(ctx, [&] {
+    if (mode < 0 || mode > 2) throw Error(RVCX_E_INVALID, "conv math mode must be 0, 1 or 2");
+    ctx->conv_math = mode;
+  });
+}
+
+int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const float* d_w, const float* d_bias, int N,
+                int taps, int dilation, int pad, int stride, int math, float* d_y, int64_t T_out, void* stream) {
+  return guard(ctx, [&] {
+    set_device(ctx);
+    ctx->check_device_status();
+    if (!d_x || !d_w || !d_y || T <= 0 || C_in <= 0 || N <= 0 || taps <= 0 || dilation <= 0 || stride <= 0 ||
+        pad < 0 || T_out <= 0 || math < 0 || math > 2)
+      throw Error(RVCX_E_INVALID, "rvcx_conv1d: bad argument");
+    if ((T_out - 1) * stride + (int64_t)(taps - 1) * dilation + 1 > T + 2 * (int64_t)pad)
+      throw Error(RVCX_E_SHAPE, "rvcx_conv1d: T_out exceeds the padded input");
+    if (T > INT32_MAX || T_out > INT32_MAX || (int64_t)taps * N * C_in > INT32_MAX)
+      throw Error(RVCX_E_SHAPE, "rvcx_conv1d: size out of range");
+    ConvArgs a;
+    a.x = d_x; a.ldx = C_in; a.T_in = (int)T; a.C_in = C_in;
+    a.w = d_w; a.ldw = C_in; a.w_ts = (long long)N * C_in; a.taps = taps; a.dil = dilation; a.pad = pad;
+    a.stride = stride;
+    a.y = d_y; a.ldy = N; a.T_out = (int)T_out; a.N = N; a.bias = d_bias;
+    a.math = math;
+    launch_conv(*ctx, a, false, static_cast<hipStream_t>(stream), -1.0);
+  });
 }
 
 int rvcx_profile(rvcx_ctx* ctx, int enable) {

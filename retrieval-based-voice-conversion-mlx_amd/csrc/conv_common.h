@@ -1,0 +1,208 @@
+// Shared pieces of the implicit-GEMM conv kernels (conv_gemm.hip: exact fp32 MFMA; conv_emu.hip: fp32 through
+// three bf16 planes): activations, the fused epilogue, and the accumulator -> HBM store of one block tile.
+#pragma once
+#include "rvcx_kernels.h"
+
+namespace rvcx {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int CONV_THREADS = 256;  // 4 waves per block in every conv kernel
+
+static __device__ __noinline__ float act_fn_slow(float v, int act, float slope) {
+  switch (act) {
+    case ACT_GELU: return 0.5f * v * (1.f + erff(v * 0.70710678118654752440f));
+    case ACT_TANH: return tanhf(v);
+    case ACT_SIGMOID: return 1.f / (1.f + expf(-v));
+    case ACT_LOGCLAMP: return logf(fmaxf(v, slope));
+    default: return v;
+  }
+}
+
+// cheap activations inline, transcendental ones out of line (keeps the unrolled epilogue small
+// enough that the accumulators stay in registers)
+static __device__ __forceinline__ float act_fn(float v, int act, float slope) {
+  if (act == ACT_NONE) return v;
+  if (act == ACT_LRELU) return v > 0.f ? v : v * slope;
+  if (act == ACT_RELU) return v > 0.f ? v : 0.f;
+  return act_fn_slow(v, act, slope);
+}
+
+static __device__ __forceinline__ void epilogue_store(const ConvArgs& a, float v, float bn, long long m, int n, int oh,
+                                                      int ow, const float* R, const float* MK, float* Y) {
+  if (a.bias) v += bn;
+  if (a.res_mode == RES_ADD_PRE) v = v + R[m * a.ldr + n];
+  if (a.alpha != 1.f) v *= a.alpha;
+  v = act_fn(v, a.act, a.slope);
+  if (a.res_mode == RES_ADD_POST) v = v + R[m * a.ldr + n];
+  else if (a.res_mode == RES_RSUB_POST) v = R[m * a.ldr + n] - v;
+  float* dst;
+  if (a.out_map == OUT_UPSAMPLE2D) {
+    const int cv = a.out_cv;
+    const int ph = n / (2 * cv), pw = (n / cv) & 1, co = n % cv;
+    dst = Y + ((long long)(2 * oh + ph) * (2 * a.W_out) + (2 * ow + pw)) * a.ldy + co;
+  } else {
+    dst = Y + m * a.ldy + n;
+  }
+  if (a.acc_mode == ACC_ADD) v = *dst + v;
+  else if (a.acc_mode == ACC_ADD_DIV) v = (*dst + v) / a.acc_div;
+  if (MK) v *= MK[m];
+  *dst = v;
+}
+
+// Where a block tile sits: output rows m0.. (1-D) or the rh x rw pixel window at (h0, w0) (2-D), output channels
+// n0.., outer/inner batch (b, bi), split-K slice zsplit of ksplit for batch entry zb.
+struct TilePos {
+  int m0, h0, w0, rw, rh, n0, b, bi, zb, zsplit, ksplit;
+};
+
+// The block's accumulators -> HBM. Wave (wm, wn) holds TM x TN 32x32 tiles in the MFMA C layout: lane (li, hk),
+// register r is row (r&3) + 8(r>>2) + 4hk, column li. Split-K slices write their partial tile to the slab
+// (splitk_reduce_kernel applies the epilogue); otherwise the fused epilogue runs here.
+template <int TM, int TN, int WM, int WN, bool TWO_D>
+__device__ __forceinline__ void conv_store_tile(const ConvArgs& a, const TilePos& p, f32x16 (&acc)[TM][TN],
+                                                float* smem) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int li = lane & 31, hk = lane >> 5;
+  const float* bias = a.bias ? a.bias + (long long)p.b * a.bias_bs + (long long)p.bi * a.bias_bs2 : nullptr;
+  const float* R = a.res ? a.res + (long long)p.b * a.res_bs + (long long)p.bi * a.res_bs2 : nullptr;
+  const float* MK = a.mask ? a.mask + (long long)p.b * a.mask_bs : nullptr;
+  float* Y = a.y + (long long)p.b * a.y_bs + (long long)p.bi * a.y_bs2;
+  auto emit = [&](float v, int ml, int n, bool n_ok, float bn) {
+    long long m;
+    int oh = 0, ow = 0;
+    bool ok;
+    if (!TWO_D) {
+      m = p.m0 + ml;
+      ok = n_ok && (m < a.T_out);
+    } else {
+      oh = p.h0 + ml / p.rw;
+      ow = p.w0 + ml % p.rw;
+      ok = n_ok && (ml < p.rh * p.rw) && (oh < a.T_out) && (ow < a.W_out);
+      m = (long long)oh * a.W_out + ow;
+    }
+    if (ok) {
+      if (p.ksplit > 1) {
+        a.ws[(((long long)p.zb * p.ksplit + p.zsplit) * a.ws_rows + m) * a.N + n] = v;
+      } else {
+        epilogue_store(a, v, bn, m, n, oh, ow, R, MK, Y);
+      }
+    }
+  };
+  if constexpr (TM * TN == 1) {
+    // one accumulator per wave: straight from registers (fully unrolled, 16 values per lane)
+    const int n = p.n0 + wn * 32 + li;
+    const bool n_ok = n < a.N;
+    const float bn = (bias && n_ok) ? bias[n] : 0.f;
+    if (!TWO_D && p.ksplit == 1 && a.out_map == OUT_ROWS) {
+      // 1-D gather first: the residual, accumulate and mask operands of the lane's 16 outputs are all loaded
+      // before the first store. The stores may alias them (an in-place residual reads the very element it
+      // writes), so the compiler cannot hoist the loads across the stores itself and would expose one load
+      // latency per output (16 per lane): the short-contraction convs (ResBlock k=3 at 32/64 channels) were
+      // latency-bound on exactly that. Each element is read and written by this lane only, so the reorder is
+      // exact.
+      const bool need_r = R && a.res_mode != RES_NONE;
+      const bool need_d = a.acc_mode != ACC_STORE;
+      // element r sits at row mb + (r&3) + 8(r>>2) of column n: per-lane base pointers, constant row offsets
+      const int mb = p.m0 + wm * 32 + 4 * hk;
+      const bool full = p.m0 + wm * 32 + 32 <= a.T_out;
+      const float* Rl = need_r ? R + (long long)mb * a.ldr + n : nullptr;
+      float* Yl = Y + (long long)mb * a.ldy + n;
+      const float* Ml = MK ? MK + mb : nullptr;
+      auto row_ok = [&](int r) { return n_ok && (full || mb + (r & 3) + 8 * (r >> 2) < a.T_out); };
+      // two halves of 8 elements: one exposed load latency each, 24 staging registers instead of 48 (the
+      // VGPR count sets the workgroups per CU of this latency-bound kernel)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float rv[8], dv[8], mv[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int r = 8 * h + i;
+          const int ro = (r & 3) + 8 * (r >> 2);
+          const bool ok = row_ok(r);
+          rv[i] = (ok && need_r) ? Rl[ro * a.ldr] : 0.f;
+          dv[i] = (ok && need_d) ? Yl[ro * a.ldy] : 0.f;
+          mv[i] = (ok && MK) ? Ml[ro] : 1.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int r = 8 * h + i;
+          if (!row_ok(r)) continue;
+          const int ro = (r & 3) + 8 * (r >> 2);
+          float v = acc[0][0][r];
+          if (a.bias) v += bn;
+          if (a.res_mode == RES_ADD_PRE) v = v + rv[i];
+          if (a.alpha != 1.f) v *= a.alpha;
+          v = act_fn(v, a.act, a.slope);
+          if (a.res_mode == RES_ADD_POST) v = v + rv[i];
+          else if (a.res_mode == RES_RSUB_POST) v = rv[i] - v;
+          if (a.acc_mode == ACC_ADD) v = dv[i] + v;
+          else if (a.acc_mode == ACC_ADD_DIV) v = (dv[i] + v) / a.acc_div;
+          if (MK) v *= mv[i];
+          Yl[ro * a.ldy] = v;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) emit(acc[0][0][r], wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hk, n, n_ok, bn);
+    }
+  } else {
+    // several accumulators per wave: stage one 32x32 tile at a time through the wave's own LDS slot
+    // (32 x 33 floats) and emit rows 2i + hk, column li; accumulator registers are only indexed with
+    // compile-time constants, so the large wave tiles keep them out of scratch
+    __syncthreads();  // every wave is done with the A/B tiles: their LDS becomes the staging area
+    float* Cs = smem + wave * (32 * 33);
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) Cs[((r & 3) + 8 * (r >> 2) + 4 * hk) * 33 + li] = acc[tm][tn][r];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int n = p.n0 + wn * TN * 32 + tn * 32 + li;
+        const bool n_ok = n < a.N;
+        const float bn = (bias && n_ok) ? bias[n] : 0.f;
+        for (int i = 0; i < 16; ++i) {
+          const int rr = 2 * i + hk;
+          emit(Cs[rr * 33 + li], wm * TM * 32 + tm * 32 + rr, n, n_ok, bn);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+    }
+  }
+}
+
+// Block -> tile: the grid is 1-D over (M tile, N tile) with N fastest when ntn > 0, and the linear workgroup id
+// is remapped so each XCD (workgroups are dealt to the 8 XCDs round-robin) owns one contiguous run of tiles: the
+// N tiles of an M tile then share its A halo through one L2 instead of re-reading it from HBM/L3 (bijective
+// remap, cdna_hip_programming.md T1). ntn = 0: the plain (x = M, y = N) grid.
+__device__ __forceinline__ void conv_block_coords(int ntn, int& bx, int& by, int& bz) {
+  bx = blockIdx.x;
+  by = blockIdx.y;
+  bz = blockIdx.z;
+  if (ntn > 0) {
+    const int X = gridDim.x, total = X * gridDim.z;
+    const int orig = blockIdx.z * X + blockIdx.x;
+    const int xcd = orig & 7, q = total >> 3, r = total & 7;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+    bz = wg / X;
+    const int t = wg - bz * X;
+    bx = t / ntn;
+    by = t - bx * ntn;
+  }
+}
+
+// conv_emu.hip: fp32 convolution on bf16 MFMA through a 3-way operand split (defined there)
+// cfg: 10.. (cfg_tile_emu); returns hipErrorInvalidValue when the tile's LDS does not fit
+hipError_t conv_emu_launch(const ConvArgs& a, int cfg, bool two_d, bool pipe, int ksplit, int ntn_enable,
+                           hipStream_t s);
+bool conv_emu_tile(int cfg, int& BM, int& BN);
+
+}  // namespace rvcx

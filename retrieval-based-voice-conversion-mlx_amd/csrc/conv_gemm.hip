@@ -16,57 +16,14 @@
 // fp32 in / fp32 accumulate MFMA is a bit-exact fp32 fma chain at the FP32 vector peak rate.
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 
-#include "rvcx_kernels.h"
+#include "conv_common.h"
 
 namespace rvcx {
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
 constexpr int CK = 32;   // contraction channels per LDS chunk
-constexpr int NTHREADS = 256;
-
-__device__ __noinline__ float act_fn_slow(float v, int act, float slope) {
-  switch (act) {
-    case ACT_GELU: return 0.5f * v * (1.f + erff(v * 0.70710678118654752440f));
-    case ACT_TANH: return tanhf(v);
-    case ACT_SIGMOID: return 1.f / (1.f + expf(-v));
-    case ACT_LOGCLAMP: return logf(fmaxf(v, slope));
-    default: return v;
-  }
-}
-
-// cheap activations inline, transcendental ones out of line (keeps the unrolled epilogue small
-// enough that the accumulators stay in registers)
-__device__ __forceinline__ float act_fn(float v, int act, float slope) {
-  if (act == ACT_NONE) return v;
-  if (act == ACT_LRELU) return v > 0.f ? v : v * slope;
-  if (act == ACT_RELU) return v > 0.f ? v : 0.f;
-  return act_fn_slow(v, act, slope);
-}
-
-__device__ __forceinline__ void epilogue_store(const ConvArgs& a, float v, float bn, long long m, int n, int oh,
-                                               int ow, const float* R, const float* MK, float* Y) {
-  if (a.bias) v += bn;
-  if (a.res_mode == RES_ADD_PRE) v = v + R[m * a.ldr + n];
-  if (a.alpha != 1.f) v *= a.alpha;
-  v = act_fn(v, a.act, a.slope);
-  if (a.res_mode == RES_ADD_POST) v = v + R[m * a.ldr + n];
-  else if (a.res_mode == RES_RSUB_POST) v = R[m * a.ldr + n] - v;
-  float* dst;
-  if (a.out_map == OUT_UPSAMPLE2D) {
-    const int cv = a.out_cv;
-    const int ph = n / (2 * cv), pw = (n / cv) & 1, co = n % cv;
-    dst = Y + ((long long)(2 * oh + ph) * (2 * a.W_out) + (2 * ow + pw)) * a.ldy + co;
-  } else {
-    dst = Y + m * a.ldy + n;
-  }
-  if (a.acc_mode == ACC_ADD) v = *dst + v;
-  else if (a.acc_mode == ACC_ADD_DIV) v = (*dst + v) / a.acc_div;
-  if (MK) v *= MK[m];
-  *dst = v;
-}
+constexpr int NTHREADS = CONV_THREADS;
 
 template <int BM, int BN, int WM, int WN, bool TWO_D, bool PIPE, int ASB, int CKT = CK>
 __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a, const int nrows_a, const int rw,
@@ -91,17 +48,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
   // id is remapped so each XCD (workgroups are dealt to the 8 XCDs round-robin) owns one contiguous run of
   // tiles: the N tiles of an M tile then share its A halo through one L2 instead of re-reading it from
   // HBM/L3 (bijective remap, cdna_hip_programming.md T1). ntn = 0: the plain (x = M, y = N) grid.
-  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-  if (ntn > 0) {
-    const int X = gridDim.x, total = X * gridDim.z;
-    const int orig = blockIdx.z * X + blockIdx.x;
-    const int xcd = orig & 7, q = total >> 3, r = total & 7;
-    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-    bz = wg / X;
-    const int t = wg - bz * X;
-    bx = t / ntn;
-    by = t - bx * ntn;
-  }
+  int bx, by, bz;
+  conv_block_coords(ntn, bx, by, bz);
   const int zsplit = bz % ksplit;     // split-K slice
   const int zb = bz / ksplit;
   const int b = zb / a.batch_inner;   // outer batch
@@ -472,116 +420,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
   }
 
   // ---- epilogue
-  const float* bias = a.bias ? a.bias + (long long)b * a.bias_bs + (long long)bi * a.bias_bs2 : nullptr;
-  const float* R = a.res ? a.res + (long long)b * a.res_bs + (long long)bi * a.res_bs2 : nullptr;
-  const float* MK = a.mask ? a.mask + (long long)b * a.mask_bs : nullptr;
-  float* Y = a.y + (long long)b * a.y_bs + (long long)bi * a.y_bs2;
-  auto emit = [&](float v, int ml, int n, bool n_ok, float bn) {
-    long long m;
-    int oh = 0, ow = 0;
-    bool ok;
-    if (!TWO_D) {
-      m = m0 + ml;
-      ok = n_ok && (m < a.T_out);
-    } else {
-      oh = h0 + ml / rw;
-      ow = w0 + ml % rw;
-      ok = n_ok && (ml < rh * rw) && (oh < a.T_out) && (ow < a.W_out);
-      m = (long long)oh * a.W_out + ow;
-    }
-    if (ok) {
-      if (ksplit > 1) {
-        a.ws[(((long long)zb * ksplit + zsplit) * a.ws_rows + m) * a.N + n] = v;
-      } else {
-        epilogue_store(a, v, bn, m, n, oh, ow, R, MK, Y);
-      }
-    }
-  };
-  if constexpr (TM * TN == 1) {
-    // one accumulator per wave: straight from registers (fully unrolled, 16 values per lane)
-    const int n = n0 + wn * 32 + li;
-    const bool n_ok = n < a.N;
-    const float bn = (bias && n_ok) ? bias[n] : 0.f;
-    if (!TWO_D && ksplit == 1 && a.out_map == OUT_ROWS) {
-      // 1-D gather first: the residual, accumulate and mask operands of the lane's 16 outputs are all loaded
-      // before the first store. The stores may alias them (an in-place residual reads the very element it
-      // writes), so the compiler cannot hoist the loads across the stores itself and would expose one load
-      // latency per output (16 per lane): the short-contraction convs (ResBlock k=3 at 32/64 channels) were
-      // latency-bound on exactly that. Each element is read and written by this lane only, so the reorder is
-      // exact.
-      const bool need_r = R && a.res_mode != RES_NONE;
-      const bool need_d = a.acc_mode != ACC_STORE;
-      // element r sits at row mb + (r&3) + 8(r>>2) of column n: per-lane base pointers, constant row offsets
-      const int mb = m0 + wm * 32 + 4 * hk;
-      const bool full = m0 + wm * 32 + 32 <= a.T_out;
-      const float* Rl = need_r ? R + (long long)mb * a.ldr + n : nullptr;
-      float* Yl = Y + (long long)mb * a.ldy + n;
-      const float* Ml = MK ? MK + mb : nullptr;
-      auto row_ok = [&](int r) { return n_ok && (full || mb + (r & 3) + 8 * (r >> 2) < a.T_out); };
-      // two halves of 8 elements: one exposed load latency each, 24 staging registers instead of 48 (the
-      // VGPR count sets the workgroups per CU of this latency-bound kernel)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        float rv[8], dv[8], mv[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int r = 8 * h + i;
-          const int ro = (r & 3) + 8 * (r >> 2);
-          const bool ok = row_ok(r);
-          rv[i] = (ok && need_r) ? Rl[ro * a.ldr] : 0.f;
-          dv[i] = (ok && need_d) ? Yl[ro * a.ldy] : 0.f;
-          mv[i] = (ok && MK) ? Ml[ro] : 1.f;
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int r = 8 * h + i;
-          if (!row_ok(r)) continue;
-          const int ro = (r & 3) + 8 * (r >> 2);
-          float v = acc[0][0][r];
-          if (a.bias) v += bn;
-          if (a.res_mode == RES_ADD_PRE) v = v + rv[i];
-          if (a.alpha != 1.f) v *= a.alpha;
-          v = act_fn(v, a.act, a.slope);
-          if (a.res_mode == RES_ADD_POST) v = v + rv[i];
-          else if (a.res_mode == RES_RSUB_POST) v = rv[i] - v;
-          if (a.acc_mode == ACC_ADD) v = dv[i] + v;
-          else if (a.acc_mode == ACC_ADD_DIV) v = (dv[i] + v) / a.acc_div;
-          if (MK) v *= mv[i];
-          Yl[ro * a.ldy] = v;
-        }
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) emit(acc[0][0][r], wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hk, n, n_ok, bn);
-    }
-  } else {
-    // several accumulators per wave: stage one 32x32 tile at a time through the wave's own LDS slot
-    // (32 x 33 floats) and emit rows 2i + hk, column li; accumulator registers are only indexed with
-    // compile-time constants, so the large wave tiles keep them out of scratch
-    __syncthreads();  // every wave is done with the A/B tiles: their LDS becomes the staging area
-    float* Cs = smem + wave * (32 * 33);
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm) {
-#pragma unroll
-      for (int tn = 0; tn < TN; ++tn) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) Cs[((r & 3) + 8 * (r >> 2) + 4 * hk) * 33 + li] = acc[tm][tn][r];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int n = n0 + wn * TN * 32 + tn * 32 + li;
-        const bool n_ok = n < a.N;
-        const float bn = (bias && n_ok) ? bias[n] : 0.f;
-        for (int i = 0; i < 16; ++i) {
-          const int rr = 2 * i + hk;
-          emit(Cs[rr * 33 + li], wm * TM * 32 + tm * 32 + rr, n, n_ok, bn);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      }
-    }
-  }
+  conv_store_tile<TM, TN, WM, WN, TWO_D>(a, TilePos{m0, h0, w0, rw, rh, n0, b, bi, zb, zsplit, ksplit}, acc, smem);
 }
 
 // split-K combine: sums the ksplit partial tiles in slice order (deterministic) and applies the epilogue
@@ -614,9 +453,21 @@ __global__ void splitk_reduce_kernel(const ConvArgs a, const int ksplit, const i
 
 namespace {
 
-struct TileCfg {
-  int BM, BN;
-};
+bool xcd_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("RVCX_NO_XCD");
+    return !(e && std::atoi(e) != 0);
+  }();
+  return v;
+}
+
+hipError_t launch_splitk_reduce(const ConvArgs& a, int ksplit, bool two_d, hipStream_t s) {
+  const long long total = (long long)a.ws_rows * a.N * a.batch * a.batch_inner;
+  long long nb = (total + 255) / 256;
+  if (nb > 8192) nb = 8192;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, ksplit, two_d ? 1 : 0);
+  return hipGetLastError();
+}
 
 template <int BM, int BN, int WM, int WN, bool TWO_D, bool PIPE = false, int ASB = 1, int CKT = CK>
 hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
@@ -644,11 +495,7 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
   int ksplit = 1;
   if (a.ws && a.ksplit > 1) ksplit = a.ksplit;
   const int ntiles = (a.N + BN - 1) / BN;
-  static const bool xcd_env = [] {
-    const char* e = std::getenv("RVCX_NO_XCD");
-    return !(e && std::atoi(e) != 0);
-  }();
-  const int ntn = xcd_env ? ntiles : 0;
+  const int ntn = xcd_enabled() ? ntiles : 0;
   dim3 grid(ntn ? mtiles * ntiles : mtiles, ntn ? 1 : ntiles, a.batch * a.batch_inner * ksplit);
   auto kern = conv_gemm_kernel<BM, BN, WM, WN, TWO_D, PIPE, ASB, CKT>;
   static size_t smem_set = 64 * 1024;  // per instantiation: raise the dynamic-LDS limit once, not per launch
@@ -661,11 +508,7 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(kern, grid, dim3(NTHREADS), smem, s, a, nrows_a, rw, rh, tiles_w, vec_a, vec_b, ksplit, ntn);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || ksplit == 1) return e;
-  const long long total = (long long)a.ws_rows * a.N * a.batch * a.batch_inner;
-  long long nb = (total + 255) / 256;
-  if (nb > 8192) nb = 8192;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, ksplit, TWO_D ? 1 : 0);
-  return hipGetLastError();
+  return launch_splitk_reduce(a, ksplit, TWO_D, s);
 }
 
 template <bool TWO_D, bool PIPE, int ASB>
@@ -710,9 +553,41 @@ inline int env_cfg(const char* name, int dflt) {
   const char* e = std::getenv(name);
   return e ? std::atoi(e) : dflt;
 }
+// contraction arithmetic: 1 = native fp32 MFMA (conv_gemm_kernel), 2 = fp32 through the 3-way bf16 split
+// (conv_emu.hip, the default); ConvArgs::math overrides RVCX_CONV_MATH (f32 | split)
+inline int conv_math(const ConvArgs& a) {
+  static const int env = [] {
+    const char* e = std::getenv("RVCX_CONV_MATH");
+    if (e && (std::string(e) == "f32" || std::string(e) == "1")) return 1;
+    return 2;
+  }();
+  return a.math > 0 ? a.math : env;
+}
+
+// Tile per shape class in split mode, from build/bench_conv on MI355X (TF/s, split vs the native fp32 kernel):
+// long-tap convs 128x32 (C128 k11 155 vs 114, C256 k11 138 vs 106), short taps and GEMMs 64x64 (C128 k3 + residual
+// 101 vs 78, HuBERT qkv 52 vs 38), narrow short convs (N <= 32, taps < 5: the 32-channel ResBlock k=3, latency
+// bound) stay on the native kernel (53 vs 47): both arithmetics are fp32 accurate, so the choice is per shape.
+// RVCX_ECFG_* override a class (measurement aid; values < 10 select native tiles).
+template <bool TWO_D>
+int pick_emu(const ConvArgs& a) {
+  static const int c_long = env_cfg("RVCX_ECFG_LONG", 12);
+  static const int c_short = env_cfg("RVCX_ECFG_SHORT", 13);
+  static const int c_narrow = env_cfg("RVCX_ECFG_NARROW", 12);
+  static const int c_narrow_short = env_cfg("RVCX_ECFG_NARROW_SHORT", 1);
+  static const int c_gemm = env_cfg("RVCX_ECFG_GEMM", 13);
+  static const int c_2d = env_cfg("RVCX_ECFG_2D", 13);  // U-Net 3x3 convs: 64x64 (C2 26.7 -> 25.9 ms vs 128x64)
+  if (TWO_D) return a.N <= 32 ? 12 : c_2d;
+  if (a.N <= 32) return a.taps >= 5 ? c_narrow : c_narrow_short;
+  if (a.taps >= 5) return c_long;
+  if (a.taps == 1 && a.stride == 1) return c_gemm;
+  return c_short;
+}
+
 template <bool TWO_D>
 int pick_cfg(const ConvArgs& a) {
   if (a.force_cfg >= 0) return a.force_cfg;
+  if (conv_math(a) == 2) return pick_emu<TWO_D>(a);
   static const int c_long = env_cfg("RVCX_CFG_LONG", 1);      // 1-D, taps >= 5, N > 32 (A/B: 32.8 vs 33.6 ms)
   static const int c_short = env_cfg("RVCX_CFG_SHORT", 3);    // everything else with N > 32
   static const int c_narrow = env_cfg("RVCX_CFG_NARROW", 1);  // N <= 32
@@ -722,6 +597,7 @@ int pick_cfg(const ConvArgs& a) {
 }
 
 inline void cfg_tile(int cfg, int& BM, int& BN) {
+  if (conv_emu_tile(cfg, BM, BN)) return;
   static const int t[10][2] = {{256, 32}, {128, 32}, {128, 64}, {64, 64}, {128, 128}, {64, 128}, {256, 64},
                                {64, 64}, {128, 32}, {128, 128}};
   BM = t[cfg][0];
@@ -753,6 +629,25 @@ hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
   }();
   const bool gemm = !TWO_D && a.taps == 1 && a.stride == 1;
   const bool pipe = gemm && (a.pipe > 0 || (a.pipe == 0 && pipe_env));
+  if (cfg >= 10) {
+    auto run = [&](int c, bool p) -> hipError_t {
+      const int ksplit = (b.ws && b.ksplit > 1) ? b.ksplit : 1;
+      hipError_t e = conv_emu_launch(b, c, TWO_D, p, ksplit, xcd_enabled() ? 1 : 0, s);
+      if (e != hipSuccess || ksplit == 1) return e;
+      return launch_splitk_reduce(b, ksplit, TWO_D, s);
+    };
+    hipError_t e = run(cfg, pipe);
+    if (e == hipErrorInvalidValue && pipe) e = run(cfg, false);  // tile without a GEMM-pipeline instantiation
+    if (e == hipErrorInvalidValue && a.force_cfg < 0) {
+      // the tile's halo does not fit in LDS (long strided taps) or the shape class has no such instantiation
+      for (int alt : {13, 12}) {
+        if (alt == cfg) continue;
+        e = run(alt, false);
+        if (e != hipErrorInvalidValue) break;
+      }
+    }
+    return e;
+  }
   hipError_t e = pipe ? launch_forced<TWO_D, true>(b, s) : launch_forced<TWO_D, false>(b, s);
   if (e == hipErrorInvalidValue && a.force_cfg < 0) {
     // the chosen tile's halo does not fit in LDS (long strided taps): fall back to smaller tiles

@@ -91,6 +91,7 @@ struct ConvArgs {
   int force_cfg = -1;
   int pipe = 0;
   int astage = 0;  // A-tile staging batch: 0 = default (RVCX_CONV_ASB or 1), 1 = serial, 4 = 4 loads in flight
+  int math = 0;    // contraction arithmetic: 0 = default (RVCX_CONV_MATH), 1 = native fp32 MFMA, 2 = fp32 via 3 bf16 planes
   // split-K: set by conv_plan_splitk; ws holds ksplit partial [rows][N] tiles per batch entry
   int ksplit = 1;
   int no_splitk = 0;

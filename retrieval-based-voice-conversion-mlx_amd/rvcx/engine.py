@@ -420,6 +420,29 @@ class Engine:
         return out
 
     # ------------------------------------------------------------------ kernel timing
+    def set_conv_math(self, mode: str):
+        """Contraction arithmetic of this context: "split" (default; fp32 via three bf16 planes on bf16 MFMA) or
+        "f32" (fp32-input MFMA). Both reproduce torch's fp32 conv to fp32 rounding (rvcx_set_conv_math)."""
+        m = {"default": 0, "f32": 1, "split": 2}[mode]
+        self._check(self.lib.rvcx_set_conv_math(self.ctx, m), "set_conv_math")
+
+    def conv1d(self, x, w, bias=None, dilation: int = 1, padding: int = 0, stride: int = 1, math: str = "default"):
+        """torch.nn.functional.conv1d(x.T[None], w, bias, stride, padding, dilation)[0].T on the device kernel:
+        x [T][C_in] (time-major), w [N][C_in][taps] (torch layout) -> [T_out][N] fp32 (rvcx_conv1d)."""
+        torch = self.torch
+        x = self._dev(x, torch.float32)
+        w = torch.as_tensor(w, dtype=torch.float32)
+        N, C, K = (int(v) for v in w.shape)
+        wk = self._dev(w.permute(2, 0, 1).contiguous(), torch.float32)
+        b = self._dev(bias, torch.float32) if bias is not None else None
+        T = int(x.shape[0])
+        T_out = (T + 2 * padding - dilation * (K - 1) - 1) // stride + 1
+        y = torch.empty((T_out, N), dtype=torch.float32, device=self.device)
+        m = {"default": 0, "f32": 1, "split": 2}[math]
+        self._check(self.lib.rvcx_conv1d(self.ctx, _ptr(x), T, C, _ptr(wk), _ptr(b), N, K, dilation, padding, stride,
+                                         m, _ptr(y), T_out, self.stream()), "conv1d")
+        return y
+
     def profile(self, enable: bool):
         self._check(self.lib.rvcx_profile(self.ctx, 1 if enable else 0), "profile")
 

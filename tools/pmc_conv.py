@@ -9,7 +9,7 @@ agg = collections.defaultdict(float)
 cnt = collections.Counter()
 for f in sorted(glob.glob(f"gpurun_out/{tag}_p*/**/*counter_collection.csv", recursive=True)):
     for r in csv.DictReader(open(f)):
-        if "conv_gemm" not in r["Kernel_Name"]:
+        if "conv_gemm" not in r["Kernel_Name"] and "conv_emu" not in r["Kernel_Name"]:
             continue
         agg[r["Counter_Name"]] += float(r["Counter_Value"])
         cnt[r["Counter_Name"]] += 1
