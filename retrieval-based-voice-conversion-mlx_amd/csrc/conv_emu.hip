@@ -278,10 +278,13 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_emu_kernel(const ConvArg
 
   // ---- A (1-D): register prefetch of a whole chunk tile, issued one chunk ahead and written (split) at the chunk
   // change; tiles up to BM + 64 rows (every halo conv of the path but HuBERT's strided feature convs)
+  // 2-D (the (rh + KH - 1) x (rw + KW - 1) pixel window) measured slower with the prefetch (U-Net 64x64 convs
+  // 2.58 vs 2.47 ms per C2 step: 134 vs 105 VGPRs), so 2-D tiles stage synchronously (AP = 1 never fits)
   constexpr int AP = TWO_D ? 1 : ((BM + 64) * EC4 + NT - 1) / NT;
   f32x4 apre[AP];
-  float apm[AP];
-  const bool a_pre = !TWO_D && !PIPE && nrows_a * EC4 <= AP * NT;
+  float apm[TWO_D ? 1 : AP];  // 1-D: 0 outside the input, else the row mask; 2-D: folded into apre
+  const bool a_pre = !PIPE && nrows_a * EC4 <= AP * NT &&
+                     (!TWO_D || a.pre_act == ACT_NONE || a.pre_act == ACT_LRELU || a.pre_act == ACT_RELU);
   const bool a_fast = vec_a && (a.C_in % EK) == 0;
   const int arow = store_row(tid / EC4), ac4 = (tid % EC4) << 2;
   auto load_a_regs = [&](int c0) {
@@ -289,12 +292,21 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_emu_kernel(const ConvArg
 #pragma unroll
     for (int v = 0; v < AP; ++v) {
       const int r = v * (NT / EC4) + arow;
-      const int g = row0 + r;
-      const bool ok = r < nrows_a && g >= 0 && g < a.T_in;
+      long long g;
+      bool ok;
+      if constexpr (!TWO_D) {
+        g = row0 + r;
+        ok = r < nrows_a && g >= 0 && g < a.T_in;
+      } else {
+        const int ah = r / aw, awi = r - ah * aw;
+        const int gh = h0 - a.padh + ah, gw = w0 - a.padw + awi;
+        ok = r < nrows_a && gh >= 0 && gh < a.T_in && gw >= 0 && gw < a.W_in;
+        g = (long long)gh * a.W_in + gw;
+      }
       f32x4 val = {0.f, 0.f, 0.f, 0.f};
-      apm[v] = 0.f;
+      if constexpr (!TWO_D) apm[v] = 0.f;
       if (ok) {
-        const float* src = src0 + (long long)g * a.ldx;
+        const float* src = src0 + g * a.ldx;
         if (a_fast) {
           val = *reinterpret_cast<const f32x4*>(src);
         } else {
@@ -302,7 +314,7 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_emu_kernel(const ConvArg
 #pragma unroll
           for (int j = 0; j < 4; ++j) val[j] = (c + j < a.C_in) ? src[j] : 0.f;
         }
-        apm[v] = PM ? PM[g] : 1.f;
+        if constexpr (!TWO_D) apm[v] = PM ? PM[g] : 1.f;
       }
       apre[v] = val;
     }
@@ -315,10 +327,12 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_emu_kernel(const ConvArg
         f32x4 val = apre[v];
         if (a.pre_act != ACT_NONE) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) val[j] = act_fn(val[j], a.pre_act, a.pre_slope);
+          for (int j = 0; j < 4; ++j) val[j] = act_fn(val[j], a.pre_act, a.pre_slope);  // act(0) = 0
         }
+        if constexpr (!TWO_D) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) val[j] *= apm[v];  // 0 outside the input, the row mask inside
+          for (int j = 0; j < 4; ++j) val[j] *= apm[v];  // 0 outside the input, the row mask inside
+        }
         put_split4(As + r * ERS, ac4, val);
       }
     }
@@ -327,19 +341,25 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_emu_kernel(const ConvArg
   // ---- MFMA: 2 K16 steps x (TM x TN tiles) x 6 plane products, smallest terms first
   auto compute = [&](const char* As, const char* Bs, int tap) {
     const int toff = (TWO_D ? (tap / a.KW) * aw + (tap % a.KW) : tap * a.dil) * ERS;
+    // every fragment of both K16 steps is requested before the first MFMA: one exposed LDS latency per tap
+    bf16x8 af2[2][TM][3], bf2[2][TN][3];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      bf16x8 af[TM][3], bfr[TN][3];
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
         for (int q = 0; q < 3; ++q)
-          af[tm][q] = *reinterpret_cast<const bf16x8*>(As + aoff[tm] + toff + q * PLANE + s * 32);
+          af2[s][tm][q] = *reinterpret_cast<const bf16x8*>(As + aoff[tm] + toff + q * PLANE + s * 32);
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
         for (int q = 0; q < 3; ++q)
-          bfr[tn][q] = *reinterpret_cast<const bf16x8*>(Bs + boff[tn] + q * PLANE + s * 32);
+          bf2[s][tn][q] = *reinterpret_cast<const bf16x8*>(Bs + boff[tn] + q * PLANE + s * 32);
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      auto& af = af2[s];
+      auto& bfr = bf2[s];
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm)
 #pragma unroll

@@ -451,7 +451,79 @@ __global__ void splitk_reduce_kernel(const ConvArgs a, const int ksplit, const i
   }
 }
 
+// Contractions far shorter than one 32-channel MFMA chunk (C_in <= 4 and at most 16 MACs per output: RMVPE's 3x3
+// and 1x1 convs on the 1-channel mel image, the generator's last 1-tap noise conv) would run the MFMA tile on
+// >= 87 % zero padding: one thread per output element instead, an fp32 fma chain over (tap, channel), then the
+// shared epilogue. (The long-tap C_in = 1 noise convs stay on the MFMA kernel: 80 dependent loads per output
+// measured 351 vs 110 us.) Outputs are n-fastest,
+// so stores and weight reads coalesce and a thread group shares its input rows through L1.
+template <bool TWO_D>
+__global__ void conv_tiny_kernel(const ConvArgs a) {
+  // 32-bit index math (launch_tiny checks the sizes): one output element per thread, n fastest
+  const int rows = TWO_D ? a.T_out * a.W_out : a.T_out;
+  const int per_b = rows * a.N;
+  const int total = per_b * a.batch * a.batch_inner;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int zb = i / per_b;
+    const int rem = i - zb * per_b;
+    const int m = rem / a.N;
+    const int n = rem - m * a.N;
+    const int b = zb / a.batch_inner, bi = zb - (zb / a.batch_inner) * a.batch_inner;
+    const float* X = a.x + (long long)b * a.x_bs + (long long)bi * a.x_bs2;
+    const float* Wb = a.w + (long long)b * a.w_bs + (long long)bi * a.w_bs2;
+    const float* PM = a.pre_mask ? a.pre_mask + (long long)b * a.pre_mask_bs : nullptr;
+    int oh = 0, ow = 0;
+    if (TWO_D) {
+      oh = m / a.W_out;
+      ow = m - oh * a.W_out;
+    }
+    float acc = 0.f;
+    for (int tap = 0; tap < a.taps; ++tap) {
+      int g;
+      if (!TWO_D) {
+        g = m * a.stride - a.pad + tap * a.dil;
+        if (g < 0 || g >= a.T_in) continue;
+      } else {
+        const int kh = tap / a.KW;
+        const int gh = oh - a.padh + kh, gw = ow - a.padw + (tap - kh * a.KW);
+        if (gh < 0 || gh >= a.T_in || gw < 0 || gw >= a.W_in) continue;
+        g = gh * a.W_in + gw;
+      }
+      const float pm = (PM && !TWO_D) ? PM[g] : 1.f;
+      const float* Wt = Wb + (long long)tap * a.w_ts;
+      for (int c = 0; c < a.C_in; ++c) {
+        const float v = act_fn(X[(long long)g * a.ldx + c], a.pre_act, a.pre_slope) * pm;
+        const float wv = a.b_kn ? Wt[(long long)c * a.ldw + n] : Wt[(long long)n * a.ldw + c];
+        acc = fmaf(v, wv, acc);
+      }
+    }
+    const float* bias = a.bias ? a.bias + (long long)b * a.bias_bs + (long long)bi * a.bias_bs2 : nullptr;
+    const float* R = a.res ? a.res + (long long)b * a.res_bs + (long long)bi * a.res_bs2 : nullptr;
+    const float* MK = a.mask ? a.mask + (long long)b * a.mask_bs : nullptr;
+    float* Y = a.y + (long long)b * a.y_bs + (long long)bi * a.y_bs2;
+    epilogue_store(a, acc, bias ? bias[n] : 0.f, m, n, oh, ow, R, MK, Y);
+  }
+}
+
 namespace {
+
+constexpr int TINY_MAX_CIN = 4;
+inline bool tiny_fits(const ConvArgs& a) {
+  const long long rows = a.W_out > 0 ? (long long)a.T_out * a.W_out : a.T_out;
+  return a.C_in <= TINY_MAX_CIN && a.C_in * a.taps <= 16 && a.force_cfg < 0 &&
+         rows * a.N * a.batch * a.batch_inner < (1LL << 30);
+}
+
+hipError_t launch_tiny(const ConvArgs& a, bool two_d, hipStream_t s) {
+  const long long rows = two_d ? (long long)a.T_out * a.W_out : a.T_out;
+  const long long total = rows * a.N * a.batch * a.batch_inner;
+  if (total >= (1LL << 31) - 65536LL * 256) return hipErrorInvalidValue;  // 32-bit indexing in the kernel
+  long long nb = (total + 255) / 256;
+  if (nb > 65536) nb = 65536;
+  if (two_d) hipLaunchKernelGGL(conv_tiny_kernel<true>, dim3((unsigned)nb), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(conv_tiny_kernel<false>, dim3((unsigned)nb), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
 
 bool xcd_enabled() {
   static const bool v = [] {
@@ -616,6 +688,7 @@ template <bool TWO_D>
 hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
   if (a.N <= 0 || a.T_out <= 0 || a.batch <= 0) return hipSuccess;
   if (a.C_in <= 0 || a.taps <= 0) return hipErrorInvalidValue;
+  if (tiny_fits(a)) return launch_tiny(a, TWO_D, s);
   // 3x3 convs with 16/32 channels: 16x16x4 MFMA fragments (conv2d_small.hip)
   if (TWO_D && a.force_cfg < 0 && small2d_enabled() && conv2d_small_fits(a)) return conv2d_small(a, s);
   const int cfg = pick_cfg<TWO_D>(a);
@@ -666,6 +739,7 @@ hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
 long long conv_plan_splitk(ConvArgs& a, bool two_d) {
   a.ksplit = 1;
   if (a.N <= 0 || a.T_out <= 0 || a.no_splitk) return 0;
+  if (tiny_fits(a)) return 0;
   if (two_d && a.force_cfg < 0 && small2d_enabled() && conv2d_small_fits(a)) return 0;
   const int cfg = two_d ? pick_cfg<true>(a) : pick_cfg<false>(a);
   int BM, BN;
