@@ -48,6 +48,10 @@ typedef struct {
   int upsample_initial_channel;
   int upsample_kernel_sizes[8];
   int spk_embed_dim, gin_channels, sr, text_enc_hidden_dim;
+  int no_f0;   /* 1: model without pitch guidance (cpt["f0"] == 0): TextEncoder without emb_pitch and the plain
+                  HiFiGANGenerator (synthesizers.py:84, :122-139, :233-239; generators/hifigan.py:9-104) */
+  int vocoder; /* decoder of a pitch-guided model (cpt["vocoder"], infer.py:478): 0 "HiFi-GAN" (NSF),
+                  1 "MRF HiFi-GAN", 2 "RefineGAN" (synthesizers.py:86-118) */
 } rvcx_synth_desc;
 
 /* Create a context on HIP device `device`. */
@@ -102,6 +106,8 @@ int rvcx_f0_post(rvcx_ctx* ctx, const double* d_f0, int64_t F, double semitones,
 int rvcx_f0_autotune(rvcx_ctx* ctx, double* d_f0, int64_t F, double strength, int skip_unvoiced, void* stream);
 
 /* Synthesizer.infer (rvc/lib/algorithm/synthesizers.py:206-243; rvc_mlx/lib/mlx/synthesizers.py:193-235).
+ * For a model without pitch guidance (no_f0) d_pitch / d_pitchf may be NULL and are ignored (:233-239); the
+ * same holds for d_f0 of rvcx_dec_only and d_pitch / d_pitchf of rvcx_voice_conversion.
  * phone [B][T][E], lengths [B], pitch [B][T], pitchf [B][T], sid [B] -> out [B][T*upp].
  * d_eps_z ([B][I][T], reference layout of randn_like(m_p)) and d_eps_src ([B][T*upp], randn_like at
  * generators/hifigan.py:223) are optional injected noise; when NULL the noise is drawn from the

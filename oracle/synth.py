@@ -214,6 +214,25 @@ def nsf_generator(w, cfg, x: Tensor, f0: Tensor, g: Tensor, eps_src: Tensor) -> 
     return x
 
 
+def hifigan_generator(w, cfg, x: Tensor, g: Tensor) -> Tensor:
+    """HiFiGANGenerator.forward (rvc/lib/algorithm/generators/hifigan.py:80-104): the decoder of models without
+    pitch guidance -- no source module; ups padding (k - u) // 2 without output_padding (:46-58)."""
+    x = F.conv1d(x, _t(w, "dec.conv_pre.weight"), _t(w, "dec.conv_pre.bias"), padding=3)
+    x = x + F.conv1d(g, _t(w, "dec.cond.weight"), _t(w, "dec.cond.bias"))
+    nk = len(cfg.resblock_kernel_sizes)
+    for i, (u, k) in enumerate(zip(cfg.upsample_rates, cfg.upsample_kernel_sizes)):
+        x = F.leaky_relu(x, 0.1)
+        x = F.conv_transpose1d(x, _t(w, f"dec.ups.{i}.weight"), _t(w, f"dec.ups.{i}.bias"), stride=u,
+                               padding=(k - u) // 2)
+        xs = 0
+        for j in range(nk):
+            xs = xs + resblock(w, f"dec.resblocks.{i * nk + j}", x, cfg.resblock_kernel_sizes[j],
+                               cfg.resblock_dilation_sizes[j])
+        x = xs / nk
+    x = F.leaky_relu(x)
+    return torch.tanh(F.conv1d(x, _t(w, "dec.conv_post.weight"), None, padding=3))
+
+
 def synth_infer(w, cfg, phone: Tensor, lengths: Tensor, pitch: Tensor, nsff0: Tensor, sid: Tensor,
                 eps_z: Tensor, eps_src: Tensor):
     """Synthesizer.infer (rvc/lib/algorithm/synthesizers.py:206-243) with the two RNG draws
@@ -221,10 +240,13 @@ def synth_infer(w, cfg, phone: Tensor, lengths: Tensor, pitch: Tensor, nsff0: Te
     Returns (o [B,1,T*upp], x_mask, (z, z_p, m_p, logs_p))."""
     with torch.no_grad():
         g = F.embedding(sid, _t(w, "emb_g.weight")).unsqueeze(-1)
-        m_p, logs_p, x_mask = text_encoder(w, cfg, phone, pitch, lengths)
+        m_p, logs_p, x_mask = text_encoder(w, cfg, phone, pitch if getattr(cfg, "use_f0", True) else None, lengths)
         z_p = (m_p + torch.exp(logs_p) * eps_z * 0.66666) * x_mask
         z = flow_reverse(w, cfg, z_p, x_mask, g)
-        o = nsf_generator(w, cfg, z * x_mask, nsff0, g, eps_src)
+        if getattr(cfg, "use_f0", True):
+            o = nsf_generator(w, cfg, z * x_mask, nsff0, g, eps_src)
+        else:  # synthesizers.py:233-239: dec(z * x_mask, g=g)
+            o = hifigan_generator(w, cfg, z * x_mask, g)
     return o, x_mask, (z, z_p, m_p, logs_p)
 
 

@@ -190,6 +190,11 @@ int rvcx_set_synth_config(rvcx_ctx* ctx, const rvcx_synth_desc* d) {
     g.gin = d->gin_channels;
     g.sr = d->sr;
     g.emb_dim = d->text_enc_hidden_dim;
+    g.f0 = d->no_f0 == 0;
+    g.vocoder = d->vocoder;
+    if (g.vocoder < 0 || g.vocoder > 0) throw Error(RVCX_E_INVALID, "unsupported vocoder id");
+    if (!g.f0 && g.vocoder != 0)
+      throw Error(RVCX_E_INVALID, "models without pitch guidance use the HiFi-GAN decoder only (synthesizers.py:119-139)");
     if (g.H % g.n_heads || g.I % 2 || g.C0 % (1 << g.ups.size()))
       throw Error(RVCX_E_INVALID, "inconsistent synthesizer dimensions");
     ctx->scfg = g;
@@ -316,8 +321,11 @@ int rvcx_synth_infer(rvcx_ctx* ctx, int B, int T, const float* d_phone, const in
                      const float* d_eps_src, uint64_t seed, float* d_out, float* d_zp, float* d_z, void* stream) {
   return guard(ctx, [&] {
     if (!ctx->ready[0]) throw Error(RVCX_E_STATE, "synthesizer weights not finalized");
-    if (B <= 0 || T <= 0 || !d_phone || !d_lengths || !d_pitch || !d_pitchf || !d_sid || !d_out)
+    if (B <= 0 || T <= 0 || !d_phone || !d_lengths || !d_sid || !d_out)
       throw Error(RVCX_E_INVALID, "rvcx_synth_infer: bad arguments");
+    if (ctx->scfg.f0 && (!d_pitch || !d_pitchf))
+      throw Error(RVCX_E_INVALID, "rvcx_synth_infer: a pitch-guided model needs pitch and pitchf");
+    if (!ctx->scfg.f0) d_pitch = nullptr, d_pitchf = nullptr;  // Synthesizer.infer ignores them (:233-239)
     set_device(ctx);
     synth_forward(*ctx, B, T, d_phone, d_lengths, d_pitch, d_pitchf, d_sid, d_eps_z, d_eps_src, seed, d_out, d_zp,
                   d_z, static_cast<hipStream_t>(stream));
@@ -328,7 +336,8 @@ int rvcx_dec_only(rvcx_ctx* ctx, int B, int T, const float* d_z, const float* d_
                   const float* d_eps_src, uint64_t seed, float* d_out, void* stream) {
   return guard(ctx, [&] {
     if (!ctx->ready[0]) throw Error(RVCX_E_STATE, "synthesizer weights not finalized");
-    if (B <= 0 || T <= 0 || !d_z || !d_f0 || !d_sid || !d_out) throw Error(RVCX_E_INVALID, "rvcx_dec_only: bad arguments");
+    if (B <= 0 || T <= 0 || !d_z || !d_sid || !d_out || (ctx->scfg.f0 && !d_f0))
+      throw Error(RVCX_E_INVALID, "rvcx_dec_only: bad arguments");
     set_device(ctx);
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int I = ctx->scfg.I;
@@ -346,7 +355,8 @@ int rvcx_voice_conversion(rvcx_ctx* ctx, const float* d_audio, int64_t n, const 
                           void* stream) {
   return guard(ctx, [&] {
     if (!ctx->ready[0] || !ctx->ready[1]) throw Error(RVCX_E_STATE, "synthesizer/hubert not finalized");
-    if (!d_audio || !d_pitch || !d_pitchf || !d_out || n <= 0) throw Error(RVCX_E_INVALID, "bad arguments");
+    if (!d_audio || !d_out || n <= 0 || (ctx->scfg.f0 && (!d_pitch || !d_pitchf)))
+      throw Error(RVCX_E_INVALID, "bad arguments");
     set_device(ctx);
     if (index_rate > 0 && !ctx->ivf) throw Error(RVCX_E_STATE, "index_rate > 0 but no feature index loaded");
     const int64_t no = vc_forward(*ctx, d_audio, n, d_pitch, d_pitchf, n / 160, sid, protect, index_rate, d_eps_z,

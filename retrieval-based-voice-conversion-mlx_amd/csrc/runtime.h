@@ -55,6 +55,8 @@ struct SynthCfg {
   std::vector<int> up_k{24, 20, 4, 4};
   int n_spk = 109, gin = 256, sr = 48000, emb_dim = 768;
   int window = 10, flow_k = 5, flow_layers = 3, flow_n = 4;
+  bool f0 = true;   // pitch-guided (NSF decoders) or not (HiFiGANGenerator): synthesizers.py:84-139
+  int vocoder = 0;  // 0 HiFi-GAN (NSF), 1 MRF HiFi-GAN, 2 RefineGAN (synthesizers.py:86-118)
   int upp() const {
     int u = 1;
     for (int x : ups) u *= x;

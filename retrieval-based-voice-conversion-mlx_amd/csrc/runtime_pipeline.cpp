@@ -114,7 +114,9 @@ int64_t vc_forward(Ctx& c, const float* audio, int64_t n, const int32_t* pitch, 
   }
   const int T = (int)std::min<int64_t>(n / 160, 2 * L);
   if (T <= 0) throw Error(RVCX_E_SHAPE, "voice_conversion: input shorter than one frame");
-  if (T > pitch_len) throw Error(RVCX_E_SHAPE, "voice_conversion: pitch track shorter than the features");
+  if (c.scfg.f0 && (!pitch || !pitchf)) throw Error(RVCX_E_INVALID, "voice_conversion: pitch-guided model needs pitch");
+  if (!c.scfg.f0) pitch = nullptr, pitchf = nullptr;  // pitch_guidance False: no protect, no pitch (pipeline.py:324-365)
+  if (pitch && T > pitch_len) throw Error(RVCX_E_SHAPE, "voice_conversion: pitch track shorter than the features");
   const int upp = c.scfg.upp();
   if ((int64_t)T * upp > cap)
     throw Error(RVCX_E_CAPACITY, "voice_conversion: output needs " + std::to_string((int64_t)T * upp) + " samples");
@@ -229,7 +231,9 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
     const int v = e ? std::atoi(e) : 6;
     return v < 0 ? 0 : (v > HUBERT_LAYERS ? HUBERT_LAYERS : v);
   }();
-  const int split = ax != s ? gate_layer : HUBERT_LAYERS;
+  // without pitch guidance there is no RMVPE (pipeline.py:461-472 skipped): HuBERT runs in one piece
+  const bool guided = c.scfg.f0;
+  const int split = (ax != s && guided) ? gate_layer : HUBERT_LAYERS;
   std::vector<HubertRun> hruns(chunks.size());
   for (size_t i = 0; i < chunks.size(); ++i) {
     const int64_t len = chunks[i].a1 - chunks[i].a0;
@@ -259,6 +263,9 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
   c.before_gru = hubert_rest;
   // 5. f0 over the whole padded input (pipeline.py:462-472) + get_f0 adjustments (:248-291)
   const int64_t F = 1 + m / W;
+  int32_t* pitch = nullptr;
+  float* pitchf = nullptr;
+  if (guided) {
   double* f0 = c.buf<double>("pl.f0", (size_t)F, s);
   rmvpe_forward(c, pad32, m, o.rmvpe_threshold > 0 ? o.rmvpe_threshold : 0.03f, f0, F, nullptr, s);
   if (c.before_gru) {  // RMVPE did not reach a BiGRU launch (cannot happen for valid input): issue it now
@@ -277,9 +284,15 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
     c.check_device_status();
     shift_semitones = o.pitch + proposed_key(h, o.proposed_pitch_threshold);
   }
-  int32_t* pitch = c.buf<int32_t>("pl.pitch", (size_t)F, s);
-  float* pitchf = c.buf<float>("pl.pitchf", (size_t)F, s);
+  pitch = c.buf<int32_t>("pl.pitch", (size_t)F, s);
+  pitchf = c.buf<float>("pl.pitchf", (size_t)F, s);
   check(f0_post(f0, (int)F, std::pow(2.0, shift_semitones / 12.0), pitch, pitchf, f0_out, s), "f0_post");
+  } else {
+    auto rest = std::move(c.before_gru);
+    c.before_gru = nullptr;
+    rest(s);
+    if (f0_out) RVCX_HIP(hipMemsetAsync(f0_out, 0, sizeof(double) * (size_t)F, s));
+  }
   join_aux(c, s, ax);
   // 6. voice conversion per chunk (pipeline.py:486-512), outputs trimmed t_pad_tgt per side
   const int upp = c.scfg.upp();
@@ -292,7 +305,8 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
     const int64_t cap_vc = (len / W) * upp;
     float* vc = c.buf<float>("pl.vc", (size_t)std::max<int64_t>(cap_vc, 1), s);
     // pitch[:, f_lo:f_hi], then [:p_len] inside voice_conversion with p_len = min(len/160, 2L)
-    const int64_t nvc = vc_forward(c, pad32 + ch.a0, len, pitch + ch.f_lo, pitchf + ch.f_lo, ch.f_hi - ch.f_lo, o.sid,
+    const int64_t nvc = vc_forward(c, pad32 + ch.a0, len, pitch ? pitch + ch.f_lo : nullptr,
+                                   pitchf ? pitchf + ch.f_lo : nullptr, ch.f_hi - ch.f_lo, o.sid,
                                    o.protect, o.index_rate, eps_z ? eps_z + ez_off : nullptr,
                                    eps_src ? eps_src + es_off : nullptr, cseed, vc, cap_vc, s, cfeats[i], cL[i]);
     const int64_t T = nvc / upp;
@@ -351,6 +365,10 @@ int64_t pipeline_forward_batch(Ctx& c, const double* audio, int64_t n, int64_t l
   float* feats = c.buf<float>("pb.feats", (size_t)B * L * E, s);
   hipStream_t ax = fork_aux(c, s);  // batched HuBERT beside batched RMVPE
   hubert_forward_b(c, pad32, m, ldm, B, hubert_version_for(c), feats, L, ax);
+  const bool guided = c.scfg.f0;  // no RMVPE, pitch or protect without pitch guidance (pipeline.py:324-365)
+  int32_t* pitch = nullptr;
+  float* pitchf = nullptr;
+  if (guided) {
   rmvpe_forward_b(c, pad32, m, ldm, B, o.rmvpe_threshold > 0 ? o.rmvpe_threshold : 0.03f, f0, F, nullptr, s);
   std::vector<double> shift(B, o.pitch);
   if (o.f0_autotune) {
@@ -366,12 +384,13 @@ int64_t pipeline_forward_batch(Ctx& c, const double* audio, int64_t n, int64_t l
       shift[b] = o.pitch + proposed_key(one, o.proposed_pitch_threshold);
     }
   }
-  int32_t* pitch = c.buf<int32_t>("pb.pitch", (size_t)B * F, s);
-  float* pitchf = c.buf<float>("pb.pitchf", (size_t)B * F, s);
+  pitch = c.buf<int32_t>("pb.pitch", (size_t)B * F, s);
+  pitchf = c.buf<float>("pb.pitchf", (size_t)B * F, s);
   for (int b = 0; b < B; ++b)
     check(f0_post(f0 + (size_t)b * F, (int)F, std::pow(2.0, shift[b] / 12.0), pitch + (size_t)b * F,
                   pitchf + (size_t)b * F, nullptr, s),
           "f0_post");
+  }
   // 3. batched HuBERT, retrieval, x2 upsample + protect (pipeline.py:327-362)
   join_aux(c, s, ax);
   const int64_t Tv = std::min<int64_t>(T, 2 * L);
@@ -384,15 +403,19 @@ int64_t pipeline_forward_batch(Ctx& c, const double* audio, int64_t n, int64_t l
     fx = fr;
   }
   float* phone = c.buf<float>("pb.phone", (size_t)B * Tv * E, s);
-  int32_t* pc = c.buf<int32_t>("pb.pc", (size_t)B * Tv, s);
-  float* pf = c.buf<float>("pb.pf", (size_t)B * Tv, s);
-  RVCX_HIP(hipMemcpy2DAsync(pc, Tv * sizeof(int32_t), pitch, F * sizeof(int32_t), Tv * sizeof(int32_t), B,
-                            hipMemcpyDeviceToDevice, s));
-  RVCX_HIP(hipMemcpy2DAsync(pf, Tv * sizeof(float), pitchf, F * sizeof(float), Tv * sizeof(float), B,
-                            hipMemcpyDeviceToDevice, s));
+  int32_t* pc = nullptr;
+  float* pf = nullptr;
+  if (guided) {
+    pc = c.buf<int32_t>("pb.pc", (size_t)B * Tv, s);
+    pf = c.buf<float>("pb.pf", (size_t)B * Tv, s);
+    RVCX_HIP(hipMemcpy2DAsync(pc, Tv * sizeof(int32_t), pitch, F * sizeof(int32_t), Tv * sizeof(int32_t), B,
+                              hipMemcpyDeviceToDevice, s));
+    RVCX_HIP(hipMemcpy2DAsync(pf, Tv * sizeof(float), pitchf, F * sizeof(float), Tv * sizeof(float), B,
+                              hipMemcpyDeviceToDevice, s));
+  }
   for (int b = 0; b < B; ++b)
     check(upsample2_protect(fx + (size_t)b * L * E, feats + (size_t)b * L * E, (int)L, E, phone + (size_t)b * Tv * E,
-                            (int)Tv, o.protect < 0.5f ? pf + (size_t)b * Tv : nullptr, o.protect, s),
+                            (int)Tv, (guided && o.protect < 0.5f) ? pf + (size_t)b * Tv : nullptr, o.protect, s),
           "upsample");
   // 4. one batched Synthesizer.infer (pipeline.py:365-372)
   int32_t* meta = c.buf<int32_t>("pb.meta", 2 * (size_t)B, s);

@@ -224,6 +224,8 @@ void rt_process(Ctx& c, RtState& s, const float* in48, const int32_t* sids, cons
   float* feats = c.buf<float>("rt.feats", (size_t)B * L * E, st);
   hipStream_t ax = fork_aux(c, st);  // batched HuBERT beside batched RMVPE (pipeline.py:233-254)
   hubert_forward_b(c, conv, s.conv16, s.conv16, B, hubert_version_for(c), feats, L, ax);
+  const bool guided = c.scfg.f0;  // no get_f0, pitch or protect without pitch guidance (pipeline.py:242-293)
+  if (guided) {
   rmvpe_forward_b(c, conv + s.silence_front, nf, s.conv16, B, 0.03f, f0, F, nullptr, st);
   std::vector<double> fac(B, std::pow(2.0, o.f0_up_key / 12.0));
   if (o.f0_autotune) {
@@ -244,6 +246,7 @@ void rt_process(Ctx& c, RtState& s, const float* in48, const int32_t* sids, cons
                  static_cast<int*>(s.pbuf[nxt].p), static_cast<const float*>(s.fbuf[s.cur].p),
                  static_cast<float*>(s.fbuf[nxt].p), s.pbuf_n, B, st),
         "rt_pitch");
+  }
   // 3. HuBERT over the B convert buffers (pipeline.py:248-254), rows [B][L][E]
   join_aux(c, st, ax);
   // 4. index retrieval of rows skip_head // 2 .. (pipeline.py:264-268, :336-352)
@@ -267,7 +270,7 @@ void rt_process(Ctx& c, RtState& s, const float* in48, const int32_t* sids, cons
   const double formant = std::ceil(s.return_length * 1.0);
   const float pscale = (float)(formant / (double)s.return_length);
   check(rt_up2(fx, feats, (int)L, E, phone, T, static_cast<const float*>(s.fbuf[nxt].p), s.pbuf_n, pscale, o.protect,
-               o.protect < 0.5f ? 1 : 0, pitch, static_cast<const int*>(s.pbuf[nxt].p), pitchf, B, st),
+               (guided && o.protect < 0.5f) ? 1 : 0, pitch, static_cast<const int*>(s.pbuf[nxt].p), pitchf, B, st),
         "rt_up2");
   // 6. one batched Synthesizer.infer over the B streams (pipeline.py:295-297), clip (:93)
   std::vector<int32_t> meta(2 * (size_t)B);
@@ -279,7 +282,8 @@ void rt_process(Ctx& c, RtState& s, const float* in48, const int32_t* sids, cons
   RVCX_HIP(hipMemcpyAsync(dmeta, meta.data(), sizeof(int32_t) * meta.size(), hipMemcpyHostToDevice, st));
   const int64_t n_model = (int64_t)T * upp;
   float* model = c.buf<float>("rt.model", (size_t)B * n_model, st);
-  synth_forward(c, B, T, phone, dmeta, pitch, pitchf, dmeta + B, eps_z, eps_src, seed, model, nullptr, nullptr, st);
+  synth_forward(c, B, T, phone, dmeta, guided ? pitch : nullptr, guided ? pitchf : nullptr, dmeta + B, eps_z, eps_src,
+                seed, model, nullptr, nullptr, st);
   (void)I;
   check(rt_clip(model, n_model, (int)n_model, B, st), "rt_clip");
   if (o.volume_envelope != 1.0) {  // pipeline.py:299-307 (source = the 16 kHz convert buffer)

@@ -126,7 +126,7 @@ void finalize_synth(Ctx& c) {
   // TextEncoder (encoders.py:88-144)
   c.alloc_weight("te.emb_phone.w", get(c, M, "enc_p.emb_phone.weight", {H, E}).v);
   c.alloc_weight("te.emb_phone.b", get(c, M, "enc_p.emb_phone.bias", {H}).v);
-  c.alloc_weight("te.emb_pitch", get(c, M, "enc_p.emb_pitch.weight", {256, H}).v);
+  if (g.f0) c.alloc_weight("te.emb_pitch", get(c, M, "enc_p.emb_pitch.weight", {256, H}).v);
   for (int i = 0; i < g.n_layers; ++i) {
     const std::string p = "enc_p.encoder.attn_layers." + std::to_string(i);
     const std::string q = "te." + std::to_string(i);
@@ -178,13 +178,14 @@ void finalize_synth(Ctx& c) {
     c.alloc_weight(q + ".post.b", get(c, M, p + ".post.bias", {I / 2}).v);
   }
   c.alloc_weight("emb_g", get(c, M, "emb_g.weight", {g.n_spk, g.gin}).v);
-  // HiFiGAN-NSF (generators/hifigan_nsf.py:55-171)
+  // HiFiGAN-NSF (generators/hifigan_nsf.py:55-171); without pitch guidance the plain HiFiGANGenerator
+  // (generators/hifigan.py:9-104): the same conv_pre / cond / ups / resblocks / conv_post, no source module
   const int C0 = g.C0;
   c.alloc_weight("dec.pre.w", pack_conv1d(get(c, M, "dec.conv_pre.weight", {C0, I, 7})));
   c.alloc_weight("dec.pre.b", get(c, M, "dec.conv_pre.bias", {C0}).v);
   c.alloc_weight("dec.cond.w", get(c, M, "dec.cond.weight", {C0, g.gin, 1}).v);
   c.alloc_weight("dec.cond.b", get(c, M, "dec.cond.bias", {C0}).v);
-  {
+  if (g.f0) {
     auto& lw = get(c, M, "dec.m_source.l_linear.weight", {1, 1}).v;
     auto& lb = get(c, M, "dec.m_source.l_linear.bias", {1}).v;
     c.alloc_weight("dec.src.lin", {lw[0], lb[0]});
@@ -194,8 +195,10 @@ void finalize_synth(Ctx& c) {
   const int nu = (int)g.ups.size();
   for (int i = 0; i < nu; ++i) {
     const int cin = C0 >> i, cout = C0 >> (i + 1), u = g.ups[i], k = g.up_k[i];
-    const int p = (u % 2 == 0) ? (k - u) / 2 : u / 2 + u % 2;
-    const int op = u % 2;
+    // NSF: padding (k - u) / 2 or u / 2 + u % 2 with output_padding u % 2 (hifigan_nsf.py:88-103);
+    // HiFiGANGenerator: padding (k - u) / 2, no output_padding (hifigan.py:46-58)
+    const int p = (!g.f0 || u % 2 == 0) ? (k - u) / 2 : u / 2 + u % 2;
+    const int op = g.f0 ? u % 2 : 0;
     if (k + op - 2 * p != u)
       throw Error(RVCX_E_SHAPE, "ConvTranspose1d stage " + std::to_string(i) + ": output length != T*u unsupported");
     const std::string n = "dec.ups." + std::to_string(i);
@@ -232,6 +235,7 @@ void finalize_synth(Ctx& c) {
     L.w = c.alloc_weight(n + ".vw", wv);
     L.b = c.alloc_weight(n + ".vb", bv);
     c.ups.push_back(L);
+    if (!g.f0) continue;
     // noise conv (C_in = 1)
     int stride = 1;
     for (int j = i + 1; j < nu; ++j) stride *= g.ups[j];
@@ -281,13 +285,16 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
   // NSF source (SineGen + l_linear + tanh)
   // har rows carry HAR_PAD zeros on both sides so every framed noise-conv read stays in its row
   const long long har_ld = Nh + 2 * HAR_PAD;
-  float* har = c.buf<float>("dec.har", (size_t)(B * har_ld), s);
-  RVCX_HIP(hipMemsetAsync(har, 0, sizeof(float) * (size_t)(B * har_ld), s));
-  double* cum = c.buf<double>("dec.cum", (size_t)B * T, s);
-  const auto& lin_wb = c.host[0].at("__src_lin__").v;
-  check(sine_source(f0, B, T, upp, (float)cf.sr, eps_src, splitmix(seed ^ 0x5352434e4f495345ull), lin_wb[0],
-                    lin_wb[1], cum, har + HAR_PAD, har_ld, s),
-        "sine_source");
+  float* har = nullptr;
+  if (cf.f0) {
+    har = c.buf<float>("dec.har", (size_t)(B * har_ld), s);
+    RVCX_HIP(hipMemsetAsync(har, 0, sizeof(float) * (size_t)(B * har_ld), s));
+    double* cum = c.buf<double>("dec.cum", (size_t)B * T, s);
+    const auto& lin_wb = c.host[0].at("__src_lin__").v;
+    check(sine_source(f0, B, T, upp, (float)cf.sr, eps_src, splitmix(seed ^ 0x5352434e4f495345ull), lin_wb[0],
+                      lin_wb[1], cum, har + HAR_PAD, har_ld, s),
+          "sine_source");
+  }
   // conv_pre + cond(g)
   float* cv = c.buf<float>("dec.cvec", (size_t)B * C0, s);
   run(c, lin(g, cf.gin, B, cf.gin, c.W("dec.cond.w"), C0, c.W("dec.cond.b"), cv, C0), s);
@@ -326,7 +333,7 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
     a.pre_slope = 0.1f;
     run(c, a, s, 2.0 * B * curT * (double)Cin * C * L.k);
     // + noise_convs[i](har) (hifigan_nsf.py:196-199): framed implicit GEMM, accumulated into y
-    {
+    if (cf.f0) {
       int stride = 1;
       for (size_t j = i + 1; j < cf.ups.size(); ++j) stride *= cf.ups[j];
       const int kern = stride == 1 ? 1 : stride * 2 - stride % 2;
@@ -396,14 +403,18 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
   float* g = c.buf<float>("spk.g", (size_t)B * cf.gin, s);
   check(gather_rows(c.W("emb_g"), cf.gin, sid, g, B, cf.gin, s), "emb_g");
   // ---- TextEncoder (encoders.py:128-144)
-  float* pe = c.buf<float>("te.pe", BT * H, s);
-  check(gather_rows(c.W("te.emb_pitch"), H, pitch, pe, (int)BT, H, s), "emb_pitch");
+  // x = emb_phone(phone) [+ emb_pitch(pitch) when pitch-guided, encoders.py:131-133]
+  float* pe = nullptr;
+  if (cf.f0) {
+    pe = c.buf<float>("te.pe", BT * H, s);
+    check(gather_rows(c.W("te.emb_pitch"), H, pitch, pe, (int)BT, H, s), "emb_pitch");
+  }
   float* x = c.buf<float>("te.x", BT * H, s);
   {
     ConvArgs a = lin(phone, E, (int)BT, E, c.W("te.emb_phone.w"), H, c.W("te.emb_phone.b"), x, H);
     a.res = pe;
     a.ldr = H;
-    a.res_mode = RES_ADD_PRE;
+    a.res_mode = pe ? RES_ADD_PRE : RES_NONE;
     a.alpha = (float)std::sqrt((double)H);
     a.act = ACT_LRELU;
     a.slope = 0.1f;

@@ -51,8 +51,11 @@ class SynthDesc(ctypes.Structure):
         ("n_upsample", ctypes.c_int), ("upsample_rates", ctypes.c_int * 8),
         ("upsample_initial_channel", ctypes.c_int), ("upsample_kernel_sizes", ctypes.c_int * 8),
         ("spk_embed_dim", ctypes.c_int), ("gin_channels", ctypes.c_int), ("sr", ctypes.c_int),
-        ("text_enc_hidden_dim", ctypes.c_int),
+        ("text_enc_hidden_dim", ctypes.c_int), ("no_f0", ctypes.c_int), ("vocoder", ctypes.c_int),
     ]
+
+
+VOCODERS = {"HiFi-GAN": 0, "MRF HiFi-GAN": 1, "RefineGAN": 2}
 
 
 class PipelineOpts(ctypes.Structure):

@@ -45,6 +45,8 @@ class SynthConfig:
     flow_kernel: int = 5  # synthesizers.py:154-161 (ResidualCouplingBlock(..., 5, 1, 3))
     flow_layers: int = 3
     flow_n: int = 4
+    use_f0: bool = True  # cpt["f0"]: pitch-guided (NSF decoders) or the plain HiFiGANGenerator (synthesizers.py:84-139)
+    vocoder: str = "HiFi-GAN"  # cpt["vocoder"] (infer.py:478): "HiFi-GAN" | "MRF HiFi-GAN" | "RefineGAN"
 
     @property
     def upp(self) -> int:

@@ -89,6 +89,10 @@ class Engine:
         d.upsample_initial_channel = cfg.upsample_initial_channel
         d.spk_embed_dim, d.gin_channels, d.sr = cfg.spk_embed_dim, cfg.gin_channels, cfg.sr
         d.text_enc_hidden_dim = cfg.text_enc_hidden_dim
+        d.no_f0 = 0 if cfg.use_f0 else 1
+        if cfg.vocoder not in _lib.VOCODERS:
+            raise ValueError(f"unknown vocoder {cfg.vocoder!r}; expected one of {sorted(_lib.VOCODERS)}")
+        d.vocoder = _lib.VOCODERS[cfg.vocoder]
         self._check(self.lib.rvcx_set_synth_config(self.ctx, ctypes.byref(d)), "set_synth_config")
         self.synth_cfg = cfg
 
@@ -201,8 +205,8 @@ class Engine:
         ph = self._dev(phone, t.float32)
         B, T = int(ph.shape[0]), int(ph.shape[1])
         ln = self._dev(lengths, t.int32).reshape(B)
-        pc = self._dev(pitch, t.int32).reshape(B, T)
-        pf = self._dev(pitchf, t.float32).reshape(B, T)
+        pc = None if pitch is None else self._dev(pitch, t.int32).reshape(B, T)
+        pf = None if pitchf is None else self._dev(pitchf, t.float32).reshape(B, T)
         sd = self._dev(sid, t.int32).reshape(B)
         ez = None if eps_z is None else self._dev(eps_z, t.float32)
         es = None if eps_src is None else self._dev(eps_src, t.float32)
@@ -210,8 +214,8 @@ class Engine:
         I = self.synth_cfg.inter_channels
         zp = t.empty((B, T, I), dtype=t.float32, device=self.device) if want_latents else None
         z = t.empty((B, T, I), dtype=t.float32, device=self.device) if want_latents else None
-        self._check(self.lib.rvcx_synth_infer(self.ctx, B, T, ph.data_ptr(), ln.data_ptr(), pc.data_ptr(),
-                                              pf.data_ptr(), sd.data_ptr(), _ptr(ez), _ptr(es),
+        self._check(self.lib.rvcx_synth_infer(self.ctx, B, T, ph.data_ptr(), ln.data_ptr(), _ptr(pc),
+                                              _ptr(pf), sd.data_ptr(), _ptr(ez), _ptr(es),
                                               ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), out.data_ptr(), _ptr(zp),
                                               _ptr(z), self.stream()), "synth_infer")
         return (out, zp, z) if want_latents else out
@@ -220,11 +224,11 @@ class Engine:
         t = self.torch
         zz = self._dev(z, t.float32)
         B, I, T = zz.shape
-        f = self._dev(f0, t.float32).reshape(B, T)
+        f = None if f0 is None else self._dev(f0, t.float32).reshape(B, T)
         sd = self._dev(sid, t.int32).reshape(B)
         es = None if eps_src is None else self._dev(eps_src, t.float32)
         out = t.empty((B, T * self.upp), dtype=t.float32, device=self.device)
-        self._check(self.lib.rvcx_dec_only(self.ctx, B, T, zz.data_ptr(), f.data_ptr(), sd.data_ptr(), _ptr(es),
+        self._check(self.lib.rvcx_dec_only(self.ctx, B, T, zz.data_ptr(), _ptr(f), sd.data_ptr(), _ptr(es),
                                            ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), out.data_ptr(),
                                            self.stream()), "dec_only")
         return out
@@ -235,14 +239,14 @@ class Engine:
         t = self.torch
         a = self._dev(audio_pad, t.float32).reshape(-1)
         n = a.numel()
-        pc = self._dev(pitch, t.int32).reshape(-1)
-        pf = self._dev(pitchf, t.float32).reshape(-1)
+        pc = None if pitch is None else self._dev(pitch, t.int32).reshape(-1)
+        pf = None if pitchf is None else self._dev(pitchf, t.float32).reshape(-1)
         cap = (n // 160) * self.upp
         out = t.empty((cap,), dtype=t.float32, device=self.device)
         no = ctypes.c_int64(0)
         ez = None if eps_z is None else self._dev(eps_z, t.float32)
         es = None if eps_src is None else self._dev(eps_src, t.float32)
-        self._check(self.lib.rvcx_voice_conversion(self.ctx, a.data_ptr(), n, pc.data_ptr(), pf.data_ptr(), int(sid),
+        self._check(self.lib.rvcx_voice_conversion(self.ctx, a.data_ptr(), n, _ptr(pc), _ptr(pf), int(sid),
                                                    float(protect), float(index_rate), _ptr(ez), _ptr(es),
                                                    ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), out.data_ptr(), cap,
                                                    ctypes.byref(no), self.stream()), "voice_conversion")

@@ -53,16 +53,16 @@ def mlx_to_reference_state(weights: Mapping[str, np.ndarray]) -> Dict[str, np.nd
 
 def load_voice_model(path: str):
     """-> (fused reference-name state, SynthConfig, version)."""
+    import dataclasses
+
     if path.endswith(".pth"):
         state, cfg_list, meta = load_rvc_checkpoint(path)
         version = meta.get("version") or "v1"
         cfg = SynthConfig.from_list(cfg_list)
         if version == "v1":
-            import dataclasses
-
             cfg = dataclasses.replace(cfg, text_enc_hidden_dim=256)
-        if not meta.get("f0", 1):
-            raise NotImplementedError(f"{path}: models without pitch guidance (f0 = 0) are not supported")
+        cfg = dataclasses.replace(cfg, use_f0=bool(meta.get("f0", 1)),
+                                  vocoder=str(meta.get("vocoder") or "HiFi-GAN"))
         return state, cfg, version
     if path.endswith(".npz") or path.endswith(".safetensors"):
         if path.endswith(".npz"):
@@ -145,6 +145,7 @@ class RVCX:
         self.engine.load_hubert(hubert_state)
         self.engine.load_rmvpe(rmvpe_state)
         self.tgt_sr = self.engine.synth_cfg.sr
+        self.use_f0 = bool(self.engine.synth_cfg.use_f0)  # pitch_guidance of infer.py:300
         self.net_g = Synthesizer(self.engine)
         self.hubert_model = HubertModel(self.engine, version)
         self.rmvpe_model = RMVPE0Predictor(self.engine)
@@ -157,7 +158,7 @@ class RVCX:
                 proposed_pitch=False, proposed_pitch_threshold=155.0, seed: int = 0) -> np.ndarray:
         """16 kHz mono audio -> converted float32 audio @tgt_sr (the body of infer_mlx.py:287-336)."""
         return self.pipeline.pipeline(self.hubert_model, self.net_g, sid, audio, pitch, f0_method, index_path,
-                                      index_rate, True, volume_envelope, self.version, protect, f0_autotune,
+                                      index_rate, self.use_f0, volume_envelope, self.version, protect, f0_autotune,
                                       f0_autotune_strength, proposed_pitch, proposed_pitch_threshold, seed=seed)
 
     def infer(self, audio_input, audio_output, pitch=0, f0_method="rmvpe", index_path=None, index_rate=0.75,

@@ -67,8 +67,11 @@ class Synthesizer:
             raise NotImplementedError("Synthesizer.infer(rate=...) (partial re-synthesis) is not supported")
         ph = _np(phone).astype(np.float32)
         B, T = ph.shape[0], ph.shape[1]
-        out, zp, z = self.engine.synth_infer(ph, _np(phone_lengths).reshape(B), _np(pitch).reshape(B, T),
-                                             _np(nsff0).reshape(B, T), _np(sid).reshape(B), eps_z=eps_z,
+        guided = bool(self.engine.synth_cfg.use_f0)  # synthesizers.py:233-239: pitch ignored without f0
+        out, zp, z = self.engine.synth_infer(ph, _np(phone_lengths).reshape(B),
+                                             _np(pitch).reshape(B, T) if guided else None,
+                                             _np(nsff0).reshape(B, T) if guided else None,
+                                             _np(sid).reshape(B), eps_z=eps_z,
                                              eps_src=eps_src, seed=seed, want_latents=True)
         lengths = _np(phone_lengths).reshape(B)
         x_mask = (np.arange(T)[None, :] < lengths[:, None]).astype(np.float32)[:, None, :]

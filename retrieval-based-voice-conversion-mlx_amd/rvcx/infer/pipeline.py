@@ -72,6 +72,14 @@ class PipelineRVCX:
         if m not in self.SUPPORTED_F0_METHODS:
             raise ValueError(f"f0_method {m!r} is not supported on this path (supported: {self.SUPPORTED_F0_METHODS})")
 
+    @staticmethod
+    def _check_guidance(eng, pitch_guidance: bool):
+        """pitch_guidance must match the loaded model (infer.py:300 passes cpt["f0"]): the reference fails on a
+        mismatch (pitchf.float() on None, pipeline.py:370; dec(z, None) for an NSF decoder); here it raises."""
+        model_f0 = bool(eng.synth_cfg.use_f0)
+        if pitch_guidance != model_f0:
+            raise ValueError(f"pitch_guidance={pitch_guidance} but the loaded model has f0={int(model_f0)}")
+
     def _engine(self, *models):
         for mdl in models + (self.hubert_model, self.rmvpe_model):
             if mdl is not None and getattr(mdl, "engine", None) is not None:
@@ -115,18 +123,20 @@ class PipelineRVCX:
 
     def voice_conversion(self, model, net_g, sid, audio0, pitch, pitchf, index=None, big_npy=None, index_rate=0.0,
                          version="v2", protect=0.33, eps_z=None, eps_src=None, seed: int = 0):
-        """One padded chunk: HuBERT -> x2 -> protect -> Synthesizer.infer. -> float32 [p_len * upp]."""
-        if pitch is None or pitchf is None:
-            raise NotImplementedError("models without pitch guidance (f0 = 0) are not supported")
+        """One padded chunk: HuBERT -> x2 -> protect -> Synthesizer.infer. -> float32 [p_len * upp].
+        pitch / pitchf None = pitch_guidance False (pipeline.py:324): no protect, the model's f0-less decoder."""
         eng = self._engine(model)
+        self._check_guidance(eng, pitch is not None and pitchf is not None)
         rate = 0.0
         if index is not None and index_rate > 0:  # pipeline.py:338-342 (big_npy is the index's own rows)
             if getattr(index, "engine", None) is not eng:
                 raise TypeError("index must be an rvcx IndexIVFFlat loaded on this pipeline's engine (read_index)")
             index._bound()
             rate = float(index_rate)
-        out = eng.voice_conversion(np.asarray(audio0, dtype=np.float32).reshape(-1), _np(pitch).reshape(-1),
-                                   _np(pitchf).reshape(-1), int(_np(sid).reshape(-1)[0]), float(protect),
+        out = eng.voice_conversion(np.asarray(audio0, dtype=np.float32).reshape(-1),
+                                   None if pitch is None else _np(pitch).reshape(-1),
+                                   None if pitchf is None else _np(pitchf).reshape(-1), int(_np(sid).reshape(-1)[0]),
+                                   float(protect),
                                    eps_z=eps_z, eps_src=eps_src, seed=seed, index_rate=rate)
         return out.cpu().numpy()
 
@@ -136,9 +146,8 @@ class PipelineRVCX:
                  eps_src=None, seed: int = 0):
         """Whole utterance -> float32 [N_out] @tgt_sr (pipeline.py:390-558)."""
         self._check_method(f0_method)
-        if not pitch_guidance:
-            raise NotImplementedError("models without pitch guidance (f0 = 0) are not supported")
         eng = self._engine(model)
+        self._check_guidance(eng, bool(pitch_guidance))
         # pipeline.py:430-436: the index is used only when the file exists and index_rate > 0 (a missing
         # file means no retrieval, as in the reference); a file that does not parse raises here.
         rate = 0.0

@@ -40,8 +40,9 @@ def synth_specs(cfg: SynthConfig = SYNTH_48K_V2) -> List[Spec]:
     s: List[Spec] = []
     # TextEncoder (encoders.py:88-144, attentions.py:6-243, normalization.py:4-26)
     s += [("enc_p.emb_phone.weight", (H, cfg.text_enc_hidden_dim), "linear"),
-          ("enc_p.emb_phone.bias", (H,), "bias"),
-          ("enc_p.emb_pitch.weight", (256, H), "embed")]
+          ("enc_p.emb_phone.bias", (H,), "bias")]
+    if cfg.use_f0:
+        s += [("enc_p.emb_pitch.weight", (256, H), "embed")]
     for i in range(cfg.n_layers):
         p = f"enc_p.encoder.attn_layers.{i}"
         for c in "qkvo":
@@ -59,7 +60,8 @@ def synth_specs(cfg: SynthConfig = SYNTH_48K_V2) -> List[Spec]:
     s += [("enc_p.proj.weight", (2 * I, H, 1), "proj"), ("enc_p.proj.bias", (2 * I,), "bias")]
     # HiFiGAN-NSF generator (generators/hifigan_nsf.py:55-171)
     C0 = cfg.upsample_initial_channel
-    s += [("dec.m_source.l_linear.weight", (1, 1), "src_lin"), ("dec.m_source.l_linear.bias", (1,), "bias")]
+    if cfg.use_f0:  # the plain HiFiGANGenerator (no pitch guidance) has no source module (hifigan.py:9-65)
+        s += [("dec.m_source.l_linear.weight", (1, 1), "src_lin"), ("dec.m_source.l_linear.bias", (1,), "bias")]
     s += [("dec.conv_pre.weight", (C0, I, 7), "conv"), ("dec.conv_pre.bias", (C0,), "bias")]
     chans = [C0 // (2 ** (i + 1)) for i in range(len(cfg.upsample_rates))]
     for i, (u, k) in enumerate(zip(cfg.upsample_rates, cfg.upsample_kernel_sizes)):
@@ -67,7 +69,7 @@ def synth_specs(cfg: SynthConfig = SYNTH_48K_V2) -> List[Spec]:
         s += _wn(f"dec.ups.{i}", (cin, chans[i], k), cin)
         s += [(f"dec.ups.{i}.bias", (chans[i],), "bias")]
     ups = list(cfg.upsample_rates)
-    for i in range(len(ups)):
+    for i in range(len(ups) if cfg.use_f0 else 0):
         stride = int(np.prod(ups[i + 1:])) if i + 1 < len(ups) else 1
         kern = 1 if stride == 1 else stride * 2 - stride % 2
         s += [(f"dec.noise_convs.{i}.weight", (chans[i], 1, kern), "noise"),

@@ -1,0 +1,83 @@
+"""Golden vectors for the synthesizer variants beside the default pitch-guided HiFi-GAN (NSF), by running the
+REFERENCE's own modules (survey container only; never on the GPU box).
+
+Run:  python tests/golden/make_golden_vocoders.py [nof0] [mrf] [refinegan]
+
+  nof0       Synthesizer(use_f0=False): TextEncoder without emb_pitch + HiFiGANGenerator
+             (rvc/lib/algorithm/synthesizers.py:84, :119-139, :233-239; generators/hifigan.py:9-104)
+Each fixture holds the inputs, the recorded RNG draws and the reference outputs; weights are regenerated from the
+seeds (rvcx.synthetic) by the tests. Harness as in make_golden.py (stubs, seeded noise streams).
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+import make_golden as mg  # noqa: E402  (sets sys.path, imports torch + transformers first)
+import torch  # noqa: E402
+
+from rvcx import synthetic  # noqa: E402
+from rvcx.config import SYNTH_48K_V2  # noqa: E402
+
+SEED_W = 21  # synthesizer weights of the variant fixtures
+SEED_IN = 23
+
+
+def build(cfg, vocoder: str):
+    from rvc.lib.algorithm.synthesizers import Synthesizer
+
+    net = Synthesizer(*cfg.as_list(), use_f0=cfg.use_f0, text_enc_hidden_dim=768, vocoder=vocoder)
+    del net.enc_q
+    net.eval()
+    sd = mg.to_torch_state(synthetic.synth_state(SEED_W, cfg))
+    ref = net.state_dict()
+    assert set(sd) == set(ref), (sorted(set(ref) - set(sd))[:8], sorted(set(sd) - set(ref))[:8])
+    for k, v in ref.items():
+        assert tuple(v.shape) == tuple(sd[k].shape), (k, v.shape, sd[k].shape)
+    net.load_state_dict(sd, strict=True)
+    return net
+
+
+def nof0():
+    cfg = dataclasses.replace(SYNTH_48K_V2, use_f0=False)
+    net = build(cfg, "HiFi-GAN")
+    rng = np.random.Generator(np.random.PCG64(SEED_IN))
+    B, T = 2, 40
+    phone = rng.standard_normal((B, T, 768)).astype(np.float32)
+    lengths = np.array([40, 33], np.int64)
+    sid = np.array([5, 100], np.int64)
+    ns = mg.NoiseStream(SEED_IN + 1)
+    orig = torch.randn_like
+    torch.randn_like = ns
+    try:
+        with torch.no_grad():
+            o, x_mask, (z, z_p, m_p, logs_p) = net.infer(torch.from_numpy(phone), torch.from_numpy(lengths), None,
+                                                         None, torch.from_numpy(sid))
+    finally:
+        torch.randn_like = orig
+    assert len(ns.draws) == 1, len(ns.draws)  # only z_p's randn_like: the HiFiGANGenerator draws nothing
+    np.savez_compressed(os.path.join(mg.OUT, "synth_nof0_b2.npz"), phone=phone, lengths=lengths, sid=sid,
+                        eps_z=ns.draws[0], o=o.numpy(), z=z.numpy(), z_p=z_p.numpy(), seed_w=SEED_W)
+    print("synth_nof0_b2: o", o.shape, float(o.abs().max()), float(o.std()))
+
+
+def main():
+    mg.install_stubs()
+    sys.path.insert(0, mg.REF)
+    os.chdir(tempfile.mkdtemp(prefix="rvc_golden_voc_"))
+    torch.manual_seed(0)
+    torch.set_num_threads(8)
+    which = set(sys.argv[1:]) or {"nof0"}
+    if "nof0" in which:
+        nof0()
+
+
+if __name__ == "__main__":
+    main()

@@ -94,3 +94,23 @@ def test_pipeline_matches_reference(synth_w, hubert_w, rmvpe_w):
     assert out.shape == g["out"].shape
     assert rel_err(out, g["out"]) < 1e-3
     assert spectrogram_correlation(out, g["out"]) > 0.9999
+
+
+def test_synth_nof0_matches_reference():
+    """Models without pitch guidance (use_f0=False): TextEncoder without emb_pitch + HiFiGANGenerator, against
+    the reference Synthesizer(use_f0=False).infer (tests/golden/make_golden_vocoders.py nof0)."""
+    import dataclasses
+
+    from oracle import synth as osynth
+    from rvcx import synthetic
+    from rvcx.weights import normalize_state
+
+    g = golden("synth_nof0_b2.npz")
+    cfg = dataclasses.replace(SYNTH_48K_V2, use_f0=False)
+    w = normalize_state(synthetic.synth_state(int(g["seed_w"]), cfg))
+    assert "enc_p.emb_pitch.weight" not in w and "dec.m_source.l_linear.weight" not in w
+    o, mask, (z, z_p, m_p, logs_p) = osynth.synth_infer(w, cfg, _t(g["phone"]), _t(g["lengths"]), None, None,
+                                                        _t(g["sid"]), _t(g["eps_z"]), None)
+    assert rel_err(z_p, g["z_p"]) < 1e-5
+    assert rel_err(z, g["z"]) < 1e-5
+    assert rel_err(o, g["o"]) < 1e-4
