@@ -126,7 +126,9 @@ class OraclePipeline:
             plen = torch.tensor([p_len]).long()
             T = feats.shape[1]
             eps_z = self.noise_fn((1, self.sc.inter_channels, T), "z")
-            eps_src = self.noise_fn((1, T * self.sc.upp), "src")
+            voc = getattr(self.sc, "vocoder", "HiFi-GAN")
+            H = 9 if voc == "MRF HiFi-GAN" else 1  # source noise per decoder (include/rvcx.h layout)
+            eps_src = self.noise_fn((1, T * self.sc.upp * H + (H if voc != "HiFi-GAN" else 0)), "src")
             o = osynth.synth_infer(self.sw, self.sc, feats.float(), plen, pitch, pitchf.float(), sid,
                                    eps_z, eps_src)[0]
             return o[0, 0].float().numpy()

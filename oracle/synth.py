@@ -233,6 +233,89 @@ def hifigan_generator(w, cfg, x: Tensor, g: Tensor) -> Tensor:
     return torch.tanh(F.conv1d(x, _t(w, "dec.conv_post.weight"), None, padding=3))
 
 
+def harmonic_source(f0_up: Tensor, sr: int, harmonics: int, eps: Tensor, rand_ini: Tensor, lin_w: Tensor,
+                    lin_b: Optional[Tensor]) -> Tensor:
+    """SineGenerator + merge of the MRF / RefineGAN decoders (generators/hifigan_mrf.py:120-230, refinegan.py:158-236)
+    on the per-sample f0 [B, N, 1]; eps = randn_like(sine_waves) [B, N, H], rand_ini = torch.rand(B, H).
+    torch.cumsum of float32 on CPU accumulates in double: written so here."""
+    B, N, _ = f0_up.shape
+    f0_buf = torch.zeros(B, N, harmonics, dtype=torch.float32)
+    f0_buf[:, :, 0] = f0_up[:, :, 0]
+    for idx in range(harmonics - 1):
+        f0_buf[:, :, idx + 1] = f0_buf[:, :, 0] * (idx + 2)
+    rad = (f0_buf / sr) % 1
+    ini = rand_ini.clone()
+    ini[:, 0] = 0
+    rad[:, 0, :] = rad[:, 0, :] + ini
+    tmp = torch.cumsum(rad.double(), 1).float() % 1
+    idx = (tmp[:, 1:, :] - tmp[:, :-1, :]) < 0
+    shift = torch.zeros_like(rad)
+    shift[:, 1:, :] = idx * -1.0
+    sines = torch.sin(torch.cumsum((rad + shift).double(), dim=1).float() * 2 * np.pi) * 0.1
+    uv = (f0_up > 0).float()
+    amp = uv * 0.003 + (1 - uv) * 0.1 / 3
+    sw = sines * uv + amp * eps
+    return torch.tanh(F.linear(sw, lin_w, lin_b))  # [B, N, 1]
+
+
+def split_src_noise(eps_src: Tensor, B: int, N: int, harmonics: int):
+    """The C-ABI's flat MRF / RefineGAN source noise: [B][N][H] randn then [B][H] initial phases."""
+    e = eps_src.reshape(-1)
+    return e[: B * N * harmonics].reshape(B, N, harmonics), e[B * N * harmonics:].reshape(B, harmonics)
+
+
+def mrf_generator(w, cfg, x: Tensor, f0: Tensor, g: Tensor, eps_src: Tensor) -> Tensor:
+    """HiFiGANMRFGenerator.forward (generators/hifigan_mrf.py:300-330): nearest f0 upsampling, 9-harmonic source,
+    MRF blocks (= the NSF ResBlock dataflow), conv_post with bias."""
+    upp = cfg.upp
+    B = x.shape[0]
+    f0_up = F.interpolate(f0[:, None, :].float(), scale_factor=float(upp), mode="nearest").transpose(-1, -2)
+    eps, ini = split_src_noise(eps_src, B, f0_up.shape[1], 9)
+    har = harmonic_source(f0_up, cfg.sr, 9, eps, ini, _t(w, "dec.m_source.l_linear.weight"),
+                          _t(w, "dec.m_source.l_linear.bias")).transpose(-1, -2)
+    x = F.conv1d(x, _t(w, "dec.conv_pre.weight"), _t(w, "dec.conv_pre.bias"), padding=3)
+    x = x + F.conv1d(g, _t(w, "dec.cond.weight"), _t(w, "dec.cond.bias"))
+    ups = list(cfg.upsample_rates)
+    nk = len(cfg.resblock_kernel_sizes)
+    for i, (u, k) in enumerate(zip(ups, cfg.upsample_kernel_sizes)):
+        x = F.leaky_relu(x, 0.1)
+        pad = (k - u) // 2 if u % 2 == 0 else u // 2 + u % 2
+        x = F.conv_transpose1d(x, _t(w, f"dec.upsamples.{i}.weight"), _t(w, f"dec.upsamples.{i}.bias"), stride=u,
+                               padding=pad, output_padding=u % 2)
+        stride = int(np.prod(ups[i + 1:])) if i + 1 < len(ups) else 1
+        kern = 1 if stride == 1 else stride * 2 - stride % 2
+        npad = 0 if stride == 1 else (kern - stride) // 2
+        x = x + F.conv1d(har, _t(w, f"dec.noise_convs.{i}.weight"), _t(w, f"dec.noise_convs.{i}.bias"),
+                         stride=stride, padding=npad)
+        xs = 0
+        for j in range(nk):
+            kk, dil = cfg.resblock_kernel_sizes[j], cfg.resblock_dilation_sizes[j]
+            y = x
+            for m, d in enumerate(dil):  # MRFLayer: x + conv2(lrelu(conv1(lrelu(x))))  (:35-56)
+                p = f"dec.mrfs.{i}.{j}.layers.{m}"
+                t = F.conv1d(F.leaky_relu(y, 0.1), _t(w, p + ".conv1.weight"), _t(w, p + ".conv1.bias"),
+                             padding=(kk * d - d) // 2, dilation=d)
+                t = F.conv1d(F.leaky_relu(t, 0.1), _t(w, p + ".conv2.weight"), _t(w, p + ".conv2.bias"),
+                             padding=kk // 2)
+                y = y + t
+            xs = xs + y
+        x = xs / nk
+    x = F.leaky_relu(x)
+    return torch.tanh(F.conv1d(x, _t(w, "dec.conv_post.weight"), _t(w, "dec.conv_post.bias"), padding=3))
+
+
+def decoder(w, cfg, x: Tensor, f0, g: Tensor, eps_src) -> Tensor:
+    """The decoder Synthesizer selects (synthesizers.py:84-139)."""
+    if not getattr(cfg, "use_f0", True):
+        return hifigan_generator(w, cfg, x, g)
+    voc = getattr(cfg, "vocoder", "HiFi-GAN")
+    if voc == "MRF HiFi-GAN":
+        return mrf_generator(w, cfg, x, f0, g, eps_src)
+    if voc == "HiFi-GAN":
+        return nsf_generator(w, cfg, x, f0, g, eps_src)
+    raise ValueError(voc)
+
+
 def synth_infer(w, cfg, phone: Tensor, lengths: Tensor, pitch: Tensor, nsff0: Tensor, sid: Tensor,
                 eps_z: Tensor, eps_src: Tensor):
     """Synthesizer.infer (rvc/lib/algorithm/synthesizers.py:206-243) with the two RNG draws
@@ -243,10 +326,7 @@ def synth_infer(w, cfg, phone: Tensor, lengths: Tensor, pitch: Tensor, nsff0: Te
         m_p, logs_p, x_mask = text_encoder(w, cfg, phone, pitch if getattr(cfg, "use_f0", True) else None, lengths)
         z_p = (m_p + torch.exp(logs_p) * eps_z * 0.66666) * x_mask
         z = flow_reverse(w, cfg, z_p, x_mask, g)
-        if getattr(cfg, "use_f0", True):
-            o = nsf_generator(w, cfg, z * x_mask, nsff0, g, eps_src)
-        else:  # synthesizers.py:233-239: dec(z * x_mask, g=g)
-            o = hifigan_generator(w, cfg, z * x_mask, g)
+        o = decoder(w, cfg, z * x_mask, nsff0, g, eps_src)  # synthesizers.py:233-239
     return o, x_mask, (z, z_p, m_p, logs_p)
 
 
@@ -254,4 +334,4 @@ def dec_only(w, cfg, z: Tensor, nsff0: Tensor, sid: Tensor, eps_src: Tensor) -> 
     """Generator alone (config C3): HiFiGAN-NSF on latent z with speaker conditioning."""
     with torch.no_grad():
         g = F.embedding(sid, _t(w, "emb_g.weight")).unsqueeze(-1)
-        return nsf_generator(w, cfg, z, nsff0, g, eps_src)
+        return decoder(w, cfg, z, nsff0, g, eps_src)

@@ -416,7 +416,7 @@ hipError_t sine_source(const float* f0, int B, int L, int upp, float sr, const f
 // The C*K weights sit in LDS too: read from global inside the FMA loop (uniform address, possibly
 // aliasing y) they were one dependent vector load per FMA (80 us at C2).
 __global__ void k_conv_post(const float* __restrict__ x, int T, int C, const float* __restrict__ wg, int K,
-                            float slope, float* __restrict__ y) {
+                            float slope, float* __restrict__ y, float bias) {
   extern __shared__ float tile[];  // [(256+K-1)][C+1], then w[C*K]
   const int b = blockIdx.y;
   const int t0 = blockIdx.x * 256;
@@ -442,12 +442,12 @@ __global__ void k_conv_post(const float* __restrict__ x, int T, int C, const flo
   float acc = 0.f;
   for (int c = 0; c < C; ++c)
     for (int k = 0; k < K; ++k) acc = fmaf(tile[(threadIdx.x + k) * ldt + c], w[c * K + k], acc);
-  y[(long long)b * T + t] = tanhf(acc);
+  y[(long long)b * T + t] = tanhf(acc + bias);  // + 0 for the bias-free HiFi-GAN / RefineGAN conv_post
 }
 hipError_t conv_post_tanh(const float* x, int B, int T, int C, const float* w, int K, float slope, float* y,
-                          hipStream_t s) {
+                          hipStream_t s, float bias) {
   const size_t smem = ((size_t)(256 + K - 1) * (C + 1) + (size_t)C * K) * sizeof(float);
-  hipLaunchKernelGGL(k_conv_post, dim3((T + 255) / 256, B), dim3(256), smem, s, x, T, C, w, K, slope, y);
+  hipLaunchKernelGGL(k_conv_post, dim3((T + 255) / 256, B), dim3(256), smem, s, x, T, C, w, K, slope, y, bias);
   return hipGetLastError();
 }
 

@@ -62,6 +62,12 @@ struct SynthCfg {
     for (int x : ups) u *= x;
     return u;
   }
+  // harmonics of the decoder's source: NSF 1 (harmonic_num 0), MRF 9 (synthesizers.py:95), RefineGAN 1
+  int src_harmonics() const { return vocoder == 1 ? 9 : 1; }
+  // floats of injected source noise per batch row of T frames (the decoder's randn_like / rand draws):
+  // NSF [T*upp]; MRF / RefineGAN [T*upp][H] noise, the B x H initial phases of all rows follow the B rows
+  long long src_noise_row(long long T) const { return f0 ? T * upp() * src_harmonics() : 0; }
+  long long src_noise_tail() const { return (f0 && vocoder != 0) ? src_harmonics() : 0; }
 };
 
 // ConvTranspose1d lowered to a polyphase conv: input row for output q, tap t is q + t - pad.

@@ -185,10 +185,15 @@ void finalize_synth(Ctx& c) {
   c.alloc_weight("dec.pre.b", get(c, M, "dec.conv_pre.bias", {C0}).v);
   c.alloc_weight("dec.cond.w", get(c, M, "dec.cond.weight", {C0, g.gin, 1}).v);
   c.alloc_weight("dec.cond.b", get(c, M, "dec.cond.bias", {C0}).v);
+  // MRF HiFi-GAN (generators/hifigan_mrf.py:234-330) has the same dataflow under other names: upsamples.i for
+  // ups.i, mrfs.i.j.layers.m.conv1/conv2 for resblocks.(i*nk+j).convs1/convs2.m, a 9-harmonic source and a
+  // conv_post bias; its weights are packed under the NSF decoder's device names
+  const bool mrf = g.vocoder == 1;
+  const int Hs = g.src_harmonics();
   if (g.f0) {
-    auto& lw = get(c, M, "dec.m_source.l_linear.weight", {1, 1}).v;
+    auto& lw = get(c, M, "dec.m_source.l_linear.weight", {1, Hs}).v;
     auto& lb = get(c, M, "dec.m_source.l_linear.bias", {1}).v;
-    c.alloc_weight("dec.src.lin", {lw[0], lb[0]});
+    c.alloc_weight("dec.src.w", lw);
     c.host[M]["__src_lin__"] = HostTensor{{lw[0], lb[0]}, {2}};
   }
   c.ups.clear();
@@ -202,8 +207,9 @@ void finalize_synth(Ctx& c) {
     if (k + op - 2 * p != u)
       throw Error(RVCX_E_SHAPE, "ConvTranspose1d stage " + std::to_string(i) + ": output length != T*u unsupported");
     const std::string n = "dec.ups." + std::to_string(i);
-    auto& w = get(c, M, n + ".weight", {cin, cout, k});
-    auto& b = get(c, M, n + ".bias", {cout});
+    const std::string nref = (mrf ? "dec.upsamples." : "dec.ups.") + std::to_string(i);
+    auto& w = get(c, M, nref + ".weight", {cin, cout, k});
+    auto& b = get(c, M, nref + ".bias", {cout});
     auto fdiv = [](int a, int bb) { return (a >= 0) ? a / bb : -((-a + bb - 1) / bb); };
     int smin = 1 << 30, smax = -(1 << 30);
     for (int r = 0; r < u; ++r) {
@@ -263,16 +269,21 @@ void finalize_synth(Ctx& c) {
       const int k = g.rb_k[j];
       const std::string rb = "dec.resblocks." + std::to_string(i * nk + j);
       for (size_t m = 0; m < g.rb_d[j].size(); ++m) {
-        for (const char* cv : {"convs1", "convs2"}) {
-          const std::string n = rb + "." + cv + "." + std::to_string(m);
-          c.alloc_weight(n + ".w", pack_conv1d(get(c, M, n + ".weight", {C, C, k})));
-          c.alloc_weight(n + ".b", get(c, M, n + ".bias", {C}).v);
+        for (int q = 0; q < 2; ++q) {
+          const std::string n = rb + (q ? ".convs2." : ".convs1.") + std::to_string(m);
+          const std::string nref = mrf ? "dec.mrfs." + std::to_string(i) + "." + std::to_string(j) + ".layers." +
+                                             std::to_string(m) + (q ? ".conv2" : ".conv1")
+                                       : n;
+          c.alloc_weight(n + ".w", pack_conv1d(get(c, M, nref + ".weight", {C, C, k})));
+          c.alloc_weight(n + ".b", get(c, M, nref + ".bias", {C}).v);
         }
       }
     }
   }
   const int Cl = C0 >> nu;
   c.alloc_weight("dec.post.w", get(c, M, "dec.conv_post.weight", {1, Cl, 7}).v);
+  const float post_b = mrf ? get(c, M, "dec.conv_post.bias", {1}).v[0] : 0.f;  // weight_norm(Conv1d(ch, 1, 7))
+  c.host[M]["__post_b__"] = HostTensor{{post_b}, {1}};
 }
 
 // ------------------------------------------------------------------ generator
@@ -289,11 +300,21 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
   if (cf.f0) {
     har = c.buf<float>("dec.har", (size_t)(B * har_ld), s);
     RVCX_HIP(hipMemsetAsync(har, 0, sizeof(float) * (size_t)(B * har_ld), s));
-    double* cum = c.buf<double>("dec.cum", (size_t)B * T, s);
     const auto& lin_wb = c.host[0].at("__src_lin__").v;
-    check(sine_source(f0, B, T, upp, (float)cf.sr, eps_src, splitmix(seed ^ 0x5352434e4f495345ull), lin_wb[0],
-                      lin_wb[1], cum, har + HAR_PAD, har_ld, s),
-          "sine_source");
+    const uint64_t sseed = splitmix(seed ^ 0x5352434e4f495345ull);
+    if (cf.vocoder == 0) {  // NSF SineGen, harmonic_num 0 (hifigan.py:156-228)
+      double* cum = c.buf<double>("dec.cum", (size_t)B * T, s);
+      check(sine_source(f0, B, T, upp, (float)cf.sr, eps_src, sseed, lin_wb[0], lin_wb[1], cum, har + HAR_PAD,
+                        har_ld, s),
+            "sine_source");
+    } else {  // MRF: 9 harmonics, per-sample phase accumulation (hifigan_mrf.py:120-230)
+      const int Hs = cf.src_harmonics();
+      double* ws = c.buf<double>("dec.harm_ws", harm_source_ws_doubles(B, T, upp, Hs), s);
+      const float* ini = eps_src ? eps_src + (size_t)B * cf.src_noise_row(T) : nullptr;
+      check(harm_source(f0, B, T, upp, (float)cf.sr, Hs, 0, eps_src, ini, sseed, c.W("dec.src.w"), lin_wb[1], ws,
+                        har + HAR_PAD, har_ld, s),
+            "harm_source");
+    }
   }
   // conv_pre + cond(g)
   float* cv = c.buf<float>("dec.cvec", (size_t)B * C0, s);
@@ -388,7 +409,8 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
     Cin = C;
   }
   // LeakyReLU(0.01) -> conv_post (no bias) -> tanh
-  check(conv_post_tanh(cur, B, curT, Cin, c.W("dec.post.w"), 7, 0.01f, out, s), "conv_post");
+  check(conv_post_tanh(cur, B, curT, Cin, c.W("dec.post.w"), 7, 0.01f, out, s, c.host[0].at("__post_b__").v[0]),
+        "conv_post");
 }
 
 // ------------------------------------------------------------------ Synthesizer.infer

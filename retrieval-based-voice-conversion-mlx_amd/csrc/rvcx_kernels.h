@@ -129,7 +129,13 @@ hipError_t upsample2_protect(const float* feats, const float* feats0, int L, int
 hipError_t sine_source(const float* f0, int B, int L, int upp, float sr, const float* eps, uint64_t seed,
                        float lin_w, float lin_b, double* cum_ws, float* har, long long har_ld, hipStream_t s);
 hipError_t conv_post_tanh(const float* x, int B, int T, int C, const float* w, int K, float slope, float* y,
-                          hipStream_t s);
+                          hipStream_t s, float bias = 0.f);
+// per-sample harmonic source of the MRF HiFi-GAN / RefineGAN decoders (source_harm.hip): f0 [B][L] -> har row b
+// at har + b*har_ld, N = L*upp samples; eps [B][N][H] and ini [B][H] injected or drawn (Philox(seed))
+size_t harm_source_ws_doubles(int B, int L, int upp, int H);
+hipError_t harm_source(const float* f0, int B, int L, int upp, float sr, int H, int linear_up, const float* eps,
+                       const float* ini, uint64_t seed, const float* lin_w, float lin_b, double* ws, float* har,
+                       long long har_ld, hipStream_t st);
 hipError_t randn(float* y, long long n, uint64_t seed, uint64_t offset, hipStream_t s);
 hipError_t zp_sample(const float* stats, int B, int T, int I, const float* eps, uint64_t seed, const float* mask,
                      float* zp, hipStream_t s);

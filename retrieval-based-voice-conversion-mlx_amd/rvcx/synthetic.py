@@ -58,16 +58,26 @@ def synth_specs(cfg: SynthConfig = SYNTH_48K_V2) -> List[Spec]:
         s += [(f"enc_p.encoder.norm_layers_2.{i}.gamma", (H,), "ln_g"),
               (f"enc_p.encoder.norm_layers_2.{i}.beta", (H,), "ln_b")]
     s += [("enc_p.proj.weight", (2 * I, H, 1), "proj"), ("enc_p.proj.bias", (2 * I,), "bias")]
-    # HiFiGAN-NSF generator (generators/hifigan_nsf.py:55-171)
+    # HiFiGAN-NSF generator (generators/hifigan_nsf.py:55-171); MRF HiFi-GAN (generators/hifigan_mrf.py:234-330)
+    # has the same dataflow under other names, a 9-harmonic source, weight-normed conv_pre and a conv_post bias
     C0 = cfg.upsample_initial_channel
+    mrf = cfg.use_f0 and cfg.vocoder == "MRF HiFi-GAN"
     if cfg.use_f0:  # the plain HiFiGANGenerator (no pitch guidance) has no source module (hifigan.py:9-65)
-        s += [("dec.m_source.l_linear.weight", (1, 1), "src_lin"), ("dec.m_source.l_linear.bias", (1,), "bias")]
-    s += [("dec.conv_pre.weight", (C0, I, 7), "conv"), ("dec.conv_pre.bias", (C0,), "bias")]
+        if mrf:
+            s += [("dec.m_source.l_linear.weight", (1, 9), "linear"), ("dec.m_source.l_linear.bias", (1,), "bias")]
+        else:
+            s += [("dec.m_source.l_linear.weight", (1, 1), "src_lin"),
+                  ("dec.m_source.l_linear.bias", (1,), "bias")]
+    if mrf:
+        s += _wn("dec.conv_pre", (C0, I, 7), C0) + [("dec.conv_pre.bias", (C0,), "bias")]
+    else:
+        s += [("dec.conv_pre.weight", (C0, I, 7), "conv"), ("dec.conv_pre.bias", (C0,), "bias")]
     chans = [C0 // (2 ** (i + 1)) for i in range(len(cfg.upsample_rates))]
+    up_name = "dec.upsamples" if mrf else "dec.ups"
     for i, (u, k) in enumerate(zip(cfg.upsample_rates, cfg.upsample_kernel_sizes)):
         cin = C0 // (2 ** i)
-        s += _wn(f"dec.ups.{i}", (cin, chans[i], k), cin)
-        s += [(f"dec.ups.{i}.bias", (chans[i],), "bias")]
+        s += _wn(f"{up_name}.{i}", (cin, chans[i], k), cin)
+        s += [(f"{up_name}.{i}.bias", (chans[i],), "bias")]
     ups = list(cfg.upsample_rates)
     for i in range(len(ups) if cfg.use_f0 else 0):
         stride = int(np.prod(ups[i + 1:])) if i + 1 < len(ups) else 1
@@ -76,13 +86,22 @@ def synth_specs(cfg: SynthConfig = SYNTH_48K_V2) -> List[Spec]:
               (f"dec.noise_convs.{i}.bias", (chans[i],), "bias")]
     j = 0
     for i in range(len(ups)):
-        for k, dil in zip(cfg.resblock_kernel_sizes, cfg.resblock_dilation_sizes):
-            for c in ("convs1", "convs2"):
+        for jj, (k, dil) in enumerate(zip(cfg.resblock_kernel_sizes, cfg.resblock_dilation_sizes)):
+            if mrf:
                 for m in range(len(dil)):
-                    s += _wn(f"dec.resblocks.{j}.{c}.{m}", (chans[i], chans[i], k), chans[i])
-                    s += [(f"dec.resblocks.{j}.{c}.{m}.bias", (chans[i],), "bias")]
+                    for c in ("conv1", "conv2"):
+                        p = f"dec.mrfs.{i}.{jj}.layers.{m}.{c}"
+                        s += _wn(p, (chans[i], chans[i], k), chans[i]) + [(f"{p}.bias", (chans[i],), "bias")]
+            else:
+                for c in ("convs1", "convs2"):
+                    for m in range(len(dil)):
+                        s += _wn(f"dec.resblocks.{j}.{c}.{m}", (chans[i], chans[i], k), chans[i])
+                        s += [(f"dec.resblocks.{j}.{c}.{m}.bias", (chans[i],), "bias")]
             j += 1
-    s += [("dec.conv_post.weight", (1, chans[-1], 7), "post")]
+    if mrf:
+        s += _wn("dec.conv_post", (1, chans[-1], 7), 1) + [("dec.conv_post.bias", (1,), "bias")]
+    else:
+        s += [("dec.conv_post.weight", (1, chans[-1], 7), "post")]
     s += [("dec.cond.weight", (C0, cfg.gin_channels, 1), "conv"), ("dec.cond.bias", (C0,), "bias")]
     # flow (residuals.py:103-258, modules.py:5-117); odd indices are Flip
     half = I // 2

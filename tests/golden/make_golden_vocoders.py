@@ -5,6 +5,8 @@ Run:  python tests/golden/make_golden_vocoders.py [nof0] [mrf] [refinegan]
 
   nof0       Synthesizer(use_f0=False): TextEncoder without emb_pitch + HiFiGANGenerator
              (rvc/lib/algorithm/synthesizers.py:84, :119-139, :233-239; generators/hifigan.py:9-104)
+  mrf        Synthesizer(vocoder="MRF HiFi-GAN"): HiFiGANMRFGenerator with the 9-harmonic source
+             (synthesizers.py:86-98; generators/hifigan_mrf.py); torch.rand (initial phases) recorded too
 Each fixture holds the inputs, the recorded RNG draws and the reference outputs; weights are regenerated from the
 seeds (rvcx.synthetic) by the tests. Harness as in make_golden.py (stubs, seeded noise streams).
 """
@@ -68,6 +70,49 @@ def nof0():
     print("synth_nof0_b2: o", o.shape, float(o.abs().max()), float(o.std()))
 
 
+class UniformStream:
+    """Replaces torch.rand: seeded PCG64 uniforms in [0, 1), recorded in call order."""
+
+    def __init__(self, seed):
+        self.rng = np.random.Generator(np.random.PCG64(seed))
+        self.draws = []
+
+    def __call__(self, *size, **kw):
+        if len(size) == 1 and isinstance(size[0], (tuple, list)):
+            size = tuple(size[0])
+        x = self.rng.random(size).astype(np.float32)
+        self.draws.append(x)
+        return torch.from_numpy(x.copy())
+
+
+def mrf():
+    cfg = dataclasses.replace(SYNTH_48K_V2, vocoder="MRF HiFi-GAN")
+    net = build(cfg, "MRF HiFi-GAN")
+    rng = np.random.Generator(np.random.PCG64(SEED_IN + 10))
+    B, T = 2, 24
+    phone = rng.standard_normal((B, T, 768)).astype(np.float32)
+    f0 = synthetic.f0_walk(B, T, seed=SEED_IN + 11)
+    pitch = rng.integers(1, 256, size=(B, T)).astype(np.int64)
+    lengths = np.array([24, 19], np.int64)
+    sid = np.array([1, 7], np.int64)
+    ns, us = mg.NoiseStream(SEED_IN + 12), UniformStream(SEED_IN + 13)
+    orig_n, orig_u = torch.randn_like, torch.rand
+    torch.randn_like, torch.rand = ns, us
+    try:
+        with torch.no_grad():
+            o, x_mask, (z, z_p, m_p, logs_p) = net.infer(torch.from_numpy(phone), torch.from_numpy(lengths),
+                                                         torch.from_numpy(pitch), torch.from_numpy(f0),
+                                                         torch.from_numpy(sid))
+    finally:
+        torch.randn_like, torch.rand = orig_n, orig_u
+    assert len(ns.draws) == 2 and len(us.draws) == 1, (len(ns.draws), len(us.draws))
+    eps_src = np.concatenate([ns.draws[1].reshape(-1), us.draws[0].reshape(-1)])  # C-ABI layout (include/rvcx.h)
+    np.savez_compressed(os.path.join(mg.OUT, "synth_mrf_b2.npz"), phone=phone, f0=f0, pitch=pitch, lengths=lengths,
+                        sid=sid, eps_z=ns.draws[0], eps_src=eps_src, o=o.numpy(), z=z.numpy(), z_p=z_p.numpy(),
+                        seed_w=SEED_W)
+    print("synth_mrf_b2: o", o.shape, float(o.abs().max()), float(o.std()))
+
+
 def main():
     mg.install_stubs()
     sys.path.insert(0, mg.REF)
@@ -77,6 +122,8 @@ def main():
     which = set(sys.argv[1:]) or {"nof0"}
     if "nof0" in which:
         nof0()
+    if "mrf" in which:
+        mrf()
 
 
 if __name__ == "__main__":

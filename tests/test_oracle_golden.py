@@ -114,3 +114,21 @@ def test_synth_nof0_matches_reference():
     assert rel_err(z_p, g["z_p"]) < 1e-5
     assert rel_err(z, g["z"]) < 1e-5
     assert rel_err(o, g["o"]) < 1e-4
+
+
+def test_synth_mrf_matches_reference():
+    """MRF HiFi-GAN decoder (9-harmonic source with per-sample phase accumulation, MRF blocks, conv_post bias)
+    against the reference Synthesizer(vocoder="MRF HiFi-GAN").infer (make_golden_vocoders.py mrf)."""
+    import dataclasses
+
+    from oracle import synth as osynth
+    from rvcx import synthetic
+    from rvcx.weights import normalize_state
+
+    g = golden("synth_mrf_b2.npz")
+    cfg = dataclasses.replace(SYNTH_48K_V2, vocoder="MRF HiFi-GAN")
+    w = normalize_state(synthetic.synth_state(int(g["seed_w"]), cfg))
+    o, mask, (z, z_p, m_p, logs_p) = osynth.synth_infer(w, cfg, _t(g["phone"]), _t(g["lengths"]), _t(g["pitch"]),
+                                                        _t(g["f0"]), _t(g["sid"]), _t(g["eps_z"]), _t(g["eps_src"]))
+    assert rel_err(z, g["z"]) < 1e-5
+    assert rel_err(o, g["o"]) < 1e-4, rel_err(o, g["o"])
