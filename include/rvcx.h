@@ -111,7 +111,9 @@ int rvcx_f0_autotune(rvcx_ctx* ctx, double* d_f0, int64_t F, double strength, in
  * phone [B][T][E], lengths [B], pitch [B][T], pitchf [B][T], sid [B] -> out [B][T*upp].
  * Source noise layout by decoder: HiFi-GAN (NSF) [B][T*upp] (randn_like, generators/hifigan.py:223); MRF HiFi-GAN
  * [B][T*upp][9] (randn_like(sine_waves), hifigan_mrf.py:222) followed by the [B][9] initial phases (torch.rand,
- * :174-178, element 0 of each row unused); no source for models without pitch guidance.
+ * :174-178, element 0 of each row unused); RefineGAN [B][T*upp] (randn_like, refinegan.py:233) then [B][1]
+ * (torch.rand, :203) then, per upsampling stage and ParallelResBlock branch j = 0..2, the AdaIN draws (in, out)
+ * [B][C_stage][T_stage] each (refinegan.py:90); no source for models without pitch guidance.
  * d_eps_z ([B][I][T], reference layout of randn_like(m_p)) and d_eps_src ([B][T*upp], randn_like at
  * generators/hifigan.py:223) are optional injected noise; when NULL the noise is drawn from the
  * context's Philox stream keyed by `seed`. d_zp / d_z (optional, [B][T][I]) receive z_p and z. */

@@ -36,8 +36,8 @@ AUDIO_SAMPLE_RATE = 48000
 
 
 def sinc_resample_kernel(orig_freq: int, new_freq: int, lowpass_filter_width: int = 6, rolloff: float = 0.99,
-                         dtype=torch.float32):
-    """torchaudio.functional.functional._get_sinc_resample_kernel (sinc_interp_hann)."""
+                         dtype=torch.float32, resampling_method: str = "sinc_interp_hann", beta=None):
+    """torchaudio.functional.functional._get_sinc_resample_kernel (sinc_interp_hann / sinc_interp_kaiser)."""
     gcd = math.gcd(int(orig_freq), int(new_freq))
     orig, new = int(orig_freq) // gcd, int(new_freq) // gcd
     base_freq = min(orig, new) * rolloff
@@ -46,12 +46,33 @@ def sinc_resample_kernel(orig_freq: int, new_freq: int, lowpass_filter_width: in
     t = torch.arange(0, -new, -1, dtype=dtype)[:, None, None] / new + idx
     t *= base_freq
     t = t.clamp_(-lowpass_filter_width, lowpass_filter_width)
-    window = torch.cos(t * math.pi / lowpass_filter_width / 2) ** 2
+    if resampling_method == "sinc_interp_hann":
+        window = torch.cos(t * math.pi / lowpass_filter_width / 2) ** 2
+    else:
+        beta_tensor = torch.tensor(float(14.769656459379492 if beta is None else beta))
+        window = torch.i0(beta_tensor * torch.sqrt(1 - (t / lowpass_filter_width) ** 2)) / torch.i0(beta_tensor)
     t *= math.pi
     scale = base_freq / orig
     kernels = torch.where(t == 0, torch.tensor(1.0).to(t), t.sin() / t)
     kernels *= window * scale
     return kernels, width, orig, new
+
+
+def functional_resample(waveform: torch.Tensor, orig_freq: int, new_freq: int, lowpass_filter_width: int = 6,
+                        rolloff: float = 0.99, resampling_method: str = "sinc_interp_hann", beta=None) -> torch.Tensor:
+    """torchaudio.functional.resample (kernel in the waveform's dtype; any leading dims)."""
+    if orig_freq == new_freq:
+        return waveform
+    kernel, width, orig, new = sinc_resample_kernel(orig_freq, new_freq, lowpass_filter_width, rolloff,
+                                                    waveform.dtype, resampling_method, beta)
+    shape = waveform.size()
+    w = waveform.reshape(-1, shape[-1])
+    length = w.shape[-1]
+    w = F.pad(w, (width, width + orig))
+    y = F.conv1d(w[:, None], kernel, stride=orig)
+    y = y.transpose(1, 2).reshape(w.shape[0], -1)
+    target = int(math.ceil(new * length / orig))
+    return y[..., :target].reshape(shape[:-1] + (min(target, y.shape[-1]),))
 
 
 def resample(x: torch.Tensor, orig_freq: int, new_freq: int) -> torch.Tensor:

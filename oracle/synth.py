@@ -304,6 +304,82 @@ def mrf_generator(w, cfg, x: Tensor, f0: Tensor, g: Tensor, eps_src: Tensor) -> 
     return torch.tanh(F.conv1d(x, _t(w, "dec.conv_post.weight"), _t(w, "dec.conv_post.bias"), padding=3))
 
 
+REFINEGAN_C0 = 512  # RefineGANGenerator(upsample_initial_channel=512, start_channels=16): not from the config
+
+
+def refinegan_noise_sizes(cfg, B: int, T: int):
+    """Sizes of the RefineGAN decoder's RNG draws in call order (refinegan.py): the source's randn_like [B, N, 1],
+    its torch.rand [B, 1], then per upsampling stage and ParallelResBlock branch the two AdaIN randn_like
+    [B, C, T_stage] (in, out)."""
+    N = T * cfg.upp
+    sizes = [B * N, B]
+    ch, t = REFINEGAN_C0, T
+    for r in cfg.upsample_rates:
+        ch, t = ch // 2, t * r
+        sizes += [B * ch * t] * 6
+    return sizes
+
+
+def refinegan_generator(w, cfg, mel: Tensor, f0: Tensor, g: Tensor, eps_src: Tensor) -> Tensor:
+    """RefineGANGenerator.forward (rvc/lib/algorithm/generators/refinegan.py:394-436): linear f0 upsampling,
+    1-harmonic source, pre_conv, leaky(0.2) + torchaudio kaiser-sinc resampling + conv per downsampling stage,
+    mel_conv + cond, then per upsampling stage leaky -> linear x rate -> concat the matching down branch ->
+    ParallelResBlock (input_conv, 3 x [AdaIN -> ResBlock(slope 0.2) -> AdaIN], mean) -> leaky -> conv_post -> tanh.
+    eps_src: the flat C-ABI layout of every draw (refinegan_noise_sizes)."""
+    from oracle.realtime import functional_resample
+
+    B, _, T = mel.shape
+    upp = cfg.upp
+    ups = list(cfg.upsample_rates)
+    sizes = refinegan_noise_sizes(cfg, B, T)
+    parts = list(torch.split(eps_src.reshape(-1), sizes))
+    N = T * upp
+    f0u = F.interpolate(f0.float().unsqueeze(1), size=N, mode="linear")  # [B, 1, N]
+    eps, ini = parts[0].reshape(B, N, 1), parts[1].reshape(B, 1)
+    har = harmonic_source(f0u.transpose(1, 2), cfg.sr, 1, eps, ini, _t(w, "dec.m_source.merge.0.weight"),
+                          None).transpose(1, 2)
+    x = F.conv1d(har, _t(w, "dec.pre_conv.weight"), _t(w, "dec.pre_conv.bias"), padding=3)
+    downs = []
+    size = upp
+    for i in range(len(ups)):
+        new_size = int(size / ups[-i - 1])
+        x = F.leaky_relu(x, 0.2)
+        downs.append(x)
+        x = functional_resample(x.contiguous(), int(T * size), int(T * new_size), lowpass_filter_width=64,
+                                rolloff=0.9475937167399596, resampling_method="sinc_interp_kaiser",
+                                beta=14.769656459379492)
+        x = F.conv1d(x, _t(w, f"dec.downsample_blocks.{i}.weight"), _t(w, f"dec.downsample_blocks.{i}.bias"),
+                     padding=3)
+        size = new_size
+    m = F.conv1d(mel, _t(w, "dec.mel_conv.weight"), _t(w, "dec.mel_conv.bias"), padding=3)
+    m = m + F.conv1d(g, _t(w, "dec.cond.weight"), _t(w, "dec.cond.bias"))
+    x = torch.cat([m, x], dim=1)
+    k = 2
+    for i, (r, down) in enumerate(zip(ups, reversed(downs))):
+        x = F.leaky_relu(x, 0.2)
+        x = F.interpolate(x, scale_factor=float(r), mode="linear")
+        x = torch.cat([x, down], dim=1)
+        p = f"dec.upsample_conv_blocks.{i}"
+        x = F.conv1d(x, _t(w, p + ".input_conv.weight"), _t(w, p + ".input_conv.bias"), padding=3)
+        outs = []
+        for j, (ks, dil) in enumerate(zip((3, 7, 11), (1, 3, 5))):
+            q = f"{p}.blocks.{j}"
+            y = F.leaky_relu(x + parts[k].reshape(x.shape) * _t(w, q + ".0.weight")[None, :, None], 0.2)
+            k += 1
+            for mm, d in enumerate((1, 3, 5)):  # refinegan.py ResBlock (:49-61)
+                t = F.conv1d(F.leaky_relu(y, 0.2), _t(w, f"{q}.1.convs1.{mm}.weight"), _t(w, f"{q}.1.convs1.{mm}.bias"),
+                             padding=(ks * d - d) // 2, dilation=d)
+                t = F.conv1d(F.leaky_relu(t, 0.2), _t(w, f"{q}.1.convs2.{mm}.weight"),
+                             _t(w, f"{q}.1.convs2.{mm}.bias"), padding=(ks - 1) // 2)
+                y = t + y
+            y = F.leaky_relu(y + parts[k].reshape(y.shape) * _t(w, q + ".2.weight")[None, :, None], 0.2)
+            k += 1
+            outs.append(y)
+        x = torch.stack(outs, dim=0).mean(dim=0)
+    x = F.leaky_relu(x, 0.2)
+    return torch.tanh(F.conv1d(x, _t(w, "dec.conv_post.weight"), None, padding=3))
+
+
 def decoder(w, cfg, x: Tensor, f0, g: Tensor, eps_src) -> Tensor:
     """The decoder Synthesizer selects (synthesizers.py:84-139)."""
     if not getattr(cfg, "use_f0", True):
@@ -313,6 +389,8 @@ def decoder(w, cfg, x: Tensor, f0, g: Tensor, eps_src) -> Tensor:
         return mrf_generator(w, cfg, x, f0, g, eps_src)
     if voc == "HiFi-GAN":
         return nsf_generator(w, cfg, x, f0, g, eps_src)
+    if voc == "RefineGAN":
+        return refinegan_generator(w, cfg, x, f0, g, eps_src)
     raise ValueError(voc)
 
 

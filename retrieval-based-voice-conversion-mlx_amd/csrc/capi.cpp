@@ -192,7 +192,7 @@ int rvcx_set_synth_config(rvcx_ctx* ctx, const rvcx_synth_desc* d) {
     g.emb_dim = d->text_enc_hidden_dim;
     g.f0 = d->no_f0 == 0;
     g.vocoder = d->vocoder;
-    if (g.vocoder < 0 || g.vocoder > 1) throw Error(RVCX_E_INVALID, "unsupported vocoder id");
+    if (g.vocoder < 0 || g.vocoder > 2) throw Error(RVCX_E_INVALID, "unsupported vocoder id");
     if (!g.f0 && g.vocoder != 0)
       throw Error(RVCX_E_INVALID, "models without pitch guidance use the HiFi-GAN decoder only (synthesizers.py:119-139)");
     if (g.H % g.n_heads || g.I % 2 || g.C0 % (1 << g.ups.size()))

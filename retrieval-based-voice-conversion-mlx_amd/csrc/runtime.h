@@ -68,6 +68,8 @@ struct SynthCfg {
   // NSF [T*upp]; MRF / RefineGAN [T*upp][H] noise, the B x H initial phases of all rows follow the B rows
   long long src_noise_row(long long T) const { return f0 ? T * upp() * src_harmonics() : 0; }
   long long src_noise_tail() const { return (f0 && vocoder != 0) ? src_harmonics() : 0; }
+  // every injected decoder draw of a B x T call (RefineGAN adds its AdaIN noise: runtime_refinegan.cpp)
+  long long src_noise_total(int B, long long T) const;
 };
 
 // ConvTranspose1d lowered to a polyphase conv: input row for output q, tap t is q + t - pad.
@@ -154,6 +156,10 @@ T* Ctx::buf(const std::string& name, size_t count, hipStream_t s) {
 
 // model forward passes (runtime_*.cpp)
 void finalize_synth(Ctx& c);
+void finalize_refinegan(Ctx& c);
+long long refinegan_noise_floats(const SynthCfg& g, int B, long long T);
+void refinegan_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, const float* f0, const float* g,
+                       const float* eps_src, uint64_t seed, float* out, hipStream_t s);
 void finalize_hubert(Ctx& c);
 void finalize_rmvpe(Ctx& c);
 int64_t hubert_forward(Ctx& c, const float* audio, int64_t n, int version, float* feats, int64_t cap,

@@ -311,7 +311,7 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
                                    eps_src ? eps_src + es_off : nullptr, cseed, vc, cap_vc, s, cfeats[i], cL[i]);
     const int64_t T = nvc / upp;
     ez_off += (int64_t)I * T;
-    es_off += c.scfg.src_noise_row(T) + c.scfg.src_noise_tail();  // this chunk's [T*upp][H] (+ [H] phases)
+    es_off += c.scfg.src_noise_total(1, T);  // this chunk's decoder draws (include/rvcx.h layouts)
     const int64_t keep = nvc - 2 * o.t_pad_tgt;
     if (keep <= 0) throw Error(RVCX_E_SHAPE, "pipeline: chunk too short for the padding");
     if (written + keep > cap)

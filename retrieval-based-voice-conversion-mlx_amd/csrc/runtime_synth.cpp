@@ -178,6 +178,10 @@ void finalize_synth(Ctx& c) {
     c.alloc_weight(q + ".post.b", get(c, M, p + ".post.bias", {I / 2}).v);
   }
   c.alloc_weight("emb_g", get(c, M, "emb_g.weight", {g.n_spk, g.gin}).v);
+  if (g.f0 && g.vocoder == 2) {  // RefineGAN (generators/refinegan.py), its own weight tree
+    finalize_refinegan(c);
+    return;
+  }
   // HiFiGAN-NSF (generators/hifigan_nsf.py:55-171); without pitch guidance the plain HiFiGANGenerator
   // (generators/hifigan.py:9-104): the same conv_pre / cond / ups / resblocks / conv_post, no source module
   const int C0 = g.C0;
@@ -291,6 +295,10 @@ void finalize_synth(Ctx& c) {
 void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, const float* f0, const float* g,
                  const float* eps_src, uint64_t seed, float* out, hipStream_t s) {
   const SynthCfg& cf = c.scfg;
+  if (cf.f0 && cf.vocoder == 2) {
+    refinegan_forward(c, B, T, z_btc, mask, f0, g, eps_src, seed, out, s);
+    return;
+  }
   const int I = cf.I, C0 = cf.C0, upp = cf.upp();
   const long long Nh = (long long)T * upp;
   // NSF source (SineGen + l_linear + tanh)

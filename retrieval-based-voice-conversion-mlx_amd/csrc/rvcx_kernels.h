@@ -133,6 +133,14 @@ hipError_t conv_post_tanh(const float* x, int B, int T, int C, const float* w, i
 // per-sample harmonic source of the MRF HiFi-GAN / RefineGAN decoders (source_harm.hip): f0 [B][L] -> har row b
 // at har + b*har_ld, N = L*upp samples; eps [B][N][H] and ini [B][H] injected or drawn (Philox(seed))
 size_t harm_source_ws_doubles(int B, int L, int upp, int H);
+// RefineGAN (refinegan.hip): depthwise kaiser-sinc downsampling by `orig` (new_freq 1), linear x rate upsampling of
+// lrelu(x) concatenated with a skip, AdaIN (mode 0 store, 1 add, 2 add then / div)
+hipError_t resample_dw(const float* x, int B, int T_in, int C, const float* ker, int K, int orig, int width, float* y,
+                       int T_out, hipStream_t s);
+hipError_t lerp_up_cat(const float* x, int B, int T, int C, int ldx, int rate, float slope, const float* skip, int Cd,
+                       float* y, int ldy, hipStream_t s);
+hipError_t adain(const float* x, int B, int T, int C, const float* w, const float* eps, uint64_t seed, float slope,
+                 float* y, int mode, float div, hipStream_t s);
 hipError_t harm_source(const float* f0, int B, int L, int upp, float sr, int H, int linear_up, const float* eps,
                        const float* ini, uint64_t seed, const float* lin_w, float lin_b, double* ws, float* har,
                        long long har_ld, hipStream_t st);

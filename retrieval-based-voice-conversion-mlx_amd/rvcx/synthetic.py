@@ -61,6 +61,9 @@ def synth_specs(cfg: SynthConfig = SYNTH_48K_V2) -> List[Spec]:
     # HiFiGAN-NSF generator (generators/hifigan_nsf.py:55-171); MRF HiFi-GAN (generators/hifigan_mrf.py:234-330)
     # has the same dataflow under other names, a 9-harmonic source, weight-normed conv_pre and a conv_post bias
     C0 = cfg.upsample_initial_channel
+    if cfg.use_f0 and cfg.vocoder == "RefineGAN":
+        s += _refinegan_specs(cfg)
+        return s + _flow_emb_specs(cfg)
     mrf = cfg.use_f0 and cfg.vocoder == "MRF HiFi-GAN"
     if cfg.use_f0:  # the plain HiFiGANGenerator (no pitch guidance) has no source module (hifigan.py:9-65)
         if mrf:
@@ -103,6 +106,41 @@ def synth_specs(cfg: SynthConfig = SYNTH_48K_V2) -> List[Spec]:
     else:
         s += [("dec.conv_post.weight", (1, chans[-1], 7), "post")]
     s += [("dec.cond.weight", (C0, cfg.gin_channels, 1), "conv"), ("dec.cond.bias", (C0,), "bias")]
+    return s + _flow_emb_specs(cfg)
+
+
+def _refinegan_specs(cfg: SynthConfig) -> List[Spec]:
+    """RefineGANGenerator (generators/refinegan.py:258-392), built by Synthesizer with start_channels 16,
+    upsample_initial_channel 512 and gin 256 fixed (synthesizers.py:99-107)."""
+    s: List[Spec] = [("dec.m_source.merge.0.weight", (1, 1), "src_lin")]
+    s += _wn("dec.pre_conv", (16, 1, 7), 16) + [("dec.pre_conv.bias", (16,), "bias")]
+    ch = 16
+    for i in range(len(cfg.upsample_rates)):
+        s += _wn(f"dec.downsample_blocks.{i}", (2 * ch, ch, 7), 2 * ch) + [(f"dec.downsample_blocks.{i}.bias", (2 * ch,),
+                                                                             "bias")]
+        ch *= 2
+    C = 512
+    s += _wn("dec.mel_conv", (C // 2, cfg.inter_channels, 7), C // 2) + [("dec.mel_conv.bias", (C // 2,), "bias")]
+    s += [("dec.cond.weight", (C // 2, 256, 1), "conv"), ("dec.cond.bias", (C // 2,), "bias")]
+    for i in range(len(cfg.upsample_rates)):
+        out, cin = C // 2, C + C // 4
+        p = f"dec.upsample_conv_blocks.{i}"
+        s += [(f"{p}.input_conv.weight", (out, cin, 7), "conv"), (f"{p}.input_conv.bias", (out,), "bias")]
+        for j, k in enumerate((3, 7, 11)):
+            q = f"{p}.blocks.{j}"
+            s += [(f"{q}.0.weight", (out,), "adain")]
+            for c in ("convs1", "convs2"):
+                for m in range(3):
+                    s += _wn(f"{q}.1.{c}.{m}", (out, out, k), out) + [(f"{q}.1.{c}.{m}.bias", (out,), "bias")]
+            s += [(f"{q}.2.weight", (out,), "adain")]
+        C = out
+    s += _wn("dec.conv_post", (1, C, 7), 1)
+    return s
+
+
+def _flow_emb_specs(cfg: SynthConfig) -> List[Spec]:
+    H, I = cfg.hidden_channels, cfg.inter_channels
+    s: List[Spec] = []
     # flow (residuals.py:103-258, modules.py:5-117); odd indices are Flip
     half = I // 2
     for f in range(cfg.flow_n):
@@ -239,6 +277,8 @@ def _init(rng: np.random.Generator, shape, kind: str) -> np.ndarray:
         w = n * (1.5 / np.sqrt(fan))
     elif kind == "src_lin":
         w = 1.0 + 0.5 * n
+    elif kind == "adain":  # reference init ones * 1e-4; larger here so the injected noise is exercised
+        w = 0.1 + 0.05 * n
     elif kind == "bias":
         w = n * 0.05
     elif kind == "embed":

@@ -17,6 +17,18 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running")
 
 
+def refinegan_noise(g):
+    import numpy as np
+
+    """Regenerate the fixture's RNG draws (make_golden_vocoders.py refinegan): z noise, then the flat C-ABI source
+    noise = source randn, initial phase (torch.rand), 24 AdaIN draws."""
+    rng = np.random.Generator(np.random.PCG64(int(g["noise_seed"])))
+    draws = [rng.standard_normal(int(n)).astype(np.float32) for n in g["draw_sizes"]]
+    ini = np.random.Generator(np.random.PCG64(int(g["uniform_seed"]))).random(int(g["phone"].shape[0]))
+    eps_src = np.concatenate([draws[1], ini.astype(np.float32)] + draws[2:])
+    return draws[0], eps_src
+
+
 def golden(name):
     import numpy as np
 

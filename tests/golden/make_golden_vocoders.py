@@ -7,6 +7,10 @@ Run:  python tests/golden/make_golden_vocoders.py [nof0] [mrf] [refinegan]
              (rvc/lib/algorithm/synthesizers.py:84, :119-139, :233-239; generators/hifigan.py:9-104)
   mrf        Synthesizer(vocoder="MRF HiFi-GAN"): HiFiGANMRFGenerator with the 9-harmonic source
              (synthesizers.py:86-98; generators/hifigan_mrf.py); torch.rand (initial phases) recorded too
+  refinegan  Synthesizer(vocoder="RefineGAN"): RefineGANGenerator (synthesizers.py:99-107; generators/refinegan.py).
+             torchaudio is absent here: torchaudio.functional.resample is replaced by oracle.realtime's restatement
+             of torchaudio 2.x (kaiser window), so that one piece is pinned to the restatement. Its noise (the AdaIN
+             draws are ~1.8 M floats) is not stored: the seeds and draw shapes are, and tests regenerate it.
 Each fixture holds the inputs, the recorded RNG draws and the reference outputs; weights are regenerated from the
 seeds (rvcx.synthetic) by the tests. Harness as in make_golden.py (stubs, seeded noise streams).
 """
@@ -113,6 +117,43 @@ def mrf():
     print("synth_mrf_b2: o", o.shape, float(o.abs().max()), float(o.std()))
 
 
+def refinegan():
+    import types
+
+    from oracle.realtime import functional_resample
+
+    ta = sys.modules.setdefault("torchaudio", types.ModuleType("torchaudio"))
+    fn = types.ModuleType("torchaudio.functional")
+    fn.resample = functional_resample
+    ta.functional = fn
+    sys.modules["torchaudio.functional"] = fn
+    cfg = dataclasses.replace(SYNTH_48K_V2, vocoder="RefineGAN")
+    net = build(cfg, "RefineGAN")
+    rng = np.random.Generator(np.random.PCG64(SEED_IN + 20))
+    B, T = 1, 6
+    phone = rng.standard_normal((B, T, 768)).astype(np.float32)
+    f0 = synthetic.f0_walk(B, T, seed=SEED_IN + 21)
+    pitch = rng.integers(1, 256, size=(B, T)).astype(np.int64)
+    lengths = np.array([T], np.int64)
+    sid = np.array([2], np.int64)
+    ns, us = mg.NoiseStream(SEED_IN + 22), UniformStream(SEED_IN + 23)
+    orig_n, orig_u = torch.randn_like, torch.rand
+    torch.randn_like, torch.rand = ns, us
+    try:
+        with torch.no_grad():
+            o, x_mask, (z, z_p, m_p, logs_p) = net.infer(torch.from_numpy(phone), torch.from_numpy(lengths),
+                                                         torch.from_numpy(pitch), torch.from_numpy(f0),
+                                                         torch.from_numpy(sid))
+    finally:
+        torch.randn_like, torch.rand = orig_n, orig_u
+    shapes = np.array([d.size for d in ns.draws], np.int64)
+    assert len(ns.draws) == 2 + 24 and len(us.draws) == 1, (len(ns.draws), len(us.draws))
+    np.savez_compressed(os.path.join(mg.OUT, "synth_refinegan_b1.npz"), phone=phone, f0=f0, pitch=pitch,
+                        lengths=lengths, sid=sid, noise_seed=SEED_IN + 22, uniform_seed=SEED_IN + 23,
+                        draw_sizes=shapes, o=o.numpy(), z=z.numpy(), seed_w=SEED_W)
+    print("synth_refinegan_b1: o", o.shape, float(o.abs().max()), float(o.std()))
+
+
 def main():
     mg.install_stubs()
     sys.path.insert(0, mg.REF)
@@ -124,6 +165,8 @@ def main():
         nof0()
     if "mrf" in which:
         mrf()
+    if "refinegan" in which:
+        refinegan()
 
 
 if __name__ == "__main__":

@@ -85,3 +85,71 @@ def test_mrf_pipeline_vs_oracle(mrf_engine, hubert_w, rmvpe_w):
     assert out.shape == ref.shape
     # the pitch track comes from RMVPE on both sides (near-tie bins may differ): spectrogram-level bar
     assert spectrogram_correlation(out, ref) >= 0.995, spectrogram_correlation(out, ref)
+
+
+@pytest.fixture(scope="module")
+def refinegan_engine(hubert_w, rmvpe_w):
+    from rvcx import synthetic
+    from rvcx.config import SYNTH_48K_V2
+    from rvcx.engine import Engine
+    from rvcx.weights import normalize_state
+
+    g = golden("synth_refinegan_b1.npz")
+    cfg = dataclasses.replace(SYNTH_48K_V2, vocoder="RefineGAN")
+    w = normalize_state(synthetic.synth_state(int(g["seed_w"]), cfg))
+    e = Engine(0)
+    e.load_synth(w, cfg)
+    e.load_hubert(hubert_w)
+    e.load_rmvpe(rmvpe_w)
+    yield e, w, cfg
+    e.close()
+
+
+def test_refinegan_synth_vs_reference(refinegan_engine):
+    """RefineGAN: linear-f0 source, kaiser-sinc downsampling branch, AdaIN-noised ParallelResBlocks
+    (refinegan.hip, runtime_refinegan.cpp) vs the reference RefineGANGenerator (torchaudio's resample restated)."""
+    from conftest import refinegan_noise
+    from oracle.metrics import spectrogram_correlation
+
+    eng, _, cfg = refinegan_engine
+    g = golden("synth_refinegan_b1.npz")
+    eps_z, eps_src = refinegan_noise(g)
+    T = g["phone"].shape[1]
+    out, zp, z = eng.synth_infer(g["phone"], g["lengths"], g["pitch"], g["f0"], g["sid"],
+                                 eps_z=eps_z.reshape(1, cfg.inter_channels, T), eps_src=eps_src, want_latents=True)
+    torch.cuda.synchronize()
+    eng.check_device_status()
+    assert rel_err(z.cpu().numpy().transpose(0, 2, 1), g["z"]) < 1e-4
+    o = out.cpu().numpy()
+    ref = g["o"].reshape(o.shape)
+    assert rel_err(o, ref) < 2e-3, rel_err(o, ref)
+    assert spectrogram_correlation(o[0], ref[0]) > 0.999
+
+
+def test_refinegan_vs_oracle_longer(refinegan_engine):
+    """A longer ragged-free batch (B=2, T=40) against the oracle with the same injected draws."""
+    from oracle import synth as osynth
+    from oracle.metrics import spectrogram_correlation
+    from rvcx import synthetic
+
+    eng, w, cfg = refinegan_engine
+    B, T = 2, 40
+    rng = np.random.Generator(np.random.PCG64(5))
+    phone = rng.standard_normal((B, T, 768)).astype(np.float32)
+    f0 = synthetic.f0_walk(B, T, seed=6)
+    pitch = rng.integers(1, 256, size=(B, T)).astype(np.int64)
+    lengths = np.array([T, T], np.int64)
+    sid = np.array([0, 3], np.int64)
+    eps_z = rng.standard_normal((B, cfg.inter_channels, T)).astype(np.float32)
+    n_src = len(osynth.refinegan_noise_sizes(cfg, B, T))
+    sizes = osynth.refinegan_noise_sizes(cfg, B, T)
+    eps_src = np.concatenate([rng.standard_normal(sizes[0]), rng.random(sizes[1])] +
+                             [rng.standard_normal(s) for s in sizes[2:]]).astype(np.float32)
+    assert n_src == 26
+    out = eng.synth_infer(phone, lengths, pitch, f0, sid, eps_z=eps_z, eps_src=eps_src).cpu().numpy()
+    t = torch.from_numpy
+    ref = osynth.synth_infer(w, cfg, t(phone), t(lengths), t(pitch), t(f0), t(sid), t(eps_z), t(eps_src))[0].numpy()
+    ref = ref.reshape(out.shape)
+    assert rel_err(out, ref) < 2e-3, rel_err(out, ref)
+    for b in range(B):
+        assert spectrogram_correlation(out[b], ref[b]) > 0.999

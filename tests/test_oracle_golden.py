@@ -132,3 +132,26 @@ def test_synth_mrf_matches_reference():
                                                         _t(g["f0"]), _t(g["sid"]), _t(g["eps_z"]), _t(g["eps_src"]))
     assert rel_err(z, g["z"]) < 1e-5
     assert rel_err(o, g["o"]) < 1e-4, rel_err(o, g["o"])
+
+
+def test_synth_refinegan_matches_reference():
+    """RefineGAN decoder against the reference Synthesizer(vocoder="RefineGAN").infer (make_golden_vocoders.py;
+    torchaudio's resample restated there and here: that piece is pinned to the restatement only)."""
+    import dataclasses
+
+    from oracle import synth as osynth
+    from rvcx import synthetic
+    from rvcx.weights import normalize_state
+
+    g = golden("synth_refinegan_b1.npz")
+    cfg = dataclasses.replace(SYNTH_48K_V2, vocoder="RefineGAN")
+    w = normalize_state(synthetic.synth_state(int(g["seed_w"]), cfg))
+    from conftest import refinegan_noise
+
+    eps_z, eps_src = refinegan_noise(g)
+    T = g["phone"].shape[1]
+    o, mask, (z, z_p, m_p, logs_p) = osynth.synth_infer(w, cfg, _t(g["phone"]), _t(g["lengths"]), _t(g["pitch"]),
+                                                        _t(g["f0"]), _t(g["sid"]),
+                                                        _t(eps_z.reshape(1, cfg.inter_channels, T)), _t(eps_src))
+    assert rel_err(z, g["z"]) < 1e-5
+    assert rel_err(o, g["o"]) < 1e-4, rel_err(o, g["o"])
