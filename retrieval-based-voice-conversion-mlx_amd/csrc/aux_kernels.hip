@@ -309,6 +309,55 @@ hipError_t softmax_rows(float* scores, int rows, int cols, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ NSF noise conv, accumulated into y
+// One thread per 4 consecutive channels of one output row: the row's kk = taps * stride source samples are
+// read once for the 4 channels, y is read and written as one float4 (coalesced along the row). The per-channel
+// sum runs over q in order as an fma chain, then + bias, then + y (the separate-launch order it replaces).
+__global__ void k_noise_add(const float* __restrict__ har, long long har_bs, int stride, int taps,
+                            const float* __restrict__ wf, const float* __restrict__ nb, float* __restrict__ y, int B,
+                            int T, int C) {
+  const int c4n = C >> 2;
+  const long long n = (long long)B * T * c4n;
+  const int kk = taps * stride;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % c4n) << 2;
+    const long long bt = i / c4n;
+    const int b = (int)(bt / T);
+    const long long t = bt - (long long)b * T;
+    const float* x = har + b * har_bs + t * stride;
+    float xs[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) xs[q] = q < kk ? x[q] : 0.f;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      if (q < kk) {
+        const int tap = q / stride, j = q - tap * stride;
+        const float* w = wf + ((long long)tap * C + c) * stride + j;
+        acc.x = fmaf(w[0], xs[q], acc.x);
+        acc.y = fmaf(w[stride], xs[q], acc.y);
+        acc.z = fmaf(w[2 * stride], xs[q], acc.z);
+        acc.w = fmaf(w[3 * stride], xs[q], acc.w);
+      }
+    }
+    float4* yp = reinterpret_cast<float4*>(y + bt * C + c);
+    float4 v = *yp;
+    v.x = v.x + (acc.x + nb[c]);
+    v.y = v.y + (acc.y + nb[c + 1]);
+    v.z = v.z + (acc.z + nb[c + 2]);
+    v.w = v.w + (acc.w + nb[c + 3]);
+    *yp = v;
+  }
+}
+hipError_t noise_conv_add(const float* har, long long har_bs, int stride, int taps, const float* wf, const float* nb,
+                          float* y, int B, int T, int C, hipStream_t s) {
+  if (C % 4 != 0 || taps * stride > 16 || taps * stride < 1 || (reinterpret_cast<uintptr_t>(y) & 15) != 0)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_noise_add, dim3(nblocks((long long)B * T * (C / 4))), dim3(TB), 0, s, har, har_bs, stride,
+                     taps, wf, nb, y, B, T, C);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ feature x2 upsample + protect blend
 // pipeline.py:344-362: feats = interpolate(x2, nearest); pitchff = 1 if pitchf > 0 else protect;
 // feats = feats * pitchff + feats0 * (1 - pitchff)   (feats0 == feats without index retrieval).

@@ -127,12 +127,14 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ g
         unsigned long long gv = 0;
 #pragma nounroll
         for (unsigned spins = 0;; ++spins) {
-          gv = __hip_atomic_load(&slot[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((unsigned)(gv >> 32) == epoch) break;
-          if (spins > spin_limit) {
+          // the limit is checked before the poll, so spin_limit 0 (test hook) fails the first hand-off
+          // deterministically instead of racing the partner
+          if (spins >= spin_limit) {
             abort_flag = 1;
             break;
           }
+          gv = __hip_atomic_load(&slot[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((unsigned)(gv >> 32) == epoch) break;
           __builtin_amdgcn_s_sleep(1);
         }
         hp[lane] = __uint_as_float((unsigned)gv);

@@ -361,7 +361,9 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
     a.pre_act = ACT_LRELU;
     a.pre_slope = 0.1f;
     run(c, a, s, 2.0 * B * curT * (double)Cin * C * L.k);
-    // + noise_convs[i](har) (hifigan_nsf.py:196-199): framed implicit GEMM, accumulated into y
+    // + noise_convs[i](har) (hifigan_nsf.py:196-199), accumulated into y: short kernels (every stage after the
+    // first, <= 16 taps) by a coalesced row kernel (one pass over y), the long first-stage kernel as a framed
+    // implicit GEMM
     if (cf.f0) {
       int stride = 1;
       for (size_t j = i + 1; j < cf.ups.size(); ++j) stride *= cf.ups[j];
@@ -371,11 +373,17 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
       if (npad > HAR_PAD || ntap * stride - npad > HAR_PAD + stride)
         throw Error(RVCX_E_SHAPE, "noise conv stride too large for the source padding");
       const std::string nn = "dec.noise_convs." + std::to_string(i);
-      ConvArgs an = conv(har + HAR_PAD - npad, stride, Ti + ntap - 1, stride, c.W(nn + ".wf"), C, ntap, 1, 0,
-                         c.W(nn + ".b"), y, C, Ti, B);
-      an.x_bs = har_ld;
-      an.acc_mode = ACC_ADD;
-      run(c, an, s, 2.0 * B * (double)Ti * C * kern);
+      if (ntap * stride <= 16 && C % 4 == 0) {
+        check(noise_conv_add(har + HAR_PAD - npad, har_ld, stride, ntap, c.W(nn + ".wf"), c.W(nn + ".b"), y, B, Ti,
+                             C, s),
+              "noise_conv_add");
+      } else {
+        ConvArgs an = conv(har + HAR_PAD - npad, stride, Ti + ntap - 1, stride, c.W(nn + ".wf"), C, ntap, 1, 0,
+                           c.W(nn + ".b"), y, C, Ti, B);
+        an.x_bs = har_ld;
+        an.acc_mode = ACC_ADD;
+        run(c, an, s, 2.0 * B * (double)Ti * C * kern);
+      }
     }
     // mean of the ResBlocks (residuals.py:71-80) accumulated into S. `cur` (= xin) is dead once the
     // ConvTranspose above has consumed it, so S reuses it and becomes the next stage's input.

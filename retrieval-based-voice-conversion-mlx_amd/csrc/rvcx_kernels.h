@@ -123,6 +123,10 @@ hipError_t gate_tanh_sigmoid(const float* xin, int ldx, const float* g, long lon
 hipError_t softmax_rel(float* scores, int T, int n_heads, int B, const float* rel, int window,
                        const float* mask, float* pband, int rows_scaled_by_band, hipStream_t s);
 hipError_t softmax_rows(float* scores, int rows, int cols, hipStream_t s);
+// y[b][t][c] += nb[c] + sum_{q < taps*stride} wf[(q / stride) * C + c][q % stride] * har[b*har_bs + t*stride + q]
+// (the NSF noise conv, hifigan_nsf.py:196-199, in its framed form); C % 4 == 0, taps*stride <= 16
+hipError_t noise_conv_add(const float* har, long long har_bs, int stride, int taps, const float* wf, const float* nb,
+                          float* y, int B, int T, int C, hipStream_t s);
 hipError_t upsample2_protect(const float* feats, const float* feats0, int L, int D, float* out, int T, const float* pitchf,
                              float protect,
                              hipStream_t s);

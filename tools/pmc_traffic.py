@@ -4,7 +4,9 @@ FETCH_SIZE and WRITE_SIZE are in KB per dispatch (rocprofv3 derived counters). O
 half the bytes of 16-B-per-lane streaming reads (MI355X_MICROARCH.md, HBM section), so it is doubled;
 WRITE_SIZE is taken as is. The bench runs warm-up + 1 timed step + 1 event pass (inline: the timed step
 carries the events), so each kernel of the step appears `steps` times; per-launch numbers are averages.
-usage: python tools/pmc_traffic.py gpurun_out [kernel-substring] > profiles/pmc_traffic.json
+usage: python tools/pmc_traffic.py gpurun_out [kernel-substring,...] > profiles/pmc_traffic.json
+Default family: the conv dispatches bench.py's roofline counts (conv_emu / conv_gemm / conv_tiny / conv2d_small);
+the split-K reduce kernels' bytes are added to the family's total, launches count the conv kernels only.
 The record carries the source-tree hash (rvcx.provenance) so bench.py can tell whether it applies.
 """
 import collections
@@ -30,11 +32,15 @@ def load(d, counter):
 
 def main():
     d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
-    key = sys.argv[2] if len(sys.argv) > 2 else "conv_gemm_kernel"
+    keys = (sys.argv[2] if len(sys.argv) > 2 else
+            "conv_emu_kernel,conv_gemm_kernel,conv_tiny_kernel,k_conv2d_small").split(",")
+    key = ",".join(keys)
+    fam = lambda k: any(s in k for s in keys)  # noqa: E731
+    bytes_fam = lambda k: fam(k) or "splitk_reduce" in k  # noqa: E731
     fe, wr = load(d, "FETCH_SIZE"), load(d, "WRITE_SIZE")
-    tot_f = sum(sum(v) for k, v in fe.items() if key in k)
-    tot_w = sum(sum(v) for k, v in wr.items() if key in k)
-    n = sum(len(v) for k, v in fe.items() if key in k)
+    tot_f = sum(sum(v) for k, v in fe.items() if bytes_fam(k))
+    tot_w = sum(sum(v) for k, v in wr.items() if bytes_fam(k))
+    n = sum(len(v) for k, v in fe.items() if fam(k))
     fetch = 2.0 * tot_f * 1024 / max(1, n)
     write = tot_w * 1024 / max(1, n)
     rec = {"kernel": key, "launches": n, "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
