@@ -33,7 +33,7 @@ typedef enum {
   RVCX_E_CAPACITY = -6 /* caller's output buffer too small */
 } rvcx_status;
 
-typedef enum { RVCX_MODEL_SYNTH = 0, RVCX_MODEL_HUBERT = 1, RVCX_MODEL_RMVPE = 2 } rvcx_model;
+typedef enum { RVCX_MODEL_SYNTH = 0, RVCX_MODEL_HUBERT = 1, RVCX_MODEL_RMVPE = 2, RVCX_MODEL_CREPE = 3 } rvcx_model;
 
 /* Synthesizer hyper-parameters = the 18-element ``cpt["config"]`` list of an RVC .pth
  * (rvc/train/process/extract_model.py:62-81) plus text_enc_hidden_dim (768 for v2). */
@@ -91,6 +91,15 @@ int rvcx_hubert_batch(rvcx_ctx* ctx, const float* d_audio, int64_t n, int64_t ld
                       int64_t cap_rows, int64_t* rows_out, void* stream);
 int rvcx_rmvpe_batch(rvcx_ctx* ctx, const float* d_audio, int64_t n, int64_t lda, int B, float thred, double* d_f0,
                      int64_t cap_frames, int64_t* frames_out, float* d_hidden, void* stream);
+
+/* CREPE (f0 methods "crepe" / "crepe-tiny"): CREPE.get_f0(audio, f0_min, f0_max, threshold) of
+ * rvc_mlx/lib/mlx/crepe.py:282-325 (the torchcrepe network of rvc/lib/predictors/f0.py:25-57; MLX dispatch
+ * rvc_mlx/lib/mlx/pitch_extractors.py:155-156). Weights: RVCX_MODEL_CREPE under torchcrepe's names (conv1..6 +
+ * _BN, classifier), full or tiny by conv1's filter count. d_audio [n] fp32 @16 kHz (n > 512) -> d_f0 [F] fp32,
+ * F = 1 + n/160; d_periodicity ([F], filtered) and d_probs ([F][360], the sigmoid outputs) are optional. */
+int rvcx_crepe(rvcx_ctx* ctx, const float* d_audio, int64_t n, float f0_min, float f0_max, float threshold,
+               float* d_f0, float* d_periodicity, float* d_probs, int64_t cap_frames, int64_t* frames_out,
+               void* stream);
 
 /* RMVPE0Predictor.decode (rvc/lib/predictors/RMVPE.py:515-540; rvc_mlx/lib/mlx/rmvpe.py:357-406):
  * salience [F][360] fp32 -> f0 [F] fp64 (argmax, +-4-bin weighted cents, threshold, 10 * 2^(c/1200), 10 -> 0). */
@@ -171,6 +180,9 @@ typedef struct {
                                        autotune skips f0 <= 0 and the pitch shift is applied after it */
   double index_rate;                /* speaker-embedding retrieval blend (pipeline.py:338-342, :378-388); 0 = off;
                                        > 0 needs rvcx_index_load */
+  int f0_method;                    /* 0 = RMVPE (default), 1 = CREPE with the loaded RVCX_MODEL_CREPE weights
+                                       (PitchExtractor.extract, pitch_extractors.py:155-156; f0_min 50, f0_max
+                                       1100, threshold 0.1) */
 } rvcx_pipeline_opts;
 
 /* Defaults of the rvc/ Config (x_pad 1, x_query 6, x_center 38, x_max 41; rvc/configs/config.py) at

@@ -205,7 +205,7 @@ int rvcx_set_synth_config(rvcx_ctx* ctx, const rvcx_synth_desc* d) {
 
 int rvcx_upload(rvcx_ctx* ctx, int model, const char* name, const float* host, const int64_t* shape, int ndim) {
   return guard(ctx, [&] {
-    if (model < 0 || model > 2 || !name || !host || (ndim > 0 && !shape) || ndim < 0 || ndim > 8)
+    if (model < 0 || model > 3 || !name || !host || (ndim > 0 && !shape) || ndim < 0 || ndim > 8)
       throw Error(RVCX_E_INVALID, "rvcx_upload: bad arguments");
     HostTensor t;
     size_t n = 1;
@@ -229,6 +229,8 @@ int rvcx_finalize(rvcx_ctx* ctx, int model) {
       finalize_hubert(*ctx);
     } else if (model == RVCX_MODEL_RMVPE) {
       finalize_rmvpe(*ctx);
+    } else if (model == RVCX_MODEL_CREPE) {
+      finalize_crepe(*ctx);
     } else {
       throw Error(RVCX_E_INVALID, "unknown model");
     }
@@ -259,6 +261,20 @@ int rvcx_rmvpe(rvcx_ctx* ctx, const float* d_audio, int64_t n, float thred, doub
     set_device(ctx);
     const int64_t F = rmvpe_forward(*ctx, d_audio, n, thred, d_f0, cap_frames, d_hidden,
                                     static_cast<hipStream_t>(stream));
+    if (frames_out) *frames_out = F;
+  });
+}
+
+int rvcx_crepe(rvcx_ctx* ctx, const float* d_audio, int64_t n, float f0_min, float f0_max, float threshold,
+               float* d_f0, float* d_periodicity, float* d_probs, int64_t cap_frames, int64_t* frames_out,
+               void* stream) {
+  return guard(ctx, [&] {
+    if (!ctx->ready[RVCX_MODEL_CREPE]) throw Error(RVCX_E_STATE, "crepe weights not finalized");
+    if (!d_audio || !d_f0 || n <= 0) throw Error(RVCX_E_INVALID, "rvcx_crepe: bad arguments");
+    if (cap_frames < 1 + n / 160) throw Error(RVCX_E_SHAPE, "rvcx_crepe: output capacity below 1 + n/160 frames");
+    set_device(ctx);
+    const int64_t F = crepe_forward(*ctx, d_audio, n, f0_min, f0_max, threshold, d_f0, nullptr, d_periodicity,
+                                    d_probs, static_cast<hipStream_t>(stream));
     if (frames_out) *frames_out = F;
   });
 }

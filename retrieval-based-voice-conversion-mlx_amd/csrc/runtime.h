@@ -90,9 +90,9 @@ struct Ctx {
   std::string err;
   SynthCfg scfg;
   bool synth_cfg_set = false;
-  std::map<std::string, HostTensor> host[3];
+  std::map<std::string, HostTensor> host[4];  // synth, hubert, rmvpe, crepe
   std::map<std::string, std::unique_ptr<DevBuf>> dev;  // packed weights
-  bool ready[3] = {false, false, false};
+  bool ready[4] = {false, false, false, false};
   std::vector<UpsLayer> ups;
   // pipeline high-pass (rvc/infer/pipeline.py:22-27), normalised so a[0] = 1
   int hp_order = 0;
@@ -162,6 +162,10 @@ void refinegan_forward(Ctx& c, int B, int T, const float* z_btc, const float* ma
                        const float* eps_src, uint64_t seed, float* out, hipStream_t s);
 void finalize_hubert(Ctx& c);
 void finalize_rmvpe(Ctx& c);
+void finalize_crepe(Ctx& c);
+// CREPE.get_f0 (rvc_mlx/lib/mlx/crepe.py:282-325) on audio [n] fp32: returns F = 1 + n/160
+int64_t crepe_forward(Ctx& c, const float* audio, int64_t n, double f0_min, double f0_max, float thr, float* f0,
+                      double* f0d, float* per, float* probs, hipStream_t s);
 int64_t hubert_forward(Ctx& c, const float* audio, int64_t n, int version, float* feats, int64_t cap,
                        hipStream_t s);
 // HuBERT in three parts, so a caller can issue the encoder's last layers later on another stream:

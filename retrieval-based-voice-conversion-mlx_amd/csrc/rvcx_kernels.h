@@ -125,6 +125,13 @@ hipError_t softmax_rel(float* scores, int T, int n_heads, int B, const float* re
 hipError_t softmax_rows(float* scores, int rows, int cols, hipStream_t s);
 // y[b][t][c] += nb[c] + sum_{q < taps*stride} wf[(q / stride) * C + c][q % stride] * har[b*har_bs + t*stride + q]
 // (the NSF noise conv, hifigan_nsf.py:196-199, in its framed form); C % 4 == 0, taps*stride <= 16
+// CREPE (crepe.hip): frames [nf][ld] (254 zeros | 1024 normalised samples | 254 zeros) of frames f_first..;
+// relu -> BatchNorm (bn = mean | 1/sqrt(var+eps) | gamma | beta, C each) -> max over row pairs [rows_in][C] ->
+// [rows_in/2][C]; decode + 3-tap filters: probs [F][360] -> f0 (fp32), f0d (fp64, optional), per (optional)
+hipError_t crepe_frames(const float* audio, long long n, long long f_first, int nf, float* out, int ld, hipStream_t s);
+hipError_t crepe_relu_bn_pool(const float* x, long long rows_in, int C, const float* bn, float* y, hipStream_t s);
+hipError_t crepe_decode(const float* probs, int F, double lo_cents, double hi_cents, float thr, float* f0_raw,
+                        float* per_raw, float* f0, double* f0d, float* per, hipStream_t s);
 hipError_t noise_conv_add(const float* har, long long har_bs, int stride, int taps, const float* wf, const float* nb,
                           float* y, int B, int T, int C, hipStream_t s);
 hipError_t upsample2_protect(const float* feats, const float* feats0, int L, int D, float* out, int T, const float* pitchf,

@@ -12,7 +12,7 @@ from typing import Optional
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RVCX_LIB", os.path.join(_HERE, "librvcx.so"))
 
-RVCX_MODEL_SYNTH, RVCX_MODEL_HUBERT, RVCX_MODEL_RMVPE = 0, 1, 2
+RVCX_MODEL_SYNTH, RVCX_MODEL_HUBERT, RVCX_MODEL_RMVPE, RVCX_MODEL_CREPE = 0, 1, 2, 3
 
 STATUS = {
     0: "RVCX_OK", -1: "RVCX_E_INVALID", -2: "RVCX_E_SHAPE", -3: "RVCX_E_HIP", -4: "RVCX_E_OOM",
@@ -28,7 +28,7 @@ EXPORTS = [
     "rvcx_index_retrieve", "rvcx_rt_default_desc", "rvcx_rt_default_opts", "rvcx_rt_create", "rvcx_rt_destroy",
     "rvcx_rt_geometry", "rvcx_rt_reset", "rvcx_rt_process", "rvcx_hubert_batch", "rvcx_rmvpe_batch",
     "rvcx_pipeline_batch", "rvcx_set_highpass_sos", "rvcx_highpass_pad", "rvcx_device_status", "rvcx_index_parse",
-    "rvcx_set_conv_math", "rvcx_conv1d",
+    "rvcx_set_conv_math", "rvcx_conv1d", "rvcx_crepe",
 ]
 
 
@@ -66,7 +66,7 @@ class PipelineOpts(ctypes.Structure):
         ("t_query", ctypes.c_int64), ("t_center", ctypes.c_int64), ("t_max", ctypes.c_int64),
         ("f0_autotune", ctypes.c_int), ("f0_autotune_strength", ctypes.c_double), ("proposed_pitch", ctypes.c_int),
         ("proposed_pitch_threshold", ctypes.c_double), ("volume_envelope", ctypes.c_double),
-        ("mlx_semantics", ctypes.c_int), ("index_rate", ctypes.c_double),
+        ("mlx_semantics", ctypes.c_int), ("index_rate", ctypes.c_double), ("f0_method", ctypes.c_int),
     ]
 
 
@@ -126,6 +126,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "rvcx_pipeline_ex": (i32, [vp, vp, i64, P(PipelineOpts), vp, vp, u64, vp, i64, P(i64), vp, vp]),
         "rvcx_f0_autotune": (i32, [vp, vp, i64, f64, i32, vp]),
         "rvcx_rmvpe_decode": (i32, [vp, vp, i64, f32, vp, vp]),
+        "rvcx_crepe": (i32, [vp, vp, i64, f32, f32, f32, vp, vp, vp, i64, P(i64), vp]),
         "rvcx_index_load": (i32, [vp, vp, i64]),
         "rvcx_index_unload": (i32, [vp]),
         "rvcx_index_info": (i32, [vp, P(i64), P(i64), P(i64), P(i64)]),

@@ -37,7 +37,7 @@ class Engine:
             raise _lib.RvcxError(rc, f"rvcx_create(device={device}) failed")
         self.ctx = ctx
         self.synth_cfg: Optional[SynthConfig] = None
-        self.loaded = {"synth": False, "hubert": False, "rmvpe": False}
+        self.loaded = {"synth": False, "hubert": False, "rmvpe": False, "crepe": None}
 
     def close(self):
         if getattr(self, "ctx", None):
@@ -119,6 +119,36 @@ class Engine:
     def load_rmvpe(self, state: Mapping[str, np.ndarray]):
         self.upload_state(_lib.RVCX_MODEL_RMVPE, normalize_state(state))
         self.loaded["rmvpe"] = True
+
+    def load_crepe(self, state: Mapping[str, np.ndarray], key=None):
+        """CREPE weights under torchcrepe's names (rvcx.weights.load_crepe_weights); the context holds one CREPE
+        model at a time (full or tiny, told apart by conv1's filter count). `key` names what was loaded so callers
+        can skip a reload."""
+        self.upload_state(_lib.RVCX_MODEL_CREPE, {k: v for k, v in state.items() if not k.endswith("num_batches_tracked")})
+        self.loaded["crepe"] = key if key is not None else ("full" if np.shape(state["conv1.weight"])[0] == 1024
+                                                           else "tiny")
+
+    def crepe(self, audio, f0_min: float = 50.0, f0_max: float = 1100.0, threshold: float = 0.1,
+              want_periodicity: bool = False, want_probs: bool = False):
+        """CREPE.get_f0 (rvc_mlx/lib/mlx/crepe.py:282-325): audio [N] (16 kHz) -> f0 fp32 [1 + N//160] on device
+        (and the filtered periodicity [F], the probabilities [F, 360])."""
+        t = self.torch
+        a = self._dev(audio, t.float32).reshape(-1)
+        n = a.numel()
+        F = 1 + n // 160
+        f0 = t.empty((F,), dtype=t.float32, device=self.device)
+        per = t.empty((F,), dtype=t.float32, device=self.device) if want_periodicity else None
+        probs = t.empty((F, 360), dtype=t.float32, device=self.device) if want_probs else None
+        fo = ctypes.c_int64(0)
+        self._check(self.lib.rvcx_crepe(self.ctx, a.data_ptr(), n, float(f0_min), float(f0_max), float(threshold),
+                                        f0.data_ptr(), _ptr(per), _ptr(probs), F, ctypes.byref(fo), self.stream()),
+                    "crepe")
+        out = [f0]
+        if want_periodicity:
+            out.append(per)
+        if want_probs:
+            out.append(probs)
+        return out[0] if len(out) == 1 else tuple(out)
 
     @property
     def upp(self) -> int:

@@ -13,6 +13,7 @@ The compute runs in librvcx.so; there is no CPU fallback.
 """
 from __future__ import annotations
 
+import os
 from types import SimpleNamespace
 
 import numpy as np
@@ -77,3 +78,75 @@ class Synthesizer:
         x_mask = (np.arange(T)[None, :] < lengths[:, None]).astype(np.float32)[:, None, :]
         o = out.cpu().numpy()[:, None, :]
         return o, x_mask, (z.transpose(1, 2).cpu().numpy(), zp.transpose(1, 2).cpu().numpy(), None, None)
+
+
+class CREPE:
+    """rvc_mlx/lib/mlx/crepe.py CREPE (:224-325) on device: CREPE(model, weights_path).get_f0(audio, f0_min,
+    f0_max, return_periodicity, threshold). Weights: the MLX npz (crepe_{model}.npz) or torchcrepe's .pth; the
+    default location is $RVCX_CREPE_DIR/crepe_{model}.npz (the reference looks in rvc_mlx/weights, :260-268)
+    and a missing file raises FileNotFoundError as the reference does (:252-256)."""
+
+    def __init__(self, model: str = "full", weights_path=None, engine: Engine = None, state=None):
+        if model not in ("full", "tiny"):
+            raise ValueError(f"Model {model} is not supported. Use 'full' or 'tiny'.")
+        if engine is None:
+            raise TypeError("CREPE needs the rvcx Engine it runs on (engine=...)")
+        self.model_type = model
+        self.engine = engine
+        key = ("crepe", model, weights_path) if state is None else ("crepe", model, "state", id(state))
+        if engine.loaded.get("crepe") != key:
+            if state is None:
+                from ..weights import load_crepe_weights
+                path = weights_path or os.path.join(os.environ.get("RVCX_CREPE_DIR", "weights"), f"crepe_{model}.npz")
+                if not os.path.exists(path):
+                    raise FileNotFoundError(f"CREPE weights not found. Expected at: {path}")
+                state = load_crepe_weights(path)
+            engine.load_crepe(state, key=key)
+
+    def get_f0(self, audio, f0_min: float = 50.0, f0_max: float = 1100.0, return_periodicity: bool = False,
+               threshold: float = 0.1):
+        f0, per = self.engine.crepe(_np(audio).reshape(-1).astype(np.float32), f0_min, f0_max, threshold,
+                                    want_periodicity=True)
+        if return_periodicity:
+            return f0.cpu().numpy(), per.cpu().numpy()
+        return f0.cpu().numpy()
+
+
+class FCPE:
+    """rvc_mlx/lib/mlx/fcpe.py FCPE (:50-163): the reference's MLX FCPE is a stub that runs RMVPE with threshold x 5
+    (:129-132); this keeps exactly that behaviour on the device RMVPE."""
+
+    def __init__(self, engine: Engine):
+        self.engine = engine
+
+    def get_f0(self, audio, f0_min: float = 50.0, f0_max: float = 1100.0, threshold: float = 0.006, **kw):
+        return self.engine.rmvpe(_np(audio).reshape(-1).astype(np.float32), threshold * 5).cpu().numpy()
+
+
+class PitchExtractor:
+    """rvc_mlx/lib/mlx/pitch_extractors.py PitchExtractor (:19-216) for the methods this path runs on device:
+    rmvpe, crepe, crepe-tiny, fcpe (the pyworld methods dio/pm/harvest are CPU algorithms outside this path)."""
+
+    METHODS = ["rmvpe", "crepe", "crepe-tiny", "fcpe"]
+
+    def __init__(self, method: str = "rmvpe", sample_rate: int = 16000, hop_size: int = 160, engine: Engine = None,
+                 crepe_weights=None):
+        if method not in self.METHODS:
+            raise ValueError(f"Unknown method: {method}")
+        self.method, self.sample_rate, self.hop_size, self.engine = method, sample_rate, hop_size, engine
+        if method in ("crepe", "crepe-tiny"):
+            self._model = CREPE("tiny" if method == "crepe-tiny" else "full", crepe_weights, engine=engine)
+        elif method == "fcpe":
+            self._model = FCPE(engine)
+        else:
+            self._model = RMVPE0Predictor(engine)
+
+    def extract(self, audio, f0_min: float = 50.0, f0_max: float = 1100.0, **kwargs):
+        audio = _np(audio)
+        if audio.ndim > 1:
+            audio = audio.mean(axis=-1)
+        if self.method == "rmvpe":
+            return self._model.infer_from_audio(audio, thred=kwargs.get("threshold", 0.03))
+        if self.method == "fcpe":
+            return self._model.get_f0(audio, f0_min=f0_min, f0_max=f0_max, threshold=kwargs.get("threshold", 0.006))
+        return self._model.get_f0(audio, f0_min=f0_min, f0_max=f0_max, **kwargs)

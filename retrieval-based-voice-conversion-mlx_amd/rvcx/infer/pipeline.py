@@ -21,7 +21,7 @@ from typing import Optional
 
 import numpy as np
 
-from .models import HubertModel, RMVPE0Predictor, Synthesizer, _np
+from .models import CREPE, HubertModel, RMVPE0Predictor, Synthesizer, _np
 
 
 class Config:
@@ -38,10 +38,15 @@ class Config:
 
 
 class PipelineRVCX:
-    SUPPORTED_F0_METHODS = ("rmvpe",)
+    # pipeline_mlx.py:82 / pitch_extractors.py:44 minus the pyworld CPU methods (dio, pm, harvest). "crepe" and
+    # "crepe-tiny" run CREPE as rvc_mlx/lib/mlx/crepe.py defines it (weighted-argmax decode; the rvc/ path's
+    # torchcrepe viterbi decoder is not reproduced); "fcpe" is the MLX stub's RMVPE with threshold 0.006 x 5
+    # (rvc_mlx/lib/mlx/fcpe.py:129-132) and needs semantics="mlx" (rvc/'s torchfcpe model is not available).
+    SUPPORTED_F0_METHODS = ("rmvpe", "crepe", "crepe-tiny", "fcpe")
 
     def __init__(self, tgt_sr, config, hubert_model: Optional[HubertModel] = None,
-                 rmvpe_model: Optional[RMVPE0Predictor] = None, f0_method: str = "rmvpe", semantics: str = "rvc"):
+                 rmvpe_model: Optional[RMVPE0Predictor] = None, f0_method: str = "rmvpe", semantics: str = "rvc",
+                 crepe_weights=None):
         if semantics not in ("rvc", "mlx"):
             raise ValueError("semantics must be 'rvc' or 'mlx'")
         self.x_pad, self.x_query, self.x_center, self.x_max = config.x_pad, config.x_query, config.x_center, \
@@ -62,6 +67,9 @@ class PipelineRVCX:
         self.hubert_model = hubert_model
         self.rmvpe_model = rmvpe_model
         self.semantics = semantics
+        # {"full": path-or-state, "tiny": ...} (or one path for "full"); None = $RVCX_CREPE_DIR/crepe_{model}.npz
+        self.crepe_weights = crepe_weights if isinstance(crepe_weights, dict) or crepe_weights is None \
+            else {"full": crepe_weights}
         self._check_method(f0_method)
         self._f0_method = f0_method
         self.engine = (hubert_model or rmvpe_model).engine if (hubert_model or rmvpe_model) else None
@@ -71,6 +79,26 @@ class PipelineRVCX:
     def _check_method(self, m):
         if m not in self.SUPPORTED_F0_METHODS:
             raise ValueError(f"f0_method {m!r} is not supported on this path (supported: {self.SUPPORTED_F0_METHODS})")
+        if m == "fcpe" and self.semantics != "mlx":
+            raise ValueError("f0_method 'fcpe' needs torchfcpe's model on the rvc/ path (rvc/lib/predictors/f0.py:60-89); "
+                             "semantics='mlx' runs the MLX port's FCPE (its RMVPE fallback)")
+
+    def _crepe(self, eng, f0_method):
+        """Load the CREPE weights f0_method names into the engine (once per model kind)."""
+        kind = "tiny" if f0_method == "crepe-tiny" else "full"
+        src = (self.crepe_weights or {}).get(kind)
+        if isinstance(src, dict):
+            return CREPE(kind, None, engine=eng, state=src)
+        return CREPE(kind, src, engine=eng)
+
+    def _f0_opts(self, eng, f0_method):
+        """(f0_method, rmvpe_threshold) of rvcx_pipeline_opts for an f0 method name."""
+        if f0_method in ("crepe", "crepe-tiny"):
+            self._crepe(eng, f0_method)
+            return 1, 0.03
+        if f0_method == "fcpe":
+            return 0, 0.006 * 5
+        return 0, 0.03
 
     @staticmethod
     def _check_guidance(eng, pitch_guidance: bool):
@@ -110,7 +138,12 @@ class PipelineRVCX:
         """-> (f0_coarse int64 [F], f0 float64 [F]) with F = 1 + len(x)//160 (pipeline.py:200-291)."""
         self._check_method(f0_method)
         eng = self._engine()
-        f0 = eng.rmvpe(np.asarray(x, dtype=np.float32).reshape(-1), 0.03)
+        method, thr = self._f0_opts(eng, f0_method)
+        xa = np.asarray(x, dtype=np.float32).reshape(-1)
+        if method == 1:  # PitchExtractor.extract -> CREPE.get_f0(x, f0_min=50, f0_max=1100) (pipeline_mlx.py:140)
+            f0 = eng.crepe(xa, self.f0_min, self.f0_max, 0.1).double()
+        else:
+            f0 = eng.rmvpe(xa, thr)
         shift = float(pitch)
         if f0_autotune:
             f0 = eng.f0_autotune(f0, f0_autotune_strength, skip_unvoiced=self.semantics == "mlx")
@@ -155,6 +188,7 @@ class PipelineRVCX:
             self.load_index(file_index, eng)
             rate = float(index_rate)
         self._ensure_highpass(eng)
+        method, thr = self._f0_opts(eng, f0_method)
         mlx = self.semantics == "mlx"
         t_pad = 1600 if mlx else self.t_pad
         t_pad_tgt = int(t_pad * self.tgt_sr / self.sample_rate) if mlx else self.t_pad_tgt
@@ -165,7 +199,7 @@ class PipelineRVCX:
             f0_autotune_strength=float(f0_autotune_strength),
             proposed_pitch=int(bool(proposed_pitch) and not mlx),
             proposed_pitch_threshold=float(proposed_pitch_threshold), volume_envelope=float(volume_envelope),
-            mlx_semantics=int(mlx), index_rate=rate)
+            mlx_semantics=int(mlx), index_rate=rate, f0_method=method, rmvpe_threshold=thr)
         y, f0 = eng.pipeline_ex(np.asarray(audio, dtype=np.float64).reshape(-1), opts, eps_z=eps_z,
                                 eps_src=eps_src, seed=seed, want_f0=True)
         self.last_f0 = f0

@@ -134,3 +134,36 @@ def unmap_mlx_keys(keys) -> Dict[str, str]:
             n = n.replace(".weight", ".gamma").replace(".bias", ".beta")
         out[k] = n
     return out
+
+
+def crepe_torch_layout(sd: Mapping[str, object]) -> Dict[str, np.ndarray]:
+    """CREPE weights in torchcrepe's names and layouts (conv{i}.weight [O][I][K][1], classifier.weight
+    [360][in]) from either torchcrepe's own state dict or the MLX npz that tools/convert_crepe_weights.py:43-70
+    writes (conv weights transposed to (O, K, 1, I), the classifier weight to (in, 360))."""
+    out = {}
+    for k, v in sd.items():
+        a = np.asarray(v.detach().cpu().numpy() if hasattr(v, "detach") else v, dtype=np.float32)
+        if k.endswith("num_batches_tracked"):
+            continue
+        if k.startswith("conv") and k.endswith(".weight") and a.ndim == 4 and "_BN" not in k:
+            if a.shape[2] == 1:  # MLX (O, K, 1, I) -> torch (O, I, K, 1) (torch dim 2 is the kernel, 512 or 64)
+                a = np.ascontiguousarray(a.transpose(0, 3, 1, 2))
+        elif k == "classifier.weight" and a.ndim == 2 and a.shape[1] == 360 and a.shape[0] != 360:
+            a = np.ascontiguousarray(a.T)  # MLX converter's (in, 360) -> (360, in)
+        out[k] = a
+    return out
+
+
+def load_crepe_weights(path: str) -> Dict[str, np.ndarray]:
+    """crepe_full.npz / crepe_tiny.npz (MLX, rvc_mlx/lib/mlx/crepe.py:270-280), .safetensors, or torchcrepe's
+    full.pth / tiny.pth (weights_only)."""
+    if path.endswith(".npz"):
+        with np.load(path, allow_pickle=False) as z:
+            return crepe_torch_layout({k: z[k] for k in z.files})
+    if path.endswith(".safetensors"):
+        from safetensors.numpy import load_file
+
+        return crepe_torch_layout(load_file(path))
+    import torch
+
+    return crepe_torch_layout(torch.load(path, map_location="cpu", weights_only=True))

@@ -1,0 +1,93 @@
+"""CREPE f0 ("crepe" / "crepe-tiny", rvc_mlx/lib/mlx/crepe.py) on device vs the oracle restatement
+(oracle/crepe.py; parity against the MLX reference itself is unpinned: mlx and torchcrepe are absent), and the
+"fcpe" method of the MLX port (its RMVPE fallback, rvc_mlx/lib/mlx/fcpe.py:129-132)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def cents(a, b):
+    return 1200.0 * np.abs(np.log2(np.maximum(a, 1e-3) / np.maximum(b, 1e-3)))
+
+
+@pytest.fixture(scope="module")
+def crepe_case():
+    from oracle import crepe as oc
+    from rvcx import synthetic
+
+    audio = synthetic.speech_like(24000, seed=7).astype(np.float32)
+    out = {}
+    for kind in ("tiny", "full"):
+        w = synthetic.crepe_state(kind, seed=11)
+        out[kind] = (w,) + tuple(oc.get_f0(w, audio, return_periodicity=True))
+    return audio, out
+
+
+@pytest.mark.parametrize("kind", ["tiny", "full"])
+def test_crepe_vs_oracle(engine, crepe_case, kind):
+    """probabilities within 1e-4 of the peak (fp32 convs in another order); where the argmax agrees the decoded
+    f0 is the same to fp32 rounding; >= 99 % of frames within 50 cents, voicing decisions agree on >= 99.5 %."""
+    audio, cases = crepe_case
+    w, f0_o, per_o, probs_o = cases[kind]
+    engine.load_crepe(w)
+    f0, per, probs = engine.crepe(audio, 50.0, 1100.0, 0.1, want_periodicity=True, want_probs=True)
+    f0, per, probs = f0.cpu().numpy(), per.cpu().numpy(), probs.cpu().numpy()
+    assert f0.shape == f0_o.shape == (1 + len(audio) // 160,)
+    err = np.abs(probs - probs_o).max() / np.abs(probs_o).max()
+    assert err < 1e-4, err
+    same_peak = np.argmax(probs, 1) == np.argmax(probs_o, 1)
+    assert same_peak.mean() > 0.98
+    voiced = (f0 > 0) & (f0_o > 0)
+    assert np.mean((f0 > 0) == (f0_o > 0)) >= 0.995
+    assert np.mean(cents(f0[voiced], f0_o[voiced]) < 50) >= 0.99
+    np.testing.assert_allclose(per, per_o, rtol=0, atol=1e-4)
+
+
+def test_crepe_decode_range_and_threshold(engine, crepe_case):
+    """f0_min / f0_max mask the bins outside the range (crepe.py:407-414) and threshold zeroes the frames whose
+    filtered periodicity falls below it (crepe.py:319-320), as in the oracle."""
+    from oracle import crepe as oc
+
+    audio, cases = crepe_case
+    w, _, _, probs_o = cases["tiny"]
+    engine.load_crepe(w)
+    for lo, hi, thr in ((100.0, 400.0, 0.1), (50.0, 1100.0, 0.6)):
+        f0, per, probs = engine.crepe(audio, lo, hi, thr, want_periodicity=True, want_probs=True)
+        f0d, perd = oc.decode(probs.cpu().numpy(), lo, hi)  # the oracle's decode on the device's own probs
+        from scipy.ndimage import median_filter, uniform_filter1d
+
+        perd = median_filter(perd, size=3)
+        f0d = uniform_filter1d(f0d, size=3)
+        f0d[perd < thr] = 0
+        np.testing.assert_allclose(f0.cpu().numpy(), f0d, rtol=2e-6, atol=0)
+        np.testing.assert_array_equal(per.cpu().numpy(), perd)
+
+
+def test_pipeline_crepe_and_fcpe(engine, crepe_case):
+    """PipelineMLX with f0_method crepe-tiny (state passed in) and fcpe (MLX semantics: RMVPE at 0.006 x 5):
+    get_f0 equals the engine-level calls, and the whole pipeline runs with those f0 tracks."""
+    from rvcx.infer import Config, HubertModel, PipelineMLX, RMVPE0Predictor, Synthesizer
+
+    audio, cases = crepe_case
+    w = cases["tiny"][0]
+    pl = PipelineMLX(48000, Config(), HubertModel(engine), RMVPE0Predictor(engine), semantics="mlx",
+                     crepe_weights={"tiny": w})
+    x = audio.astype(np.float64)
+    coarse, f0 = pl.get_f0(x, len(x) // 160, f0_method="crepe-tiny")
+    ref = engine.crepe(audio, 50.0, 1100.0, 0.1).double()
+    c_ref, _, f_ref = engine.f0_post(ref, 0.0)
+    np.testing.assert_array_equal(coarse, c_ref.cpu().numpy())
+    np.testing.assert_array_equal(f0, f_ref.cpu().numpy())
+    coarse2, f02 = pl.get_f0(x, len(x) // 160, f0_method="fcpe")
+    np.testing.assert_array_equal(f02, engine.f0_post(engine.rmvpe(audio, 0.03), 0.0)[2].cpu().numpy())
+    net_g = Synthesizer(engine)
+    y = pl.pipeline(None, net_g, 0, x, f0_method="crepe-tiny", seed=3)
+    assert y.ndim == 1 and np.isfinite(y).all() and np.abs(y).max() > 0
+    # the pipeline's f0 is CREPE on the high-passed, 1600-padded input (pipeline_mlx.py:284-318), then f0_post
+    _, p32 = engine.highpass_pad(x, 1600)
+    want = engine.f0_post(engine.crepe(p32, 50.0, 1100.0, 0.1).double(), 0.0)[2]
+    np.testing.assert_array_equal(pl.last_f0.cpu().numpy(), want.cpu().numpy())
+    with pytest.raises(ValueError):
+        PipelineMLX(48000, Config(), HubertModel(engine), RMVPE0Predictor(engine)).get_f0(x, 0, f0_method="fcpe")

@@ -148,8 +148,11 @@ def test_pipeline_mlx_semantics_runs(api):
 
 def test_unsupported_options_raise(api):
     hub, rm, net_g, PipelineMLX, Config = api
-    with pytest.raises(ValueError):
-        PipelineMLX(48000, Config(), hub, rm, f0_method="crepe")
+    for m in ("harvest", "dio", "pm"):  # pyworld CPU methods: outside this path
+        with pytest.raises(ValueError):
+            PipelineMLX(48000, Config(), hub, rm, f0_method=m)
+    with pytest.raises(ValueError):  # torchfcpe on the rvc/ path (the MLX port's fcpe is its RMVPE fallback)
+        PipelineMLX(48000, Config(), hub, rm, f0_method="fcpe")
     pipe = PipelineMLX(48000, Config(), hub, rm)
     with pytest.raises(ValueError):  # pitch_guidance=False with a pitch-guided model (the reference crashes there)
         pipe.pipeline(hub, net_g, 0, np.zeros(32000), 0, "rmvpe", None, 0.0, False, 1.0, "v2", 0.33, False, 1.0,
