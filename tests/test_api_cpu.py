@@ -125,6 +125,6 @@ def test_api_names_exist():
 
     for name in ("RVC_MLX", "PipelineMLX", "Config", "HubertModel", "RMVPE0Predictor", "Synthesizer"):
         assert hasattr(ri, name)
-    assert ri.PipelineMLX.SUPPORTED_F0_METHODS == ("rmvpe",)
+    assert ri.PipelineMLX.SUPPORTED_F0_METHODS == ("rmvpe", "crepe", "crepe-tiny", "fcpe")
     for m in ("pipeline", "get_f0", "voice_conversion"):
         assert callable(getattr(ri.PipelineMLX, m))
