@@ -101,6 +101,14 @@ int rvcx_crepe(rvcx_ctx* ctx, const float* d_audio, int64_t n, float f0_min, flo
                float* d_f0, float* d_periodicity, float* d_probs, int64_t cap_frames, int64_t* frames_out,
                void* stream);
 
+/* split_audio.process_audio (rvc/lib/tools/split_audio.py:5-27; rvc/infer/infer.py:282-284): the non-silent
+ * intervals librosa.effects.split(audio, top_db=-silence_thresh_db, frame_length=int(min_silence_len_ms/1000*sr),
+ * hop_length=frame_length//2) returns. d_audio [n] fp64 on device; intervals (HOST [cap][2] int64, start/end
+ * samples) receives *count of them; the call synchronises the stream (the edges are host logic over the frame
+ * RMS computed on device). RVCX_E_CAPACITY when more than cap intervals. */
+int rvcx_split_audio(rvcx_ctx* ctx, const double* d_audio, int64_t n, int sr, double silence_thresh_db,
+                     int min_silence_len_ms, int64_t* intervals, int64_t cap, int64_t* count, void* stream);
+
 /* RMVPE0Predictor.decode (rvc/lib/predictors/RMVPE.py:515-540; rvc_mlx/lib/mlx/rmvpe.py:357-406):
  * salience [F][360] fp32 -> f0 [F] fp64 (argmax, +-4-bin weighted cents, threshold, 10 * 2^(c/1200), 10 -> 0). */
 int rvcx_rmvpe_decode(rvcx_ctx* ctx, const float* d_hidden, int64_t F, float thred, double* d_f0, void* stream);

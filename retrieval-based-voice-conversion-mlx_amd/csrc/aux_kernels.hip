@@ -1070,6 +1070,29 @@ __global__ void k_rms_frames(const T* x, long long n, int frame, int hop, float*
   }
   if (threadIdx.x == 0) rms[blockIdx.x] = (float)sqrt(red[0] / frame);
 }
+// librosa.feature.rms (center=True, zero pad frame/2) kept in fp64 for librosa.effects.split's power_to_db test
+// (rvc/lib/tools/split_audio.py:19-24): rms[k] = sqrt(mean over the frame of x^2), frame k centred at k*hop.
+__global__ void k_rms_frames_f64(const double* x, long long n, int frame, int hop, double* rms) {
+  const long long start = (long long)blockIdx.x * hop - frame / 2;
+  double acc = 0.0;
+  for (int j = threadIdx.x; j < frame; j += blockDim.x) {
+    const long long q = start + j;
+    if (q >= 0 && q < n) acc += x[q] * x[q];
+  }
+  __shared__ double red[TB];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = TB / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) rms[blockIdx.x] = sqrt(red[0] / frame);
+}
+hipError_t rms_frames_f64(const double* x, long long n, int frame, int hop, double* rms, int nframes, hipStream_t s) {
+  if (frame <= 0 || hop <= 0 || nframes <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_rms_frames_f64, dim3(nframes), dim3(TB), 0, s, x, n, frame, hop, rms);
+  return hipGetLastError();
+}
 __device__ __forceinline__ float interp_linear(const float* r, int n_in, long long i, long long n_out) {
   const float scale = (float)n_in / (float)n_out;
   float src = scale * ((float)i + 0.5f) - 0.5f;

@@ -279,6 +279,17 @@ int rvcx_crepe(rvcx_ctx* ctx, const float* d_audio, int64_t n, float f0_min, flo
   });
 }
 
+int rvcx_split_audio(rvcx_ctx* ctx, const double* d_audio, int64_t n, int sr, double silence_thresh_db,
+                     int min_silence_len_ms, int64_t* intervals, int64_t cap, int64_t* count, void* stream) {
+  return guard(ctx, [&] {
+    if (!d_audio || !intervals || n <= 0 || sr <= 0 || cap < 0 || !count)
+      throw Error(RVCX_E_INVALID, "rvcx_split_audio: bad arguments");
+    set_device(ctx);
+    *count = split_intervals(*ctx, d_audio, n, sr, silence_thresh_db, min_silence_len_ms, intervals, cap,
+                             static_cast<hipStream_t>(stream));
+  });
+}
+
 int rvcx_hubert_batch(rvcx_ctx* ctx, const float* d_audio, int64_t n, int64_t lda, int B, int version, float* d_feats,
                       int64_t cap_rows, int64_t* rows_out, void* stream) {
   return guard(ctx, [&] {

@@ -163,6 +163,9 @@ void refinegan_forward(Ctx& c, int B, int T, const float* z_btc, const float* ma
 void finalize_hubert(Ctx& c);
 void finalize_rmvpe(Ctx& c);
 void finalize_crepe(Ctx& c);
+// librosa.effects.split of split_audio.process_audio (rvc/lib/tools/split_audio.py:5-27): intervals [cnt][2]
+int64_t split_intervals(Ctx& c, const double* audio, int64_t n, int sr, double silence_thresh_db, int min_silence_ms,
+                        int64_t* iv, int64_t cap, hipStream_t s);
 // CREPE.get_f0 (rvc_mlx/lib/mlx/crepe.py:282-325) on audio [n] fp32: returns F = 1 + n/160
 int64_t crepe_forward(Ctx& c, const float* audio, int64_t n, double f0_min, double f0_max, float thr, float* f0,
                       double* f0d, float* per, float* probs, hipStream_t s);

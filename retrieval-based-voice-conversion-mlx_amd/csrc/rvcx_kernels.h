@@ -194,6 +194,8 @@ hipError_t f0_autotune(double* f0, int F, double strength, int skip_unvoiced, hi
 hipError_t split_points(const double* x, long long n, int window, long long t_center, long long t_query,
                         double* sum_ws, long long* ts, int nts, hipStream_t s);
 int rms_frame_count(long long n, int sr);
+// fp64 frame RMS (librosa.feature.rms, center=True, constant pad): nframes = 1 + (n + 2*(frame/2) - frame)/hop
+hipError_t rms_frames_f64(const double* x, long long n, int frame, int hop, double* rms, int nframes, hipStream_t s);
 hipError_t change_rms(const double* src, long long n_src, int sr_src, float* y, long long n_y, int sr_y, float rate,
                       float* ws, hipStream_t s);
 

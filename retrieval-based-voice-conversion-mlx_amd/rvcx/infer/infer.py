@@ -155,19 +155,27 @@ class RVCX:
 
     def convert(self, audio: np.ndarray, pitch=0, f0_method="rmvpe", index_path=None, index_rate=0.75,
                 volume_envelope=1.0, protect=0.5, f0_autotune=False, f0_autotune_strength=1.0, sid=0,
-                proposed_pitch=False, proposed_pitch_threshold=155.0, seed: int = 0) -> np.ndarray:
-        """16 kHz mono audio -> converted float32 audio @tgt_sr (the body of infer_mlx.py:287-336)."""
-        return self.pipeline.pipeline(self.hubert_model, self.net_g, sid, audio, pitch, f0_method, index_path,
-                                      index_rate, self.use_f0, volume_envelope, self.version, protect, f0_autotune,
-                                      f0_autotune_strength, proposed_pitch, proposed_pitch_threshold, seed=seed)
+                proposed_pitch=False, proposed_pitch_threshold=155.0, seed: int = 0,
+                split_audio: bool = False) -> np.ndarray:
+        """16 kHz mono audio -> converted float32 audio @tgt_sr (the body of infer_mlx.py:287-336). split_audio
+        converts the non-silent intervals one by one and merges them back with the gaps restored
+        (rvc/infer/infer.py:282-316)."""
+        from ..split import merge_audio, process_audio
+
+        chunks, intervals = process_audio(self.engine, audio, 16000) if split_audio else ([audio], None)
+        outs = [self.pipeline.pipeline(self.hubert_model, self.net_g, sid, c, pitch, f0_method, index_path,
+                                       index_rate, self.use_f0, volume_envelope, self.version, protect, f0_autotune,
+                                       f0_autotune_strength, proposed_pitch, proposed_pitch_threshold, seed=seed)
+                for c in chunks]
+        return merge_audio(chunks, outs, intervals, 16000, self.tgt_sr) if split_audio else outs[0]
 
     def infer(self, audio_input, audio_output, pitch=0, f0_method="rmvpe", index_path=None, index_rate=0.75,
-              volume_envelope=1.0, protect=0.5, f0_autotune=False, f0_autotune_strength=1.0):
+              volume_envelope=1.0, protect=0.5, f0_autotune=False, f0_autotune_strength=1.0, split_audio=False):
         from scipy.io import wavfile
 
         audio = load_audio(audio_input)
         out = self.convert(audio, pitch, f0_method, index_path, index_rate, volume_envelope, protect, f0_autotune,
-                           f0_autotune_strength)
+                           f0_autotune_strength, split_audio=split_audio)
         wavfile.write(audio_output, self.tgt_sr, out.astype(np.float32))
         return out
 
