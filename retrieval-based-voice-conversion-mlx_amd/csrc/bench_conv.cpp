@@ -76,7 +76,7 @@ int main(int argc, char** argv) {
                        pad, 1);
     std::vector<float> ref((size_t)T * N), out((size_t)T * N);
     CK_(hipMemcpy(ref.data(), yr, ref.size() * 4, hipMemcpyDeviceToHost));
-    for (int cfg : {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16})
+    for (int cfg : {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 20, 21, 22})
       for (int pipe : {-1}) {
         ConvArgs a;
         a.x = x; a.ldx = C; a.T_in = T; a.C_in = C;
@@ -84,8 +84,15 @@ int main(int argc, char** argv) {
         a.y = y; a.ldy = N; a.T_out = T; a.N = N; a.bias = b;
         a.pre_act = ACT_LRELU; a.pre_slope = 0.1f;
         a.force_cfg = cfg; a.pipe = pipe;
+        void* wsb = nullptr;
+        if (cfg >= 20) {  // weight-streamed split kernel: pre-split weight image
+          CK_(hipMalloc(&wsb, conv_wsplit_bytes(a)));
+          CK_(conv_wsplit_build(a, wsb, 0));
+          a.wsplit = wsb; a.wsplit_npad = conv_wsplit_npad(a.N); a.math = 2;
+        }
         CK_(hipMemset(y, 0, (size_t)T * N * 4));
         CK_(conv1d(a, 0));
+        if (wsb) (void)hipFree(wsb);
         CK_(hipDeviceSynchronize());
         CK_(hipMemcpy(out.data(), y, out.size() * 4, hipMemcpyDeviceToHost));
         double md = 0, mr = 0;
@@ -180,7 +187,7 @@ int main(int argc, char** argv) {
     const double flops = 2.0 * cs.T * cs.N * (double)cs.Cin * cs.taps;
     // variants: (cfg, math, pipe); cfg -1 = the library's policy for that math
     struct V { int cfg, math, pipe; };
-    std::vector<V> vars = {{-1, 2, 0}, {10, 2, -1}, {11, 2, -1}, {12, 2, -1}, {13, 2, -1}, {14, 2, -1}, {15, 2, -1},
+    std::vector<V> vars = {{-1, 2, 0}, {20, 2, -1}, {21, 2, -1}, {22, 2, -1}, {10, 2, -1}, {11, 2, -1}, {12, 2, -1}, {13, 2, -1}, {14, 2, -1}, {15, 2, -1},
                            {16, 2, -1}, {-1, 1, 0}, {1, 1, -1}, {3, 1, -1}};
     if (cs.taps == 1)
       for (int c : {10, 12, 13, 14, 15}) vars.push_back({c, 2, 1});
@@ -203,11 +210,23 @@ int main(int argc, char** argv) {
         }
         a.force_cfg = vv.cfg; a.pipe = vv.pipe; a.math = vv.math;
         float* wsp = nullptr;
+        void* wsb = nullptr;
+        if (vv.cfg >= 20) {
+          if (!conv_wsb_eligible(a)) break;
+          CK_(hipMalloc(&wsb, conv_wsplit_bytes(a)));
+          CK_(conv_wsplit_build(a, wsb, 0));
+          a.wsplit = wsb; a.wsplit_npad = conv_wsplit_npad(a.N);
+        }
         if (vv.cfg < 0) {
           const long long need = conv_plan_splitk(a, false);
           if (need > 0) { CK_(hipMalloc(&wsp, need * 4)); a.ws = wsp; }
         }
-        if (conv1d(a, 0) != hipSuccess) { (void)hipGetLastError(); if (wsp) (void)hipFree(wsp); break; }
+        if (conv1d(a, 0) != hipSuccess) {
+          (void)hipGetLastError();
+          if (wsp) (void)hipFree(wsp);
+          if (wsb) (void)hipFree(wsb);
+          break;
+        }
         for (int i = 0; i < 3; ++i) CK_(conv1d(a, 0));
         CK_(hipDeviceSynchronize());
         hipEvent_t e0, e1;
@@ -223,6 +242,7 @@ int main(int argc, char** argv) {
         best = std::max(best, flops / ms / 1e9);
         ksp = a.ksplit;
         if (wsp) (void)hipFree(wsp);
+        if (wsb) (void)hipFree(wsb);
       }
       printf(" %s%d%s:%6.1f%s", vv.math == 2 ? "e" : "f", vv.cfg, vv.pipe > 0 ? "p" : "", best, ksp > 1 ? "*" : " ");
     }

@@ -104,10 +104,34 @@ void join_aux(Ctx& c, hipStream_t s, hipStream_t ax) {
   RVCX_HIP(hipStreamWaitEvent(s, c.ev_join, 0));
 }
 
+// the weight tensor's pre-split image (built once on first use; the stream then synchronises so a later use on
+// another stream never races the build)
+const void* Ctx::wsplit_for(const ConvArgs& a, hipStream_t s) {
+  const auto key = std::make_tuple(static_cast<const void*>(a.w), a.ldw, a.w_ts, a.N, a.C_in, a.taps);
+  auto& slot = wsplit_cache[key];
+  if (!slot) {
+    std::unique_ptr<DevBuf> b(new DevBuf());
+    const size_t bytes = (size_t)conv_wsplit_bytes(a);
+    if (hipMalloc(&b->p, bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      throw Error(RVCX_E_OOM, "split-weight allocation failed");
+    }
+    b->bytes = bytes;
+    check(conv_wsplit_build(a, b->p, s), "conv_wsplit_build");
+    RVCX_HIP(hipStreamSynchronize(s));
+    slot = std::move(b);
+  }
+  return slot->p;
+}
+
 void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double flops) {
   ConvArgs a = a_in;
   if (c.conv_math > 0 && a.math == 0) a.math = c.conv_math;
   const long long need = conv_plan_splitk(a, two_d);
+  if (!two_d && a.w_static && conv_wsb_wants(a)) {
+    a.wsplit = c.wsplit_for(a, s);
+    a.wsplit_npad = conv_wsplit_npad(a.N);
+  }
   // split-K slabs are per stream: the aux stream's convs run concurrently with the caller's
   if (need > 0) a.ws = c.buf<float>(c.aux && s == c.aux ? "conv.splitk.aux" : "conv.splitk", (size_t)need, s);
   if (flops < 0) {
@@ -235,6 +259,7 @@ int rvcx_finalize(rvcx_ctx* ctx, int model) {
       throw Error(RVCX_E_INVALID, "unknown model");
     }
     RVCX_HIP(hipDeviceSynchronize());
+    ctx->wsplit_cache.clear();  // weights may have been re-packed at new addresses
     ctx->ready[model] = true;
   });
 }

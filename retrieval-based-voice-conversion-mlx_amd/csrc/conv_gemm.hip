@@ -684,11 +684,26 @@ inline bool small2d_enabled() {
   return v;
 }
 
+// weight-streamed split kernel (conv_wsb.hip) tiles: 256x32 for N <= 32, 128x64 for N <= 64, else 128x128
+// (RVCX_WCFG_* override). bench_conv on MI355X (TF/s, vs the LDS-staged split kernel's best tile): C128 k11
+// 189 vs 155, C128 k7 166 vs 138; C64 k11 141 vs 139; the short-tap and 32-channel convs lose (C32 k11 94 vs
+// 112, C64 k3 + residual 33 vs 70), so conv_wsb_wants admits N >= 128 with >= 5 taps only.
+inline int pick_wsb(const ConvArgs& a) {
+  static const int c_narrow = env_cfg("RVCX_WCFG_NARROW", 20);
+  static const int c_mid = env_cfg("RVCX_WCFG_MID", 21);
+  static const int c_wide = env_cfg("RVCX_WCFG_WIDE", 22);
+  return a.N <= 32 ? c_narrow : (a.N <= 64 ? c_mid : c_wide);
+}
+
 template <bool TWO_D>
 hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
   if (a.N <= 0 || a.T_out <= 0 || a.batch <= 0) return hipSuccess;
   if (a.C_in <= 0 || a.taps <= 0) return hipErrorInvalidValue;
   if (tiny_fits(a)) return launch_tiny(a, TWO_D, s);
+  if (!TWO_D && a.wsplit && (a.force_cfg < 0 || a.force_cfg >= 20) && conv_math(a) == 2 && conv_wsb_eligible(a)) {
+    const hipError_t e = conv_wsb_launch(a, a.force_cfg >= 20 ? a.force_cfg : pick_wsb(a), xcd_enabled() ? 1 : 0, s);
+    if (e != hipErrorInvalidValue) return e;
+  }
   // 3x3 convs with 16/32 channels: 16x16x4 MFMA fragments (conv2d_small.hip)
   if (TWO_D && a.force_cfg < 0 && small2d_enabled() && conv2d_small_fits(a)) return conv2d_small(a, s);
   const int cfg = pick_cfg<TWO_D>(a);
@@ -771,6 +786,18 @@ long long conv_plan_splitk(ConvArgs& a, bool two_d) {
   a.ksplit = ks;
   a.ws_rows = two_d ? (long long)a.T_out * a.W_out : a.T_out;
   return (long long)ks * a.ws_rows * a.N * a.batch * a.batch_inner;
+}
+
+bool conv_wsb_wants(const ConvArgs& a) {
+  static const bool off = [] {
+    const char* e = std::getenv("RVCX_NO_WSB");
+    return e && std::atoi(e) != 0;
+  }();
+  if (off || conv_math(a) != 2 || !conv_wsb_eligible(a)) return false;
+  if (a.N < 128 || a.taps < 5) return false;  // where it measured faster (pick_wsb)
+  // the grid must fill the chip several times over (the generator's long convs): 128 x 64 tiles
+  const long long tiles = (long long)((a.T_out + 127) / 128) * ((a.N + 63) / 64) * a.batch;
+  return tiles >= 1024;
 }
 
 hipError_t conv1d(const ConvArgs& a, hipStream_t s) { return dispatch<false>(a, s); }

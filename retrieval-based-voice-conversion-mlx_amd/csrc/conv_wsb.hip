@@ -1,0 +1,259 @@
+// fp32 implicit-GEMM convolution with the weights pre-split in HBM ("weight-streamed B"), for the long 1-D convs of
+// the generator (ResBlocks, ConvTranspose phases, conv_pre): the same exact 3-plane bf16 arithmetic as
+// conv_emu.hip (x = x0 + x1 + x2, six plane products smallest first, one fp32 accumulator), restructured so the
+// (chunk, tap) loop has no barrier and no conversion work:
+//   * the weights are split ONCE (k_wsplit, cached per weight tensor by the runtime) into rows of
+//     [hi | mid | lo] x 32 channels per (chunk, tap, output channel), so every lane loads its MFMA B fragments
+//     straight from L2/L1 as 16-byte vectors, one iteration ahead, into registers (two register sets);
+//   * only the activation halo goes through LDS (split once per 32-channel chunk and reused by every tap); the
+//     next chunk's halo is prefetched into registers during the current chunk's taps;
+//   * per-wave tiles of 64 x 32 (two accumulators) double the MFMA work per LDS A fragment read.
+// A (chunk, tap) step is then 6*TN global B loads, 6*TM LDS reads and 12*TM*TN MFMAs; barriers only at chunk
+// changes (two per 32 input channels).
+#include <algorithm>
+#include <cstdlib>
+
+#include "conv_common.h"
+#include "split_bf16.h"
+
+namespace rvcx {
+
+namespace {
+
+using namespace splitbf16;
+
+constexpr int WROW = 3 * PLANE;  // bytes of one (chunk, tap, column) row of split weights in HBM
+constexpr int WSB_HALO = 64;     // max (taps - 1) * dil: the A prefetch registers cover BM + 64 rows
+
+// w [tap][n][c] (ldw, w_ts) -> out rows ((ch * taps + tap) * Npad + n) of [hi | mid | lo] x 32 bf16; zero
+// beyond N and C_in. The plane arithmetic is put_split1's.
+__global__ void k_wsplit(const float* __restrict__ w, int ldw, long long w_ts, int N, int C_in, int taps, int nchunks,
+                         int Npad, unsigned short* __restrict__ out) {
+  const long long total = (long long)nchunks * taps * Npad * EK;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % EK);
+    const long long r = i / EK;
+    const int n = (int)(r % Npad);
+    const long long ct = r / Npad;
+    const int tap = (int)(ct % taps), ch = (int)(ct / taps);
+    const int cc = ch * EK + c;
+    const float v = (n < N && cc < C_in) ? w[tap * w_ts + (long long)n * ldw + cc] : 0.f;
+    const unsigned h = pk_bf16(v, 0.f);
+    const float rr = v - lo_f(h);
+    const unsigned m = pk_bf16(rr, 0.f);
+    const unsigned l = pk_bf16(rr - lo_f(m), 0.f);
+    unsigned short* o = out + r * (3 * EK);
+    o[c] = (unsigned short)h;
+    o[EK + c] = (unsigned short)m;
+    o[2 * EK + c] = (unsigned short)l;
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(CONV_THREADS, 2) void conv_wsb_kernel(const ConvArgs a, const char* __restrict__ wsp,
+                                                                   const int Npad, const int nrows_a, const int ntn) {
+  constexpr int NT = CONV_THREADS;
+  constexpr int TM = BM / (WM * 32);
+  constexpr int TN = BN / (WN * 32);
+  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves, whole 32x32 sub-tiles");
+  extern __shared__ __attribute__((aligned(16))) char smem_w[];
+  char* const As = smem_w;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int li = lane & 31, hk = lane >> 5;
+  int bx, by, bz;
+  conv_block_coords(ntn, bx, by, bz);
+  const int b = bz;
+  const int n0 = by * BN, m0 = bx * BM;
+  const float* X = a.x + (long long)b * a.x_bs;
+  const float* PM = a.pre_mask ? a.pre_mask + (long long)b * a.pre_mask_bs : nullptr;
+  const int row0 = m0 - a.pad;
+
+  int aoff[TM];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm) aoff[tm] = (wm * TM * 32 + tm * 32 + li) * ERS + hk * 16;
+  const char* bp[TN];
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) bp[tn] = wsp + (size_t)(n0 + wn * TN * 32 + tn * 32 + li) * WROW + hk * 16;
+  const size_t bstep = (size_t)Npad * WROW;  // one (chunk, tap) iteration
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[tm][tn][r] = 0.f;
+
+  // ---- A: the chunk's nrows_a x 32 halo tile, prefetched into registers one chunk ahead
+  constexpr int AP = ((BM + WSB_HALO) * EC4 + NT - 1) / NT;
+  f32x4 apre[AP];
+  float apm[AP];
+  const int arow = store_row(tid / EC4), ac4 = (tid % EC4) << 2;
+  auto load_a_regs = [&](int c0) __attribute__((always_inline)) {
+    const float* src0 = X + c0 + ac4;
+#pragma unroll
+    for (int v = 0; v < AP; ++v) {
+      const int r = v * (NT / EC4) + arow;
+      const int g = row0 + r;
+      const bool ok = r < nrows_a && g >= 0 && g < a.T_in;
+      apre[v] = ok ? *reinterpret_cast<const f32x4*>(src0 + (long long)g * a.ldx) : f32x4{0.f, 0.f, 0.f, 0.f};
+      apm[v] = ok ? (PM ? PM[g] : 1.f) : 0.f;
+    }
+  };
+  auto write_a_regs = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int v = 0; v < AP; ++v) {
+      const int r = v * (NT / EC4) + arow;
+      if (r < nrows_a) {
+        f32x4 val = apre[v];
+        if (a.pre_act != ACT_NONE) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) val[j] = act_fn(val[j], a.pre_act, a.pre_slope);  // act(0) = 0
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) val[j] *= apm[v];
+        put_split4(As + r * ERS, ac4, val);
+      }
+    }
+  };
+
+  // ---- B fragments of one iteration: [tn][s * 3 + plane], 16 B per lane each
+  typedef bf16x8 BFrag[TN][6];
+  auto load_b = [&](int it, BFrag& dst) __attribute__((always_inline)) {
+    const size_t o = (size_t)it * bstep;
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          dst[tn][s * 3 + q] = *reinterpret_cast<const bf16x8*>(bp[tn] + o + q * PLANE + s * 32);
+  };
+  auto compute = [&](int tap, const BFrag& bf) __attribute__((always_inline)) {
+    const int toff = tap * a.dil * ERS;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 af[TM][3];
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          af[tm][q] = *reinterpret_cast<const bf16x8*>(As + aoff[tm] + toff + q * PLANE + s * 32);
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+          f32x16 c = acc[tm][tn];
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm][2], bf[tn][s * 3 + 0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm][1], bf[tn][s * 3 + 1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm][0], bf[tn][s * 3 + 2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm][1], bf[tn][s * 3 + 0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm][0], bf[tn][s * 3 + 1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm][0], bf[tn][s * 3 + 0], c, 0, 0, 0);
+          acc[tm][tn] = c;
+        }
+    }
+  };
+
+  const int nch = a.C_in / EK, taps = a.taps, total = nch * taps;
+  BFrag b0, b1;
+  load_a_regs(0);
+  write_a_regs();
+  if (nch > 1) load_a_regs(EK);
+  load_b(0, b0);
+  __syncthreads();
+  int ch = 0, tap = 0;
+  // one (chunk, tap) iteration: prefetch the next iteration's B, MFMAs on this one's, switch chunks after the
+  // last tap (every wave done reading the halo -> write the prefetched one -> prefetch the chunk after)
+  auto step = [&](int it, const BFrag& cur, BFrag& nxt) __attribute__((always_inline)) {
+    if (it + 1 < total) load_b(it + 1, nxt);
+    compute(tap, cur);
+    if (++tap == taps) {
+      tap = 0;
+      if (++ch < nch) {
+        __syncthreads();
+        write_a_regs();
+        if (ch + 1 < nch) load_a_regs((ch + 1) * EK);
+        __syncthreads();
+      }
+    }
+  };
+  for (int it = 0; it < total; it += 2) {
+    step(it, b0, b1);
+    if (it + 1 < total) step(it + 1, b1, b0);
+  }
+
+  conv_store_tile<TM, TN, WM, WN, false>(a, TilePos{m0, 0, 0, 0, 0, n0, b, 0, b, 0, 1}, acc,
+                                         reinterpret_cast<float*>(smem_w));
+}
+
+template <int BM, int BN, int WM, int WN>
+hipError_t launch_wsb(const ConvArgs& a, int ntn_enable, hipStream_t s) {
+  const int nrows_a = BM + (a.taps - 1) * a.dil;
+  const size_t smem = std::max((size_t)nrows_a * ERS, (size_t)4 * 32 * 33 * sizeof(float));
+  if (a.wsplit_npad % BN != 0) return hipErrorInvalidValue;
+  const int mtiles = (a.T_out + BM - 1) / BM;
+  const int ntiles = (a.N + BN - 1) / BN;
+  const int ntn = ntn_enable ? ntiles : 0;
+  dim3 grid(ntn ? mtiles * ntiles : mtiles, ntn ? 1 : ntiles, a.batch);
+  auto kern = conv_wsb_kernel<BM, BN, WM, WN>;
+  static size_t smem_set = 64 * 1024;
+  if (smem > smem_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return e;
+    smem_set = smem;
+  }
+  hipLaunchKernelGGL(kern, grid, dim3(CONV_THREADS), smem, s, a, static_cast<const char*>(a.wsplit), a.wsplit_npad,
+                     nrows_a, ntn);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool conv_wsb_eligible(const ConvArgs& a) {
+  const bool vec_a = ((a.ldx & 3) == 0) && ((reinterpret_cast<uintptr_t>(a.x) & 15) == 0) && ((a.x_bs & 3) == 0);
+  return a.stride == 1 && a.batch_inner == 1 && !a.b_kn && a.C_in % EK == 0 && a.C_in > 0 && a.taps >= 1 &&
+         (a.taps - 1) * a.dil <= WSB_HALO && a.dil >= 1 && vec_a && a.ksplit <= 1 && a.out_map == OUT_ROWS;
+}
+
+int conv_wsplit_npad(int N) { return (N + 127) / 128 * 128; }
+
+long long conv_wsplit_bytes(const ConvArgs& a) {
+  return (long long)(a.C_in / EK) * a.taps * conv_wsplit_npad(a.N) * WROW;
+}
+
+hipError_t conv_wsplit_build(const ConvArgs& a, void* out, hipStream_t s) {
+  const int nch = a.C_in / EK, Npad = conv_wsplit_npad(a.N);
+  const long long total = (long long)nch * a.taps * Npad * EK;
+  const long long nb = std::min<long long>((total + 255) / 256, 1 << 20);
+  hipLaunchKernelGGL(k_wsplit, dim3((unsigned)nb), dim3(256), 0, s, a.w, a.ldw, a.w_ts, a.N, a.C_in, a.taps, nch, Npad,
+                     static_cast<unsigned short*>(out));
+  return hipGetLastError();
+}
+
+// cfg 20: 256 x 32 (4 x 1 waves of 64 x 32), 21: 128 x 64 (2 x 2 waves of 64 x 32), 22: 128 x 128 (2 x 2 of 64 x 64)
+bool conv_wsb_tile(int cfg, int& BM, int& BN) {
+  static const int t[3][2] = {{256, 32}, {128, 64}, {128, 128}};
+  if (cfg < 20 || cfg > 22) return false;
+  BM = t[cfg - 20][0];
+  BN = t[cfg - 20][1];
+  return true;
+}
+
+hipError_t conv_wsb_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream_t s) {
+  if (!a.wsplit || !conv_wsb_eligible(a)) return hipErrorInvalidValue;
+  switch (cfg) {
+    case 20: return launch_wsb<256, 32, 4, 1>(a, ntn_enable, s);
+    case 21: return launch_wsb<128, 64, 2, 2>(a, ntn_enable, s);
+    case 22: return launch_wsb<128, 128, 2, 2>(a, ntn_enable, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace rvcx

@@ -8,6 +8,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "../../include/rvcx.h"
@@ -114,6 +115,9 @@ struct Ctx {
   std::vector<ProfRec> prof_recs;
   std::vector<hipEvent_t> prof_pool;
   std::unique_ptr<IvfIndex> ivf;  // speaker-embedding index (optional)
+  // pre-split weight images of the weight-streamed conv kernel, per (weight, layout); cleared by rvcx_finalize
+  std::map<std::tuple<const void*, int, long long, int, int, int>, std::unique_ptr<DevBuf>> wsplit_cache;
+  const void* wsplit_for(const ConvArgs& a, hipStream_t s);
   // second stream for work independent of the caller's stream (HuBERT beside RMVPE), created lazily
   hipStream_t aux = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_gate = nullptr;

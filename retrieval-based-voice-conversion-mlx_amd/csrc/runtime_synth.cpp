@@ -358,6 +358,7 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
     const int C = L.cout, u = L.u, Ti = curT * u;
     // LeakyReLU(0.1) -> ConvTranspose1d (polyphase) ; output [B][curT][u*C] == [B][Ti][C]
     ConvArgs a = conv(cur, Cin, curT, Cin, L.w, u * C, L.taps, 1, L.pad, L.b, y, u * C, curT, B);
+    a.w_static = 1;
     a.pre_act = ACT_LRELU;
     a.pre_slope = 0.1f;
     run(c, a, s, 2.0 * B * curT * (double)Cin * C * L.k);
@@ -400,6 +401,7 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
         const std::string n1 = rb + ".convs1." + std::to_string(m);
         const std::string n2 = rb + ".convs2." + std::to_string(m);
         ConvArgs a1 = conv(r_in, C, Ti, C, c.W(n1 + ".w"), C, k, d, (k * d - d) / 2, c.W(n1 + ".b"), T1, C, Ti, B);
+        a1.w_static = 1;
         a1.pre_act = ACT_LRELU;
         a1.pre_slope = 0.1f;
         a1.act = ACT_LRELU;
@@ -408,6 +410,7 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
         const bool last = (m + 1 == dil.size());
         float* dst = last ? S : RR;
         ConvArgs a2 = conv(T1, C, Ti, C, c.W(n2 + ".w"), C, k, 1, (k - 1) / 2, c.W(n2 + ".b"), dst, C, Ti, B);
+        a2.w_static = 1;
         a2.res = r_in;
         a2.ldr = C;
         a2.res_bs = (long long)Ti * C;

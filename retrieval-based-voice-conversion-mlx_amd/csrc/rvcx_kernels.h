@@ -93,6 +93,10 @@ struct ConvArgs {
   int astage = 0;  // A-tile staging batch: 0 = default (RVCX_CONV_ASB or 1), 1 = serial, 4 = 4 loads in flight
   int math = 0;    // contraction arithmetic: 0 = default (RVCX_CONV_MATH), 1 = native fp32 MFMA, 2 = fp32 via 3 bf16 planes
   // split-K: set by conv_plan_splitk; ws holds ksplit partial [rows][N] tiles per batch entry
+  // weight-streamed split kernel (conv_wsb.hip): w pre-split into bf16 planes, set by the runtime for static weights
+  int w_static = 0;             // the B operand is a constant weight tensor (callers set it; enables the cache)
+  const void* wsplit = nullptr;  // ((chunk * taps + tap) * wsplit_npad + n) rows of [hi|mid|lo] x 32 bf16
+  int wsplit_npad = 0;
   int ksplit = 1;
   int no_splitk = 0;
   long long ws_rows = 0;
@@ -125,6 +129,15 @@ hipError_t softmax_rel(float* scores, int T, int n_heads, int B, const float* re
 hipError_t softmax_rows(float* scores, int rows, int cols, hipStream_t s);
 // y[b][t][c] += nb[c] + sum_{q < taps*stride} wf[(q / stride) * C + c][q % stride] * har[b*har_bs + t*stride + q]
 // (the NSF noise conv, hifigan_nsf.py:196-199, in its framed form); C % 4 == 0, taps*stride <= 16
+// weight-streamed split conv (conv_wsb.hip): eligibility (1-D, stride 1, C_in % 32 == 0, halo <= 64 rows, no
+// split-K), the pre-split weight image and its launch; conv_wsb_wants = eligible + split arithmetic + a grid
+// large enough to fill the chip (conv_gemm.hip policy)
+bool conv_wsb_eligible(const ConvArgs& a);
+bool conv_wsb_wants(const ConvArgs& a);
+int conv_wsplit_npad(int N);
+long long conv_wsplit_bytes(const ConvArgs& a);
+hipError_t conv_wsplit_build(const ConvArgs& a, void* out, hipStream_t s);
+hipError_t conv_wsb_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream_t s);
 // CREPE (crepe.hip): frames [nf][ld] (254 zeros | 1024 normalised samples | 254 zeros) of frames f_first..;
 // relu -> BatchNorm (bn = mean | 1/sqrt(var+eps) | gamma | beta, C each) -> max over row pairs [rows_in][C] ->
 // [rows_in/2][C]; decode + 3-tap filters: probs [F][360] -> f0 (fp32), f0d (fp64, optional), per (optional)
