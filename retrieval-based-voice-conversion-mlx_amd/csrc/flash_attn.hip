@@ -1,0 +1,338 @@
+// Fused multi-head attention without a [B][heads][T][T] score buffer (flash-style online softmax), for the
+// TextEncoder's windowed relative-position attention (rvc/lib/algorithm/attentions.py:79-185: scores =
+// (q/sqrt(d)) k^T + band of (q/sqrt(d)) rel_k^T, masked_fill(mask == 0, -1e4), softmax, p v + band(p) rel_v) and
+// HuBERT's plain attention (modeling_hubert.py HubertAttention: softmax((q * d^-0.5) k^T) v).
+//
+// One wave per (32-query block, key split, batch x head). The wave works in the transposed frame so that no
+// fragment needs an LDS transpose: S^T = K Q^T (A = K rows, B = Q^T; MFMA C layout puts one query per lane
+// column), the softmax statistics of a query are a lane's own 16 registers plus its partner lane (lane ^ 32),
+// and O^T = V^T P^T takes P^T straight from the S^T registers as the B fragment (the K16 slots of a lane are its
+// C rows, the same key permutation on the A side). Every product uses the exact 3-plane bf16 split of
+// conv_emu.hip (fp32 accurate). Key splits write unnormalised partials (O, running max, running sum) that
+// k_flash_combine merges; the relative-value band is folded into each split's O before it is written.
+#include <algorithm>
+#include <cmath>
+
+#include "split_bf16.h"
+
+namespace rvcx {
+
+namespace {
+
+using namespace splitbf16;
+
+constexpr int FA_Q = 32;    // queries per wave
+constexpr int FA_K = 32;    // keys per block
+constexpr int FA_NW = 32;   // max relative window 2w+1 (LDS table width)
+
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8 (&out)[3]) {
+  char buf[3 * 16];
+  // reuse the 4-wide splitter on a private 3-plane row of 8 channels
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    f32x4 x = {v[4 * h], v[4 * h + 1], v[4 * h + 2], v[4 * h + 3]};
+    uint2 hi, mi, lo;
+    hi.x = pk_bf16(x[0], x[1]);
+    hi.y = pk_bf16(x[2], x[3]);
+    float r0 = x[0] - lo_f(hi.x), r1 = x[1] - hi_f(hi.x), r2 = x[2] - lo_f(hi.y), r3 = x[3] - hi_f(hi.y);
+    mi.x = pk_bf16(r0, r1);
+    mi.y = pk_bf16(r2, r3);
+    r0 -= lo_f(mi.x);
+    r1 -= hi_f(mi.x);
+    r2 -= lo_f(mi.y);
+    r3 -= hi_f(mi.y);
+    lo.x = pk_bf16(r0, r1);
+    lo.y = pk_bf16(r2, r3);
+    *reinterpret_cast<uint2*>(buf + 8 * h) = hi;
+    *reinterpret_cast<uint2*>(buf + 16 + 8 * h) = mi;
+    *reinterpret_cast<uint2*>(buf + 32 + 8 * h) = lo;
+  }
+#pragma unroll
+  for (int q = 0; q < 3; ++q) out[q] = *reinterpret_cast<const bf16x8*>(buf + 16 * q);
+}
+
+__device__ __forceinline__ f32x16 mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
+  return c;
+}
+
+// key row of C register r for the half-wave hk (MFMA 32x32 C layout)
+__device__ __forceinline__ int crow(int r, int hk) { return (r & 3) + 8 * (r >> 2) + 4 * hk; }
+
+// qkv [B][T][ldq]: q at col h*DK, k at H + h*DK, v at 2H + h*DK. part_o [nsplit][BH][T][DK], part_ml
+// [nsplit][BH][T][2] (running max, running sum).
+template <int DK>
+__global__ __launch_bounds__(64) void k_flash_attn(const float* __restrict__ qkv, int ldq, int T, int nh, int H,
+                                                   float qscale, int kb_per_split, const float* __restrict__ rel_k,
+                                                   const float* __restrict__ rel_v, int window,
+                                                   const float* __restrict__ mask, float* __restrict__ part_o,
+                                                   float* __restrict__ part_ml) {
+  constexpr int NS = DK / 16;  // K16 steps over the head dimension
+  constexpr int NT = DK / 32;  // 32-dim tiles of O^T
+  __shared__ float relq[FA_Q][FA_NW + 1];
+  __shared__ float pband[FA_Q][FA_NW + 1];
+  const int lane = threadIdx.x, li = lane & 31, hk = lane >> 5;
+  const int q0 = blockIdx.x * FA_Q, split = blockIdx.y, bh = blockIdx.z;
+  const int b = bh / nh, h = bh % nh;
+  const int nsplit = gridDim.y;
+  const int BH = gridDim.z;
+  const float* base = qkv + (long long)b * T * ldq;
+  const int i = q0 + li;
+  const bool qok = i < T;
+  const int nw = rel_k ? 2 * window + 1 : 0;
+  const float* mk = mask ? mask + (long long)b * T : nullptr;
+  const float mi = (mk && qok) ? mk[i] : 1.f;
+
+  // Q^T fragments (scaled), kept for the whole key range
+  bf16x8 qf[NS][3];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (qok) {
+      const float4* src = reinterpret_cast<const float4*>(base + (long long)i * ldq + h * DK + 16 * s + 8 * hk);
+      const float4 x0 = src[0], x1 = src[1];
+      v[0] = x0.x * qscale; v[1] = x0.y * qscale; v[2] = x0.z * qscale; v[3] = x0.w * qscale;
+      v[4] = x1.x * qscale; v[5] = x1.y * qscale; v[6] = x1.z * qscale; v[7] = x1.w * qscale;
+    }
+    split8(v, qf[s]);
+  }
+  const int nkb = (T + FA_K - 1) / FA_K;
+  const int kb0 = split * kb_per_split, kb1 = min(nkb, kb0 + kb_per_split);
+  // does this split's key range reach the relative-position band of this query block?
+  const bool band_split = nw && kb0 < kb1 && (kb1 * FA_K - 1 >= q0 - window) && (kb0 * FA_K <= q0 + FA_Q - 1 + window);
+  // relative key logits of this wave's queries as one MFMA tile: relq^T[o][i] = rel_k[o] . (q_i * qscale)
+  if (band_split) {
+    f32x16 rq;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) rq[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (li < nw) {
+        const float* src = rel_k + li * DK + 16 * s + 8 * hk;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = src[e];
+      }
+      bf16x8 rf[3];
+      split8(v, rf);
+      rq = mfma6(rf, qf[s], rq);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int od = crow(r, hk);
+      relq[li][od] = rq[r];
+      pband[li][od] = 0.f;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+  f32x16 o[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+
+  for (int kb = kb0; kb < kb1; ++kb) {
+    const int j0 = kb * FA_K;
+    // S^T = K Q^T for keys j0.. (rows) x this wave's queries (columns)
+    f32x16 sc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sc[r] = 0.f;
+    {
+      const int j = j0 + li;
+      const bool kok = j < T;
+      const float* kr = base + (long long)j * ldq + H + h * DK + 8 * hk;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (kok) {
+          const float4 x0 = *reinterpret_cast<const float4*>(kr + 16 * s);
+          const float4 x1 = *reinterpret_cast<const float4*>(kr + 16 * s + 4);
+          v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w;
+          v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+        }
+        bf16x8 kf[3];
+        split8(v, kf);
+        sc = mfma6(kf, qf[s], sc);
+      }
+    }
+    // relative-position band, mask fill (-1e4), keys past T excluded
+    float mloc = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int j = j0 + crow(r, hk);
+      float v = sc[r];
+      if (nw) {
+        const int od = j - i + window;
+        if (od >= 0 && od < nw) v = v + relq[li][od];
+      }
+      if (mk && j < T && mi * mk[j] == 0.f) v = -1e4f;
+      if (j >= T) v = -INFINITY;
+      sc[r] = v;
+      mloc = fmaxf(mloc, v);
+    }
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32));
+    const float m_new = fmaxf(m_run, mloc);
+    const float alpha = expf(m_run - m_new);
+    float lsum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sc[r] = expf(sc[r] - m_new);
+      lsum += sc[r];
+    }
+    lsum += __shfl_xor(lsum, 32);
+    l_run = l_run * alpha + lsum;
+    m_run = m_new;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+    if (band_split) {
+      // keys of this block inside the band: rescale the band sums (once per query), then add
+      const bool band = (j0 + FA_K - 1 >= q0 - window) && (j0 <= q0 + FA_Q - 1 + window);
+      if (hk == 0)
+        for (int od = 0; od < nw; ++od) pband[li][od] *= alpha;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (band) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int od = j0 + crow(r, hk) - i + window;
+          if (od >= 0 && od < nw) pband[li][od] += sc[r];
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    // O^T += V^T P^T: the B fragment of K16 step s2 is P^T's registers 8 s2 .. 8 s2 + 7 (keys crow(.)+16 s2)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      float pv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) pv[e] = sc[8 * s2 + e];
+      bf16x8 pf[3];
+      split8(pv, pf);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int j = j0 + crow(8 * s2 + e, hk);
+          v[e] = j < T ? base[(long long)j * ldq + 2 * H + h * DK + 32 * t + li] : 0.f;
+        }
+        bf16x8 vf[3];
+        split8(v, vf);
+        o[t] = mfma6(vf, pf, o[t]);
+      }
+    }
+  }
+  // the relative-value band of this split as MFMAs: O^T[d][i] += sum_o rel_v^T[d][o] pband^T[o][i] (o < 32)
+  if (band_split) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      float pv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) pv[e] = pband[li][16 * s2 + 8 * hk + e];
+      bf16x8 pf[3];
+      split8(pv, pf);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int od = 16 * s2 + 8 * hk + e;
+          v[e] = od < nw ? rel_v[od * DK + 32 * t + li] : 0.f;
+        }
+        bf16x8 vf[3];
+        split8(v, vf);
+        o[t] = mfma6(vf, pf, o[t]);
+      }
+    }
+  }
+  if (!qok) return;
+  const long long row = ((long long)split * BH + bh) * T + i;
+  float* po = part_o + row * DK;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) po[32 * t + crow(r, hk)] = o[t][r];
+  if (hk == 0) {
+    part_ml[2 * row] = m_run;
+    part_ml[2 * row + 1] = l_run;
+  }
+  (void)nsplit;
+}
+
+// out[b][i][h*DK + d] = sum_s O_s[d] e^(m_s - M) / sum_s l_s e^(m_s - M)
+__global__ void k_flash_combine(const float* __restrict__ part_o, const float* __restrict__ part_ml, int nsplit,
+                                int BH, int T, int DK, int nh, float* __restrict__ out, int ldo) {
+  const long long n = (long long)BH * T * DK;
+  for (long long x = blockIdx.x * (long long)blockDim.x + threadIdx.x; x < n; x += (long long)gridDim.x * blockDim.x) {
+    const int d = (int)(x % DK);
+    const long long bt = x / DK;
+    const int i = (int)(bt % T);
+    const int bh = (int)(bt / T);
+    float M = -INFINITY;
+    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, part_ml[2 * (((long long)s * BH + bh) * T + i)]);
+    float L = 0.f, acc = 0.f;
+    for (int s = 0; s < nsplit; ++s) {
+      const long long row = ((long long)s * BH + bh) * T + i;
+      const float ms = part_ml[2 * row];
+      if (ms == -INFINITY) continue;  // an empty split
+      const float e = expf(ms - M);
+      L += part_ml[2 * row + 1] * e;
+      acc += part_o[row * DK + d] * e;
+    }
+    const int b = bh / nh, h = bh % nh;
+    out[((long long)b * T + i) * ldo + h * DK + d] = acc / L;
+  }
+}
+
+}  // namespace
+
+// key splits: enough waves for two per SIMD (the kernel is latency-bound per key block), at least 2 key blocks
+// per split
+int flash_attn_splits(int B, int nh, int T) {
+  const int qb = (T + FA_Q - 1) / FA_Q, kb = (T + FA_K - 1) / FA_K;
+  int ns = (2048 + qb * B * nh - 1) / (qb * B * nh);
+  ns = std::max(1, std::min(ns, std::max(1, kb / 2)));
+  return ns;
+}
+
+hipError_t flash_attn(const float* qkv, int ldq, int B, int T, int nh, int dk, float qscale, const float* rel_k,
+                      const float* rel_v, int window, const float* mask, float* part_o, float* part_ml, int nsplit,
+                      float* out, int ldo, hipStream_t s) {
+  if (T <= 0) return hipSuccess;
+  if ((ldq & 3) != 0 || (reinterpret_cast<uintptr_t>(qkv) & 15) != 0) return hipErrorInvalidValue;  // float4 rows
+  if ((rel_k != nullptr) != (rel_v != nullptr) || (rel_k && 2 * window + 1 > FA_NW) || nsplit < 1)
+    return hipErrorInvalidValue;
+  const int H = nh * dk;
+  const int qb = (T + FA_Q - 1) / FA_Q, kb = (T + FA_K - 1) / FA_K;
+  const int per = (kb + nsplit - 1) / nsplit;
+  dim3 grid(qb, nsplit, B * nh);
+  if (dk == 64)
+    hipLaunchKernelGGL(k_flash_attn<64>, grid, dim3(64), 0, s, qkv, ldq, T, nh, H, qscale, per, rel_k, rel_v, window,
+                       mask, part_o, part_ml);
+  else if (dk == 96)
+    hipLaunchKernelGGL(k_flash_attn<96>, grid, dim3(64), 0, s, qkv, ldq, T, nh, H, qscale, per, rel_k, rel_v, window,
+                       mask, part_o, part_ml);
+  else
+    return hipErrorInvalidValue;
+  const long long n = (long long)B * nh * T * dk;
+  const long long nb = std::min<long long>((n + 255) / 256, 1 << 20);
+  hipLaunchKernelGGL(k_flash_combine, dim3((unsigned)nb), dim3(256), 0, s, part_o, part_ml, nsplit, B * nh, T, dk, nh,
+                     out, ldo);
+  return hipGetLastError();
+}
+
+}  // namespace rvcx

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <functional>
 #include <map>
 #include <memory>
@@ -248,6 +249,16 @@ hipStream_t fork_aux(Ctx& c, hipStream_t s);
 void join_aux(Ctx& c, hipStream_t s, hipStream_t ax);
 // launch one implicit-GEMM conv (1-D or 2-D) with optional event timing; flops = algorithmic FLOPs
 void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double flops = -1.0);
+
+// fused attention (flash_attn.hip) for the TextEncoder and HuBERT; RVCX_NO_FLASH=1 restores the materialised
+// score path (A/B measurement aid)
+inline bool flash_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("RVCX_NO_FLASH");
+    return !(e && std::atoi(e) != 0);
+  }();
+  return v;
+}
 
 inline void check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw Error(RVCX_E_HIP, std::string(what) + ": " + hipGetErrorString(e));

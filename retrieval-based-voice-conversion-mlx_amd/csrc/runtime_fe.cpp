@@ -223,13 +223,22 @@ void hubert_layers(Ctx& c, const HubertRun& run, int l0, int l1, hipStream_t s) 
   float* hs = c.buf<float>("hb.hs", (size_t)BL * HD, s);
   float* hs2 = c.buf<float>("hb.hs2", (size_t)BL * HD, s);
   float* qkv = c.buf<float>("hb.qkv", (size_t)BL * 3 * HD, s);
-  float* sc = c.buf<float>("hb.scores", (size_t)B * HHEADS * L * L, s);
+  const bool fused = flash_enabled();
+  const int nsplit = flash_attn_splits(B, HHEADS, L);
+  float* sc = fused ? nullptr : c.buf<float>("hb.scores", (size_t)B * HHEADS * L * L, s);
+  float* part_o = fused ? c.buf<float>("hb.fa_o", (size_t)nsplit * B * HHEADS * L * (HD / HHEADS), s) : nullptr;
+  float* part_ml = fused ? c.buf<float>("hb.fa_ml", (size_t)nsplit * B * HHEADS * L * 2, s) : nullptr;
   float* att = c.buf<float>("hb.att", (size_t)BL * HD, s);
   float* ff = c.buf<float>("hb.ff", (size_t)BL * HFF, s);
   const int hd = HD / HHEADS;
   for (int i = l0; i < l1; ++i) {
     const std::string q = "hb." + std::to_string(i);
     run1(c, lin(hs, HD, BL, HD, c.W(q + ".qkv.w"), 3 * HD, c.W(q + ".qkv.b"), qkv, 3 * HD), s);
+    if (fused) {  // softmax((q * hd^-0.5) k^T) v per head in one pass (flash_attn.hip): no [B][12][L][L] scores
+      check(flash_attn(qkv, 3 * HD, B, L, HHEADS, hd, (float)std::pow((double)hd, -0.5), nullptr, nullptr, 0, nullptr,
+                       part_o, part_ml, nsplit, att, HD, s),
+            "flash_attn");
+    } else {
     {
       ConvArgs a1 = lin(qkv, 3 * HD, L, hd, qkv + HD, L, nullptr, sc, L);
       a1.ldw = 3 * HD;
@@ -257,6 +266,7 @@ void hubert_layers(Ctx& c, const HubertRun& run, int l0, int l1, hipStream_t s) 
       a2.w_bs = (long long)L * 3 * HD;
       a2.y_bs = (long long)L * HD;
       run1(c, a2, s);
+    }
     }
     {
       ConvArgs a3 = lin(att, HD, BL, HD, c.W(q + ".o.w"), HD, c.W(q + ".o.b"), hs2, HD);

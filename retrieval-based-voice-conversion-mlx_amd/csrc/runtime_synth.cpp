@@ -463,9 +463,13 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
     run(c, a, s);
   }
   float* qkv = c.buf<float>("te.qkv", BT * 3 * H, s);
-  float* sc = c.buf<float>("te.scores", (size_t)B * nh * T * T, s);
-  float* rel = c.buf<float>("te.rel", (size_t)B * nh * T * nw, s);
-  float* pband = c.buf<float>("te.pband", (size_t)B * nh * T * nw, s);
+  const bool fused = flash_enabled();
+  const int nsplit = flash_attn_splits(B, nh, T);
+  float* sc = fused ? nullptr : c.buf<float>("te.scores", (size_t)B * nh * T * T, s);
+  float* rel = fused ? nullptr : c.buf<float>("te.rel", (size_t)B * nh * T * nw, s);
+  float* pband = fused ? nullptr : c.buf<float>("te.pband", (size_t)B * nh * T * nw, s);
+  float* part_o = fused ? c.buf<float>("te.fa_o", (size_t)nsplit * B * nh * T * dk, s) : nullptr;
+  float* part_ml = fused ? c.buf<float>("te.fa_ml", (size_t)nsplit * B * nh * T * 2, s) : nullptr;
   float* att = c.buf<float>("te.att", BT * H, s);
   float* o = c.buf<float>("te.o", BT * H, s);
   float* h1 = c.buf<float>("te.h1", BT * F, s);
@@ -473,6 +477,11 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
   for (int i = 0; i < cf.n_layers; ++i) {
     const std::string q = "te." + std::to_string(i);
     run(c, lin(x, H, (int)BT, H, c.W(q + ".qkv.w"), 3 * H, c.W(q + ".qkv.b"), qkv, 3 * H), s);
+    if (fused) {  // attentions.py:79-185 in one pass per query block (flash_attn.hip): no [B][nh][T][T] scores
+      check(flash_attn(qkv, 3 * H, B, T, nh, dk, qscale, c.W(q + ".rel_k"), c.W(q + ".rel_v"), cf.window, mask, part_o,
+                       part_ml, nsplit, att, H, s),
+            "flash_attn");
+    } else {
     {  // scores = (q / sqrt(dk)) k^T   (attentions.py:96)
       ConvArgs a = lin(qkv, 3 * H, T, dk, qkv + H, T, nullptr, sc, T);
       a.ldw = 3 * H;
@@ -525,6 +534,7 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
       a.y_bs2 = dk;
       a.acc_mode = ACC_ADD;
       run(c, a, s);
+    }
     }
     run(c, lin(att, H, (int)BT, H, c.W(q + ".o.w"), H, c.W(q + ".o.b"), o, H), s);
     check(layernorm_rows(x, o, x, c.W(q + ".ln1.g"), c.W(q + ".ln1.b"), (int)BT, H, 1e-5f, nullptr, s), "ln1");

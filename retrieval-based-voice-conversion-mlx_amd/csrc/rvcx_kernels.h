@@ -138,6 +138,13 @@ int conv_wsplit_npad(int N);
 long long conv_wsplit_bytes(const ConvArgs& a);
 hipError_t conv_wsplit_build(const ConvArgs& a, void* out, hipStream_t s);
 hipError_t conv_wsb_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream_t s);
+// fused attention (flash_attn.hip): qkv [B][T][ldq] (q | k | v, heads of dk inside each), optional relative
+// window (rel_k / rel_v [2w+1][dk]) and key/query mask [B][T]; partials part_o [nsplit][B*nh][T][dk], part_ml
+// [nsplit][B*nh][T][2]; out [B][T][ldo] at column h*dk
+int flash_attn_splits(int B, int nh, int T);
+hipError_t flash_attn(const float* qkv, int ldq, int B, int T, int nh, int dk, float qscale, const float* rel_k,
+                      const float* rel_v, int window, const float* mask, float* part_o, float* part_ml, int nsplit,
+                      float* out, int ldo, hipStream_t s);
 // CREPE (crepe.hip): frames [nf][ld] (254 zeros | 1024 normalised samples | 254 zeros) of frames f_first..;
 // relu -> BatchNorm (bn = mean | 1/sqrt(var+eps) | gamma | beta, C each) -> max over row pairs [rows_in][C] ->
 // [rows_in/2][C]; decode + 3-tap filters: probs [F][360] -> f0 (fp32), f0d (fp64, optional), per (optional)
