@@ -321,7 +321,9 @@ int rvcx_set_conv_math(rvcx_ctx* ctx, int mode);
 /* One Conv1d forward, time-major: d_x [T][C_in], d_w [taps][N][C_in] (torch weight [N][C_in][taps] permuted),
  * d_bias [N] (optional), d_y [T_out][N]; y[t] = bias + sum_k W[k] x[t*stride - pad + k*dilation] (zero outside).
  * The kernel family behind every contraction of the path, exposed for numerics tests; replaces
- * torch.nn.Conv1d.forward as used throughout rvc/lib/algorithm (e.g. residuals.py:34-80). math as above. */
+ * torch.nn.Conv1d.forward as used throughout rvc/lib/algorithm (e.g. residuals.py:34-80). math as above, plus
+ * 3 = the split arithmetic on the weight-streamed kernel (weights pre-split in HBM; 1-D stride-1 convs with
+ * C_in % 32 == 0 and (taps - 1) * dilation <= 64, else RVCX_E_SHAPE). */
 int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const float* d_w, const float* d_bias, int N,
                 int taps, int dilation, int pad, int stride, int math, float* d_y, int64_t T_out, void* stream);
 

@@ -128,7 +128,7 @@ void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double
   ConvArgs a = a_in;
   if (c.conv_math > 0 && a.math == 0) a.math = c.conv_math;
   const long long need = conv_plan_splitk(a, two_d);
-  if (!two_d && a.w_static && conv_wsb_wants(a)) {
+  if (!two_d && a.w_static && (a.force_cfg >= 20 || conv_wsb_wants(a))) {
     a.wsplit = c.wsplit_for(a, s);
     a.wsplit_npad = conv_wsplit_npad(a.N);
   }
@@ -516,7 +516,7 @@ int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const floa
     set_device(ctx);
     ctx->check_device_status();
     if (!d_x || !d_w || !d_y || T <= 0 || C_in <= 0 || N <= 0 || taps <= 0 || dilation <= 0 || stride <= 0 ||
-        pad < 0 || T_out <= 0 || math < 0 || math > 2)
+        pad < 0 || T_out <= 0 || math < 0 || math > 3)
       throw Error(RVCX_E_INVALID, "rvcx_conv1d: bad argument");
     if ((T_out - 1) * stride + (int64_t)(taps - 1) * dilation + 1 > T + 2 * (int64_t)pad)
       throw Error(RVCX_E_SHAPE, "rvcx_conv1d: T_out exceeds the padded input");
@@ -527,7 +527,13 @@ int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const floa
     a.w = d_w; a.ldw = C_in; a.w_ts = (long long)N * C_in; a.taps = taps; a.dil = dilation; a.pad = pad;
     a.stride = stride;
     a.y = d_y; a.ldy = N; a.T_out = (int)T_out; a.N = N; a.bias = d_bias;
-    a.math = math;
+    a.math = math == 3 ? 2 : math;
+    if (math == 3) {  // the weight-streamed split kernel (conv_wsb.hip) whatever the size policy would pick
+      if (!conv_wsb_eligible(a)) throw Error(RVCX_E_SHAPE, "rvcx_conv1d: shape not eligible for the weight-streamed kernel");
+      a.w_static = 1;
+      a.force_cfg = N <= 32 ? 20 : (N <= 64 ? 21 : 22);
+      a.no_splitk = 1;
+    }
     launch_conv(*ctx, a, false, static_cast<hipStream_t>(stream), -1.0);
   });
 }
