@@ -327,6 +327,18 @@ int rvcx_set_conv_math(rvcx_ctx* ctx, int mode);
 int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const float* d_w, const float* d_bias, int N,
                 int taps, int dilation, int pad, int stride, int math, float* d_y, int64_t T_out, void* stream);
 
+/* One ResBlock dilation pair as one fused kernel (csrc/resblock_fused.hip), time-major: d_x, d_y [B][T][C] (distinct
+ * buffers), d_w1 / d_w2 [k][C][C] (torch weight [C][C][k] permuted), d_b1 / d_b2 [C]:
+ *     out = conv2(lrelu(conv1_d(lrelu(x), 0.1) + b1, 0.1)) + b2 + x     (zero padding; conv2 dilation 1)
+ *     acc_mode 0: y = out; 1: y = y + out; 2: y = (y + out) / acc_div
+ * Replaces one iteration of ResBlock.forward (rvc/lib/algorithm/residuals.py:71-80) and MRFLayer.forward
+ * (generators/hifigan_mrf.py:45-50), plus the ResBlock mean of HiFiGANNSFGenerator.forward (hifigan_nsf.py:190-207)
+ * on the last pair. C in {32, 64}, odd k, (k - 1) / 2 * dilation <= 30, else RVCX_E_SHAPE. cfg 0 = default
+ * tile (RVCX_RB_CFG in the pipeline). Exposed for numerics tests and A/B timing. */
+int rvcx_resblock_pair(rvcx_ctx* ctx, const float* d_x, int B, int64_t T, int C, const float* d_w1, const float* d_b1,
+                       const float* d_w2, const float* d_b2, int k, int dilation, int acc_mode, float acc_div, int cfg,
+                       float* d_y, void* stream);
+
 /* Upsampling factor of the loaded synthesizer (prod(upsample_rates); net_g.dec.upp). */
 int rvcx_synth_upp(const rvcx_ctx* ctx);
 

@@ -124,6 +124,50 @@ const void* Ctx::wsplit_for(const ConvArgs& a, hipStream_t s) {
   return slot->p;
 }
 
+const void* Ctx::rb_wsplit_for(const float* w, int C, int k, hipStream_t s) {
+  auto& slot = rb_wsplit_cache[static_cast<const void*>(w)];
+  if (!slot) {
+    std::unique_ptr<DevBuf> b(new DevBuf());
+    const size_t bytes = (size_t)rb_wsplit_bytes(C, k);
+    if (hipMalloc(&b->p, bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      throw Error(RVCX_E_OOM, "split-weight allocation failed");
+    }
+    b->bytes = bytes;
+    check(rb_wsplit_build(w, C, k, b->p, s), "rb_wsplit_build");
+    RVCX_HIP(hipStreamSynchronize(s));
+    slot = std::move(b);
+  }
+  return slot->p;
+}
+
+void launch_rb_pair(Ctx& c, const RbPairArgs& a, hipStream_t s) {
+  static const int cfg = [] {
+    const char* e = std::getenv("RVCX_RB_CFG");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (!c.prof) {
+    check(rb_pair(a, cfg, s), "rb_pair");
+    return;
+  }
+  hipEvent_t ev[2];
+  for (auto& e : ev) {
+    if (!c.prof_pool.empty()) {
+      e = c.prof_pool.back();
+      c.prof_pool.pop_back();
+    } else {
+      RVCX_HIP(hipEventCreate(&e));
+    }
+  }
+  // algorithmic work: the two convs over the valid rows
+  const double flops = 2.0 * 2.0 * a.B * (double)a.T * a.C * a.C * a.k;
+  Ctx::ProfRec r{ev[0], ev[1], flops, 0, a.T, a.C, a.C, -a.k, a.B, 1};
+  RVCX_HIP(hipEventRecord(r.a, s));
+  check(rb_pair(a, cfg, s), "rb_pair");
+  RVCX_HIP(hipEventRecord(r.b, s));
+  c.prof_recs.push_back(r);
+}
+
 void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double flops) {
   ConvArgs a = a_in;
   if (c.conv_math > 0 && a.math == 0) a.math = c.conv_math;
@@ -260,6 +304,7 @@ int rvcx_finalize(rvcx_ctx* ctx, int model) {
     }
     RVCX_HIP(hipDeviceSynchronize());
     ctx->wsplit_cache.clear();  // weights may have been re-packed at new addresses
+    ctx->rb_wsplit_cache.clear();
     ctx->ready[model] = true;
   });
 }
@@ -535,6 +580,43 @@ int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const floa
       a.no_splitk = 1;
     }
     launch_conv(*ctx, a, false, static_cast<hipStream_t>(stream), -1.0);
+  });
+}
+
+int rvcx_resblock_pair(rvcx_ctx* ctx, const float* d_x, int B, int64_t T, int C, const float* d_w1, const float* d_b1,
+                       const float* d_w2, const float* d_b2, int k, int dilation, int acc_mode, float acc_div, int cfg,
+                       float* d_y, void* stream) {
+  return guard(ctx, [&] {
+    set_device(ctx);
+    ctx->check_device_status();
+    if (!d_x || !d_y || !d_w1 || !d_w2 || !d_b1 || !d_b2 || B <= 0 || T <= 0 || acc_mode < 0 || acc_mode > 2 ||
+        d_x == d_y || cfg < 0)
+      throw Error(RVCX_E_INVALID, "rvcx_resblock_pair: bad argument");
+    if (!rb_pair_fits(C, k, dilation) || T > INT32_MAX / C)
+      throw Error(RVCX_E_SHAPE, "rvcx_resblock_pair: shape not supported by the fused kernel");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    // fresh split images every call (test entry: the weight pointers may be reused by the caller)
+    void* w1s = ctx->buf<char>("rb.test.w1s", (size_t)rb_wsplit_bytes(C, k), s);
+    void* w2s = ctx->buf<char>("rb.test.w2s", (size_t)rb_wsplit_bytes(C, k), s);
+    check(rb_wsplit_build(d_w1, C, k, w1s, s), "rb_wsplit_build");
+    check(rb_wsplit_build(d_w2, C, k, w2s, s), "rb_wsplit_build");
+    RbPairArgs a;
+    a.x = d_x;
+    a.x_bs = T * C;
+    a.w1s = w1s;
+    a.b1 = d_b1;
+    a.w2s = w2s;
+    a.b2 = d_b2;
+    a.C = C;
+    a.k = k;
+    a.d = dilation;
+    a.T = (int)T;
+    a.B = B;
+    a.y = d_y;
+    a.y_bs = T * C;
+    a.acc_mode = acc_mode;
+    a.acc_div = acc_div;
+    check(rb_pair(a, cfg, s), "rb_pair");
   });
 }
 

@@ -1,0 +1,385 @@
+// One ResBlock dilation pair of the HiFi-GAN generators as ONE kernel (residuals.py:71-80, ResBlock.forward;
+// hifigan_mrf.py:45-50, MRFLayer.forward):
+//     t   = lrelu(conv1_d(lrelu(x)) + b1)          (k taps, dilation d, zero padding)
+//     out = conv2(t) + b2 + x                      (k taps, dilation 1, zero padding)
+//     y   = out | y + out | (y + out) / div        (the ResBlock mean of hifigan_nsf.py:190-207 on the last pair)
+// The intermediate t never leaves the CU: a workgroup loads its x tile (+ both convs' halo) once, splits lrelu(x)
+// into bf16 planes in LDS, runs conv1 into a second LDS image of t and conv2 out of it, and writes only the pair's
+// output. Per pair that is one read and one write of the [T][C] activation instead of five passes (x, t written,
+// t read, x re-read as the residual, out), and one launch instead of two latency-bound ones at 32/64 channels.
+//
+// Arithmetic: the exact 3-plane bf16 split of conv_emu.hip (x = x0 + x1 + x2, six plane products with i + j <= 2
+// summed smallest first into one fp32 accumulator per output).
+//
+// Orientation: D[out channel][time] = W[out ch][in ch] * X^T[in ch][time] on v_mfma_f32_32x32x16_bf16, so a lane
+// of the accumulator holds 16 output channels of ONE time step. Inside each 16-channel chunk the contraction slots
+// are permuted (slot j <-> channel rb_pi(j), bits 2 and 3 swapped) so those 16 registers are exactly two chunks'
+// worth of 8 consecutive slots: conv1's epilogue writes its t image with 16-byte LDS stores (6 per 32x32 tile),
+// already in conv2's B-fragment layout. Weights are pre-split once into the same slot order, per lane one 16-byte
+// A fragment per (tap, chunk, plane), loaded from L1/L2 one step ahead.
+#include <algorithm>
+
+#include "conv_common.h"
+#include "split_bf16.h"
+
+namespace rvcx {
+
+namespace {
+
+using namespace splitbf16;
+
+constexpr int RB_THREADS = 256;
+constexpr int RB_MAXH1 = 30;  // conv1 halo rows per side supported: (k - 1) / 2 * d
+
+__host__ __device__ constexpr int rb_pi(int j) { return (j & 3) | (((j >> 3) & 1) << 2) | (((j >> 2) & 1) << 3); }
+
+template <int C>
+struct RbGeo {
+  static constexpr int NCH = C / 16;               // 16-channel contraction chunks
+  static constexpr int ROW = NCH * 3 * 32 + 16;    // LDS bytes per time row: [chunk][plane][16 slots] + pad
+};
+
+// w [tap][C_out][C_in] fp32 -> ((tap * NCH + s) * 3 + q) planes of [C_out][16 slots] bf16, slot j = channel
+// 16 s + rb_pi(j) (put_split1's arithmetic)
+__global__ void k_rb_wsplit(const float* __restrict__ w, int C, int k, unsigned short* __restrict__ out) {
+  const int NCH = C / 16;
+  const long long total = (long long)k * NCH * C * 16;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(i & 15);
+    long long r = i >> 4;
+    const int och = (int)(r % C);
+    r /= C;
+    const int s = (int)(r % NCH), tap = (int)(r / NCH);
+    const float v = w[((long long)tap * C + och) * C + 16 * s + rb_pi(j)];
+    const unsigned h = pk_bf16(v, 0.f);
+    const float rr = v - lo_f(h);
+    const unsigned m = pk_bf16(rr, 0.f);
+    const unsigned l = pk_bf16(rr - lo_f(m), 0.f);
+    const long long base = (((long long)(tap * NCH + s) * 3) * C + och) * 16 + j;
+    out[base] = (unsigned short)h;
+    out[base + (long long)C * 16] = (unsigned short)m;
+    out[base + 2LL * C * 16] = (unsigned short)l;
+  }
+}
+
+// 8 fp32 values -> three 16-byte planes (hi, mid, lo)
+__device__ __forceinline__ void split8(const float (&v)[8], uint4& h, uint4& m, uint4& l) {
+  unsigned hh[4], mm[4], ll[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    hh[p] = pk_bf16(v[2 * p], v[2 * p + 1]);
+    float r0 = v[2 * p] - lo_f(hh[p]), r1 = v[2 * p + 1] - hi_f(hh[p]);
+    mm[p] = pk_bf16(r0, r1);
+    r0 -= lo_f(mm[p]);
+    r1 -= hi_f(mm[p]);
+    ll[p] = pk_bf16(r0, r1);
+  }
+  h = make_uint4(hh[0], hh[1], hh[2], hh[3]);
+  m = make_uint4(mm[0], mm[1], mm[2], mm[3]);
+  l = make_uint4(ll[0], ll[1], ll[2], ll[3]);
+}
+
+__device__ __forceinline__ float lrelu01(float v) { return v > 0.f ? v : v * 0.1f; }
+
+// C channels, NBT 32-row time blocks per workgroup tile, TN time blocks per wave unit
+template <int C, int NBT, int TN>
+__global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, const int ntiles) {
+  constexpr int NCH = RbGeo<C>::NCH, ROW = RbGeo<C>::ROW, OB = C / 32;
+  constexpr int UNITS = OB * NBT / TN;  // wave work units per conv: (out-channel block, TN time blocks)
+  static_assert(UNITS % 4 == 0, "whole units per wave");
+  constexpr int UPW = UNITS / 4;
+  constexpr int C4 = C / 4;
+  constexpr int XROWS_MAX = NBT * 32 + 2 * RB_MAXH1;
+  constexpr int XITER = (XROWS_MAX * C4 + RB_THREADS - 1) / RB_THREADS;
+  extern __shared__ __attribute__((aligned(16))) char rb_smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, hk = lane >> 5;
+  const int k = a.k, h2 = (k - 1) / 2, h1 = h2 * a.d;
+  const int nx = NBT * 32 + 2 * h1;  // XS rows: conv1 inputs
+  const int TT = NBT * 32 - 2 * h2;  // valid outputs per tile
+  char* const XS = rb_smem;
+  char* const TS = rb_smem + (size_t)nx * ROW;
+  // persistent: workgroup g takes tiles g, g + G, ... of the B * ntiles (batch-major) tiles; the next tile's x is
+  // loaded into registers while the current one computes
+  const int total = ntiles * a.B;
+
+  // ---- the wave's jobs: UPW conv1 units, then UPW conv2 units. A unit is one 32-channel output block x TN time
+  // blocks; one (tap, chunk) step of it is 3 A fragments (weights, global/L2, a PF-deep register ring issued PF
+  // steps ahead and across job boundaries), 3 * TN B fragments (LDS, one step ahead) and 6 * TN MFMAs.
+  constexpr int PF = 2;
+  constexpr size_t QS = (size_t)C * 32;  // bytes of one plane of one (tap, chunk) step of the weight image
+  typedef bf16x8 AFrag[3];
+  typedef bf16x8 BFrag[TN][3];
+  const int nsteps = k * NCH;
+  auto unit_ob = [&](int job) { return (wave + 4 * (job % UPW)) % OB; };
+  auto unit_tg = [&](int job) { return (wave + 4 * (job % UPW)) / OB; };
+  auto wl_of = [&](int job) {
+    const char* w = static_cast<const char*>(job < UPW ? a.w1s : a.w2s);
+    return w + (size_t)(unit_ob(job) * 32 + li) * 32 + hk * 16;
+  };
+  auto load_a = [&](const char* wl, int st, AFrag& f) __attribute__((always_inline)) {
+    const char* p = wl + (size_t)st * 3 * QS;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) f[q] = *reinterpret_cast<const bf16x8*>(p + q * QS);
+  };
+  auto load_b = [&](const char* bl, int dil, int st, BFrag& f) __attribute__((always_inline)) {
+    const int tap = st / NCH, s = st - tap * NCH;
+    const char* bp = bl + (size_t)tap * dil * ROW + s * 96;
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) f[tn][q] = *reinterpret_cast<const bf16x8*>(bp + (size_t)tn * 32 * ROW + q * 32);
+  };
+  auto mma = [&](const AFrag& af, const BFrag& bf, f32x16(&acc)[TN]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      f32x16 c = acc[tn];
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bf[tn][0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bf[tn][1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bf[tn][2], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bf[tn][0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bf[tn][1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bf[tn][0], c, 0, 0, 0);
+      acc[tn] = c;
+    }
+  };
+  AFrag ring[PF];
+  auto prefetch_ring = [&](const char* wl) __attribute__((always_inline)) {
+#pragma unroll
+    for (int p = 0; p < PF; ++p)
+      if (p < nsteps) load_a(wl, p, ring[p]);
+  };
+  // acc[tn] = sum over steps; ring[] holds steps 0..PF-1 on entry
+  auto run_conv = [&](const char* wl, const char* bl, int dil, f32x16(&acc)[TN]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[tn][r] = 0.f;
+    BFrag b0, b1;
+    load_b(bl, dil, 0, b0);
+    for (int st = 0; st < nsteps; st += PF) {
+#pragma unroll
+      for (int p = 0; p < PF; ++p) {
+        const int cur = st + p;
+        if (cur < nsteps) {
+          if (cur + 1 < nsteps) load_b(bl, dil, cur + 1, (p & 1) ? b0 : b1);
+          mma(ring[p], (p & 1) ? b1 : b0, acc);
+          if (cur + PF < nsteps) load_a(wl, cur + PF, ring[p]);
+        }
+      }
+    }
+  };
+
+  // ---- x tile -> XS = split(lrelu(x)); row r <-> time t0 - h2 - h1 + r, zero outside [0, T) (conv1's padding)
+  f32x4 xv[XITER];
+  auto load_x = [&](int tile) __attribute__((always_inline)) {
+    const int bb = tile / ntiles, tb = (tile - bb * ntiles) * TT - h2 - h1;
+    const float* Xb = a.x + (long long)bb * a.x_bs;
+#pragma unroll
+    for (int it = 0; it < XITER; ++it) {
+      const int i = it * RB_THREADS + tid;
+      const int r = i / C4, c4 = (i % C4) * 4;
+      const int t = tb + r;
+      const bool ok = r < nx && t >= 0 && t < a.T;
+      xv[it] = ok ? *reinterpret_cast<const f32x4*>(Xb + (long long)t * C + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto write_x = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int it = 0; it < XITER; ++it) {
+      const int i = it * RB_THREADS + tid;
+      const int r = i / C4, c4 = (i % C4) * 4;
+      if (r < nx) {
+        // channels 16 s + 8 p + 4 q + e sit at slots 8 q + 4 p + e
+        const int s = c4 >> 4, o = c4 & 15;
+        const int slot = ((o >> 2) & 1) * 8 + (o >> 3) * 4;
+        char* row = XS + (size_t)r * ROW + s * 96 + slot * 2;
+        const float x0 = lrelu01(xv[it][0]), x1 = lrelu01(xv[it][1]), x2 = lrelu01(xv[it][2]),
+                    x3 = lrelu01(xv[it][3]);
+        uint2 hh, mm, ll;
+        hh.x = pk_bf16(x0, x1);
+        hh.y = pk_bf16(x2, x3);
+        float r0 = x0 - lo_f(hh.x), r1 = x1 - hi_f(hh.x), r2 = x2 - lo_f(hh.y), r3 = x3 - hi_f(hh.y);
+        mm.x = pk_bf16(r0, r1);
+        mm.y = pk_bf16(r2, r3);
+        r0 -= lo_f(mm.x);
+        r1 -= hi_f(mm.x);
+        r2 -= lo_f(mm.y);
+        r3 -= hi_f(mm.y);
+        ll.x = pk_bf16(r0, r1);
+        ll.y = pk_bf16(r2, r3);
+        *reinterpret_cast<uint2*>(row) = hh;
+        *reinterpret_cast<uint2*>(row + 32) = mm;
+        *reinterpret_cast<uint2*>(row + 64) = ll;
+      }
+    }
+  };
+
+  int tile = blockIdx.x;
+  if (tile >= total) return;
+  // the first job's weights and the first tile's x are in flight together
+  prefetch_ring(wl_of(0));
+  load_x(tile);
+#pragma unroll 1
+  for (; tile < total; tile += gridDim.x) {
+  const int b = tile / ntiles;
+  const int t0 = (tile - b * ntiles) * TT;
+  const float* X = a.x + (long long)b * a.x_bs;
+  // XS is dead once every wave passed the previous tile's mid barrier; the barrier below also orders this tile's
+  // conv1 (writing TS) after every wave's conv2 of the previous tile (reading TS)
+  write_x();
+  __syncthreads();
+  if (tile + (int)gridDim.x < total) load_x(tile + gridDim.x);
+  float* Y = a.y + (long long)b * a.y_bs;
+#pragma unroll 1
+  for (int job = 0; job < 2 * UPW; ++job) {
+    const bool second = job >= UPW;
+    if (job == UPW) __syncthreads();  // TS complete (XS dead)
+    const int ob = unit_ob(job), tg = unit_tg(job);
+    const float* bias = second ? a.b2 : a.b1;
+    float bv[4][4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[m][e] = bias[ob * 32 + 8 * m + 4 * hk + e];
+    // conv2: the residual (and the accumulate target) of the lane's outputs, loaded before the MFMAs
+    f32x4 rv[TN][4], dv[TN][4];
+    if (second) {
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int o = (tg * TN + tn) * 32 + li;
+        const int t = t0 + o;
+        const bool ok = o < TT && t < a.T;
+        const long long off = (long long)(ok ? t : 0) * C + ob * 32 + 4 * hk;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          rv[tn][m] = ok ? *reinterpret_cast<const f32x4*>(X + off + 8 * m) : f32x4{0.f, 0.f, 0.f, 0.f};
+          dv[tn][m] = (ok && a.acc_mode != ACC_STORE) ? *reinterpret_cast<const f32x4*>(Y + off + 8 * m)
+                                                      : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+    }
+    f32x16 acc[TN];
+    run_conv(wl_of(job), (second ? TS : XS) + (size_t)(tg * TN * 32 + li) * ROW + hk * 16, second ? 1 : a.d, acc);
+    if (job + 1 < 2 * UPW) prefetch_ring(wl_of(job + 1));
+    else if (tile + (int)gridDim.x < total) prefetch_ring(wl_of(0));
+    if (!second) {
+      // conv1 -> TS = split(lrelu(conv1 + b1)); TS row p <-> time t0 - h2 + p, zero outside [0, T)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int p = (tg * TN + tn) * 32 + li;
+        const int t = t0 - h2 + p;
+        const bool ok = t >= 0 && t < a.T;
+        char* row = TS + (size_t)p * ROW + hk * 16;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          float v[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int r = 8 * hh + i;
+            const float x = lrelu01(acc[tn][r] + bv[r >> 2][r & 3]);
+            v[i] = ok ? x : 0.f;
+          }
+          uint4 H, M, L;
+          split8(v, H, M, L);
+          char* dst = row + (2 * ob + hh) * 96;
+          *reinterpret_cast<uint4*>(dst) = H;
+          *reinterpret_cast<uint4*>(dst + 32) = M;
+          *reinterpret_cast<uint4*>(dst + 64) = L;
+        }
+      }
+    } else {
+      // conv2 + b2 + x -> y (acc mode); output row o <-> time t0 + o, valid for o < TT, t < T
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int o = (tg * TN + tn) * 32 + li;
+        const int t = t0 + o;
+        if (o < TT && t < a.T) {
+          const long long off = (long long)t * C + ob * 32 + 4 * hk;
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            f32x4 o4;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float v = acc[tn][4 * m + e] + bv[m][e];
+              v = v + rv[tn][m][e];
+              if (a.acc_mode == ACC_ADD) v = dv[tn][m][e] + v;
+              else if (a.acc_mode == ACC_ADD_DIV) v = (dv[tn][m][e] + v) / a.acc_div;
+              o4[e] = v;
+            }
+            *reinterpret_cast<f32x4*>(Y + off + 8 * m) = o4;
+          }
+        }
+      }
+    }
+  }
+  }  // tiles
+}
+
+template <int C, int NBT, int TN>
+hipError_t launch_rb(const RbPairArgs& a, hipStream_t s) {
+  constexpr int ROW = RbGeo<C>::ROW;
+  const int h2 = (a.k - 1) / 2, h1 = h2 * a.d;
+  const int TT = NBT * 32 - 2 * h2;
+  const size_t smem = (size_t)(NBT * 32 + 2 * h1) * ROW + (size_t)(NBT * 32 + 2 * h2) * ROW;
+  auto kern = k_rb_pair<C, NBT, TN>;
+  static size_t smem_set = 64 * 1024;
+  if (smem > smem_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)smem);
+    if (e != hipSuccess) return e;
+    smem_set = smem;
+  }
+  const int ntiles = (a.T + TT - 1) / TT;
+  // persistent grid: as many workgroups as fit on the chip at once (LDS-limited), at most one per tile
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || ncu <= 0)
+      ncu = 256;
+  }
+  const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / smem)));
+  const long long tiles = (long long)ntiles * a.B;
+  const int grid = (int)std::min<long long>(tiles, (long long)ncu * per_cu);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(RB_THREADS), smem, s, a, ntiles);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool rb_pair_fits(int C, int k, int d) {
+  if (!(C == 32 || C == 64)) return false;
+  if (k < 1 || (k & 1) == 0 || d < 1) return false;
+  const int h2 = (k - 1) / 2;
+  return h2 * d <= RB_MAXH1 && 2 * h2 < 32;
+}
+
+long long rb_wsplit_bytes(int C, int k) { return (long long)k * (C / 16) * 3 * C * 32; }
+
+hipError_t rb_wsplit_build(const float* w, int C, int k, void* out, hipStream_t s) {
+  if (C % 16 != 0 || k < 1) return hipErrorInvalidValue;
+  const long long total = (long long)k * (C / 16) * C * 16;
+  const long long nb = std::min<long long>((total + 255) / 256, 1 << 20);
+  hipLaunchKernelGGL(k_rb_wsplit, dim3((unsigned)nb), dim3(256), 0, s, w, C, k, static_cast<unsigned short*>(out));
+  return hipGetLastError();
+}
+
+// cfg 0 = default per C; otherwise (C, NBT, TN) = 32: 1 (4,1) 2 (8,2); 64: 1 (2,1) 2 (4,2)
+hipError_t rb_pair(const RbPairArgs& a, int cfg, hipStream_t s) {
+  if (!rb_pair_fits(a.C, a.k, a.d) || a.T < 1 || a.B < 1 || !a.x || !a.y || !a.w1s || !a.w2s || !a.b1 || !a.b2 ||
+      a.x == a.y)
+    return hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(a.x) & 15) || (reinterpret_cast<uintptr_t>(a.y) & 15) || (a.x_bs & 3) ||
+      (a.y_bs & 3))
+    return hipErrorInvalidValue;
+  switch (a.C) {
+    case 32: return cfg == 2 ? launch_rb<32, 8, 2>(a, s) : launch_rb<32, 4, 1>(a, s);
+    case 64: return cfg == 2 ? launch_rb<64, 4, 2>(a, s) : launch_rb<64, 2, 1>(a, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace rvcx

@@ -119,6 +119,9 @@ struct Ctx {
   // pre-split weight images of the weight-streamed conv kernel, per (weight, layout); cleared by rvcx_finalize
   std::map<std::tuple<const void*, int, long long, int, int, int>, std::unique_ptr<DevBuf>> wsplit_cache;
   const void* wsplit_for(const ConvArgs& a, hipStream_t s);
+  // pre-split images of the fused ResBlock pair kernel (resblock_fused.hip), per weight tensor
+  std::map<const void*, std::unique_ptr<DevBuf>> rb_wsplit_cache;
+  const void* rb_wsplit_for(const float* w, int C, int k, hipStream_t s);
   // second stream for work independent of the caller's stream (HuBERT beside RMVPE), created lazily
   hipStream_t aux = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_gate = nullptr;
@@ -249,6 +252,17 @@ hipStream_t fork_aux(Ctx& c, hipStream_t s);
 void join_aux(Ctx& c, hipStream_t s, hipStream_t ax);
 // launch one implicit-GEMM conv (1-D or 2-D) with optional event timing; flops = algorithmic FLOPs
 void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double flops = -1.0);
+// one fused ResBlock pair (resblock_fused.hip) with optional event timing (counted with the conv family)
+void launch_rb_pair(Ctx& c, const RbPairArgs& a, hipStream_t s);
+// the fused pair is used for every ResBlock pair rb_pair_fits accepts; RVCX_NO_RBFUSE=1 restores two conv launches
+// (A/B measurement aid), RVCX_RB_CFG picks a tile configuration
+inline bool rb_fuse_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("RVCX_NO_RBFUSE");
+    return !(e && std::atoi(e) != 0);
+  }();
+  return v;
+}
 
 // fused attention (flash_attn.hip) for the TextEncoder and HuBERT; RVCX_NO_FLASH=1 restores the materialised
 // score path (A/B measurement aid)

@@ -396,6 +396,39 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
       const auto& dil = cf.rb_d[j];
       const std::string rb = "dec.resblocks." + std::to_string(i * nk + j);
       const float* r_in = y;
+      bool fuse = rb_fuse_enabled();
+      for (int d : dil) fuse = fuse && rb_pair_fits(C, k, d);
+      if (fuse) {
+        // each dilation pair as one fused kernel (resblock_fused.hip); pairs ping-pong between RR and T1 (a pair
+        // reads its neighbours' halo rows, so it never writes its own input), the last one accumulates into S
+        for (size_t m = 0; m < dil.size(); ++m) {
+          const std::string n1 = rb + ".convs1." + std::to_string(m);
+          const std::string n2 = rb + ".convs2." + std::to_string(m);
+          const bool last = (m + 1 == dil.size());
+          float* dst = last ? S : (m % 2 == 0 ? RR : T1);
+          RbPairArgs p;
+          p.x = r_in;
+          p.x_bs = (long long)Ti * C;
+          p.w1s = c.rb_wsplit_for(c.W(n1 + ".w"), C, k, s);
+          p.b1 = c.W(n1 + ".b");
+          p.w2s = c.rb_wsplit_for(c.W(n2 + ".w"), C, k, s);
+          p.b2 = c.W(n2 + ".b");
+          p.C = C;
+          p.k = k;
+          p.d = dil[m];
+          p.T = Ti;
+          p.B = B;
+          p.y = dst;
+          p.y_bs = (long long)Ti * C;
+          if (last) {
+            p.acc_mode = (j == 0) ? ACC_STORE : ((j + 1 == nk) ? ACC_ADD_DIV : ACC_ADD);
+            p.acc_div = (float)nk;
+          }
+          launch_rb_pair(c, p, s);
+          r_in = dst;
+        }
+        continue;
+      }
       for (size_t m = 0; m < dil.size(); ++m) {
         const int d = dil[m];
         const std::string n1 = rb + ".convs1." + std::to_string(m);

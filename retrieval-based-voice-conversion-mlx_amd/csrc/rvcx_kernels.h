@@ -138,6 +138,26 @@ int conv_wsplit_npad(int N);
 long long conv_wsplit_bytes(const ConvArgs& a);
 hipError_t conv_wsplit_build(const ConvArgs& a, void* out, hipStream_t s);
 hipError_t conv_wsb_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream_t s);
+// fused ResBlock dilation pair (resblock_fused.hip): y (acc_mode) <- conv2(lrelu(conv1_d(lrelu(x)) + b1)) + b2 + x,
+// x / y [B][T][C] (x != y), C in {32, 64}, odd k, (k - 1) / 2 * d <= 30; w1s / w2s are rb_wsplit_build images
+// of [k][C][C] fp32 weights
+struct RbPairArgs {
+  const float* x = nullptr;
+  long long x_bs = 0;
+  const void* w1s = nullptr;
+  const float* b1 = nullptr;
+  const void* w2s = nullptr;
+  const float* b2 = nullptr;
+  int C = 0, k = 0, d = 1, T = 0, B = 1;
+  float* y = nullptr;
+  long long y_bs = 0;
+  int acc_mode = ACC_STORE;
+  float acc_div = 1.f;
+};
+bool rb_pair_fits(int C, int k, int d);
+long long rb_wsplit_bytes(int C, int k);
+hipError_t rb_wsplit_build(const float* w, int C, int k, void* out, hipStream_t s);
+hipError_t rb_pair(const RbPairArgs& a, int cfg, hipStream_t s);
 // fused attention (flash_attn.hip): qkv [B][T][ldq] (q | k | v, heads of dk inside each), optional relative
 // window (rel_k / rel_v [2w+1][dk]) and key/query mask [B][T]; partials part_o [nsplit][B*nh][T][dk], part_ml
 // [nsplit][B*nh][T][2]; out [B][T][ldo] at column h*dk

@@ -477,6 +477,25 @@ class Engine:
                                          m, _ptr(y), T_out, self.stream()), "conv1d")
         return y
 
+    def resblock_pair(self, x, w1, b1, w2, b2, dilation: int, acc=None, acc_mode: int = 0, acc_div: float = 1.0,
+                      cfg: int = 0):
+        """One ResBlock dilation pair on the fused kernel (rvcx_resblock_pair): x [B][T][C] time-major, w1/w2
+        [C][C][k] (torch layout) -> conv2(lrelu(conv1_d(lrelu(x)) + b1)) + b2 + x, stored (acc_mode 0) or
+        accumulated into `acc` (1: acc + out, 2: (acc + out) / acc_div)."""
+        torch = self.torch
+        x = self._dev(x, torch.float32)
+        B, T, C = (int(v) for v in x.shape)
+        k = int(np.shape(w1)[2])
+        w1k = self._dev(torch.as_tensor(w1, dtype=torch.float32).permute(2, 0, 1).contiguous(), torch.float32)
+        w2k = self._dev(torch.as_tensor(w2, dtype=torch.float32).permute(2, 0, 1).contiguous(), torch.float32)
+        b1d, b2d = self._dev(b1, torch.float32), self._dev(b2, torch.float32)
+        y = (self._dev(acc, torch.float32).clone() if acc is not None
+             else torch.empty((B, T, C), dtype=torch.float32, device=self.device))
+        self._check(self.lib.rvcx_resblock_pair(self.ctx, _ptr(x), B, T, C, _ptr(w1k), _ptr(b1d), _ptr(w2k), _ptr(b2d),
+                                                k, dilation, acc_mode, float(acc_div), cfg, _ptr(y), self.stream()),
+                    "resblock_pair")
+        return y
+
     def profile(self, enable: bool):
         self._check(self.lib.rvcx_profile(self.ctx, 1 if enable else 0), "profile")
 

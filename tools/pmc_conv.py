@@ -5,11 +5,12 @@ import glob
 import sys
 
 tag = sys.argv[1] if len(sys.argv) > 1 else "pmc_c3_g1"
+kern = sys.argv[2:] or ["conv_gemm", "conv_emu"]
 agg = collections.defaultdict(float)
 cnt = collections.Counter()
 for f in sorted(glob.glob(f"gpurun_out/{tag}_p*/**/*counter_collection.csv", recursive=True)):
     for r in csv.DictReader(open(f)):
-        if "conv_gemm" not in r["Kernel_Name"] and "conv_emu" not in r["Kernel_Name"]:
+        if not any(k in r["Kernel_Name"] for k in kern):
             continue
         agg[r["Counter_Name"]] += float(r["Counter_Value"])
         cnt[r["Counter_Name"]] += 1
