@@ -311,19 +311,31 @@ hipError_t softmax_rows(float* scores, int rows, int cols, hipStream_t s) {
 
 // ------------------------------------------------------------------ NSF noise conv, accumulated into y
 // One thread per 4 consecutive channels of one output row: the row's kk = taps * stride source samples are
-// read once for the 4 channels, y is read and written as one float4 (coalesced along the row). The per-channel
-// sum runs over q in order as an fma chain, then + bias, then + y (the separate-launch order it replaces).
-__global__ void k_noise_add(const float* __restrict__ har, long long har_bs, int stride, int taps,
-                            const float* __restrict__ wf, const float* __restrict__ nb, float* __restrict__ y, int B,
-                            int T, int C) {
-  const int c4n = C >> 2;
-  const long long n = (long long)B * T * c4n;
+// read once for the 4 channels, y is read and written as one float4 (coalesced along the row). The weights are
+// staged once per block into LDS as [q][C] so each (q, 4 channels) is one 16-byte read. The per-channel sum runs
+// over q in order as an fma chain, then + bias, then + y (the separate-launch order it replaces).
+constexpr int NOISE_LDS_FLOATS = 4096;
+__global__ __launch_bounds__(256) void k_noise_add(const float* __restrict__ har, long long har_bs, int stride,
+                                                   int taps, const float* __restrict__ wf,
+                                                   const float* __restrict__ nb, float* __restrict__ y, int B, int T,
+                                                   int C) {
+  __shared__ __attribute__((aligned(16))) float wq[NOISE_LDS_FLOATS];
   const int kk = taps * stride;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % c4n) << 2;
-    const long long bt = i / c4n;
-    const int b = (int)(bt / T);
-    const long long t = bt - (long long)b * T;
+  for (int i = threadIdx.x; i < kk * C; i += blockDim.x) {
+    const int q = i / C, c = i - q * C;
+    const int tap = q / stride, j = q - tap * stride;
+    wq[i] = wf[((long long)tap * C + c) * stride + j];
+  }
+  __syncthreads();
+  // 32-bit index arithmetic (the launcher checks B * T * C / 4 < 2^31): 64-bit divisions cost more than the
+  // whole per-element body
+  const unsigned c4n = (unsigned)C >> 2;
+  const unsigned n = (unsigned)B * (unsigned)T * c4n;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const unsigned bt = i / c4n;
+    const int c = (int)(i - bt * c4n) << 2;
+    const unsigned b = bt / (unsigned)T;
+    const long long t = bt - b * (unsigned)T;
     const float* x = har + b * har_bs + t * stride;
     float xs[16];
 #pragma unroll
@@ -332,15 +344,14 @@ __global__ void k_noise_add(const float* __restrict__ har, long long har_bs, int
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       if (q < kk) {
-        const int tap = q / stride, j = q - tap * stride;
-        const float* w = wf + ((long long)tap * C + c) * stride + j;
-        acc.x = fmaf(w[0], xs[q], acc.x);
-        acc.y = fmaf(w[stride], xs[q], acc.y);
-        acc.z = fmaf(w[2 * stride], xs[q], acc.z);
-        acc.w = fmaf(w[3 * stride], xs[q], acc.w);
+        const float4 w = *reinterpret_cast<const float4*>(wq + q * C + c);
+        acc.x = fmaf(w.x, xs[q], acc.x);
+        acc.y = fmaf(w.y, xs[q], acc.y);
+        acc.z = fmaf(w.z, xs[q], acc.z);
+        acc.w = fmaf(w.w, xs[q], acc.w);
       }
     }
-    float4* yp = reinterpret_cast<float4*>(y + bt * C + c);
+    float4* yp = reinterpret_cast<float4*>(y + (long long)bt * C + c);
     float4 v = *yp;
     v.x = v.x + (acc.x + nb[c]);
     v.y = v.y + (acc.y + nb[c + 1]);
@@ -351,9 +362,12 @@ __global__ void k_noise_add(const float* __restrict__ har, long long har_bs, int
 }
 hipError_t noise_conv_add(const float* har, long long har_bs, int stride, int taps, const float* wf, const float* nb,
                           float* y, int B, int T, int C, hipStream_t s) {
-  if (C % 4 != 0 || taps * stride > 16 || taps * stride < 1 || (reinterpret_cast<uintptr_t>(y) & 15) != 0)
+  if (C % 4 != 0 || taps * stride > 16 || taps * stride < 1 || (reinterpret_cast<uintptr_t>(y) & 15) != 0 ||
+      (long long)B * T * (C / 4) >= (1LL << 31) || taps * stride * C > NOISE_LDS_FLOATS)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_noise_add, dim3(nblocks((long long)B * T * (C / 4))), dim3(TB), 0, s, har, har_bs, stride,
+  // grid-stride over a capped grid: each block stages the weights once
+  hipLaunchKernelGGL(k_noise_add, dim3(std::min(nblocks((long long)B * T * (C / 4)), 4096u)), dim3(TB), 0, s, har,
+                     har_bs, stride,
                      taps, wf, nb, y, B, T, C);
   return hipGetLastError();
 }

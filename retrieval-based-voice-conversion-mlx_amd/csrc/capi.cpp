@@ -141,11 +141,17 @@ const void* Ctx::rb_wsplit_for(const float* w, int C, int k, hipStream_t s) {
   return slot->p;
 }
 
-void launch_rb_pair(Ctx& c, const RbPairArgs& a, hipStream_t s) {
+void launch_rb_pair(Ctx& c, const RbPairArgs& a_in, hipStream_t s) {
   static const int cfg = [] {
     const char* e = std::getenv("RVCX_RB_CFG");
     return e ? std::atoi(e) : 0;
   }();
+  static const int flags = [] {
+    const char* e = std::getenv("RVCX_RB_FLAGS");
+    return e ? std::atoi(e) : 0;
+  }();
+  RbPairArgs a = a_in;
+  a.flags = flags;
   if (!c.prof) {
     check(rb_pair(a, cfg, s), "rb_pair");
     return;

@@ -220,10 +220,12 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
   int tile = blockIdx.x;
   if (tile >= total) return;
   // the first job's weights and the first tile's x are in flight together
+  const bool pre = (a.flags & 1) == 0;
   prefetch_ring(wl_of(0));
-  load_x(tile);
+  if (pre) load_x(tile);
 #pragma unroll 1
   for (; tile < total; tile += gridDim.x) {
+  if (!pre) load_x(tile);
   const int b = tile / ntiles;
   const int t0 = (tile - b * ntiles) * TT;
   const float* X = a.x + (long long)b * a.x_bs;
@@ -231,7 +233,7 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
   // conv1 (writing TS) after every wave's conv2 of the previous tile (reading TS)
   write_x();
   __syncthreads();
-  if (tile + (int)gridDim.x < total) load_x(tile + gridDim.x);
+  if (pre && tile + (int)gridDim.x < total) load_x(tile + gridDim.x);
   float* Y = a.y + (long long)b * a.y_bs;
 #pragma unroll 1
   for (int job = 0; job < 2 * UPW; ++job) {

@@ -374,7 +374,7 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
       if (npad > HAR_PAD || ntap * stride - npad > HAR_PAD + stride)
         throw Error(RVCX_E_SHAPE, "noise conv stride too large for the source padding");
       const std::string nn = "dec.noise_convs." + std::to_string(i);
-      if (ntap * stride <= 16 && C % 4 == 0) {
+      if (ntap * stride <= 16 && C % 4 == 0 && (long long)B * Ti * (C / 4) < (1LL << 31) && ntap * stride * C <= 4096) {
         check(noise_conv_add(har + HAR_PAD - npad, har_ld, stride, ntap, c.W(nn + ".wf"), c.W(nn + ".b"), y, B, Ti,
                              C, s),
               "noise_conv_add");
