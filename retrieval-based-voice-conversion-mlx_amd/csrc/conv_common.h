@@ -92,63 +92,72 @@ __device__ __forceinline__ void conv_store_tile(const ConvArgs& a, const TilePos
       }
     }
   };
+  if (!TWO_D && p.ksplit == 1 && a.out_map == OUT_ROWS) {
+    // 1-D rows: every accumulator of the wave straight from registers, one 32x32 tile after another, gather
+    // first: the residual, accumulate and mask operands of the lane's 16 outputs of a tile are all loaded before
+    // the first store. The stores may alias them (an in-place residual reads the very element it writes), so
+    // the compiler cannot hoist the loads across the stores itself and would expose one load latency per output
+    // (16 per lane): the short-contraction convs (ResBlock k=3 at 32/64 channels) were latency-bound on exactly
+    // that. Each element is read and written by this lane only, so the reorder is exact.
+    const bool need_r = R && a.res_mode != RES_NONE;
+    const bool need_d = a.acc_mode != ACC_STORE;
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int n = p.n0 + wn * TN * 32 + tn * 32 + li;
+        const bool n_ok = n < a.N;
+        const float bn = (bias && n_ok) ? bias[n] : 0.f;
+        // element r sits at row mb + (r&3) + 8(r>>2) of column n: per-lane base pointers, constant row offsets
+        const int mb = p.m0 + wm * TM * 32 + tm * 32 + 4 * hk;
+        const bool full = p.m0 + wm * TM * 32 + tm * 32 + 32 <= a.T_out;
+        const float* Rl = need_r ? R + (long long)mb * a.ldr + n : nullptr;
+        float* Yl = Y + (long long)mb * a.ldy + n;
+        const float* Ml = MK ? MK + mb : nullptr;
+        auto row_ok = [&](int r) { return n_ok && (full || mb + (r & 3) + 8 * (r >> 2) < a.T_out); };
+        // two halves of 8 elements: one exposed load latency each, 24 staging registers instead of 48 (the
+        // VGPR count sets the workgroups per CU of this latency-bound kernel)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          float rv[8], dv[8], mv[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int r = 8 * h + i;
+            const int ro = (r & 3) + 8 * (r >> 2);
+            const bool ok = row_ok(r);
+            rv[i] = (ok && need_r) ? Rl[ro * a.ldr] : 0.f;
+            dv[i] = (ok && need_d) ? Yl[ro * a.ldy] : 0.f;
+            mv[i] = (ok && MK) ? Ml[ro] : 1.f;
+          }
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int r = 8 * h + i;
+            if (!row_ok(r)) continue;
+            const int ro = (r & 3) + 8 * (r >> 2);
+            float v = acc[tm][tn][r];
+            if (a.bias) v += bn;
+            if (a.res_mode == RES_ADD_PRE) v = v + rv[i];
+            if (a.alpha != 1.f) v *= a.alpha;
+            v = act_fn(v, a.act, a.slope);
+            if (a.res_mode == RES_ADD_POST) v = v + rv[i];
+            else if (a.res_mode == RES_RSUB_POST) v = rv[i] - v;
+            if (a.acc_mode == ACC_ADD) v = dv[i] + v;
+            else if (a.acc_mode == ACC_ADD_DIV) v = (dv[i] + v) / a.acc_div;
+            if (MK) v *= mv[i];
+            Yl[ro * a.ldy] = v;
+          }
+        }
+      }
+    }
+    return;
+  }
   if constexpr (TM * TN == 1) {
     // one accumulator per wave: straight from registers (fully unrolled, 16 values per lane)
     const int n = p.n0 + wn * 32 + li;
     const bool n_ok = n < a.N;
     const float bn = (bias && n_ok) ? bias[n] : 0.f;
-    if (!TWO_D && p.ksplit == 1 && a.out_map == OUT_ROWS) {
-      // 1-D gather first: the residual, accumulate and mask operands of the lane's 16 outputs are all loaded
-      // before the first store. The stores may alias them (an in-place residual reads the very element it
-      // writes), so the compiler cannot hoist the loads across the stores itself and would expose one load
-      // latency per output (16 per lane): the short-contraction convs (ResBlock k=3 at 32/64 channels) were
-      // latency-bound on exactly that. Each element is read and written by this lane only, so the reorder is
-      // exact.
-      const bool need_r = R && a.res_mode != RES_NONE;
-      const bool need_d = a.acc_mode != ACC_STORE;
-      // element r sits at row mb + (r&3) + 8(r>>2) of column n: per-lane base pointers, constant row offsets
-      const int mb = p.m0 + wm * 32 + 4 * hk;
-      const bool full = p.m0 + wm * 32 + 32 <= a.T_out;
-      const float* Rl = need_r ? R + (long long)mb * a.ldr + n : nullptr;
-      float* Yl = Y + (long long)mb * a.ldy + n;
-      const float* Ml = MK ? MK + mb : nullptr;
-      auto row_ok = [&](int r) { return n_ok && (full || mb + (r & 3) + 8 * (r >> 2) < a.T_out); };
-      // two halves of 8 elements: one exposed load latency each, 24 staging registers instead of 48 (the
-      // VGPR count sets the workgroups per CU of this latency-bound kernel)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        float rv[8], dv[8], mv[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int r = 8 * h + i;
-          const int ro = (r & 3) + 8 * (r >> 2);
-          const bool ok = row_ok(r);
-          rv[i] = (ok && need_r) ? Rl[ro * a.ldr] : 0.f;
-          dv[i] = (ok && need_d) ? Yl[ro * a.ldy] : 0.f;
-          mv[i] = (ok && MK) ? Ml[ro] : 1.f;
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int r = 8 * h + i;
-          if (!row_ok(r)) continue;
-          const int ro = (r & 3) + 8 * (r >> 2);
-          float v = acc[0][0][r];
-          if (a.bias) v += bn;
-          if (a.res_mode == RES_ADD_PRE) v = v + rv[i];
-          if (a.alpha != 1.f) v *= a.alpha;
-          v = act_fn(v, a.act, a.slope);
-          if (a.res_mode == RES_ADD_POST) v = v + rv[i];
-          else if (a.res_mode == RES_RSUB_POST) v = rv[i] - v;
-          if (a.acc_mode == ACC_ADD) v = dv[i] + v;
-          else if (a.acc_mode == ACC_ADD_DIV) v = (dv[i] + v) / a.acc_div;
-          if (MK) v *= mv[i];
-          Yl[ro * a.ldy] = v;
-        }
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) emit(acc[0][0][r], wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hk, n, n_ok, bn);
-    }
+    for (int r = 0; r < 16; ++r) emit(acc[0][0][r], wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * hk, n, n_ok, bn);
   } else {
     // several accumulators per wave: stage one 32x32 tile at a time through the wave's own LDS slot
     // (32 x 33 floats) and emit rows 2i + hk, column li; accumulator registers are only indexed with

@@ -684,14 +684,14 @@ inline bool small2d_enabled() {
   return v;
 }
 
-// weight-streamed split kernel (conv_wsb.hip) tiles: 256x32 for N <= 32, 128x64 for N <= 64, else 128x128
-// (RVCX_WCFG_* override). bench_conv on MI355X (TF/s, vs the LDS-staged split kernel's best tile): C128 k11
-// 189 vs 155, C128 k7 166 vs 138; C64 k11 141 vs 139; the short-tap and 32-channel convs lose (C32 k11 94 vs
-// 112, C64 k3 + residual 33 vs 70), so conv_wsb_wants admits N >= 128 with >= 5 taps only.
+// weight-streamed split kernel (conv_wsb.hip) tiles: 256x32 for N <= 32, else 128x64 (2 x 2 waves of 64 x 32;
+// RVCX_WCFG_* override). bench_conv on MI355X with the register epilogue (TF/s, vs the LDS-staged split kernel's
+// best tile): C256 k11 174 vs 142, C128 k11 204 vs 160, C128 k7 185 vs 144, C128 k3 124 vs 118, ConvTranspose
+// phases 105 / 124 / 94 vs 95 / 117 / 96; the 32-channel convs lose (C32 k11 95 vs 115).
 inline int pick_wsb(const ConvArgs& a) {
   static const int c_narrow = env_cfg("RVCX_WCFG_NARROW", 20);
   static const int c_mid = env_cfg("RVCX_WCFG_MID", 21);
-  static const int c_wide = env_cfg("RVCX_WCFG_WIDE", 22);
+  static const int c_wide = env_cfg("RVCX_WCFG_WIDE", 21);
   return a.N <= 32 ? c_narrow : (a.N <= 64 ? c_mid : c_wide);
 }
 
@@ -794,10 +794,14 @@ bool conv_wsb_wants(const ConvArgs& a) {
     return e && std::atoi(e) != 0;
   }();
   if (off || conv_math(a) != 2 || !conv_wsb_eligible(a)) return false;
-  if (a.N < 128 || a.taps < 5) return false;  // where it measured faster (pick_wsb)
-  // the grid must fill the chip several times over (the generator's long convs): 128 x 64 tiles
+  // where it measured faster (bench_conv, profiles/r02i_bench_conv.txt: 128 x 64 tiles of 2 x 2 waves of 64 x 32
+  // with the register epilogue): N >= 128 with >= 2 taps (ResBlock convs at 128/256 channels incl. k = 3, the
+  // polyphase ConvTranspose phases), on a grid that fills the chip (RVCX_WSB_MINTAPS / RVCX_WSB_MINTILES: A/B aid)
+  static const int min_taps = env_cfg("RVCX_WSB_MINTAPS", 2);
+  static const int min_tiles = env_cfg("RVCX_WSB_MINTILES", 512);
+  if (a.N < 128 || a.taps < min_taps) return false;
   const long long tiles = (long long)((a.T_out + 127) / 128) * ((a.N + 63) / 64) * a.batch;
-  return tiles >= 1024;
+  return tiles >= min_tiles;
 }
 
 hipError_t conv1d(const ConvArgs& a, hipStream_t s) { return dispatch<false>(a, s); }
