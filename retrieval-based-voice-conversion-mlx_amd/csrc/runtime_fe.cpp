@@ -661,14 +661,16 @@ static void e2e_chunk(Ctx& c, float* img, int Fc, float* sal, hipStream_t s, int
   float* go = c.buf<float>("rm.gruout", (size_t)B * Fc * 2 * GRU_H, s);
   unsigned long long* xchg = c.buf<unsigned long long>("rm.xchg", gru_xchg_words(B), s);
   unsigned* status = c.device_status();  // sticky until the host reads it (Ctx::check_device_status)
-  if (c.before_gru) {  // work the caller wants issued beside the BiGRU (which occupies 4 CUs)
-    auto hook = std::move(c.before_gru);
-    c.before_gru = nullptr;
-    hook(s);
-  }
+  // work the caller wants issued beside the BiGRU (which occupies 4 CUs): the gate event marks this point of the
+  // stream, the BiGRU goes out first and the hook's (many) launches after it, so the host time spent issuing
+  // them overlaps the BiGRU instead of delaying its launch
+  std::function<void(hipStream_t)> hook = std::move(c.before_gru);
+  c.before_gru = nullptr;
+  if (hook && c.ev_gate) RVCX_HIP(hipEventRecord(c.ev_gate, s));
   check(gru_bidir(gi, c.W("rm.gru.whh_f"), c.W("rm.gru.bhh_f"), c.W("rm.gru.whh_b"), c.W("rm.gru.bhh_b"), Fc, go,
                   xchg, status, s, B),
         "gru");
+  if (hook) hook(s);
   ConvArgs f = lin(go, 2 * GRU_H, B * Fc, 2 * GRU_H, c.W("rm.fc.w"), NCLS, c.W("rm.fc.b"), sal, NCLS);
   f.act = ACT_SIGMOID;
   run1(c, f, s);

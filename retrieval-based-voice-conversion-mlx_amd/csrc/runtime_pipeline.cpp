@@ -231,7 +231,7 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
   hipStream_t ax = fork_aux(c, s);
   static const int gate_layer = [] {
     const char* e = std::getenv("RVCX_HUBERT_GATE");  // first layer issued beside the BiGRU (12: none)
-    const int v = e ? std::atoi(e) : 6;
+    const int v = e ? std::atoi(e) : 4;  // A/B on MI355X: 4 23.65 ms, 6 23.93, 2 23.83, 0 24.2
     return v < 0 ? 0 : (v > HUBERT_LAYERS ? HUBERT_LAYERS : v);
   }();
   // without pitch guidance there is no RMVPE (pipeline.py:461-472 skipped): HuBERT runs in one piece
@@ -250,12 +250,13 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
       cL[i] = hubert_tail(c, hruns[i], ax);
     }
   }
+  // the caller records c.ev_gate on `main` where the rest may start (gate_here), then calls this
+  auto gate_here = [&](hipStream_t main) {
+    if (ax != main && c.ev_gate) RVCX_HIP(hipEventRecord(c.ev_gate, main));
+  };
   auto hubert_rest = [&](hipStream_t main) {
     if (chunks.size() != 1) return;
-    if (split < HUBERT_LAYERS && ax != main) {
-      RVCX_HIP(hipEventRecord(c.ev_gate, main));
-      RVCX_HIP(hipStreamWaitEvent(ax, c.ev_gate, 0));
-    }
+    if (split < HUBERT_LAYERS && ax != main) RVCX_HIP(hipStreamWaitEvent(ax, c.ev_gate, 0));
     hubert_layers(c, hruns[0], split, HUBERT_LAYERS, ax);
     cL[0] = hubert_tail(c, hruns[0], ax);
   };
@@ -277,6 +278,7 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
     if (c.before_gru) {
       auto rest = std::move(c.before_gru);
       c.before_gru = nullptr;
+      gate_here(s);
       rest(s);
     }
     float* f0f = c.buf<float>("pl.f0f", (size_t)F, s);
@@ -287,6 +289,7 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
   if (c.before_gru) {  // RMVPE did not reach a BiGRU launch (cannot happen for valid input): issue it now
     auto rest = std::move(c.before_gru);
     c.before_gru = nullptr;
+    gate_here(s);
     rest(s);
   }
   double shift_semitones = o.pitch;
@@ -306,6 +309,7 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
   } else {
     auto rest = std::move(c.before_gru);
     c.before_gru = nullptr;
+    gate_here(s);
     rest(s);
     if (f0_out) RVCX_HIP(hipMemsetAsync(f0_out, 0, sizeof(double) * (size_t)F, s));
   }
