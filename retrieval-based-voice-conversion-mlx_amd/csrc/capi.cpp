@@ -167,7 +167,9 @@ void launch_rb_pair(Ctx& c, const RbPairArgs& a_in, hipStream_t s) {
   }
   // algorithmic work: the two convs over the valid rows
   const double flops = 2.0 * 2.0 * a.B * (double)a.T * a.C * a.C * a.k;
-  Ctx::ProfRec r{ev[0], ev[1], flops, 0, a.T, a.C, a.C, -a.k, a.B, 1};
+  // x read, y written (+ read when accumulating), both weight tensors
+  const double bytes = 4.0 * ((double)a.B * a.T * a.C * (2 + (a.acc_mode != ACC_STORE ? 1 : 0)) + 2.0 * a.k * a.C * a.C);
+  Ctx::ProfRec r{ev[0], ev[1], flops, 0, a.T, a.C, a.C, -a.k, a.B, 1, bytes};
   RVCX_HIP(hipEventRecord(r.a, s));
   check(rb_pair(a, cfg, s), "rb_pair");
   RVCX_HIP(hipEventRecord(r.b, s));
@@ -202,8 +204,14 @@ void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double
     }
     return e;
   };
+  // input rows read once, weights once, output written once (+ read again for a residual / accumulate)
+  const double in_rows = two_d ? (double)a.T_in * a.W_in : (double)a.T_in;
+  const double out_el = (two_d ? (double)a.T_out * a.W_out : (double)a.T_out) * a.N * a.batch * a.batch_inner;
+  const double alg_bytes = 4.0 * (in_rows * a.C_in * a.batch * a.batch_inner + (double)a.taps * a.N * a.C_in +
+                                  out_el * (1 + (a.res && a.res_mode != RES_NONE ? 1 : 0) +
+                                            (a.acc_mode != ACC_STORE ? 1 : 0)));
   Ctx::ProfRec r{get_ev(), get_ev(), flops, two_d ? 1 : 0, two_d ? a.T_out * a.W_out : a.T_out, a.N, a.C_in,
-                 a.taps, a.batch * a.batch_inner, a.ksplit};
+                 a.taps, a.batch * a.batch_inner, a.ksplit, alg_bytes};
   RVCX_HIP(hipEventRecord(r.a, s));
   check(two_d ? conv2d(a, s) : conv1d(a, s), two_d ? "conv2d" : "conv1d");
   RVCX_HIP(hipEventRecord(r.b, s));
@@ -641,8 +649,8 @@ int rvcx_profile_read(rvcx_ctx* ctx, double* total_ms, double* total_flops, int6
       float t = 0.f;
       RVCX_HIP(hipEventElapsedTime(&t, r.a, r.b));
       if (fd)
-        std::fprintf(fd, "%d,%d,%d,%d,%d,%d,%d,%.6f,%.0f\n", r.two_d, r.M, r.N, r.C_in, r.taps, r.batch, r.ksplit, t,
-                     r.flops);
+        std::fprintf(fd, "%d,%d,%d,%d,%d,%d,%d,%.6f,%.0f,%.0f\n", r.two_d, r.M, r.N, r.C_in, r.taps, r.batch, r.ksplit, t,
+                     r.flops, r.bytes);
       ms += t;
       fl += r.flops;
       ctx->prof_pool.push_back(r.a);

@@ -423,29 +423,37 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
   conv_store_tile<TM, TN, WM, WN, TWO_D>(a, TilePos{m0, h0, w0, rw, rh, n0, b, bi, zb, zsplit, ksplit}, acc, smem);
 }
 
-// split-K combine: sums the ksplit partial tiles in slice order (deterministic) and applies the epilogue
+// split-K combine: sums the ksplit partial tiles in slice order (deterministic) and applies the epilogue. Grid
+// (x: elements of one batch entry, y: batch entry); 32-bit element index within an entry (launch checks), all
+// ksplit slab loads of an element issued before the ordered sum
 __global__ void splitk_reduce_kernel(const ConvArgs a, const int ksplit, const int two_d) {
-  const long long rows = a.ws_rows;
-  const long long per_b = rows * a.N;
-  const long long total = per_b * a.batch * a.batch_inner;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const long long zb = i / per_b;
-    const long long rem = i - zb * per_b;
-    const long long m = rem / a.N;
-    const int n = (int)(rem - m * a.N);
-    const int b = (int)(zb / a.batch_inner), bi = (int)(zb % a.batch_inner);
-    const float* p = a.ws + (zb * ksplit) * per_b + m * a.N + n;
+  const unsigned per_b = (unsigned)(a.ws_rows * a.N);
+  const int zb = blockIdx.y;
+  const int b = zb / a.batch_inner, bi = zb - (zb / a.batch_inner) * a.batch_inner;
+  const float* bias = a.bias ? a.bias + (long long)b * a.bias_bs + (long long)bi * a.bias_bs2 : nullptr;
+  const float* R = a.res ? a.res + (long long)b * a.res_bs + (long long)bi * a.res_bs2 : nullptr;
+  const float* MK = a.mask ? a.mask + (long long)b * a.mask_bs : nullptr;
+  float* Y = a.y + (long long)b * a.y_bs + (long long)bi * a.y_bs2;
+  const float* base = a.ws + (long long)zb * ksplit * per_b;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < per_b; i += gridDim.x * blockDim.x) {
+    const unsigned m = i / (unsigned)a.N;
+    const int n = (int)(i - m * (unsigned)a.N);
+    const float* p = base + i;
     float v = 0.f;
-    for (int s = 0; s < ksplit; ++s) v += p[(long long)s * per_b];
-    const float* bias = a.bias ? a.bias + (long long)b * a.bias_bs + (long long)bi * a.bias_bs2 : nullptr;
-    const float* R = a.res ? a.res + (long long)b * a.res_bs + (long long)bi * a.res_bs2 : nullptr;
-    const float* MK = a.mask ? a.mask + (long long)b * a.mask_bs : nullptr;
-    float* Y = a.y + (long long)b * a.y_bs + (long long)bi * a.y_bs2;
+    int s = 0;
+    for (; s + 4 <= ksplit; s += 4) {
+      const float p0 = p[(long long)s * per_b], p1 = p[(long long)(s + 1) * per_b];
+      const float p2 = p[(long long)(s + 2) * per_b], p3 = p[(long long)(s + 3) * per_b];
+      v += p0;
+      v += p1;
+      v += p2;
+      v += p3;
+    }
+    for (; s < ksplit; ++s) v += p[(long long)s * per_b];
     int oh = 0, ow = 0;
     if (two_d) {
-      oh = (int)(m / a.W_out);
-      ow = (int)(m % a.W_out);
+      oh = (int)(m / (unsigned)a.W_out);
+      ow = (int)(m - (unsigned)oh * (unsigned)a.W_out);
     }
     epilogue_store(a, v, bias ? bias[n] : 0.f, m, n, oh, ow, R, MK, Y);
   }
@@ -534,10 +542,13 @@ bool xcd_enabled() {
 }
 
 hipError_t launch_splitk_reduce(const ConvArgs& a, int ksplit, bool two_d, hipStream_t s) {
-  const long long total = (long long)a.ws_rows * a.N * a.batch * a.batch_inner;
-  long long nb = (total + 255) / 256;
+  const long long per_b = (long long)a.ws_rows * a.N;
+  const int nz = a.batch * a.batch_inner;
+  if (per_b >= (1LL << 31) || nz > 65535) return hipErrorInvalidValue;  // 32-bit element index, grid y
+  long long nb = (per_b + 255) / 256;
   if (nb > 8192) nb = 8192;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, ksplit, two_d ? 1 : 0);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)nb, (unsigned)nz), dim3(256), 0, s, a, ksplit,
+                     two_d ? 1 : 0);
   return hipGetLastError();
 }
 

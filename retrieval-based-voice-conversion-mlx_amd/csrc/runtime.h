@@ -112,6 +112,7 @@ struct Ctx {
     hipEvent_t a, b;
     double flops;
     int two_d, M, N, C_in, taps, batch, ksplit;  // shape, for RVCX_PROF_DUMP
+    double bytes;  // algorithmic HBM bytes: operands read once, result written once (RVCX_PROF_DUMP)
   };
   std::vector<ProfRec> prof_recs;
   std::vector<hipEvent_t> prof_pool;

@@ -5,7 +5,8 @@ half the bytes of 16-B-per-lane streaming reads (MI355X_MICROARCH.md, HBM sectio
 WRITE_SIZE is taken as is. The bench runs warm-up + 1 timed step + 1 event pass (inline: the timed step
 carries the events), so each kernel of the step appears `steps` times; per-launch numbers are averages.
 usage: python tools/pmc_traffic.py gpurun_out [kernel-substring,...] > profiles/pmc_traffic.json
-Default family: the conv dispatches bench.py's roofline counts (conv_emu / conv_gemm / conv_tiny / conv2d_small);
+Default family: the conv dispatches bench.py's roofline counts (conv_emu / conv_wsb / k_rb_pair / conv_gemm /
+conv_tiny / conv2d_small);
 the split-K reduce kernels' bytes are added to the family's total, launches count the conv kernels only.
 The record carries the source-tree hash (rvcx.provenance) so bench.py can tell whether it applies.
 """
@@ -33,7 +34,7 @@ def load(d, counter):
 def main():
     d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
     keys = (sys.argv[2] if len(sys.argv) > 2 else
-            "conv_emu_kernel,conv_gemm_kernel,conv_tiny_kernel,k_conv2d_small").split(",")
+            "conv_emu_kernel,conv_wsb_kernel,k_rb_pair,conv_gemm_kernel,conv_tiny_kernel,k_conv2d_small").split(",")
     key = ",".join(keys)
     fam = lambda k: any(s in k for s in keys)  # noqa: E731
     bytes_fam = lambda k: fam(k) or "splitk_reduce" in k  # noqa: E731
