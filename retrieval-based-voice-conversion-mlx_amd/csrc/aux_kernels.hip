@@ -478,26 +478,43 @@ hipError_t sine_source(const float* f0, int B, int L, int upp, float sr, const f
 // ------------------------------------------------------------------ conv_post: tanh(conv1d(lrelu(x, 0.01), w[1][C][K], pad K/2)), no bias
 // The C*K weights sit in LDS too: read from global inside the FMA loop (uniform address, possibly
 // aliasing y) they were one dependent vector load per FMA (80 us at C2).
-__global__ void k_conv_post(const float* __restrict__ x, int T, int C, const float* __restrict__ wg, int K,
-                            float slope, float* __restrict__ y, float bias) {
-  extern __shared__ float tile[];  // [(256+K-1)][C+1], then w[C*K]
+// LeakyReLU -> Conv1d(C -> 1, K taps) -> tanh over 256 output samples per block. The lrelu'd input tile (+ halo)
+// is staged in LDS with an odd row stride (conflict-free column reads); it is fetched as float4 loads all issued
+// before the first LDS store (CP_IT per thread), so a block waits for one load latency, not one per element.
+constexpr int CP_T = 256, CP_IT = 24;  // C <= 92 at K = 7
+__global__ __launch_bounds__(CP_T) void k_conv_post(const float* __restrict__ x, int T, int C,
+                                                    const float* __restrict__ wg, int K, float slope,
+                                                    float* __restrict__ y, float bias) {
+  extern __shared__ float tile[];  // [(CP_T+K-1)][C+1], then w[C*K]
   const int b = blockIdx.y;
-  const int t0 = blockIdx.x * 256;
+  const int t0 = blockIdx.x * CP_T;
   const int pad = K / 2;
-  const int rows = 256 + K - 1;
+  const int rows = CP_T + K - 1;
   const int ldt = C + 1;
+  const int C4 = C >> 2;
   float* w = tile + rows * ldt;
   for (int i = threadIdx.x; i < C * K; i += blockDim.x) w[i] = wg[i];
   const float* xb = x + (long long)b * T * C;
-  for (int idx = threadIdx.x; idx < rows * C; idx += blockDim.x) {
-    const int r = idx / C, c = idx % C;
+  f32x4v v[CP_IT];
+#pragma unroll
+  for (int it = 0; it < CP_IT; ++it) {
+    const int idx = it * CP_T + threadIdx.x;
+    const int r = idx / C4, c4 = (idx - r * C4) * 4;
     const int g = t0 - pad + r;
-    float v = 0.f;
-    if (g >= 0 && g < T) {
-      v = xb[(long long)g * C + c];
-      v = v > 0.f ? v : v * slope;
+    v[it] = (r < rows && g >= 0 && g < T) ? *reinterpret_cast<const f32x4v*>(xb + (long long)g * C + c4)
+                                          : f32x4v{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int it = 0; it < CP_IT; ++it) {
+    const int idx = it * CP_T + threadIdx.x;
+    const int r = idx / C4, c4 = (idx - r * C4) * 4;
+    if (r < rows) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float u = v[it][e];
+        tile[r * ldt + c4 + e] = u > 0.f ? u : u * slope;
+      }
     }
-    tile[r * ldt + c] = v;
   }
   __syncthreads();
   const int t = t0 + threadIdx.x;
@@ -509,8 +526,12 @@ __global__ void k_conv_post(const float* __restrict__ x, int T, int C, const flo
 }
 hipError_t conv_post_tanh(const float* x, int B, int T, int C, const float* w, int K, float slope, float* y,
                           hipStream_t s, float bias) {
-  const size_t smem = ((size_t)(256 + K - 1) * (C + 1) + (size_t)C * K) * sizeof(float);
-  hipLaunchKernelGGL(k_conv_post, dim3((T + 255) / 256, B), dim3(256), smem, s, x, T, C, w, K, slope, y, bias);
+  // the staged fetch covers (CP_T + K - 1) rows of C / 4 float4 in CP_IT rounds of CP_T threads
+  if (C % 4 != 0 || (long long)(CP_T + K - 1) * (C / 4) > (long long)CP_IT * CP_T ||
+      (reinterpret_cast<uintptr_t>(x) & 15) != 0)
+    return hipErrorInvalidValue;
+  const size_t smem = ((size_t)(CP_T + K - 1) * (C + 1) + (size_t)C * K) * sizeof(float);
+  hipLaunchKernelGGL(k_conv_post, dim3((T + CP_T - 1) / CP_T, B), dim3(CP_T), smem, s, x, T, C, w, K, slope, y, bias);
   return hipGetLastError();
 }
 

@@ -101,7 +101,7 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
   const int TT = NBT * 32 - 2 * h2;  // valid outputs per tile
   char* const XS = rb_smem;
   char* const TS = rb_smem + (size_t)nx * ROW;
-  // persistent: workgroup g takes tiles g, g + G, ... of the B * ntiles (batch-major) tiles; the next tile's x is
+  // persistent: workgroup g takes a contiguous run of the B * ntiles (batch-major) tiles; the next tile's x is
   // loaded into registers while the current one computes
   const int total = ntiles * a.B;
 
@@ -217,14 +217,18 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
     }
   };
 
-  int tile = blockIdx.x;
-  if (tile >= total) return;
+  // contiguous runs of tiles per workgroup: the next tile's halo rows were just read by this workgroup (same XCD
+  // L2), instead of by a neighbour on another XCD
+  const int per = (total + (int)gridDim.x - 1) / (int)gridDim.x;
+  int tile = blockIdx.x * per;
+  const int tile_end = min(total, tile + per);
+  if (tile >= tile_end) return;
   // the first job's weights and the first tile's x are in flight together
-  const bool pre = (a.flags & 1) == 0;
+  const bool pre = (a.flags & 1) != 0;  // contiguous runs: the next tile mostly sits in L2 already (A/B: off 22.19, on 22.30 ms)
   prefetch_ring(wl_of(0));
   if (pre) load_x(tile);
 #pragma unroll 1
-  for (; tile < total; tile += gridDim.x) {
+  for (; tile < tile_end; ++tile) {
   if (!pre) load_x(tile);
   const int b = tile / ntiles;
   const int t0 = (tile - b * ntiles) * TT;
@@ -233,7 +237,7 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
   // conv1 (writing TS) after every wave's conv2 of the previous tile (reading TS)
   write_x();
   __syncthreads();
-  if (pre && tile + (int)gridDim.x < total) load_x(tile + gridDim.x);
+  if (pre && tile + 1 < tile_end) load_x(tile + 1);
   float* Y = a.y + (long long)b * a.y_bs;
 #pragma unroll 1
   for (int job = 0; job < 2 * UPW; ++job) {
@@ -266,7 +270,7 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
     f32x16 acc[TN];
     run_conv(wl_of(job), (second ? TS : XS) + (size_t)(tg * TN * 32 + li) * ROW + hk * 16, second ? 1 : a.d, acc);
     if (job + 1 < 2 * UPW) prefetch_ring(wl_of(job + 1));
-    else if (tile + (int)gridDim.x < total) prefetch_ring(wl_of(0));
+    else if (tile + 1 < tile_end) prefetch_ring(wl_of(0));
     if (!second) {
       // conv1 -> TS = split(lrelu(conv1 + b1)); TS row p <-> time t0 - h2 + p, zero outside [0, T)
 #pragma unroll

@@ -153,7 +153,7 @@ struct RbPairArgs {
   long long y_bs = 0;
   int acc_mode = ACC_STORE;
   float acc_div = 1.f;
-  int flags = 0;  // bit 0: no next-tile x prefetch (measurement aid, RVCX_RB_FLAGS)
+  int flags = 0;  // bit 0: next-tile x prefetch into registers (measurement aid, RVCX_RB_FLAGS)
 };
 bool rb_pair_fits(int C, int k, int d);
 long long rb_wsplit_bytes(int C, int k);
