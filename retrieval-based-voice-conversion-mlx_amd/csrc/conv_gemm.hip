@@ -711,7 +711,8 @@ hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
   if (a.N <= 0 || a.T_out <= 0 || a.batch <= 0) return hipSuccess;
   if (a.C_in <= 0 || a.taps <= 0) return hipErrorInvalidValue;
   if (tiny_fits(a)) return launch_tiny(a, TWO_D, s);
-  if (!TWO_D && a.wsplit && (a.force_cfg < 0 || a.force_cfg >= 20) && conv_math(a) == 2 && conv_wsb_eligible(a)) {
+  if (!TWO_D && a.wsplit && (a.force_cfg >= 20 || (a.force_cfg < 0 && conv_wsb_wants(a))) && conv_math(a) == 2 &&
+      conv_wsb_eligible(a)) {
     const hipError_t e = conv_wsb_launch(a, a.force_cfg >= 20 ? a.force_cfg : pick_wsb(a), xcd_enabled() ? 1 : 0, s);
     if (e != hipErrorInvalidValue) return e;
   }

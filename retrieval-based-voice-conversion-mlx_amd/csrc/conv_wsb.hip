@@ -224,12 +224,14 @@ bool conv_wsb_eligible(const ConvArgs& a) {
 
 int conv_wsplit_npad(int N) { return (N + 127) / 128 * 128; }
 
+// chunks of 32 input channels, the last one zero-padded
 long long conv_wsplit_bytes(const ConvArgs& a) {
-  return (long long)(a.C_in / EK) * a.taps * conv_wsplit_npad(a.N) * WROW;
+  return (long long)((a.C_in + EK - 1) / EK) * a.taps * conv_wsplit_npad(a.N) * WROW;
 }
 
 hipError_t conv_wsplit_build(const ConvArgs& a, void* out, hipStream_t s) {
-  const int nch = a.C_in / EK, Npad = conv_wsplit_npad(a.N);
+  const int nch = (a.C_in + EK - 1) / EK, Npad = conv_wsplit_npad(a.N);
+  if (nch < 1 || a.taps < 1 || a.N < 1) return hipErrorInvalidValue;
   const long long total = (long long)nch * a.taps * Npad * EK;
   const long long nb = std::min<long long>((total + 255) / 256, 1 << 20);
   hipLaunchKernelGGL(k_wsplit, dim3((unsigned)nb), dim3(256), 0, s, a.w, a.ldw, a.w_ts, a.N, a.C_in, a.taps, nch, Npad,
