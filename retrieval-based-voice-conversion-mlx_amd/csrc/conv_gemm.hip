@@ -788,9 +788,12 @@ long long conv_plan_splitk(ConvArgs& a, bool two_d) {
   // ~1.5-2 us each (global B load -> LDS -> barrier -> MFMA), so a handful of tiles walking >= 16 steps
   // is latency-bound whatever the FLOP count (RMVPE's deepest levels at streaming sizes: 8 tiles x 144
   // steps = 264 us unsplit)
-  static const int target = env_cfg("RVCX_SPLITK_TARGET", 768);   // workgroups a split launch aims for
-  static const int min_tiles = env_cfg("RVCX_SPLITK_TILES", 384);  // grids with at least this many tiles stay unsplit
-  if (tiles >= min_tiles || iters < 8 || (flops < 1.0e8 && iters < 16)) return 0;
+  // same-box A/B of C2 (round 2, with the 32-bit combine): (target, tiles, min_iters) = (512, 192, 4) 22.59 ms,
+  // (768, 384, 8) 22.82, (512, 256, 4) 22.70, (384, 256, 4) 22.64, (1024, 384, 8) 23.33
+  static const int target = env_cfg("RVCX_SPLITK_TARGET", 512);   // workgroups a split launch aims for
+  static const int min_tiles = env_cfg("RVCX_SPLITK_TILES", 192);  // grids with at least this many tiles stay unsplit
+  static const int min_iters = env_cfg("RVCX_SPLITK_MINITERS", 4);  // shortest contraction worth a split
+  if (tiles >= min_tiles || iters < min_iters || (flops < 1.0e8 && iters < 16)) return 0;
   int ks = (int)((target + tiles - 1) / tiles);
   ks = std::min(ks, iters / 2);
   ks = std::min(ks, 32);
