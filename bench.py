@@ -30,8 +30,9 @@ BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense BF16 MFMA (no sparsity)
 # algorithmic fp32 FLOP/s is the dense bf16 peak / 6. A few launches still take the native f32 MFMA (ceiling
 # 157.3); pricing every FLOP against the higher ceiling keeps frac a lower bound.
 SPLIT_PEAK_TFLOPS = round(BF16_PEAK_TFLOPS / 6.0, 1)
-CONV_KERNEL = ("conv_emu_kernel / conv_gemm_kernel / conv_tiny_kernel / k_conv2d_small (+ splitk_reduce): every "
-               "conv, linear and matmul launch of the step, Σ algorithmic fp32 FLOPs / Σ HIP-event kernel time")
+CONV_KERNEL = ("conv_emu_kernel / conv_wsb_kernel / k_rb_pair / conv_gemm_kernel / conv_tiny_kernel / k_conv2d_small "
+               "(+ splitk_reduce): every conv, linear and matmul launch of the step, Σ algorithmic fp32 FLOPs / Σ "
+               "HIP-event kernel time")
 SR_IN = 16000
 C2_SAMPLES = 216100  # 13.50625 s (the reference's 13.5 s benchmark clip length)
 
