@@ -810,11 +810,12 @@ bool conv_wsb_wants(const ConvArgs& a) {
   }();
   if (off || conv_math(a) != 2 || !conv_wsb_eligible(a)) return false;
   // where it measured faster (bench_conv, profiles/r02i_bench_conv.txt: 128 x 64 tiles of 2 x 2 waves of 64 x 32
-  // with the register epilogue): N >= 128 with >= 2 taps (ResBlock convs at 128/256 channels incl. k = 3, the
-  // polyphase ConvTranspose phases), on a grid that fills the chip (RVCX_WSB_MINTAPS / RVCX_WSB_MINTILES: A/B aid)
+  // with the register epilogue; C2 A/B): N >= 64 with >= 2 taps (ResBlock convs at 64-256 channels incl. k = 3, the
+  // polyphase ConvTranspose phases), on a grid that fills the chip (RVCX_WSB_MINN / _MINTAPS / _MINTILES: A/B aid)
   static const int min_taps = env_cfg("RVCX_WSB_MINTAPS", 2);
   static const int min_tiles = env_cfg("RVCX_WSB_MINTILES", 512);
-  if (a.N < 128 || a.taps < min_taps) return false;
+  static const int min_n = env_cfg("RVCX_WSB_MINN", 64);  // A/B: the 64-channel stage on 128x64 tiles beat the fused pair
+  if (a.N < min_n || a.taps < min_taps) return false;
   const long long tiles = (long long)((a.T_out + 127) / 128) * ((a.N + 63) / 64) * a.batch;
   return tiles >= min_tiles;
 }

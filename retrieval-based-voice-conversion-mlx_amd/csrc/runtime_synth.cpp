@@ -396,7 +396,13 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
       const auto& dil = cf.rb_d[j];
       const std::string rb = "dec.resblocks." + std::to_string(i * nk + j);
       const float* r_in = y;
-      bool fuse = rb_fuse_enabled();
+      static const int rb_maxc = [] {
+        // widest stage taking the fused pair: 32 channels (same-box A/B of C2: fused 32 + weight-streamed 64
+        // 21.97 ms, fused 32 + 64 22.46, weight-streamed both 23.07; RVCX_RB_MAXC overrides)
+        const char* e = std::getenv("RVCX_RB_MAXC");
+        return e ? std::atoi(e) : 32;
+      }();
+      bool fuse = rb_fuse_enabled() && C <= rb_maxc;
       for (int d : dil) fuse = fuse && rb_pair_fits(C, k, d);
       if (fuse) {
         // each dilation pair as one fused kernel (resblock_fused.hip); pairs ping-pong between RR and T1 (a pair
