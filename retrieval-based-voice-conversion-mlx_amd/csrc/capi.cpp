@@ -179,8 +179,12 @@ void launch_rb_pair(Ctx& c, const RbPairArgs& a_in, hipStream_t s) {
 void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double flops) {
   ConvArgs a = a_in;
   if (c.conv_math > 0 && a.math == 0) a.math = c.conv_math;
+  // weight-streamed kernel: forced (numerics tests / benchmarks: force_cfg >= 20 on a w_static weight) or routed by
+  // the policy for a packed (static) weight; decided before the split-K plan, whose geometry depends on it
+  const bool stat = a.w_static || c.is_weight(a.w);
+  a.wsb = stat && ((a.force_cfg >= 20 && !two_d) || (a.force_cfg < 0 && conv_wsb_route(a, two_d))) ? 1 : 0;
   const long long need = conv_plan_splitk(a, two_d);
-  if (!two_d && a.w_static && (a.force_cfg >= 20 || conv_wsb_wants(a))) {
+  if (a.wsb) {
     a.wsplit = c.wsplit_for(a, s);
     a.wsplit_npad = conv_wsplit_npad(a.N);
   }

@@ -711,9 +711,11 @@ hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
   if (a.N <= 0 || a.T_out <= 0 || a.batch <= 0) return hipSuccess;
   if (a.C_in <= 0 || a.taps <= 0) return hipErrorInvalidValue;
   if (tiny_fits(a)) return launch_tiny(a, TWO_D, s);
-  if (!TWO_D && a.wsplit && (a.force_cfg >= 20 || (a.force_cfg < 0 && conv_wsb_wants(a))) && conv_math(a) == 2 &&
-      conv_wsb_eligible(a)) {
-    const hipError_t e = conv_wsb_launch(a, a.force_cfg >= 20 ? a.force_cfg : pick_wsb(a), xcd_enabled() ? 1 : 0, s);
+  if (a.wsb && a.wsplit && conv_math(a) == 2 && conv_wsb_eligible(a, TWO_D)) {
+    const int ks = (a.ws && a.ksplit > 1) ? a.ksplit : 1;
+    const int cfg = TWO_D ? 21 : (a.force_cfg >= 20 ? a.force_cfg : pick_wsb(a));
+    hipError_t e = conv_wsb_launch(a, cfg, xcd_enabled() ? 1 : 0, s, TWO_D, ks);
+    if (e == hipSuccess && ks > 1) e = launch_splitk_reduce(a, ks, TWO_D, s);
     if (e != hipErrorInvalidValue) return e;
   }
   // 3x3 convs with 16/32 channels: 16x16x4 MFMA fragments (conv2d_small.hip)
@@ -768,9 +770,12 @@ long long conv_plan_splitk(ConvArgs& a, bool two_d) {
   if (a.N <= 0 || a.T_out <= 0 || a.no_splitk) return 0;
   if (tiny_fits(a)) return 0;
   if (two_d && a.force_cfg < 0 && small2d_enabled() && conv2d_small_fits(a)) return 0;
-  const int cfg = two_d ? pick_cfg<true>(a) : pick_cfg<false>(a);
   int BM, BN;
-  cfg_tile(cfg, BM, BN);
+  if (a.wsb) {  // the weight-streamed tile (pick_wsb; 2-D: 128 x 64)
+    conv_wsb_tile(two_d ? 21 : (a.force_cfg >= 20 ? a.force_cfg : pick_wsb(a)), BM, BN);
+  } else {
+    cfg_tile(two_d ? pick_cfg<true>(a) : pick_cfg<false>(a), BM, BN);
+  }
   long long mtiles;
   if (!two_d) {
     mtiles = (a.T_out + BM - 1) / BM;
@@ -818,6 +823,15 @@ bool conv_wsb_wants(const ConvArgs& a) {
   if (a.N < min_n || a.taps < min_taps) return false;
   const long long tiles = (long long)((a.T_out + 127) / 128) * ((a.N + 63) / 64) * a.batch;
   return tiles >= min_tiles;
+}
+
+bool conv_wsb_route(const ConvArgs& a, bool two_d) {
+  static const bool split_1d = env_cfg("RVCX_WSB_SPLIT", 0) != 0;  // small 1-D grids with split-K
+  static const bool route_2d = env_cfg("RVCX_WSB_2D", 0) != 0;     // 3x3 2-D convs, >= 64 channels
+  if (conv_math(a) != 2 || !conv_wsb_eligible(a, two_d) || tiny_fits(a)) return false;
+  if (two_d) return route_2d && a.N >= 64 && a.C_in >= 64 && !(small2d_enabled() && conv2d_small_fits(a));
+  if (conv_wsb_wants(a)) return true;
+  return split_1d && a.N >= 64;
 }
 
 hipError_t conv1d(const ConvArgs& a, hipStream_t s) { return dispatch<false>(a, s); }

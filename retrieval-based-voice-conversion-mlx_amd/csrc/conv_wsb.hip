@@ -24,6 +24,7 @@ using namespace splitbf16;
 
 constexpr int WROW = 3 * PLANE;  // bytes of one (chunk, tap, column) row of split weights in HBM
 constexpr int WSB_HALO = 64;     // max (taps - 1) * dil: the A prefetch registers cover BM + 64 rows
+constexpr int WSB_ROWS_2D = 224;  // 2-D: pixel-window rows the A prefetch registers cover (3x3 windows of 128 px)
 
 // w [tap][n][c] (ldw, w_ts) -> out rows ((ch * taps + tap) * Npad + n) of [hi | mid | lo] x 32 bf16; zero
 // beyond N and C_in. The plane arithmetic is put_split1's.
@@ -50,9 +51,11 @@ __global__ void k_wsplit(const float* __restrict__ w, int ldw, long long w_ts, i
   }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, bool TWO_D>
 __global__ __launch_bounds__(CONV_THREADS, 2) void conv_wsb_kernel(const ConvArgs a, const char* __restrict__ wsp,
-                                                                   const int Npad, const int nrows_a, const int ntn) {
+                                                                   const int Npad, const int nrows_a, const int ntn,
+                                                                   const int ksplit, const int rw, const int rh,
+                                                                   const int tiles_w) {
   constexpr int NT = CONV_THREADS;
   constexpr int TM = BM / (WM * 32);
   constexpr int TN = BN / (WN * 32);
@@ -67,15 +70,28 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_wsb_kernel(const ConvArg
   const int li = lane & 31, hk = lane >> 5;
   int bx, by, bz;
   conv_block_coords(ntn, bx, by, bz);
-  const int b = bz;
-  const int n0 = by * BN, m0 = bx * BM;
+  const int zsplit = bz % ksplit;  // split-K slice
+  const int b = bz / ksplit;
+  const int n0 = by * BN;
+  int m0 = 0, h0 = 0, w0 = 0;
+  if (!TWO_D) {
+    m0 = bx * BM;
+  } else {
+    h0 = (bx / tiles_w) * rh;
+    w0 = (bx % tiles_w) * rw;
+  }
   const float* X = a.x + (long long)b * a.x_bs;
-  const float* PM = a.pre_mask ? a.pre_mask + (long long)b * a.pre_mask_bs : nullptr;
-  const int row0 = m0 - a.pad;
+  const float* PM = (!TWO_D && a.pre_mask) ? a.pre_mask + (long long)b * a.pre_mask_bs : nullptr;
+  const int row0 = TWO_D ? 0 : m0 - a.pad;
+  const int aw = TWO_D ? rw + a.KW - 1 : 0;  // 2-D: the (rh + KH - 1) x (rw + KW - 1) pixel window, row-major
 
   int aoff[TM];
 #pragma unroll
-  for (int tm = 0; tm < TM; ++tm) aoff[tm] = (wm * TM * 32 + tm * 32 + li) * ERS + hk * 16;
+  for (int tm = 0; tm < TM; ++tm) {
+    const int ml = wm * TM * 32 + tm * 32 + li;
+    const int r = !TWO_D ? ml : ((ml < rh * rw) ? (ml / rw) * aw + (ml % rw) : 0);
+    aoff[tm] = r * ERS + hk * 16;
+  }
   const char* bp[TN];
 #pragma unroll
   for (int tn = 0; tn < TN; ++tn) bp[tn] = wsp + (size_t)(n0 + wn * TN * 32 + tn * 32 + li) * WROW + hk * 16;
@@ -89,8 +105,9 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_wsb_kernel(const ConvArg
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[tm][tn][r] = 0.f;
 
-  // ---- A: the chunk's nrows_a x 32 halo tile, prefetched into registers one chunk ahead
-  constexpr int AP = ((BM + WSB_HALO) * EC4 + NT - 1) / NT;
+  // ---- A: the chunk's nrows_a x 32 halo tile (1-D rows / 2-D pixel window), prefetched into registers one chunk
+  // ahead
+  constexpr int AP = ((TWO_D ? WSB_ROWS_2D : BM + WSB_HALO) * EC4 + NT - 1) / NT;
   f32x4 apre[AP];
   float apm[AP];
   const int arow = store_row(tid / EC4), ac4 = (tid % EC4) << 2;
@@ -99,9 +116,18 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_wsb_kernel(const ConvArg
 #pragma unroll
     for (int v = 0; v < AP; ++v) {
       const int r = v * (NT / EC4) + arow;
-      const int g = row0 + r;
-      const bool ok = r < nrows_a && g >= 0 && g < a.T_in;
-      apre[v] = ok ? *reinterpret_cast<const f32x4*>(src0 + (long long)g * a.ldx) : f32x4{0.f, 0.f, 0.f, 0.f};
+      long long g;
+      bool ok;
+      if constexpr (!TWO_D) {
+        g = row0 + r;
+        ok = r < nrows_a && g >= 0 && g < a.T_in;
+      } else {
+        const int ah = r / aw, awi = r - ah * aw;
+        const int gh = h0 - a.padh + ah, gw = w0 - a.padw + awi;
+        ok = r < nrows_a && gh >= 0 && gh < a.T_in && gw >= 0 && gw < a.W_in;
+        g = (long long)gh * a.W_in + gw;
+      }
+      apre[v] = ok ? *reinterpret_cast<const f32x4*>(src0 + g * a.ldx) : f32x4{0.f, 0.f, 0.f, 0.f};
       apm[v] = ok ? (PM ? PM[g] : 1.f) : 0.f;
     }
   };
@@ -135,7 +161,7 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_wsb_kernel(const ConvArg
           dst[tn][s * 3 + q] = *reinterpret_cast<const bf16x8*>(bp[tn] + o + q * PLANE + s * 32);
   };
   auto compute = [&](int tap, const BFrag& bf) __attribute__((always_inline)) {
-    const int toff = tap * a.dil * ERS;
+    const int toff = (TWO_D ? (tap / a.KW) * aw + (tap % a.KW) : tap * a.dil) * ERS;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       bf16x8 af[TM][3];
@@ -160,48 +186,63 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_wsb_kernel(const ConvArg
     }
   };
 
-  const int nch = a.C_in / EK, taps = a.taps, total = nch * taps;
-  BFrag b0, b1;
-  load_a_regs(0);
-  write_a_regs();
-  if (nch > 1) load_a_regs(EK);
-  load_b(0, b0);
-  __syncthreads();
-  int ch = 0, tap = 0;
-  // one (chunk, tap) iteration: prefetch the next iteration's B, MFMAs on this one's, switch chunks after the
-  // last tap (every wave done reading the halo -> write the prefetched one -> prefetch the chunk after)
-  auto step = [&](int it, const BFrag& cur, BFrag& nxt) __attribute__((always_inline)) {
-    if (it + 1 < total) load_b(it + 1, nxt);
-    compute(tap, cur);
-    if (++tap == taps) {
-      tap = 0;
-      if (++ch < nch) {
-        __syncthreads();
-        write_a_regs();
-        if (ch + 1 < nch) load_a_regs((ch + 1) * EK);
-        __syncthreads();
+  // (chunk, tap) iterations [it0, it1) of this split-K slice (an empty slice stores its zero partial tile)
+  const int taps = a.taps, total = (a.C_in / EK) * taps;
+  const int per = (total + ksplit - 1) / ksplit;
+  const int it0 = zsplit * per, it1 = min(total, it0 + per);
+  if (it0 < it1) {
+    BFrag b0, b1;
+    int ch = it0 / taps, tap = it0 - ch * taps;
+    load_a_regs(ch * EK);
+    write_a_regs();
+    if ((ch + 1) * taps < it1) load_a_regs((ch + 1) * EK);
+    load_b(it0, b0);
+    __syncthreads();
+    // one (chunk, tap) iteration: prefetch the next iteration's B, MFMAs on this one's, switch chunks after the
+    // last tap (every wave done reading the halo -> write the prefetched one -> prefetch the chunk after)
+    auto step = [&](int it, const BFrag& cur, BFrag& nxt) __attribute__((always_inline)) {
+      if (it + 1 < it1) load_b(it + 1, nxt);
+      compute(tap, cur);
+      if (++tap == taps) {
+        tap = 0;
+        if (++ch * taps < it1) {
+          __syncthreads();
+          write_a_regs();
+          if ((ch + 1) * taps < it1) load_a_regs((ch + 1) * EK);
+          __syncthreads();
+        }
       }
+    };
+    for (int it = it0; it < it1; it += 2) {
+      step(it, b0, b1);
+      if (it + 1 < it1) step(it + 1, b1, b0);
     }
-  };
-  for (int it = 0; it < total; it += 2) {
-    step(it, b0, b1);
-    if (it + 1 < total) step(it + 1, b1, b0);
   }
 
-  conv_store_tile<TM, TN, WM, WN, false>(a, TilePos{m0, 0, 0, 0, 0, n0, b, 0, b, 0, 1}, acc,
+  conv_store_tile<TM, TN, WM, WN, TWO_D>(a, TilePos{m0, h0, w0, rw, rh, n0, b, 0, b, zsplit, ksplit}, acc,
                                          reinterpret_cast<float*>(smem_w));
 }
 
-template <int BM, int BN, int WM, int WN>
-hipError_t launch_wsb(const ConvArgs& a, int ntn_enable, hipStream_t s) {
-  const int nrows_a = BM + (a.taps - 1) * a.dil;
+template <int BM, int BN, int WM, int WN, bool TWO_D>
+hipError_t launch_wsb(const ConvArgs& a, int ntn_enable, int ksplit, hipStream_t s) {
+  int nrows_a, rw = 0, rh = 0, tiles_w = 1, mtiles;
+  if (!TWO_D) {
+    nrows_a = BM + (a.taps - 1) * a.dil;
+    mtiles = (a.T_out + BM - 1) / BM;
+  } else {
+    rw = a.W_out < BM ? a.W_out : BM;
+    rh = BM / rw;
+    tiles_w = (a.W_out + rw - 1) / rw;
+    mtiles = ((a.T_out + rh - 1) / rh) * tiles_w;
+    nrows_a = (rh + a.KH - 1) * (rw + a.KW - 1);
+    if (nrows_a > WSB_ROWS_2D) return hipErrorInvalidValue;  // the window outgrows the A prefetch registers
+  }
   const size_t smem = std::max((size_t)nrows_a * ERS, (size_t)4 * 32 * 33 * sizeof(float));
-  if (a.wsplit_npad % BN != 0) return hipErrorInvalidValue;
-  const int mtiles = (a.T_out + BM - 1) / BM;
+  if (a.wsplit_npad % BN != 0 || ksplit < 1 || (ksplit > 1 && !a.ws)) return hipErrorInvalidValue;
   const int ntiles = (a.N + BN - 1) / BN;
   const int ntn = ntn_enable ? ntiles : 0;
-  dim3 grid(ntn ? mtiles * ntiles : mtiles, ntn ? 1 : ntiles, a.batch);
-  auto kern = conv_wsb_kernel<BM, BN, WM, WN>;
+  dim3 grid(ntn ? mtiles * ntiles : mtiles, ntn ? 1 : ntiles, a.batch * ksplit);
+  auto kern = conv_wsb_kernel<BM, BN, WM, WN, TWO_D>;
   static size_t smem_set = 64 * 1024;
   if (smem > smem_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -210,16 +251,21 @@ hipError_t launch_wsb(const ConvArgs& a, int ntn_enable, hipStream_t s) {
     smem_set = smem;
   }
   hipLaunchKernelGGL(kern, grid, dim3(CONV_THREADS), smem, s, a, static_cast<const char*>(a.wsplit), a.wsplit_npad,
-                     nrows_a, ntn);
+                     nrows_a, ntn, ksplit, rw, rh, tiles_w);
   return hipGetLastError();
 }
 
 }  // namespace
 
-bool conv_wsb_eligible(const ConvArgs& a) {
+bool conv_wsb_eligible(const ConvArgs& a, bool two_d) {
   const bool vec_a = ((a.ldx & 3) == 0) && ((reinterpret_cast<uintptr_t>(a.x) & 15) == 0) && ((a.x_bs & 3) == 0);
-  return a.stride == 1 && a.batch_inner == 1 && !a.b_kn && a.C_in % EK == 0 && a.C_in > 0 && a.taps >= 1 &&
-         (a.taps - 1) * a.dil <= WSB_HALO && a.dil >= 1 && vec_a && a.ksplit <= 1 && a.out_map == OUT_ROWS;
+  const bool common = a.batch_inner == 1 && !a.b_kn && a.C_in % EK == 0 && a.C_in > 0 && a.taps >= 1 && vec_a &&
+                      a.out_map == OUT_ROWS;
+  if (!two_d) return common && a.stride == 1 && (a.taps - 1) * a.dil <= WSB_HALO && a.dil >= 1;
+  // 2-D: stride 1, taps = KH x KW, the window of a 128-pixel tile within the prefetch registers
+  if (!common || a.taps != a.KH * a.KW || a.W_out < 1 || a.pre_mask) return false;
+  const int rw = a.W_out < 128 ? a.W_out : 128, rh = 128 / rw;
+  return a.W_out == a.W_in && a.T_out == a.T_in && (rh + a.KH - 1) * (rw + a.KW - 1) <= WSB_ROWS_2D;
 }
 
 int conv_wsplit_npad(int N) { return (N + 127) / 128 * 128; }
@@ -248,12 +294,13 @@ bool conv_wsb_tile(int cfg, int& BM, int& BN) {
   return true;
 }
 
-hipError_t conv_wsb_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream_t s) {
-  if (!a.wsplit || !conv_wsb_eligible(a)) return hipErrorInvalidValue;
+hipError_t conv_wsb_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream_t s, bool two_d, int ksplit) {
+  if (!a.wsplit || !conv_wsb_eligible(a, two_d)) return hipErrorInvalidValue;
+  if (two_d) return cfg == 21 ? launch_wsb<128, 64, 2, 2, true>(a, ntn_enable, ksplit, s) : hipErrorInvalidValue;
   switch (cfg) {
-    case 20: return launch_wsb<256, 32, 4, 1>(a, ntn_enable, s);
-    case 21: return launch_wsb<128, 64, 2, 2>(a, ntn_enable, s);
-    case 22: return launch_wsb<128, 128, 2, 2>(a, ntn_enable, s);
+    case 20: return launch_wsb<256, 32, 4, 1, false>(a, ntn_enable, ksplit, s);
+    case 21: return launch_wsb<128, 64, 2, 2, false>(a, ntn_enable, ksplit, s);
+    case 22: return launch_wsb<128, 128, 2, 2, false>(a, ntn_enable, ksplit, s);
     default: return hipErrorInvalidValue;
   }
 }

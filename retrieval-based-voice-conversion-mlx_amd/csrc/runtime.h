@@ -140,6 +140,9 @@ struct Ctx {
   ~Ctx();
 
   float* W(const std::string& name) const;
+  // address ranges of the packed weights (alloc_weight): a contraction whose B operand lies in one is static
+  std::map<uintptr_t, uintptr_t> wranges;
+  bool is_weight(const void* p) const;
   float* alloc_weight(const std::string& name, const std::vector<float>& data);
   template <class T>
   T* buf(const std::string& name, size_t count, hipStream_t s);

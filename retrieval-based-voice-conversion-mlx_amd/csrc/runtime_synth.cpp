@@ -114,8 +114,19 @@ float* Ctx::alloc_weight(const std::string& name, const std::vector<float>& data
   b->bytes = bytes;
   RVCX_HIP(hipMemcpy(b->p, data.data(), data.size() * sizeof(float), hipMemcpyHostToDevice));
   float* p = static_cast<float*>(b->p);
+  auto old = dev.find(name);
+  if (old != dev.end()) wranges.erase(reinterpret_cast<uintptr_t>(old->second->p));
+  wranges[reinterpret_cast<uintptr_t>(p)] = reinterpret_cast<uintptr_t>(p) + bytes;
   dev[name] = std::move(b);
   return p;
+}
+
+bool Ctx::is_weight(const void* q) const {
+  const uintptr_t u = reinterpret_cast<uintptr_t>(q);
+  auto it = wranges.upper_bound(u);
+  if (it == wranges.begin()) return false;
+  --it;
+  return u < it->second;
 }
 
 // ------------------------------------------------------------------ weight repacking

@@ -97,6 +97,7 @@ struct ConvArgs {
   int w_static = 0;             // the B operand is a constant weight tensor (callers set it; enables the cache)
   const void* wsplit = nullptr;  // ((chunk * taps + tap) * wsplit_npad + n) rows of [hi|mid|lo] x 32 bf16
   int wsplit_npad = 0;
+  int wsb = 0;  // set by the runtime (conv_wsb_route on a static weight): run on the weight-streamed kernel
   int ksplit = 1;
   int no_splitk = 0;
   long long ws_rows = 0;
@@ -132,12 +133,17 @@ hipError_t softmax_rows(float* scores, int rows, int cols, hipStream_t s);
 // weight-streamed split conv (conv_wsb.hip): eligibility (1-D, stride 1, C_in % 32 == 0, halo <= 64 rows, no
 // split-K), the pre-split weight image and its launch; conv_wsb_wants = eligible + split arithmetic + a grid
 // large enough to fill the chip (conv_gemm.hip policy)
-bool conv_wsb_eligible(const ConvArgs& a);
+bool conv_wsb_eligible(const ConvArgs& a, bool two_d = false);
 bool conv_wsb_wants(const ConvArgs& a);
+// route a contraction with a static weight to the weight-streamed kernel: the big 1-D grids (conv_wsb_wants), and
+// behind RVCX_WSB_SPLIT / RVCX_WSB_2D the small 1-D grids (with split-K) and the 3x3 2-D convs with >= 64 channels
+bool conv_wsb_route(const ConvArgs& a, bool two_d);
+bool conv_wsb_tile(int cfg, int& BM, int& BN);  // cfg 20..22 -> tile
 int conv_wsplit_npad(int N);
 long long conv_wsplit_bytes(const ConvArgs& a);
 hipError_t conv_wsplit_build(const ConvArgs& a, void* out, hipStream_t s);
-hipError_t conv_wsb_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream_t s);
+hipError_t conv_wsb_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream_t s, bool two_d = false,
+                           int ksplit = 1);
 // fused ResBlock dilation pair (resblock_fused.hip): y (acc_mode) <- conv2(lrelu(conv1_d(lrelu(x)) + b1)) + b2 + x,
 // x / y [B][T][C] (x != y), C in {32, 64}, odd k, (k - 1) / 2 * d <= 30; w1s / w2s are rb_wsplit_build images
 // of [k][C][C] fp32 weights
