@@ -27,6 +27,8 @@ __device__ __forceinline__ float act_small(float v, int act, float slope) {
 }
 }  // namespace
 
+constexpr int SIT = 17;  // staging rounds of 256 float4 per block: (RH + 2) x (W + 2) x CIN / 4 <= 17 x 256 (all U-Net levels)
+
 template <int CIN, int NOUT, int PIX>
 __global__ __launch_bounds__(256) void k_conv2d_small(const ConvArgs a, const int RH) {
   constexpr int CP = CIN + 4;   // LDS floats per pixel
@@ -42,24 +44,46 @@ __global__ __launch_bounds__(256) void k_conv2d_small(const ConvArgs a, const in
   const int h0 = blockIdx.x * RH;
   const float* X = a.x + (long long)b * a.x_bs;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // ---- stage the halo tile and the weights
+  // ---- stage the halo tile and the weights: every thread's loads are issued before its first LDS store (the
+  // tile is <= SIT rounds of 256 float4), so a block waits for one load latency instead of one per round
   const int rows = RH + 2;
-  for (int idx = tid; idx < rows * AW * (CIN / 4); idx += 256) {
-    const int q = idx % (CIN / 4);
-    const int pix = idx / (CIN / 4);
-    const int r = pix / AW, cc = pix % AW;
-    const int gh = h0 - 1 + r, gw = cc - 1;
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if (gh >= 0 && gh < H && gw >= 0 && gw < W)
-      v = *reinterpret_cast<const f32x4*>(X + ((long long)gh * W + gw) * a.ldx + 4 * q);
-    *reinterpret_cast<f32x4*>(As + (size_t)pix * CP + 4 * q) = v;
-  }
-  for (int idx = tid; idx < 9 * NOUT * (CIN / 4); idx += 256) {
-    const int q = idx % (CIN / 4);
-    const int tn = idx / (CIN / 4);  // tap * NOUT + n
-    const int tap = tn / NOUT, n = tn % NOUT;
-    const f32x4 v = *reinterpret_cast<const f32x4*>(a.w + (long long)tap * a.w_ts + (long long)n * a.ldw + 4 * q);
-    *reinterpret_cast<f32x4*>(Bs + (size_t)tn * CP + 4 * q) = v;
+  const int na = rows * AW * (CIN / 4);
+  constexpr int NW = 9 * NOUT * (CIN / 4);
+  constexpr int WIT = (NW + 255) / 256;
+  {
+    f32x4 v[SIT];
+    f32x4 wv[WIT];
+#pragma unroll
+    for (int it = 0; it < SIT; ++it) {
+      const int idx = it * 256 + tid;
+      const int q = idx % (CIN / 4);
+      const int pix = idx / (CIN / 4);
+      const int r = pix / AW, cc = pix - r * AW;
+      const int gh = h0 - 1 + r, gw = cc - 1;
+      v[it] = (idx < na && gh >= 0 && gh < H && gw >= 0 && gw < W)
+                  ? *reinterpret_cast<const f32x4*>(X + ((long long)gh * W + gw) * a.ldx + 4 * q)
+                  : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int it = 0; it < WIT; ++it) {
+      const int idx = it * 256 + tid;
+      const int q = idx % (CIN / 4);
+      const int tn = idx / (CIN / 4);  // tap * NOUT + n
+      const int tap = tn / NOUT, n = tn % NOUT;
+      if (NW % 256 == 0 || idx < NW)
+        wv[it] = *reinterpret_cast<const f32x4*>(a.w + (long long)tap * a.w_ts + (long long)n * a.ldw + 4 * q);
+    }
+#pragma unroll
+    for (int it = 0; it < SIT; ++it) {
+      const int idx = it * 256 + tid;
+      if (idx < na) *reinterpret_cast<f32x4*>(As + (size_t)(idx / (CIN / 4)) * CP + 4 * (idx % (CIN / 4))) = v[it];
+    }
+#pragma unroll
+    for (int it = 0; it < WIT; ++it) {
+      const int idx = it * 256 + tid;
+      if (NW % 256 == 0 || idx < NW)
+        *reinterpret_cast<f32x4*>(Bs + (size_t)(idx / (CIN / 4)) * CP + 4 * (idx % (CIN / 4))) = wv[it];
+    }
   }
   __syncthreads();
   // ---- MFMA main loop: 9 taps x CG channel groups x TPW pixel fragments x NT output fragments x 4
@@ -127,7 +151,7 @@ hipError_t launch_small(const ConvArgs& a, hipStream_t s) {
   const int W = a.W_out;
   const int RH = PIX / W;
   const size_t lds = ((size_t)(RH + 2) * (W + 2) * (CIN + 4) + (size_t)9 * NOUT * (CIN + 4)) * sizeof(float);
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (lds > 160 * 1024 || (long long)(RH + 2) * (W + 2) * (CIN / 4) > (long long)SIT * 256) return hipErrorInvalidValue;
   auto kern = k_conv2d_small<CIN, NOUT, PIX>;
   static size_t lds_set = 64 * 1024;  // per instantiation: raise the dynamic-LDS limit once, not per launch
   if (lds > lds_set) {
@@ -148,6 +172,7 @@ bool conv2d_small_fits(const ConvArgs& a) {
   if (!shape) return false;
   const int pix = a.C_in == 16 ? 512 : 256;
   if (a.W_out < 16 || pix % a.W_out) return false;
+  if ((long long)(pix / a.W_out + 2) * (a.W_out + 2) * (a.C_in / 4) > (long long)SIT * 256) return false;
   const bool epi = a.out_map == OUT_ROWS && a.acc_mode == ACC_STORE && !a.mask && a.pre_act == ACT_NONE &&
                    !a.pre_mask && a.batch_inner == 1 && !a.b_kn && a.stride == 1 &&
                    (a.res_mode == RES_NONE || a.res_mode == RES_ADD_POST) &&
