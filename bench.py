@@ -14,7 +14,9 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
@@ -50,6 +52,9 @@ def parse():
     ap.add_argument("--streams", type=int, default=16, help="c5: concurrent streams")
     ap.add_argument("--batch", type=int, default=8, help="c4: 30 s utterances per batched pipeline pass")
     ap.add_argument("--c4-utterances", type=int, default=512, help="c4: job size (BASELINE configs[3]: 512)")
+    ap.add_argument("--selftest-launch", action="store_true",
+                    help="exercise the --gpus N self-launch and the collectives on the CPU (RVCX_DIST_BACKEND=gloo): "
+                         "every rank runs a tiny host loop instead of the device pipeline; no GPU is touched")
     ap.add_argument("--roofline-pass", choices=["inline", "after"], default="after",
                     help="inline: HIP events around every conv launch of the timed steps; after: the timed steps "
                          "run without events and an identical K-step pass right after carries them")
@@ -169,6 +174,7 @@ def bench_c3(args, eng, dev, dist, rank, world):
     f0 = torch.as_tensor(synthetic.f0_walk(B, T, seed=3), dtype=torch.float32, device=dev)
     sid = torch.zeros(B, dtype=torch.int32, device=dev)
     el = _timed(lambda i: eng.dec_only(z, f0, sid, seed=i), args, dev, dist)
+    eng.check_device_status()
     # roofline: an identical K-step pass right after the timed one carries the per-conv events (they are not
     # in the timed region)
     eng.profile_read()
@@ -281,6 +287,7 @@ def bench_c5(args, eng, dev, dist, rank, world):
         lat.append(time.perf_counter() - t0)
 
     el = _timed(step, args, dev, dist)
+    eng.check_device_status()
     lat = np.array(lat[args.warmup:]) * 1e3
     hop_sec = block / 48000.0
     tot = reduce_throughput(dist, args.steps * S * hop_sec, el, device=dev)
@@ -295,11 +302,76 @@ def bench_c5(args, eng, dev, dist, rank, world):
                            "p99": round(float(np.percentile(lat, 99)), 3), "budget": round(hop_sec * 1e3, 1)}}
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def self_launch(n: int) -> int:
+    """`--gpus N` without an external launcher: start N fresh worker processes of this script, one per GPU, each
+    with RANK = LOCAL_RANK = r, WORLD_SIZE = N and a 127.0.0.1 rendezvous, and wait for them (the reference's
+    pattern: one process per device over files[i::len(devices)], rvc/train/extract/extract.py:101-117, :150-170).
+    This process never touches the GPU (it only starts children; nothing is exec'd). Rank 0's stdout carries the
+    JSON line. A worker that fails takes the others down (a rank left waiting at a barrier would hang). Returns
+    the first non-zero exit code, else 0."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.2)
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.terminate()
+    return rc
+
+
+def selftest_launch(args, rank, world):
+    """--selftest-launch: the N-rank plumbing of main() (rendezvous, barrier-bracketed timing, SUM/MAX reduction,
+    rank-0 JSON) with a host loop standing in for the device step."""
+    import torch.distributed as dist
+
+    from rvcx.sharding import gather_records, reduce_throughput
+
+    dist.init_process_group(os.environ.get("RVCX_DIST_BACKEND", "gloo"))
+    x = torch.ones(64, 64)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        x = x @ x / 64.0
+    dist.barrier()
+    tot = reduce_throughput(dist, float(args.steps), time.perf_counter() - t0)
+    pids = gather_records(dist, [(rank, os.getpid(), int(os.environ.get("LOCAL_RANK", "-1")))])
+    if rank == 0:
+        print(json.dumps({"metric": "launcher self-test (host loop, no GPU)", "value": round(tot["value"], 3),
+                          "unit": "steps/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ranks": [list(p) for p in pids], "backend": dist.get_backend()}))
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.selftest_launch:
+        return selftest_launch(args, rank, world)
     # one process per GPU; ranks beyond the visible GPUs wrap around (rehearsing N > 1 on a 1-GPU box
     # with RVCX_DIST_BACKEND=gloo) -- device_count() does not initialise the GPU
     local = local % max(1, torch.cuda.device_count())
@@ -366,6 +438,7 @@ def main():
             step(args.warmup + i)
         eng.profile(False)
     k_ms, k_flops, k_launches = eng.profile_read()
+    eng.check_device_status()  # a device-side fault flag (BiGRU hand-off) voids the run
     from rvcx.sharding import reduce_throughput
 
     audio_sec = n / SR_IN

@@ -213,11 +213,13 @@ int rvcx_pipeline_ex(rvcx_ctx* ctx, const double* d_audio, int64_t n, const rvcx
 /* Batched offline conversion (config C4): B equal-length utterances (each n + 160 <= t_max, i.e. one chunk),
  * d_audio row b at d_audio + b*lda (fp64 @16 kHz), sids host [B]. Every stage runs once for the whole batch
  * (batched RMVPE, HuBERT and Synthesizer.infer); row b of d_out (stride ldo) receives Pipeline.pipeline's
- * output for utterance b, n_out samples. Noise when injected: d_eps_z [B][inter][T], d_eps_src [B][T*upp]. */
+ * output for utterance b, n_out samples. Noise when injected: d_eps_z [B][inter][T], d_eps_src [B][T*upp].
+ * Optional outputs: d_f0 [B][F] the adjusted f0 of each row (as rvcx_pipeline_ex's d_f0), d_hidden [B][F][360] the
+ * RMVPE salience each row's f0 was decoded from (RMVPE f0 method only), F = 1 + (n + 2 t_pad)/160. */
 int rvcx_pipeline_batch(rvcx_ctx* ctx, const double* d_audio, int64_t n, int64_t lda, int B,
                         const rvcx_pipeline_opts* opts, const int32_t* sids, const float* d_eps_z,
                         const float* d_eps_src, uint64_t seed, float* d_out, int64_t ldo, int64_t* n_out,
-                        void* stream);
+                        double* d_f0, float* d_hidden, void* stream);
 
 /* Single-chunk shorthand of rvcx_pipeline_ex (t_max = 0, defaults otherwise). */
 int rvcx_pipeline(rvcx_ctx* ctx, const double* d_audio, int64_t n, int sid, double semitones, float protect,

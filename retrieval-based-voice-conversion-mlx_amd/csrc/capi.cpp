@@ -185,7 +185,7 @@ void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double
   a.wsb = stat && ((a.force_cfg >= 20 && !two_d) || (a.force_cfg < 0 && conv_wsb_route(a, two_d))) ? 1 : 0;
   const long long need = conv_plan_splitk(a, two_d);
   if (a.wsb) {
-    a.wsplit = c.wsplit_for(a, s);
+    if (!a.wsplit) a.wsplit = c.wsplit_for(a, s);  // a caller-built image (rvcx_conv1d) is used as given
     a.wsplit_npad = conv_wsplit_npad(a.N);
   }
   // split-K slabs are per stream: the aux stream's convs run concurrently with the caller's
@@ -596,6 +596,11 @@ int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const floa
       a.w_static = 1;
       a.force_cfg = N <= 32 ? 20 : (N <= 64 ? 21 : 22);
       a.no_splitk = 1;
+      // a fresh split image every call, never the address-keyed cache: the caller may reuse d_w (or torch's
+      // allocator may hand the address back) with new weights of the same shape
+      void* img = ctx->buf<char>("conv.test.wsplit", (size_t)conv_wsplit_bytes(a), static_cast<hipStream_t>(stream));
+      check(conv_wsplit_build(a, img, static_cast<hipStream_t>(stream)), "conv_wsplit_build");
+      a.wsplit = img;
     }
     launch_conv(*ctx, a, false, static_cast<hipStream_t>(stream), -1.0);
   });
@@ -808,14 +813,16 @@ int rvcx_rt_process(rvcx_ctx* ctx, rvcx_rt* rt, const float* d_in, const int32_t
 int rvcx_pipeline_batch(rvcx_ctx* ctx, const double* d_audio, int64_t n, int64_t lda, int B,
                         const rvcx_pipeline_opts* opts, const int32_t* sids, const float* d_eps_z,
                         const float* d_eps_src, uint64_t seed, float* d_out, int64_t ldo, int64_t* n_out,
-                        void* stream) {
+                        double* d_f0, float* d_hidden, void* stream) {
   return guard(ctx, [&] {
     if (!ctx->ready[0] || !ctx->ready[1] || !ctx->ready[2]) throw Error(RVCX_E_STATE, "models not finalized");
     if (!d_audio || !opts || !sids || !d_out || n <= 0 || B < 1 || lda < n)
       throw Error(RVCX_E_INVALID, "rvcx_pipeline_batch: bad arguments");
     set_device(ctx);
+    if (d_hidden && (opts->f0_method != 0 || !ctx->scfg.f0))
+      throw Error(RVCX_E_INVALID, "rvcx_pipeline_batch: d_hidden needs the RMVPE f0 method and a pitch-guided model");
     const int64_t no = pipeline_forward_batch(*ctx, d_audio, n, lda, B, *opts, sids, d_eps_z, d_eps_src, seed, d_out,
-                                              ldo, static_cast<hipStream_t>(stream));
+                                              ldo, d_f0, d_hidden, static_cast<hipStream_t>(stream));
     if (n_out) *n_out = no;
   });
 }

@@ -244,7 +244,7 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
                             double* f0_out, hipStream_t s);
 int64_t pipeline_forward_batch(Ctx& c, const double* audio, int64_t n, int64_t lda, int B, const rvcx_pipeline_opts& o,
                                const int32_t* sids, const float* eps_z, const float* eps_src, uint64_t seed,
-                               float* out, int64_t ldo, hipStream_t s);
+                               float* out, int64_t ldo, double* f0_out, float* hidden_out, hipStream_t s);
 rvcx_pipeline_opts default_pipeline_opts();
 int proposed_key(const std::vector<double>& f0, double threshold);
 int64_t hubert_frames(int64_t n);  // HuBERT output rows for n samples (0 when too short)

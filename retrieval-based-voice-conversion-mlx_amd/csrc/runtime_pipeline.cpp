@@ -358,7 +358,7 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
 // every GEMM (B x rows). audio row b at audio + b*lda (fp64); out row b at out + b*ldo, n_out samples each.
 int64_t pipeline_forward_batch(Ctx& c, const double* audio, int64_t n, int64_t lda, int B, const rvcx_pipeline_opts& o,
                                const int32_t* sids, const float* eps_z, const float* eps_src, uint64_t seed,
-                               float* out, int64_t ldo, hipStream_t s) {
+                               float* out, int64_t ldo, double* f0_out, float* hidden_out, hipStream_t s) {
   if (B < 1) throw Error(RVCX_E_INVALID, "pipeline_batch: B < 1");
   if (c.hp_order == 0) throw Error(RVCX_E_STATE, "pipeline: high-pass filter not configured");
   if (o.t_pad < 0 || o.t_pad_tgt < 0 || o.t_pad >= n) throw Error(RVCX_E_INVALID, "pipeline: bad t_pad");
@@ -397,7 +397,7 @@ int64_t pipeline_forward_batch(Ctx& c, const double* audio, int64_t n, int64_t l
     for (int b = 0; b < B; ++b)
       crepe_forward(c, pad32 + (size_t)b * ldm, m, 50.0, 1100.0, 0.1f, f0f, f0 + (size_t)b * F, nullptr, nullptr, s);
   } else {
-    rmvpe_forward_b(c, pad32, m, ldm, B, o.rmvpe_threshold > 0 ? o.rmvpe_threshold : 0.03f, f0, F, nullptr, s);
+    rmvpe_forward_b(c, pad32, m, ldm, B, o.rmvpe_threshold > 0 ? o.rmvpe_threshold : 0.03f, f0, F, hidden_out, s);
   }
   std::vector<double> shift(B, o.pitch);
   if (o.f0_autotune) {
@@ -417,8 +417,10 @@ int64_t pipeline_forward_batch(Ctx& c, const double* audio, int64_t n, int64_t l
   pitchf = c.buf<float>("pb.pitchf", (size_t)B * F, s);
   for (int b = 0; b < B; ++b)
     check(f0_post(f0 + (size_t)b * F, (int)F, std::pow(2.0, shift[b] / 12.0), pitch + (size_t)b * F,
-                  pitchf + (size_t)b * F, nullptr, s),
+                  pitchf + (size_t)b * F, f0_out ? f0_out + (size_t)b * F : nullptr, s),
           "f0_post");
+  } else if (f0_out) {
+    RVCX_HIP(hipMemsetAsync(f0_out, 0, sizeof(double) * (size_t)B * F, s));
   }
   // 3. batched HuBERT, retrieval, x2 upsample + protect (pipeline.py:327-362)
   join_aux(c, s, ax);

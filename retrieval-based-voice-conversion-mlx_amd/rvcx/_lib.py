@@ -136,7 +136,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "rvcx_index_reconstruct_n": (i32, [vp, i64, i64, vp, vp]),
         "rvcx_index_retrieve": (i32, [vp, vp, i64, i32, f64, vp, vp]),
         "rvcx_pipeline_batch": (i32, [vp, vp, i64, i64, i32, P(PipelineOpts), P(ctypes.c_int32), vp, vp, u64, vp, i64,
-                                      P(i64), vp]),
+                                      P(i64), vp, vp, vp]),
         "rvcx_set_highpass_sos": (i32, [vp, vp, i32]),
         "rvcx_highpass_pad": (i32, [vp, vp, i64, i64, vp, vp, vp]),
         "rvcx_hubert_batch": (i32, [vp, vp, i64, i64, i32, i32, vp, i64, P(i64), vp]),

@@ -61,6 +61,12 @@ class Engine:
         a device-side fault flag (e.g. the RMVPE BiGRU hand-off timed out: that call's outputs are invalid)."""
         self._check(self.lib.rvcx_device_status(self.ctx, self.stream()), "device status")
 
+    def host(self, t):
+        """Device tensor -> numpy at the API edge: synchronises, then raises RvcxError if a kernel of this (or an
+        earlier) call raised a device-side fault flag, so a faulted result never leaves as data."""
+        self.check_device_status()
+        return t.cpu().numpy()
+
     def stream(self) -> int:
         return self.torch.cuda.current_stream(self.device).cuda_stream
 
@@ -371,9 +377,10 @@ class Engine:
         return (res, f0) if want_f0 else res
 
     def pipeline_batch(self, audio, opts: "_lib.PipelineOpts", sids=0, eps_z=None, eps_src=None, seed: int = 0,
-                       out=None):
+                       out=None, want_f0: bool = False, want_hidden: bool = False):
         """B equal-length utterances (fp64 [B, n] @16 kHz, each within t_max) through one batched pass.
-        Returns fp32 [B, n_out] on device (row b = Pipeline.pipeline of utterance b)."""
+        Returns fp32 [B, n_out] on device (row b = Pipeline.pipeline of utterance b); with want_f0 / want_hidden
+        also the rows' adjusted f0 fp64 [B, F] / RMVPE salience fp32 [B, F, 360]."""
         t = self.torch
         a = self._dev(audio, t.float64)
         B, n = int(a.shape[0]), int(a.shape[1])
@@ -386,11 +393,17 @@ class Engine:
         no = ctypes.c_int64(0)
         ez = None if eps_z is None else self._dev(eps_z, t.float32)
         es = None if eps_src is None else self._dev(eps_src, t.float32)
+        F = 1 + m // 160
+        f0 = t.empty((B, F), dtype=t.float64, device=self.device) if want_f0 else None
+        hid = t.empty((B, F, 360), dtype=t.float32, device=self.device) if want_hidden else None
         self._check(self.lib.rvcx_pipeline_batch(self.ctx, a.data_ptr(), n, n, B, ctypes.byref(opts), sarr, _ptr(ez),
                                                  _ptr(es), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF),
-                                                 out.data_ptr(), ldo, ctypes.byref(no), self.stream()),
+                                                 out.data_ptr(), ldo, ctypes.byref(no), _ptr(f0), _ptr(hid),
+                                                 self.stream()),
                     "pipeline_batch")
-        return out.reshape(-1)[: B * ldo].reshape(B, ldo)[:, : no.value]
+        y = out.reshape(-1)[: B * ldo].reshape(B, ldo)[:, : no.value]
+        extra = [v for v, w in ((f0, want_f0), (hid, want_hidden)) if w]
+        return (y, *extra) if extra else y
 
     def f0_autotune(self, f0, strength: float = 1.0, skip_unvoiced: bool = False):
         """Autotune.autotune_f0 on device; returns a new fp64 tensor."""

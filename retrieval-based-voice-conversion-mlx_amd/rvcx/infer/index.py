@@ -50,17 +50,17 @@ class IndexIVFFlat:
         """-> (D float32 [n, k], I int64 [n, k]) like faiss Index.search."""
         self._bound()
         d, i = self.engine.index_search(np.ascontiguousarray(x, dtype=np.float32), int(k))
-        return d.cpu().numpy(), i.cpu().numpy()
+        return self.engine.host(d), self.engine.host(i)
 
     def reconstruct_n(self, i0: int, ni: int) -> np.ndarray:
         self._bound()
-        return self.engine.index_reconstruct_n(i0, ni).cpu().numpy()
+        return self.engine.host(self.engine.index_reconstruct_n(i0, ni))
 
     def retrieve(self, feats, index_rate: float) -> np.ndarray:
         """Pipeline._retrieve_speaker_embeddings (pipeline.py:378-388) for feats [L, d] (or [1, L, d])."""
         self._bound()
         f = np.asarray(feats, dtype=np.float32)
-        out = self.engine.index_retrieve(f.reshape(-1, f.shape[-1]), index_rate).cpu().numpy()
+        out = self.engine.host(self.engine.index_retrieve(f.reshape(-1, f.shape[-1]), index_rate))
         return out.reshape(f.shape)
 
 

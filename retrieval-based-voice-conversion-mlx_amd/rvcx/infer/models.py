@@ -21,6 +21,19 @@ import numpy as np
 from ..engine import Engine
 
 
+def _fingerprint(state) -> str:
+    """Content hash of a weight dict (a reload key that cannot collide the way id() of a freed dict can)."""
+    import hashlib
+
+    h = hashlib.sha1()
+    for k in sorted(state):
+        a = np.ascontiguousarray(_np(state[k]), dtype=np.float32)
+        h.update(k.encode())
+        h.update(str(a.shape).encode())
+        h.update(a.tobytes())
+    return h.hexdigest()
+
+
 def _np(x):
     if hasattr(x, "detach"):
         return x.detach().cpu().numpy()
@@ -37,7 +50,7 @@ class HubertModel:
     def __call__(self, audio):
         a = _np(audio).reshape(-1)
         feats = self.engine.hubert(a, self.version)
-        return feats.unsqueeze(0).cpu().numpy()
+        return self.engine.host(feats.unsqueeze(0))
 
 
 class RMVPE0Predictor:
@@ -48,11 +61,11 @@ class RMVPE0Predictor:
 
     def infer_from_audio(self, audio, thred: float = 0.03):
         f0 = self.engine.rmvpe(_np(audio).reshape(-1), thred)
-        return f0.cpu().numpy()
+        return self.engine.host(f0)
 
     def infer_from_audio_with_hidden(self, audio, thred: float = 0.03):
         f0, hidden = self.engine.rmvpe(_np(audio).reshape(-1), thred, want_hidden=True)
-        return f0.cpu().numpy(), hidden.cpu().numpy()
+        return self.engine.host(f0), self.engine.host(hidden)
 
 
 class Synthesizer:
@@ -76,8 +89,8 @@ class Synthesizer:
                                              eps_src=eps_src, seed=seed, want_latents=True)
         lengths = _np(phone_lengths).reshape(B)
         x_mask = (np.arange(T)[None, :] < lengths[:, None]).astype(np.float32)[:, None, :]
-        o = out.cpu().numpy()[:, None, :]
-        return o, x_mask, (z.transpose(1, 2).cpu().numpy(), zp.transpose(1, 2).cpu().numpy(), None, None)
+        o = self.engine.host(out)[:, None, :]
+        return o, x_mask, (self.engine.host(z.transpose(1, 2)), self.engine.host(zp.transpose(1, 2)), None, None)
 
 
 class CREPE:
@@ -93,7 +106,7 @@ class CREPE:
             raise TypeError("CREPE needs the rvcx Engine it runs on (engine=...)")
         self.model_type = model
         self.engine = engine
-        key = ("crepe", model, weights_path) if state is None else ("crepe", model, "state", id(state))
+        key = ("crepe", model, weights_path) if state is None else ("crepe", model, "state", _fingerprint(state))
         if engine.loaded.get("crepe") != key:
             if state is None:
                 from ..weights import load_crepe_weights
@@ -108,8 +121,8 @@ class CREPE:
         f0, per = self.engine.crepe(_np(audio).reshape(-1).astype(np.float32), f0_min, f0_max, threshold,
                                     want_periodicity=True)
         if return_periodicity:
-            return f0.cpu().numpy(), per.cpu().numpy()
-        return f0.cpu().numpy()
+            return self.engine.host(f0), self.engine.host(per)
+        return self.engine.host(f0)
 
 
 class FCPE:
@@ -120,7 +133,7 @@ class FCPE:
         self.engine = engine
 
     def get_f0(self, audio, f0_min: float = 50.0, f0_max: float = 1100.0, threshold: float = 0.006, **kw):
-        return self.engine.rmvpe(_np(audio).reshape(-1).astype(np.float32), threshold * 5).cpu().numpy()
+        return self.engine.host(self.engine.rmvpe(_np(audio).reshape(-1).astype(np.float32), threshold * 5))
 
 
 class PitchExtractor:

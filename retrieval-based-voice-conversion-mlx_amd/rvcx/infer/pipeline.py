@@ -39,9 +39,11 @@ class Config:
 
 class PipelineRVCX:
     # pipeline_mlx.py:82 / pitch_extractors.py:44 minus the pyworld CPU methods (dio, pm, harvest). "crepe" and
-    # "crepe-tiny" run CREPE as rvc_mlx/lib/mlx/crepe.py defines it (weighted-argmax decode; the rvc/ path's
-    # torchcrepe viterbi decoder is not reproduced); "fcpe" is the MLX stub's RMVPE with threshold 0.006 x 5
-    # (rvc_mlx/lib/mlx/fcpe.py:129-132) and needs semantics="mlx" (rvc/'s torchfcpe model is not available).
+    # "crepe-tiny" run CREPE as rvc_mlx/lib/mlx/crepe.py defines it (reflect padding, biased std, weighted-argmax
+    # decode) and therefore need semantics="mlx": the rvc/ path calls torchcrepe.predict (zero padding, unbiased
+    # std, viterbi decode; rvc/lib/predictors/f0.py:40-53), which is not reproduced. "fcpe" is the MLX stub's RMVPE
+    # with threshold 0.006 x 5 (rvc_mlx/lib/mlx/fcpe.py:129-132) and needs semantics="mlx" too (rvc/'s torchfcpe
+    # model is not available).
     SUPPORTED_F0_METHODS = ("rmvpe", "crepe", "crepe-tiny", "fcpe")
 
     def __init__(self, tgt_sr, config, hubert_model: Optional[HubertModel] = None,
@@ -82,6 +84,10 @@ class PipelineRVCX:
         if m == "fcpe" and self.semantics != "mlx":
             raise ValueError("f0_method 'fcpe' needs torchfcpe's model on the rvc/ path (rvc/lib/predictors/f0.py:60-89); "
                              "semantics='mlx' runs the MLX port's FCPE (its RMVPE fallback)")
+        if m in ("crepe", "crepe-tiny") and self.semantics != "mlx":
+            raise ValueError(f"f0_method {m!r} on the rvc/ path is torchcrepe.predict with its viterbi decoder "
+                             "(rvc/lib/predictors/f0.py:40-53), which this path does not reproduce; semantics='mlx' "
+                             "runs the MLX port's CREPE (rvc_mlx/lib/mlx/crepe.py: weighted-argmax decode)")
 
     def _crepe(self, eng, f0_method):
         """Load the CREPE weights f0_method names into the engine (once per model kind)."""
@@ -150,9 +156,9 @@ class PipelineRVCX:
             if self.semantics == "rvc":
                 shift = 0.0
         elif proposed_pitch and self.semantics == "rvc":
-            shift += proposed_key(f0.cpu().numpy(), proposed_pitch_threshold)
+            shift += proposed_key(eng.host(f0), proposed_pitch_threshold)
         coarse, _, fs = eng.f0_post(f0, shift)
-        return coarse.cpu().numpy().astype(np.int64), fs.cpu().numpy()
+        return eng.host(coarse).astype(np.int64), eng.host(fs)
 
     def voice_conversion(self, model, net_g, sid, audio0, pitch, pitchf, index=None, big_npy=None, index_rate=0.0,
                          version="v2", protect=0.33, eps_z=None, eps_src=None, seed: int = 0):
@@ -171,7 +177,7 @@ class PipelineRVCX:
                                    None if pitchf is None else _np(pitchf).reshape(-1), int(_np(sid).reshape(-1)[0]),
                                    float(protect),
                                    eps_z=eps_z, eps_src=eps_src, seed=seed, index_rate=rate)
-        return out.cpu().numpy()
+        return eng.host(out)
 
     def pipeline(self, model, net_g, sid, audio, pitch=0, f0_method="rmvpe", file_index=None, index_rate=0.0,
                  pitch_guidance=True, volume_envelope=1.0, version="v2", protect=0.33, f0_autotune=False,
@@ -203,7 +209,7 @@ class PipelineRVCX:
         y, f0 = eng.pipeline_ex(np.asarray(audio, dtype=np.float64).reshape(-1), opts, eps_z=eps_z,
                                 eps_src=eps_src, seed=seed, want_f0=True)
         self.last_f0 = f0
-        return y.cpu().numpy()
+        return eng.host(y)
 
 
 PipelineMLX = PipelineRVCX

@@ -129,7 +129,8 @@ class VoiceChanger:
                             proposed_pitch, proposed_pitch_threshold)
         out, vol = self.group.process(np.asarray(audio_input, dtype=np.float32)[None], o, eps_z, eps_src, self.seed)
         self.seed += 1
-        return out[0].cpu().numpy(), float(vol[0].item())
+        out0 = self.group.engine.host(out[0])
+        return out0, float(vol[0].item())
 
     def on_request(self, audio_input: np.ndarray, f0_up_key=0, index_rate=0.5, protect=0.5, volume_envelope=1,
                    f0_autotune=False, f0_autotune_strength=1, proposed_pitch=False, proposed_pitch_threshold=155.0):

@@ -162,3 +162,27 @@ def test_gru_handoff_timeout_is_reported(engine, monkeypatch):
     f0 = engine.rmvpe(audio)
     engine.check_device_status()
     assert bool(torch.isfinite(f0).all())
+
+
+def test_gru_handoff_timeout_raises_at_the_api_edge(engine, monkeypatch):
+    """The drop-in API surfaces a device fault from the call that produced it: with the
+    BiGRU hand-off forced to time out, RMVPE0Predictor.infer_from_audio and PipelineMLX.pipeline raise RvcxError
+    themselves instead of returning garbage, and the next call is clean."""
+    from rvcx import _lib, synthetic
+    from rvcx.infer import Config, HubertModel, PipelineMLX, RMVPE0Predictor, Synthesizer
+
+    audio = synthetic.speech_like(24000, seed=4)
+    hub, rm, net_g = HubertModel(engine), RMVPE0Predictor(engine), Synthesizer(engine)
+    pipe = PipelineMLX(48000, Config(), hub, rm)
+    engine.check_device_status()
+    monkeypatch.setenv("RVCX_GRU_SPIN_LIMIT", "0")
+    with pytest.raises(_lib.RvcxError) as e:
+        rm.infer_from_audio(audio.astype(np.float32))
+    assert e.value.code == -3
+    with pytest.raises(_lib.RvcxError) as e:
+        pipe.pipeline(hub, net_g, 0, audio, 0, "rmvpe", None, 0.0, True, 1.0, "v2", 0.33, False, 1.0, False, 155.0)
+    assert e.value.code == -3
+    monkeypatch.delenv("RVCX_GRU_SPIN_LIMIT")
+    engine.check_device_status()
+    y = pipe.pipeline(hub, net_g, 0, audio, 0, "rmvpe", None, 0.0, True, 1.0, "v2", 0.33, False, 1.0, False, 155.0)
+    assert np.isfinite(y).all()
