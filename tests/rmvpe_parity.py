@@ -8,14 +8,16 @@ real error:
 
   1. salience error  err = max |device - reference| over the exact fp32 values the reference decoded (argmax
      +- 4 bins and the runner-up), raised to the lower bound the fp16 copy of the whole matrix implies; it must
-     itself be small (<= 1e-4 absolute, salience in [0, 1]);
+     itself be within what fp32 arithmetic explains: 3x the reference's own fp32-vs-fp64 salience gap on the clip
+     (8.7e-5 .. 1.5e-4, tests/golden/add_salience_noise.py);
   2. near-tied frames  top-1 - top-2 <= 2 err (the argmax may flip) or |top-1 - 0.03| <= err (voicing may flip);
   3. every frame whose device argmax differs from the reference's must be near-tied;
   4. every other frame's f0 must agree within the bound the salience error implies for decode's weighted
      average (sum_j |c_j - avg| err / (sum_j s_j - 9 err), x1.5), and its voicing must agree.
 
-The waveform is then compared sample by sample only before the first flipped frame (minus the generator's
-receptive field), and by spectrogram correlation over the whole output.
+The waveform is compared sample by sample where f0 cannot move it: the synthesis path fed the reference's own
+pitch track (the strict gate), and the pipeline's output against that path fed the device's own f0 (consistency);
+the end-to-end output against the reference by spectrogram correlation.
 """
 from __future__ import annotations
 
@@ -45,10 +47,11 @@ def _cents(f):
     return out
 
 
-def check_rmvpe(dev_f0, dev_hidden, ref, ref_f0, thred=THRED, max_err=1e-4):
+def check_rmvpe(dev_f0, dev_hidden, ref, ref_f0, thred=THRED, max_err=None):
     """Principled f0 parity (module docstring). ref: mapping with sal_* (and optionally hidden16). The salience
-    error itself must stay <= max_err (absolute, salience in [0, 1]): beyond that it is a real error, and the
-    near-tie set it would open up is meaningless.
+    error itself must stay <= max_err (absolute, salience in [0, 1]); default 3 x the fixture's sal_fp32_noise
+    (how far the reference's own fp32 salience sits from fp64 on this clip, tests/golden/add_salience_noise.py):
+    beyond that it is a real error, and the near-tie set it would open up is meaningless.
     Returns dict(err, n_near, flips (frame indices), first_flip (or None))."""
     F = len(ref_f0)
     h = np.asarray(dev_hidden, np.float32)[:F]
@@ -66,7 +69,14 @@ def check_rmvpe(dev_f0, dev_hidden, ref, ref_f0, thred=THRED, max_err=1e-4):
         d = np.abs(h - h16.astype(np.float32))
         assert float(d.max()) <= 1e-3 * float(np.abs(h16).max()), float(d.max())
         err = max(err, float((d - np.spacing(h16).astype(np.float32) / 2).max()))
-    assert err <= max_err, f"salience error {err:.3e} > {max_err:.1e}"
+    if max_err is None:
+        max_err = 3.0 * float(ref["sal_fp32_noise"])
+    if err > max_err:
+        ew = np.abs(win - ref["sal_win"]).max(1)
+        blk = [float(ew[i:i + 256].max()) for i in range(0, F, 256)]
+        raise AssertionError(f"salience error {err:.3e} > {max_err:.1e}: window err max {ew.max():.3e} at frame "
+                             f"{int(ew.argmax())}, p50 {np.median(ew):.2e}, p99 {np.percentile(ew, 99):.2e}; per 256 "
+                             f"frames {['%.1e' % v for v in blk]}")
     near_arg = np.asarray(ref["sal_margin"]) <= 2 * err + 1e-7
     near_thr = np.abs(np.asarray(ref["sal_thr_margin"])) <= err + 1e-7
     dev_arg = np.argmax(h, axis=1)
@@ -96,24 +106,9 @@ def rel_err(a, b):
     return float(np.abs(a - b).max() / (np.abs(b).max() + 1e-12))
 
 
-def check_waveform(out, ref, first_flip, t_pad_tgt=48000, upp=480, rf_frames=8, tol=2e-3, corr=0.999):
-    """Whole output: spectrogram correlation >= corr. Samples before the first flipped frame (minus rf_frames of
-    generator receptive field): rel err <= tol of the reference peak. When a flip lies inside the clip and both
-    outputs were peak-normalised to 0.99 (pipeline.py:550-552), the prefix is compared with the device's
-    normalisation gain matched to the reference's (the flip may move the global peak)."""
-    from oracle.metrics import spectrogram_correlation
-
-    out, ref = np.asarray(out, np.float64), np.asarray(ref, np.float64)
-    assert out.shape == ref.shape, (out.shape, ref.shape)
-    c = spectrogram_correlation(out.astype(np.float32), ref.astype(np.float32))
-    assert c >= corr, c
-    end = len(ref) if first_flip is None else max(0, (first_flip - rf_frames) * upp - t_pad_tgt)
-    if end == 0:
-        return {"spec_corr": c, "prefix": 0, "rel": None}
-    a, b = out[:end], ref[:end]
-    if first_flip is not None and abs(np.abs(out).max() - 0.99) < 1e-6 and abs(np.abs(ref).max() - 0.99) < 1e-6:
-        g = float((a * b).sum() / max((a * a).sum(), 1e-30))
-        a = a * g
-    r = float(np.abs(a - b).max() / (np.abs(ref).max() + 1e-12))
-    assert r <= tol, (r, end)
-    return {"spec_corr": c, "prefix": end, "rel": r}
+def trim_normalize(vc, t_pad_tgt=48000):
+    """voice_conversion output -> Pipeline.pipeline's: trim t_pad_tgt per side, peak-normalise (pipeline.py:494,
+    :550-552)."""
+    y = np.asarray(vc, np.float32)[t_pad_tgt:-t_pad_tgt]
+    mx = np.abs(y).max() / 0.99
+    return y / mx if mx > 1 else y

@@ -9,9 +9,10 @@ Tolerances (fp32 throughout, as the reference):
     argmax that differs from the reference's only on frames whose reference top-1/top-2 margin is within twice
     the measured salience error; every other frame's f0 within the cents bound that error implies
     (tests/rmvpe_parity.py) -- a summation-order change can only fail this through a real salience error;
-  * the pipeline's own f0 equals the standalone RMVPE call's on the same padded input (bitwise);
-  * whole pipeline: spectrogram correlation >= 0.999; samples before the first flipped frame within 2e-3 of
-    the peak (none flipped: the whole clip);
+  * the pipeline's own f0 equals the standalone RMVPE call's on the same padded input (bitwise), and its output
+    equals voice_conversion fed that f0, trimmed and normalised (rel <= 1e-6: the same kernels);
+  * whole pipeline vs the reference: spectrogram correlation >= 0.999 (a sample-level bar here would measure the
+    NSF phase drift of fp32-noise f0 differences, not the kernels);
   * voice_conversion fed the reference's pitch track (the strict sample-level gate): rel <= 1e-4;
   * HuBERT rel <= 1e-3 (fixture in fp16); the coarse pitch of the reference's own f0 bit-exact.
 """
@@ -19,7 +20,7 @@ import numpy as np
 import pytest
 
 from conftest import c2_audio, fixture_noise, golden
-from rmvpe_parity import check_rmvpe, check_waveform, rel_err
+from rmvpe_parity import check_rmvpe, rel_err, trim_normalize
 
 pytestmark = pytest.mark.gpu
 
@@ -28,6 +29,8 @@ CLIPS = ["ios", "synth"]
 
 @pytest.mark.parametrize("clip", CLIPS)
 def test_c2_pipeline_vs_reference(engine, clip):
+    from oracle.metrics import spectrogram_correlation
+
     g = golden(f"pipeline_c2_{clip}.npz")
     ez, es = fixture_noise(g)
     engine.set_pipeline_highpass()
@@ -40,10 +43,17 @@ def test_c2_pipeline_vs_reference(engine, clip):
     out, f0p, f0d, hid = (v.cpu().numpy() for v in (out, f0p, f0d, hid))
     np.testing.assert_array_equal(f0p, f0d)
     r = check_rmvpe(f0d, hid, g, g["f0_raw"])
-    w = check_waveform(out, g["out"], r["first_flip"])
-    print(f"\nC2 {clip}: salience err {r['err']:.2e}, {r['n_near']} near-tied frames, flips {list(r['flips'])}, "
-          f"spec corr {w['spec_corr']:.6f}, prefix {w['prefix']} samples rel {w['rel']}")
     assert out.shape == g["out"].shape == (648000,)
+    c = spectrogram_correlation(out, g["out"])
+    assert c >= 0.999
+    p_len = p32.shape[0] // 160
+    coarse, pitchf, _ = engine.f0_post(f0d, 0.0)
+    vc = engine.voice_conversion(p32, coarse[:p_len], pitchf[:p_len], 0, 0.33, eps_z=ez, eps_src=es).cpu().numpy()
+    cons = rel_err(out, trim_normalize(vc))
+    assert cons <= 1e-6, cons
+    print(f"\nC2 {clip}: salience err {r['err']:.2e} (bound {3 * float(g['sal_fp32_noise']):.2e}), {r['n_near']} "
+          f"near-tied frames, flips {list(r['flips'])}, spec corr {c:.6f}, rel to reference {rel_err(out, g['out']):.2e}, "
+          f"pipeline vs staged {cons:.1e}")
 
 
 @pytest.mark.parametrize("clip", CLIPS)
@@ -72,10 +82,7 @@ def test_c2_voice_conversion_on_reference_pitch(engine, clip):
     p_len = x.shape[0] // 160
     vc = engine.voice_conversion(x, g["pitch"][:p_len], g["f0_raw"][:p_len].astype(np.float32), 0, 0.33, eps_z=ez,
                                  eps_src=es).cpu().numpy()
-    vc = vc[48000:-48000]
-    mx = np.abs(vc).max() / 0.99
-    if mx > 1:
-        vc = vc / mx
+    vc = trim_normalize(vc)
     ref = g["out"]
     assert vc.shape == ref.shape
     assert spectrogram_correlation(vc, ref) >= 0.9999
