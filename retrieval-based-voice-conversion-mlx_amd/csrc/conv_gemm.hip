@@ -699,10 +699,13 @@ inline bool small2d_enabled() {
 // RVCX_WCFG_* override). bench_conv on MI355X with the register epilogue (TF/s, vs the LDS-staged split kernel's
 // best tile): C256 k11 174 vs 142, C128 k11 204 vs 160, C128 k7 185 vs 144, C128 k3 124 vs 118, ConvTranspose
 // phases 105 / 124 / 94 vs 95 / 117 / 96; the 32-channel convs lose (C32 k11 95 vs 115).
+// Round 3: the same tiles on v_mfma_f32_16x16x32_bf16 (cfg 24 / 23) hold a higher clock under the power-limited load
+// (bench_conv r03h, same box, 32x32x16 -> 16x16x32 TF/s: C128 k11 198 -> 214, k7 181 -> 194, k3 124 -> 131, C256 k11
+// 171 -> 182, C64 k11 177 -> 190, ConvTranspose phases 108 / 125 / 94 -> 114 / 129 / 99).
 inline int pick_wsb(const ConvArgs& a) {
-  static const int c_narrow = env_cfg("RVCX_WCFG_NARROW", 20);
-  static const int c_mid = env_cfg("RVCX_WCFG_MID", 21);
-  static const int c_wide = env_cfg("RVCX_WCFG_WIDE", 21);
+  static const int c_narrow = env_cfg("RVCX_WCFG_NARROW", 24);
+  static const int c_mid = env_cfg("RVCX_WCFG_MID", 23);
+  static const int c_wide = env_cfg("RVCX_WCFG_WIDE", 23);
   return a.N <= 32 ? c_narrow : (a.N <= 64 ? c_mid : c_wide);
 }
 

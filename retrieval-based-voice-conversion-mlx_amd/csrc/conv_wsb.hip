@@ -22,6 +22,13 @@ namespace {
 
 using namespace splitbf16;
 
+#ifndef WSB_AFRAG_BATCH
+#define WSB_AFRAG_BATCH 0
+#endif
+#ifndef WSB_BPREFETCH_UNCOND
+#define WSB_BPREFETCH_UNCOND 1
+#endif
+
 constexpr int WROW = 3 * PLANE;  // bytes of one (chunk, tap, column) row of split weights in HBM
 constexpr int WSB_HALO = 64;     // max (taps - 1) * dil: the A prefetch registers cover BM + 64 rows
 constexpr int WSB_ROWS_2D = 224;  // 2-D: pixel-window rows the A prefetch registers cover (3x3 windows of 128 px)
@@ -51,8 +58,12 @@ __global__ void k_wsplit(const float* __restrict__ w, int ldw, long long w_ts, i
   }
 }
 
+#ifndef WSB_WAVES_128x64
+#define WSB_WAVES_128x64 3
+#endif
+
 template <int BM, int BN, int WM, int WN, bool TWO_D>
-__global__ __launch_bounds__(CONV_THREADS, 2) void conv_wsb_kernel(const ConvArgs a, const char* __restrict__ wsp,
+__global__ __launch_bounds__(CONV_THREADS, (BM == 128 && BN == 64 && !TWO_D) ? WSB_WAVES_128x64 : 2) void conv_wsb_kernel(const ConvArgs a, const char* __restrict__ wsp,
                                                                    const int Npad, const int nrows_a, const int ntn,
                                                                    const int ksplit, const int rw, const int rh,
                                                                    const int tiles_w) {
@@ -162,14 +173,29 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_wsb_kernel(const ConvArg
   };
   auto compute = [&](int tap, const BFrag& bf) __attribute__((always_inline)) {
     const int toff = (TWO_D ? (tap / a.KW) * aw + (tap % a.KW) : tap * a.dil) * ERS;
+#if WSB_AFRAG_BATCH
+    // every A fragment of the step requested before the first MFMA (one exposed LDS latency per step)
+    bf16x8 af2[2][TM][3];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          af2[s][tm][q] = *reinterpret_cast<const bf16x8*>(As + aoff[tm] + toff + q * PLANE + s * 32);
+#endif
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
+#if WSB_AFRAG_BATCH
+      auto& af = af2[s];
+#else
       bf16x8 af[TM][3];
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
         for (int q = 0; q < 3; ++q)
           af[tm][q] = *reinterpret_cast<const bf16x8*>(As + aoff[tm] + toff + q * PLANE + s * 32);
+#endif
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
@@ -201,7 +227,16 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_wsb_kernel(const ConvArg
     // one (chunk, tap) iteration: prefetch the next iteration's B, MFMAs on this one's, switch chunks after the
     // last tap (every wave done reading the halo -> write the prefetched one -> prefetch the chunk after)
     auto step = [&](int it, const BFrag& cur, BFrag& nxt) __attribute__((always_inline)) {
+#if WSB_BPREFETCH_UNCOND
+      // unconditional (the last step reloads its own fragments): with a conditional load the waitcnt pass merges
+      // the load-issued and load-skipped paths and waits for the prefetch itself inside this step; the scheduling
+      // barrier keeps the loads at the top of the step (the machine scheduler otherwise sinks them below the MFMAs,
+      // so the next step waits out their whole latency)
+      load_b(it + 1 < it1 ? it + 1 : it, nxt);
+      __builtin_amdgcn_sched_barrier(0);
+#else
       if (it + 1 < it1) load_b(it + 1, nxt);
+#endif
       compute(tap, cur);
       if (++tap == taps) {
         tap = 0;
@@ -221,6 +256,222 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_wsb_kernel(const ConvArg
 
   conv_store_tile<TM, TN, WM, WN, TWO_D>(a, TilePos{m0, h0, w0, rw, rh, n0, b, 0, b, zsplit, ksplit}, acc,
                                          reinterpret_cast<float*>(smem_w));
+}
+
+// ---- the same contraction on v_mfma_f32_16x16x32_bf16 (1-D only). One MFMA covers a whole 32-channel chunk (lane
+// group g = lane / 16 holds channels 8g..8g+7 of its row / column), so a (chunk, tap) step is, per wave of TM16 x TN16
+// 16x16 tiles, 3*TM16 LDS reads, 3*TN16 global B loads and 6*TM16*TN16 MFMAs of 16 cycles: the same bytes and MFMA
+// cycles per step as the 32x32x16 form at the same wave tile. The chip sustains a higher clock on this shape under
+// power-limited load (MI355X_MICROARCH.md "DVFS give-back" item 7), which is the point.
+// C layout of a 16x16 tile: lane l holds column l % 16, rows 4 (l / 16) + r, r = 0..3.
+template <int TM16, int TN16, int WM, int WN>
+__device__ __forceinline__ void conv_store_tile16(const ConvArgs& a, const TilePos& p, f32x4 (&acc)[TM16][TN16]) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int lc = lane & 15, lg = lane >> 4;
+  const float* bias = a.bias ? a.bias + (long long)p.b * a.bias_bs : nullptr;
+  const float* R = a.res ? a.res + (long long)p.b * a.res_bs : nullptr;
+  const float* MK = a.mask ? a.mask + (long long)p.b * a.mask_bs : nullptr;
+  float* Y = a.y + (long long)p.b * a.y_bs;
+  const bool need_r = R && a.res_mode != RES_NONE;
+  const bool need_d = a.acc_mode != ACC_STORE;
+#pragma unroll
+  for (int tn = 0; tn < TN16; ++tn) {
+    const int n = p.n0 + wn * TN16 * 16 + tn * 16 + lc;
+    const bool n_ok = n < a.N;
+    const float bn = (bias && n_ok) ? bias[n] : 0.f;
+#pragma unroll
+    for (int tm = 0; tm < TM16; ++tm) {
+      const int mb = p.m0 + wm * TM16 * 16 + tm * 16 + 4 * lg;
+      if (p.ksplit > 1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (n_ok && mb + r < a.T_out)
+            a.ws[(((long long)p.zb * p.ksplit + p.zsplit) * a.ws_rows + mb + r) * a.N + n] = acc[tm][tn][r];
+        continue;
+      }
+      // gather first (residual / accumulate / mask operands of the lane's 4 outputs), then store
+      float rv[4], dv[4], mv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool ok = n_ok && mb + r < a.T_out;
+        rv[r] = (ok && need_r) ? R[(long long)(mb + r) * a.ldr + n] : 0.f;
+        dv[r] = (ok && need_d) ? Y[(long long)(mb + r) * a.ldy + n] : 0.f;
+        mv[r] = (ok && MK) ? MK[mb + r] : 1.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (!(n_ok && mb + r < a.T_out)) continue;
+        float v = acc[tm][tn][r];
+        if (a.bias) v += bn;
+        if (a.res_mode == RES_ADD_PRE) v = v + rv[r];
+        if (a.alpha != 1.f) v *= a.alpha;
+        v = act_fn(v, a.act, a.slope);
+        if (a.res_mode == RES_ADD_POST) v = v + rv[r];
+        else if (a.res_mode == RES_RSUB_POST) v = rv[r] - v;
+        if (a.acc_mode == ACC_ADD) v = dv[r] + v;
+        else if (a.acc_mode == ACC_ADD_DIV) v = (dv[r] + v) / a.acc_div;
+        if (MK) v *= mv[r];
+        Y[(long long)(mb + r) * a.ldy + n] = v;
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(CONV_THREADS, 3) void conv_wsb16_kernel(const ConvArgs a, const char* __restrict__ wsp,
+                                                                     const int Npad, const int nrows_a, const int ntn,
+                                                                     const int ksplit) {
+  constexpr int NT = CONV_THREADS;
+  constexpr int TM16 = BM / (WM * 16);
+  constexpr int TN16 = BN / (WN * 16);
+  static_assert(WM * WN == 4 && TM16 >= 1 && TN16 >= 1, "4 waves, whole 16x16 sub-tiles");
+  extern __shared__ __attribute__((aligned(16))) char smem_w16[];
+  char* const As = smem_w16;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int lc = lane & 15, lg = lane >> 4;
+  int bx, by, bz;
+  conv_block_coords(ntn, bx, by, bz);
+  const int zsplit = bz % ksplit;
+  const int b = bz / ksplit;
+  const int n0 = by * BN;
+  const int m0 = bx * BM;
+  const float* X = a.x + (long long)b * a.x_bs;
+  const float* PM = a.pre_mask ? a.pre_mask + (long long)b * a.pre_mask_bs : nullptr;
+  const int row0 = m0 - a.pad;
+
+  int aoff[TM16];
+#pragma unroll
+  for (int tm = 0; tm < TM16; ++tm) aoff[tm] = (wm * TM16 * 16 + tm * 16 + lc) * ERS + lg * 16;
+  const char* bp[TN16];
+#pragma unroll
+  for (int tn = 0; tn < TN16; ++tn) bp[tn] = wsp + (size_t)(n0 + wn * TN16 * 16 + tn * 16 + lc) * WROW + lg * 16;
+  const size_t bstep = (size_t)Npad * WROW;
+
+  f32x4 acc[TM16][TN16];
+#pragma unroll
+  for (int tm = 0; tm < TM16; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < TN16; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  constexpr int AP = ((BM + WSB_HALO) * EC4 + NT - 1) / NT;
+  f32x4 apre[AP];
+  float apm[AP];
+  const int arow = store_row(tid / EC4), ac4 = (tid % EC4) << 2;
+  auto load_a_regs = [&](int c0) __attribute__((always_inline)) {
+    const float* src0 = X + c0 + ac4;
+#pragma unroll
+    for (int v = 0; v < AP; ++v) {
+      const int r = v * (NT / EC4) + arow;
+      const long long g = row0 + r;
+      const bool ok = r < nrows_a && g >= 0 && g < a.T_in;
+      apre[v] = ok ? *reinterpret_cast<const f32x4*>(src0 + g * a.ldx) : f32x4{0.f, 0.f, 0.f, 0.f};
+      apm[v] = ok ? (PM ? PM[g] : 1.f) : 0.f;
+    }
+  };
+  auto write_a_regs = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int v = 0; v < AP; ++v) {
+      const int r = v * (NT / EC4) + arow;
+      if (r < nrows_a) {
+        f32x4 val = apre[v];
+        if (a.pre_act != ACT_NONE) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) val[j] = act_fn(val[j], a.pre_act, a.pre_slope);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) val[j] *= apm[v];
+        put_split4(As + r * ERS, ac4, val);
+      }
+    }
+  };
+  typedef bf16x8 BFrag[TN16][3];
+  auto load_b = [&](int it, BFrag& dst) __attribute__((always_inline)) {
+    const size_t o = (size_t)it * bstep;
+#pragma unroll
+    for (int tn = 0; tn < TN16; ++tn)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) dst[tn][q] = *reinterpret_cast<const bf16x8*>(bp[tn] + o + q * PLANE);
+  };
+  auto compute = [&](int tap, const BFrag& bf) __attribute__((always_inline)) {
+    const int toff = tap * a.dil * ERS;
+#pragma unroll
+    for (int tm = 0; tm < TM16; ++tm) {
+      bf16x8 af[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) af[q] = *reinterpret_cast<const bf16x8*>(As + aoff[tm] + toff + q * PLANE);
+#pragma unroll
+      for (int tn = 0; tn < TN16; ++tn) {
+        f32x4 c = acc[tm][tn];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], bf[tn][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[tn][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[tn][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[tn][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[tn][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[tn][0], c, 0, 0, 0);
+        acc[tm][tn] = c;
+      }
+    }
+  };
+
+  const int taps = a.taps, total = (a.C_in / EK) * taps;
+  const int per = (total + ksplit - 1) / ksplit;
+  const int it0 = zsplit * per, it1 = min(total, it0 + per);
+  if (it0 < it1) {
+    BFrag b0, b1;
+    int ch = it0 / taps, tap = it0 - ch * taps;
+    load_a_regs(ch * EK);
+    write_a_regs();
+    if ((ch + 1) * taps < it1) load_a_regs((ch + 1) * EK);
+    load_b(it0, b0);
+    __syncthreads();
+    auto step = [&](int it, const BFrag& cur, BFrag& nxt) __attribute__((always_inline)) {
+      load_b(it + 1 < it1 ? it + 1 : it, nxt);  // unconditional and pinned at the top (see conv_wsb_kernel)
+      __builtin_amdgcn_sched_barrier(0);
+      compute(tap, cur);
+      if (++tap == taps) {
+        tap = 0;
+        if (++ch * taps < it1) {
+          __syncthreads();
+          write_a_regs();
+          if ((ch + 1) * taps < it1) load_a_regs((ch + 1) * EK);
+          __syncthreads();
+        }
+      }
+    };
+    for (int it = it0; it < it1; it += 2) {
+      step(it, b0, b1);
+      if (it + 1 < it1) step(it + 1, b1, b0);
+    }
+  }
+  conv_store_tile16<TM16, TN16, WM, WN>(a, TilePos{m0, 0, 0, 0, 0, n0, b, 0, b, zsplit, ksplit}, acc);
+}
+
+template <int BM, int BN, int WM, int WN>
+hipError_t launch_wsb16(const ConvArgs& a, int ntn_enable, int ksplit, hipStream_t s) {
+  const int nrows_a = BM + (a.taps - 1) * a.dil;
+  const int mtiles = (a.T_out + BM - 1) / BM;
+  const size_t smem = (size_t)nrows_a * ERS;
+  if (a.wsplit_npad % BN != 0 || ksplit < 1 || (ksplit > 1 && !a.ws)) return hipErrorInvalidValue;
+  const int ntiles = (a.N + BN - 1) / BN;
+  const int ntn = ntn_enable ? ntiles : 0;
+  dim3 grid(ntn ? mtiles * ntiles : mtiles, ntn ? 1 : ntiles, a.batch * ksplit);
+  auto kern = conv_wsb16_kernel<BM, BN, WM, WN>;
+  static size_t smem_set = 64 * 1024;
+  if (smem > smem_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return e;
+    smem_set = smem;
+  }
+  hipLaunchKernelGGL(kern, grid, dim3(CONV_THREADS), smem, s, a, static_cast<const char*>(a.wsplit), a.wsplit_npad,
+                     nrows_a, ntn, ksplit);
+  return hipGetLastError();
 }
 
 template <int BM, int BN, int WM, int WN, bool TWO_D>
@@ -285,10 +536,11 @@ hipError_t conv_wsplit_build(const ConvArgs& a, void* out, hipStream_t s) {
   return hipGetLastError();
 }
 
-// cfg 20: 256 x 32 (4 x 1 waves of 64 x 32), 21: 128 x 64 (2 x 2 waves of 64 x 32), 22: 128 x 128 (2 x 2 of 64 x 64)
+// cfg 20: 256 x 32 (4 x 1 waves of 64 x 32), 21: 128 x 64 (2 x 2 waves of 64 x 32), 22: 128 x 128 (2 x 2 of 64 x 64);
+// cfg 23 / 24: the 21 / 20 tiles on v_mfma_f32_16x16x32_bf16 (1-D)
 bool conv_wsb_tile(int cfg, int& BM, int& BN) {
-  static const int t[3][2] = {{256, 32}, {128, 64}, {128, 128}};
-  if (cfg < 20 || cfg > 22) return false;
+  static const int t[5][2] = {{256, 32}, {128, 64}, {128, 128}, {128, 64}, {256, 32}};
+  if (cfg < 20 || cfg > 24) return false;
   BM = t[cfg - 20][0];
   BN = t[cfg - 20][1];
   return true;
@@ -301,6 +553,8 @@ hipError_t conv_wsb_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream
     case 20: return launch_wsb<256, 32, 4, 1, false>(a, ntn_enable, ksplit, s);
     case 21: return launch_wsb<128, 64, 2, 2, false>(a, ntn_enable, ksplit, s);
     case 22: return launch_wsb<128, 128, 2, 2, false>(a, ntn_enable, ksplit, s);
+    case 23: return launch_wsb16<128, 64, 2, 2>(a, ntn_enable, ksplit, s);
+    case 24: return launch_wsb16<256, 32, 4, 1>(a, ntn_enable, ksplit, s);
     default: return hipErrorInvalidValue;
   }
 }
