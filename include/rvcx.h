@@ -325,7 +325,8 @@ int rvcx_set_conv_math(rvcx_ctx* ctx, int mode);
  * The kernel family behind every contraction of the path, exposed for numerics tests; replaces
  * torch.nn.Conv1d.forward as used throughout rvc/lib/algorithm (e.g. residuals.py:34-80). math as above, plus
  * 3 = the split arithmetic on the weight-streamed kernel (weights pre-split in HBM; 1-D stride-1 convs with
- * C_in % 32 == 0 and (taps - 1) * dilation <= 64, else RVCX_E_SHAPE). */
+ * C_in % 32 == 0 and (taps - 1) * dilation <= 64, else RVCX_E_SHAPE), 4 = the split arithmetic on the gather-streamed
+ * kernel (weights pre-split in HBM, A gathered per step, split-K by the size policy; C_in % 32 == 0). */
 int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const float* d_w, const float* d_bias, int N,
                 int taps, int dilation, int pad, int stride, int math, float* d_y, int64_t T_out, void* stream);
 

@@ -37,6 +37,7 @@ int main(int argc, char** argv) {
   CK_(hipMalloc(&b, hb.size() * 4));
   CK_(hipMalloc(&out, (size_t)B * T * 2 * H * 4));
   CK_(hipMalloc(&xchg, gru_xchg_words(B) * 8));
+  CK_(hipMemset(xchg, 0, gru_xchg_words(B) * 8));
   CK_(hipMalloc(&status, 4));
   CK_(hipMemset(status, 0, 4));
   CK_(hipMemcpy(gi, hgi.data(), hgi.size() * 4, hipMemcpyHostToDevice));

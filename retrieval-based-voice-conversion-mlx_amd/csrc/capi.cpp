@@ -182,7 +182,9 @@ void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double
   // weight-streamed kernel: forced (numerics tests / benchmarks: force_cfg >= 20 on a w_static weight) or routed by
   // the policy for a packed (static) weight; decided before the split-K plan, whose geometry depends on it
   const bool stat = a.w_static || c.is_weight(a.w);
-  a.wsb = stat && ((a.force_cfg >= 20 && !two_d) || (a.force_cfg < 0 && conv_wsb_route(a, two_d))) ? 1 : 0;
+  a.wsb = !stat ? 0
+          : (a.force_cfg >= 30 ? 2
+             : (a.force_cfg >= 20 && !two_d) ? 1 : (a.force_cfg < 0 ? conv_wsb_route(a, two_d) : 0));
   const long long need = conv_plan_splitk(a, two_d);
   if (a.wsb) {
     if (!a.wsplit) a.wsplit = c.wsplit_for(a, s);  // a caller-built image (rvcx_conv1d) is used as given
@@ -579,7 +581,7 @@ int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const floa
     set_device(ctx);
     ctx->check_device_status();
     if (!d_x || !d_w || !d_y || T <= 0 || C_in <= 0 || N <= 0 || taps <= 0 || dilation <= 0 || stride <= 0 ||
-        pad < 0 || T_out <= 0 || math < 0 || math > 3)
+        pad < 0 || T_out <= 0 || math < 0 || math > 4)
       throw Error(RVCX_E_INVALID, "rvcx_conv1d: bad argument");
     if ((T_out - 1) * stride + (int64_t)(taps - 1) * dilation + 1 > T + 2 * (int64_t)pad)
       throw Error(RVCX_E_SHAPE, "rvcx_conv1d: T_out exceeds the padded input");
@@ -590,7 +592,7 @@ int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const floa
     a.w = d_w; a.ldw = C_in; a.w_ts = (long long)N * C_in; a.taps = taps; a.dil = dilation; a.pad = pad;
     a.stride = stride;
     a.y = d_y; a.ldy = N; a.T_out = (int)T_out; a.N = N; a.bias = d_bias;
-    a.math = math == 3 ? 2 : math;
+    a.math = math >= 3 ? 2 : math;
     if (math == 3) {  // the weight-streamed split kernel (conv_wsb.hip) whatever the size policy would pick
       if (!conv_wsb_eligible(a)) throw Error(RVCX_E_SHAPE, "rvcx_conv1d: shape not eligible for the weight-streamed kernel");
       a.w_static = 1;
@@ -598,6 +600,14 @@ int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const floa
       a.no_splitk = 1;
       // a fresh split image every call, never the address-keyed cache: the caller may reuse d_w (or torch's
       // allocator may hand the address back) with new weights of the same shape
+      void* img = ctx->buf<char>("conv.test.wsplit", (size_t)conv_wsplit_bytes(a), static_cast<hipStream_t>(stream));
+      check(conv_wsplit_build(a, img, static_cast<hipStream_t>(stream)), "conv_wsplit_build");
+      a.wsplit = img;
+    }
+    if (math == 4) {  // the gather-streamed split kernel (conv_gs.hip), split-K by the size policy
+      if (!conv_gs_eligible(a, false)) throw Error(RVCX_E_SHAPE, "rvcx_conv1d: shape not eligible for the gather-streamed kernel");
+      a.w_static = 1;
+      a.force_cfg = 30;
       void* img = ctx->buf<char>("conv.test.wsplit", (size_t)conv_wsplit_bytes(a), static_cast<hipStream_t>(stream));
       check(conv_wsplit_build(a, img, static_cast<hipStream_t>(stream)), "conv_wsplit_build");
       a.wsplit = img;

@@ -706,15 +706,25 @@ inline int pick_wsb(const ConvArgs& a) {
   static const int c_narrow = env_cfg("RVCX_WCFG_NARROW", 24);
   static const int c_mid = env_cfg("RVCX_WCFG_MID", 23);
   static const int c_wide = env_cfg("RVCX_WCFG_WIDE", 23);
+  static const int c_gs = env_cfg("RVCX_GCFG", 30);
+  if (a.wsb == 2) return c_gs;  // gather-streamed (conv_gs.hip): the short contractions
   return a.N <= 32 ? c_narrow : (a.N <= 64 ? c_mid : c_wide);
 }
+inline bool cfg_is_gs(int cfg) { return cfg >= 30; }
 
 template <bool TWO_D>
 hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
   if (a.N <= 0 || a.T_out <= 0 || a.batch <= 0) return hipSuccess;
   if (a.C_in <= 0 || a.taps <= 0) return hipErrorInvalidValue;
   if (tiny_fits(a)) return launch_tiny(a, TWO_D, s);
-  if (a.wsb && a.wsplit && conv_math(a) == 2 && conv_wsb_eligible(a, TWO_D)) {
+  if (a.wsb == 2 && a.wsplit && conv_math(a) == 2 && conv_gs_eligible(a, TWO_D)) {
+    const int ks = (a.ws && a.ksplit > 1) ? a.ksplit : 1;
+    const int cfg = a.force_cfg >= 30 ? a.force_cfg : pick_wsb(a);
+    hipError_t e = conv_gs_launch(a, cfg, xcd_enabled() ? 1 : 0, s, TWO_D, ks);
+    if (e == hipSuccess && ks > 1) e = launch_splitk_reduce(a, ks, TWO_D, s);
+    if (e != hipErrorInvalidValue) return e;
+  }
+  if (a.wsb == 1 && a.wsplit && conv_math(a) == 2 && conv_wsb_eligible(a, TWO_D)) {
     const int ks = (a.ws && a.ksplit > 1) ? a.ksplit : 1;
     const int cfg = TWO_D ? 21 : (a.force_cfg >= 20 ? a.force_cfg : pick_wsb(a));
     hipError_t e = conv_wsb_launch(a, cfg, xcd_enabled() ? 1 : 0, s, TWO_D, ks);
@@ -774,7 +784,9 @@ long long conv_plan_splitk(ConvArgs& a, bool two_d) {
   if (tiny_fits(a)) return 0;
   if (two_d && a.force_cfg < 0 && small2d_enabled() && conv2d_small_fits(a)) return 0;
   int BM, BN;
-  if (a.wsb) {  // the weight-streamed tile (pick_wsb; 2-D: 128 x 64)
+  if (a.wsb == 2) {  // the gather-streamed tile
+    conv_gs_tile(a.force_cfg >= 30 ? a.force_cfg : pick_wsb(a), BM, BN);
+  } else if (a.wsb) {  // the weight-streamed tile (pick_wsb; 2-D: 128 x 64)
     conv_wsb_tile(two_d ? 21 : (a.force_cfg >= 20 ? a.force_cfg : pick_wsb(a)), BM, BN);
   } else {
     cfg_tile(two_d ? pick_cfg<true>(a) : pick_cfg<false>(a), BM, BN);
@@ -828,13 +840,21 @@ bool conv_wsb_wants(const ConvArgs& a) {
   return tiles >= min_tiles;
 }
 
-bool conv_wsb_route(const ConvArgs& a, bool two_d) {
+int conv_wsb_route(const ConvArgs& a, bool two_d) {
   static const bool split_1d = env_cfg("RVCX_WSB_SPLIT", 0) != 0;  // small 1-D grids with split-K
   static const bool route_2d = env_cfg("RVCX_WSB_2D", 0) != 0;     // 3x3 2-D convs, >= 64 channels
-  if (conv_math(a) != 2 || !conv_wsb_eligible(a, two_d) || tiny_fits(a)) return false;
-  if (two_d) return route_2d && a.N >= 64 && a.C_in >= 64 && !(small2d_enabled() && conv2d_small_fits(a));
-  if (conv_wsb_wants(a)) return true;
-  return split_1d && a.N >= 64;
+  static const bool gs_on = env_cfg("RVCX_NO_GS", 0) == 0;         // the gather-streamed kernel (A/B aid)
+  static const int gs_min_n = env_cfg("RVCX_GS_MINN", 64);
+  if (conv_math(a) != 2 || tiny_fits(a)) return 0;
+  if (two_d && small2d_enabled() && conv2d_small_fits(a)) return 0;
+  if (conv_wsb_eligible(a, two_d)) {
+    if (two_d && route_2d && a.N >= 64 && a.C_in >= 64) return 1;
+    if (!two_d && conv_wsb_wants(a)) return 1;
+    if (!two_d && split_1d && a.N >= 64) return 1;
+  }
+  // everything else with a static weight, 32-channel chunks and >= 64 outputs: the short contractions
+  if (gs_on && a.N >= gs_min_n && conv_gs_eligible(a, two_d)) return 2;
+  return 0;
 }
 
 hipError_t conv1d(const ConvArgs& a, hipStream_t s) { return dispatch<false>(a, s); }

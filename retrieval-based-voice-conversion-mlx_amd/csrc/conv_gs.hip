@@ -1,0 +1,295 @@
+// fp32 implicit-GEMM convolution for the SHORT contractions of the path (HuBERT's linears and feature convs, the
+// TextEncoder / flow convs, the RMVPE U-Net's 3x3 convs, split-K partial tiles): "gather-streamed" on
+// v_mfma_f32_16x16x32_bf16, same exact 3-plane bf16 arithmetic as conv_emu.hip / conv_wsb.hip.
+//
+// These contractions have few output tiles (M = 196..3200 rows) and short per-tile K walks (after split-K, 4..24
+// (chunk, tap) steps), so the LDS-staged kernel's one-step register prefetch leaves every step waiting out a full
+// global-load latency (~1-2 us per step against ~0.2 us of MFMA work). Here both operands run a 3-deep register
+// prefetch ring and nothing waits on a load issued less than two steps earlier:
+//   * B: the weights pre-split once into bf16 plane rows in HBM (conv_wsb.hip's image, k_wsplit), per lane one
+//     16-byte fragment per (plane, 16-column tile) straight from L2 into registers -- no LDS, no conversion;
+//   * A: every (chunk, tap) step GATHERS its BM rows x 32 channels from global memory (no halo reuse: the taps of
+//     these convs are 1..9, so re-reading the shifted rows from L2 costs less than a serial halo stage), a
+//     1-D row at m * stride - pad + tap * dil, a 2-D output pixel's input pixel at (oh - padh + kh, ow - padw + kw);
+//     the pre-activation and row mask are applied and the tile split into an LDS double buffer (one barrier/step).
+// Split-K slices write partial tiles to the slab (splitk_reduce_kernel applies the epilogue), as elsewhere.
+#include <algorithm>
+#include <cstdlib>
+
+#include "conv_common.h"
+#include "split_bf16.h"
+
+namespace rvcx {
+
+namespace {
+
+using namespace splitbf16;
+
+constexpr int GS_WROW = 3 * PLANE;  // bytes of one (chunk, tap, column) row of the pre-split weight image
+constexpr int GS_D = 3;             // prefetch ring depth (steps in flight per operand)
+
+// The accumulator tiles of a wave -> HBM / split-K slab. C layout of a 16x16 tile: lane l holds column l % 16, rows
+// 4 (l / 16) + r, r = 0..3. Rows are output rows (1-D) or flattened output pixels oh * W_out + ow (2-D, OUT_ROWS).
+template <int TM16, int TN16, int WM, int WN>
+__device__ __forceinline__ void gs_store(const ConvArgs& a, int m0, int n0, int b, int zsplit, int ksplit, long long Mtot,
+                                         f32x4 (&acc)[TM16][TN16]) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int lc = lane & 15, lg = lane >> 4;
+  const float* bias = a.bias ? a.bias + (long long)b * a.bias_bs : nullptr;
+  const float* R = a.res ? a.res + (long long)b * a.res_bs : nullptr;
+  const float* MK = a.mask ? a.mask + (long long)b * a.mask_bs : nullptr;
+  float* Y = a.y + (long long)b * a.y_bs;
+  const bool need_r = R && a.res_mode != RES_NONE;
+  const bool need_d = a.acc_mode != ACC_STORE;
+#pragma unroll
+  for (int tn = 0; tn < TN16; ++tn) {
+    const int n = n0 + wn * TN16 * 16 + tn * 16 + lc;
+    const bool n_ok = n < a.N;
+    const float bn = (bias && n_ok) ? bias[n] : 0.f;
+#pragma unroll
+    for (int tm = 0; tm < TM16; ++tm) {
+      const long long mb = (long long)m0 + wm * TM16 * 16 + tm * 16 + 4 * lg;
+      if (ksplit > 1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (n_ok && mb + r < Mtot) a.ws[(((long long)b * ksplit + zsplit) * a.ws_rows + mb + r) * a.N + n] = acc[tm][tn][r];
+        continue;
+      }
+      float rv[4], dv[4], mv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool ok = n_ok && mb + r < Mtot;
+        rv[r] = (ok && need_r) ? R[(mb + r) * a.ldr + n] : 0.f;
+        dv[r] = (ok && need_d) ? Y[(mb + r) * a.ldy + n] : 0.f;
+        mv[r] = (ok && MK) ? MK[mb + r] : 1.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (!(n_ok && mb + r < Mtot)) continue;
+        float v = acc[tm][tn][r];
+        if (a.bias) v += bn;
+        if (a.res_mode == RES_ADD_PRE) v = v + rv[r];
+        if (a.alpha != 1.f) v *= a.alpha;
+        v = act_fn(v, a.act, a.slope);
+        if (a.res_mode == RES_ADD_POST) v = v + rv[r];
+        else if (a.res_mode == RES_RSUB_POST) v = rv[r] - v;
+        if (a.acc_mode == ACC_ADD) v = dv[r] + v;
+        else if (a.acc_mode == ACC_ADD_DIV) v = (dv[r] + v) / a.acc_div;
+        if (MK) v *= mv[r];
+        Y[(mb + r) * a.ldy + n] = v;
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN, bool TWO_D>
+__global__ __launch_bounds__(CONV_THREADS, 2) void conv_gs16_kernel(const ConvArgs a, const char* __restrict__ wsp,
+                                                                    const int Npad, const int ntn, const int ksplit) {
+  constexpr int NT = CONV_THREADS;
+  constexpr int TM16 = BM / (WM * 16);
+  constexpr int TN16 = BN / (WN * 16);
+  constexpr int AV = BM * EC4 / NT;  // float4 groups of the A tile per thread
+  static_assert(WM * WN == 4 && TM16 >= 1 && TN16 >= 1 && BM * EC4 % NT == 0, "tile shape");
+  extern __shared__ __attribute__((aligned(16))) char smem_gs[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int lc = lane & 15, lg = lane >> 4;
+  int bx, by, bz;
+  conv_block_coords(ntn, bx, by, bz);
+  const int zsplit = bz % ksplit;
+  const int b = bz / ksplit;
+  const int n0 = by * BN;
+  const int m0 = bx * BM;
+  const long long Mtot = TWO_D ? (long long)a.T_out * a.W_out : a.T_out;
+  const float* X = a.x + (long long)b * a.x_bs;
+  const float* PM = (!TWO_D && a.pre_mask) ? a.pre_mask + (long long)b * a.pre_mask_bs : nullptr;
+
+  // ---- A gather: thread rows r_v = v * 32 + arow, channels ac4..ac4+3 of the step's chunk
+  const int arow = store_row(tid / EC4), ac4 = (tid % EC4) << 2;
+  int g0[AV];   // 1-D: input row of tap 0 (m * stride - pad); 2-D: oh
+  int w0v[AV];  // 2-D: ow
+  bool rok[AV];
+#pragma unroll
+  for (int v = 0; v < AV; ++v) {
+    const long long m = (long long)m0 + v * (NT / EC4) + arow;
+    rok[v] = m < Mtot;
+    if constexpr (!TWO_D) {
+      g0[v] = (int)m * a.stride - a.pad;
+      w0v[v] = 0;
+    } else {
+      const int mm = rok[v] ? (int)m : 0;
+      g0[v] = mm / a.W_out;
+      w0v[v] = mm - g0[v] * a.W_out;
+    }
+  }
+  f32x4 ar[GS_D][AV];
+  float am[GS_D][AV];
+  auto load_a = [&](int st, f32x4 (&dst)[AV], float (&dm)[AV]) __attribute__((always_inline)) {
+    const int ch = st / a.taps, tap = st - ch * a.taps;
+    const float* src = X + ch * EK + ac4;
+#pragma unroll
+    for (int v = 0; v < AV; ++v) {
+      long long g;
+      bool ok;
+      if constexpr (!TWO_D) {
+        g = g0[v] + tap * a.dil;
+        ok = rok[v] && g >= 0 && g < a.T_in;
+      } else {
+        const int kh = tap / a.KW, kw = tap - kh * a.KW;
+        const int ih = g0[v] - a.padh + kh, iw = w0v[v] - a.padw + kw;
+        ok = rok[v] && ih >= 0 && ih < a.T_in && iw >= 0 && iw < a.W_in;
+        g = (long long)ih * a.W_in + iw;
+      }
+      dst[v] = ok ? *reinterpret_cast<const f32x4*>(src + g * a.ldx) : f32x4{0.f, 0.f, 0.f, 0.f};
+      dm[v] = ok ? (PM ? PM[g] : 1.f) : 0.f;
+    }
+  };
+  auto store_a = [&](char* As, const f32x4 (&src)[AV], const float (&sm)[AV]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int v = 0; v < AV; ++v) {
+      f32x4 val = src[v];
+      if (a.pre_act != ACT_NONE) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) val[j] = act_fn(val[j], a.pre_act, a.pre_slope);  // act(0) = 0
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) val[j] *= sm[v];
+      put_split4(As + (v * (NT / EC4) + arow) * ERS, ac4, val);
+    }
+  };
+
+  // ---- B: pre-split fragments from L2
+  typedef bf16x8 BFrag[TN16][3];
+  BFrag br[GS_D];
+  const char* bp = wsp + (size_t)(n0 + wn * TN16 * 16 + lc) * GS_WROW + lg * 16;
+  const size_t bstep = (size_t)Npad * GS_WROW;
+  auto load_b = [&](int st, BFrag& dst) __attribute__((always_inline)) {
+    const char* p = bp + (size_t)st * bstep;
+#pragma unroll
+    for (int tn = 0; tn < TN16; ++tn)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) dst[tn][q] = *reinterpret_cast<const bf16x8*>(p + (size_t)tn * 16 * GS_WROW + q * PLANE);
+  };
+
+  f32x4 acc[TM16][TN16];
+#pragma unroll
+  for (int tm = 0; tm < TM16; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < TN16; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int aoff[TM16];
+#pragma unroll
+  for (int tm = 0; tm < TM16; ++tm) aoff[tm] = (wm * TM16 * 16 + tm * 16 + lc) * ERS + lg * 16;
+  auto compute = [&](const char* As, const BFrag& bf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int tm = 0; tm < TM16; ++tm) {
+      bf16x8 af[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) af[q] = *reinterpret_cast<const bf16x8*>(As + aoff[tm] + q * PLANE);
+#pragma unroll
+      for (int tn = 0; tn < TN16; ++tn) {
+        f32x4 c = acc[tm][tn];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], bf[tn][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[tn][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[tn][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[tn][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[tn][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[tn][0], c, 0, 0, 0);
+        acc[tm][tn] = c;
+      }
+    }
+  };
+
+  // (chunk, tap) steps [it0, it1) of this split-K slice. Step i: issue B(i + D - 1), MFMAs on A(i) (LDS buffer
+  // i % 2) and B(i), then A(i + 1) -> LDS buffer (i + 1) % 2, issue A(i + D), one barrier (load indices clamped to
+  // the slice: the tail reloads its last step, harmlessly). Ring slots are (step - it0) % D, compile-time after the
+  // D-fold unroll.
+  const int total = (a.C_in / EK) * a.taps;
+  const int per = (total + ksplit - 1) / ksplit;
+  const int it0 = zsplit * per, it1 = min(total, it0 + per);
+  if (it0 < it1) {
+    const int last = it1 - 1;
+    auto clampst = [&](int st) { return st < last ? st : last; };
+#pragma unroll
+    for (int p = 0; p < GS_D; ++p) load_a(clampst(it0 + p), ar[p], am[p]);
+#pragma unroll
+    for (int p = 0; p < GS_D - 1; ++p) load_b(clampst(it0 + p), br[p]);
+    store_a(smem_gs, ar[0], am[0]);
+    __syncthreads();
+    for (int base = it0; base < it1; base += GS_D) {
+#pragma unroll
+      for (int p = 0; p < GS_D; ++p) {
+        const int i = base + p;
+        if (i < it1) {
+          load_b(clampst(i + GS_D - 1), br[(p + GS_D - 1) % GS_D]);
+          __builtin_amdgcn_sched_barrier(0);
+          compute(smem_gs + (size_t)((i - it0) & 1) * BM * ERS, br[p]);
+          // A(i + 1) -> the other LDS buffer (on the last step a harmless copy of A(last) nobody reads), then A(i + D)
+          // into the slot A(i) left
+          store_a(smem_gs + (size_t)((i + 1 - it0) & 1) * BM * ERS, ar[(p + 1) % GS_D], am[(p + 1) % GS_D]);
+          load_a(clampst(i + GS_D), ar[p], am[p]);
+          __syncthreads();
+        }
+      }
+    }
+  }
+  gs_store<TM16, TN16, WM, WN>(a, m0, n0, b, zsplit, ksplit, Mtot, acc);
+}
+
+template <int BM, int BN, int WM, int WN, bool TWO_D>
+hipError_t launch_gs(const ConvArgs& a, int ntn_enable, int ksplit, hipStream_t s) {
+  const long long Mtot = TWO_D ? (long long)a.T_out * a.W_out : a.T_out;
+  const long long mtiles = (Mtot + BM - 1) / BM;
+  if (mtiles > INT32_MAX / 64 || a.wsplit_npad % BN != 0 || ksplit < 1 || (ksplit > 1 && !a.ws)) return hipErrorInvalidValue;
+  const int ntiles = (a.N + BN - 1) / BN;
+  const int ntn = ntn_enable ? ntiles : 0;
+  dim3 grid((unsigned)(ntn ? mtiles * ntiles : mtiles), ntn ? 1 : ntiles, a.batch * ksplit);
+  const size_t smem = (size_t)2 * BM * ERS;
+  hipLaunchKernelGGL((conv_gs16_kernel<BM, BN, WM, WN, TWO_D>), grid, dim3(CONV_THREADS), smem, s, a,
+                     static_cast<const char*>(a.wsplit), a.wsplit_npad, ntn, ksplit);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool conv_gs_eligible(const ConvArgs& a, bool two_d) {
+  const bool vec_a = ((a.ldx & 3) == 0) && ((reinterpret_cast<uintptr_t>(a.x) & 15) == 0) && ((a.x_bs & 3) == 0);
+  const bool common = a.batch_inner == 1 && !a.b_kn && a.C_in % EK == 0 && a.C_in > 0 && a.taps >= 1 && vec_a &&
+                      a.out_map == OUT_ROWS && a.stride >= 1 && a.dil >= 1;
+  if (!common) return false;
+  if (!two_d) return (long long)a.T_out * a.stride < INT32_MAX / 2 && a.T_in < INT32_MAX / 2;
+  return a.taps == a.KH * a.KW && !a.pre_mask && a.stride == 1 && a.W_out >= 1 && a.W_in >= 1;
+}
+
+// cfg 30: 64 x 64 (2 x 2 waves of 32 x 32), 31: 128 x 64 (2 x 2 waves of 64 x 32), 32: 64 x 128 (2 x 2 of 32 x 64)
+bool conv_gs_tile(int cfg, int& BM, int& BN) {
+  static const int t[3][2] = {{64, 64}, {128, 64}, {64, 128}};
+  if (cfg < 30 || cfg > 32) return false;
+  BM = t[cfg - 30][0];
+  BN = t[cfg - 30][1];
+  return true;
+}
+
+hipError_t conv_gs_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream_t s, bool two_d, int ksplit) {
+  if (!a.wsplit || !conv_gs_eligible(a, two_d)) return hipErrorInvalidValue;
+  if (two_d) {
+    switch (cfg) {
+      case 30: return launch_gs<64, 64, 2, 2, true>(a, ntn_enable, ksplit, s);
+      case 31: return launch_gs<128, 64, 2, 2, true>(a, ntn_enable, ksplit, s);
+      case 32: return launch_gs<64, 128, 2, 2, true>(a, ntn_enable, ksplit, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
+  switch (cfg) {
+    case 30: return launch_gs<64, 64, 2, 2, false>(a, ntn_enable, ksplit, s);
+    case 31: return launch_gs<128, 64, 2, 2, false>(a, ntn_enable, ksplit, s);
+    case 32: return launch_gs<64, 128, 2, 2, false>(a, ntn_enable, ksplit, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace rvcx

@@ -4,7 +4,7 @@
 // launched before this kernel. What is left is 2 x T dependent steps of h' = GRUCell(gi_t, h)
 // with W_hh = 768 x 256 fp32 (786 KB per direction: more than one CU's VGPRs + LDS can hold).
 //
-// Design: one launch of 4 workgroups = 2 directions x 2 halves of the hidden units. A workgroup
+// Design: 4 working workgroups per sequence = 2 directions x 2 halves of the hidden units (partners on one XCD). A workgroup
 // owns 128 hidden units = 384 rows of W_hh (its units' r, z, n rows) and keeps ALL of them in
 // VGPRs: 768 threads, thread (j, r) holds 128 columns of row r: columns [64j, 64j+64) of its OWN
 // half of h and the same 64 columns of the PARTNER's half, as packed pairs for v_pk_fma_f32.
@@ -18,7 +18,7 @@
 // wave polls the 64 granules its lanes need (one per lane) with agent-scope relaxed loads (sc1,
 // L1-bypassing). Spins are bounded: on timeout *status is set and the kernel exits (no hang); the
 // runtime reports it as an error (RVCX_E_HIP, "gru: partner hand-off timed out") at its next check.
-// The granule buffer is zeroed before every launch (hipMemsetAsync in gru_bidir).
+// Tags continue across launches (gru_bidir), so the granule buffer needs no zeroing between them.
 //
 // Cell arithmetic follows ATen GRUCell: r = sig(hg_r + ig_r), z = sig(hg_z + ig_z),
 // n = tanh(ig_n + hg_n * r), h' = (h - n) * z + n, with hg = W_hh h + b_hh.
@@ -46,19 +46,24 @@ __device__ __forceinline__ float tanh_g(float v) { return 1.f - 2.f * __frcp_rn(
 __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ gi, const float* whh_f,
                                                      const float* bhh_f, const float* whh_b, const float* bhh_b,
                                                      int T, float* out, unsigned long long* xchg,
-                                                     unsigned* status, unsigned spin_limit) {
+                                                     unsigned* status, unsigned spin_limit, unsigned tag0) {
   __shared__ __attribute__((aligned(16))) float h_own[UNITS];
   __shared__ __attribute__((aligned(16))) float h_pw[NT / 64][HALF];  // per-wave copy of its partner columns
   __shared__ float part[2][ROWS];
   __shared__ float bias_h[ROWS];
   __shared__ int abort_flag;
 
-  const int d = blockIdx.x >> 1;  // direction
-  const int q = blockIdx.x & 1;   // half
-  // blockIdx.y = independent sequence (batched streams / utterances of one length)
-  gi += (long long)blockIdx.y * T * 6 * H;
-  out += (long long)blockIdx.y * T * 2 * H;
-  xchg += (long long)blockIdx.y * 4 * 2 * UNITS;
+  // 16 blocks per sequence, 4 of them working: block w = 0 / 8 are direction 0's two halves, 1 / 9 direction 1's.
+  // Blocks are dealt round-robin to the 8 XCDs (MI355X_MICROARCH.md), so each partner pair shares one XCD and its
+  // L2: the per-step hand-off stays inside that L2 instead of crossing XCDs through memory.
+  const int w = blockIdx.x & 15;
+  if ((w & 7) > 1) return;
+  const int d = w & 1;   // direction
+  const int q = w >> 3;  // half
+  const int seq = blockIdx.x >> 4;  // independent sequence (batched streams / utterances of one length)
+  gi += (long long)seq * T * 6 * H;
+  out += (long long)seq * T * 2 * H;
+  xchg += (long long)seq * 4 * 2 * UNITS;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int j = tid / ROWS;        // column quarter within each half (wave-uniform: ROWS % 64 == 0)
@@ -122,7 +127,7 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ g
     {
       float* hp = h_pw[wave];
       if (s > 0) {
-        const unsigned epoch = (unsigned)s;
+        const unsigned epoch = tag0 + (unsigned)s;
         const unsigned long long* slot = theirs + ((s - 1) & 1) * UNITS + j * HALF;
         unsigned long long gv = 0;
 #pragma nounroll
@@ -167,7 +172,7 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ g
       h_own[tid] = hnew;
       out[(long long)t * (2 * H) + d * H + gunit] = hnew;
       const unsigned long long g =
-          ((unsigned long long)(unsigned)(s + 1) << 32) | (unsigned long long)__float_as_uint(hnew);
+          ((unsigned long long)(tag0 + (unsigned)(s + 1)) << 32) | (unsigned long long)__float_as_uint(hnew);
       __hip_atomic_store(&mine[(s & 1) * UNITS + tid], g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
@@ -178,14 +183,27 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ g
 hipError_t gru_bidir(const float* gi, const float* whh_f, const float* bhh_f, const float* whh_b,
                      const float* bhh_b, int T, float* out, unsigned long long* xchg, unsigned* status,
                      hipStream_t s, int B) {
-  // the two halves of a direction spin on each other: all 4B workgroups (1 per CU) must be co-resident
-  if (B < 1 || 4 * B > 256) return hipErrorInvalidValue;
-  hipError_t e = hipMemsetAsync(xchg, 0, sizeof(unsigned long long) * gru_xchg_words(B), s);
-  if (e != hipSuccess) return e;
+  // the two halves of a direction spin on each other: all 4B working workgroups (1 per CU) must be co-resident;
+  // the 12B idle ones exit at once
+  if (B < 1 || B > 16) return hipErrorInvalidValue;
+  // granule tags run on across launches (tag0 advances by T + 1 per launch), so whatever a buffer holds from an
+  // earlier launch never matches a tag this launch waits for and no per-launch zeroing is needed; the buffer is
+  // zeroed only when the 32-bit tag space wraps
+  static unsigned next_tag = 1u << 31;
+  const unsigned tag0 = next_tag;
+  if ((unsigned long long)tag0 + (unsigned)T + 1 >= (1ull << 32)) {
+    next_tag = 0;
+    return gru_bidir(gi, whh_f, bhh_f, whh_b, bhh_b, T, out, xchg, status, s, B);
+  }
+  next_tag = tag0 + (unsigned)T + 1;
+  if (tag0 == 0) {
+    hipError_t e = hipMemsetAsync(xchg, 0, sizeof(unsigned long long) * gru_xchg_words(B), s);
+    if (e != hipSuccess) return e;
+  }
   unsigned spin = SPIN_LIMIT;  // test hook: a tiny RVCX_GRU_SPIN_LIMIT forces the timeout path
   if (const char* e = std::getenv("RVCX_GRU_SPIN_LIMIT")) spin = (unsigned)std::strtoul(e, nullptr, 10);
-  hipLaunchKernelGGL(k_gru_bidir, dim3(4, B), dim3(NT), 0, s, gi, whh_f, bhh_f, whh_b, bhh_b, T, out, xchg, status,
-                     spin);
+  hipLaunchKernelGGL(k_gru_bidir, dim3(16 * B), dim3(NT), 0, s, gi, whh_f, bhh_f, whh_b, bhh_b, T, out, xchg, status,
+                     spin, tag0);
   return hipGetLastError();
 }
 

@@ -133,6 +133,8 @@ struct Ctx {
   // Kernels store into it; the host reads it after a synchronisation: every compute entry point checks
   // it on entry (faults of earlier, completed calls), the pipeline at its own sync points, and
   // rvcx_device_status after synchronising the caller's stream.
+  const void* gru_xchg_zeroed = nullptr;  // the BiGRU hand-off buffer last zeroed, and its words (runtime_fe.cpp)
+  size_t gru_xchg_words = 0;
   unsigned* status_host = nullptr;
   unsigned* status_dev = nullptr;
   unsigned* device_status();

@@ -660,6 +660,12 @@ static void e2e_chunk(Ctx& c, float* img, int Fc, float* sal, hipStream_t s, int
   run1(c, lin(feat, 3 * NMEL, B * Fc, 3 * NMEL, c.W("rm.gru.wih"), 6 * GRU_H, c.W("rm.gru.bih"), gi, 6 * GRU_H), s);
   float* go = c.buf<float>("rm.gruout", (size_t)B * Fc * 2 * GRU_H, s);
   unsigned long long* xchg = c.buf<unsigned long long>("rm.xchg", gru_xchg_words(B), s);
+  if (xchg != c.gru_xchg_zeroed || gru_xchg_words(B) > c.gru_xchg_words) {
+    // a new (or grown) allocation holds garbage tags: zero it once (gru_bidir never does)
+    RVCX_HIP(hipMemsetAsync(xchg, 0, sizeof(unsigned long long) * gru_xchg_words(B), s));
+    c.gru_xchg_zeroed = xchg;
+    c.gru_xchg_words = gru_xchg_words(B);
+  }
   unsigned* status = c.device_status();  // sticky until the host reads it (Ctx::check_device_status)
   // work the caller wants issued beside the BiGRU (which occupies 4 CUs): the gate event marks this point of the
   // stream, the BiGRU goes out first and the hook's (many) launches after it, so the host time spent issuing
@@ -667,9 +673,11 @@ static void e2e_chunk(Ctx& c, float* img, int Fc, float* sal, hipStream_t s, int
   std::function<void(hipStream_t)> hook = std::move(c.before_gru);
   c.before_gru = nullptr;
   if (hook && c.ev_gate) RVCX_HIP(hipEventRecord(c.ev_gate, s));
-  check(gru_bidir(gi, c.W("rm.gru.whh_f"), c.W("rm.gru.bhh_f"), c.W("rm.gru.whh_b"), c.W("rm.gru.bhh_b"), Fc, go,
-                  xchg, status, s, B),
-        "gru");
+  for (int g0 = 0; g0 < B; g0 += 16)  // at most 16 sequences per launch (16 x 4 working workgroups co-resident)
+    check(gru_bidir(gi + (size_t)g0 * Fc * 6 * GRU_H, c.W("rm.gru.whh_f"), c.W("rm.gru.bhh_f"), c.W("rm.gru.whh_b"),
+                    c.W("rm.gru.bhh_b"), Fc, go + (size_t)g0 * Fc * 2 * GRU_H, xchg + gru_xchg_words(g0), status, s,
+                    std::min(16, B - g0)),
+          "gru");
   if (hook) hook(s);
   ConvArgs f = lin(go, 2 * GRU_H, B * Fc, 2 * GRU_H, c.W("rm.fc.w"), NCLS, c.W("rm.fc.b"), sal, NCLS);
   f.act = ACT_SIGMOID;

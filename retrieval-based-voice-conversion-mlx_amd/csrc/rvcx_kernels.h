@@ -97,7 +97,7 @@ struct ConvArgs {
   int w_static = 0;             // the B operand is a constant weight tensor (callers set it; enables the cache)
   const void* wsplit = nullptr;  // ((chunk * taps + tap) * wsplit_npad + n) rows of [hi|mid|lo] x 32 bf16
   int wsplit_npad = 0;
-  int wsb = 0;  // set by the runtime (conv_wsb_route on a static weight): run on the weight-streamed kernel
+  int wsb = 0;  // set by the runtime (conv_wsb_route on a static weight): 1 weight-streamed kernel, 2 gather-streamed
   int ksplit = 1;
   int no_splitk = 0;
   long long ws_rows = 0;
@@ -137,8 +137,15 @@ bool conv_wsb_eligible(const ConvArgs& a, bool two_d = false);
 bool conv_wsb_wants(const ConvArgs& a);
 // route a contraction with a static weight to the weight-streamed kernel: the big 1-D grids (conv_wsb_wants), and
 // behind RVCX_WSB_SPLIT / RVCX_WSB_2D the small 1-D grids (with split-K) and the 3x3 2-D convs with >= 64 channels
-bool conv_wsb_route(const ConvArgs& a, bool two_d);
-bool conv_wsb_tile(int cfg, int& BM, int& BN);  // cfg 20..22 -> tile
+// 0: not routed (conv_emu / conv_gemm), 1: conv_wsb.hip, 2: conv_gs.hip
+int conv_wsb_route(const ConvArgs& a, bool two_d);
+bool conv_wsb_tile(int cfg, int& BM, int& BN);  // cfg 20..26 -> tile
+// gather-streamed split conv (conv_gs.hip) for the short contractions: pre-split weights (the conv_wsb image) in a
+// register ring, A gathered per (chunk, tap) step; 1-D (any stride / dilation) and 2-D (stride 1, OUT_ROWS), C_in % 32
+// == 0, split-K capable. cfg 30..32 -> tile
+bool conv_gs_eligible(const ConvArgs& a, bool two_d);
+bool conv_gs_tile(int cfg, int& BM, int& BN);
+hipError_t conv_gs_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream_t s, bool two_d, int ksplit);
 int conv_wsplit_npad(int N);
 long long conv_wsplit_bytes(const ConvArgs& a);
 hipError_t conv_wsplit_build(const ConvArgs& a, void* out, hipStream_t s);

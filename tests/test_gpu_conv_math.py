@@ -24,6 +24,8 @@ CASES = [  # T, C_in, N, taps, dil, stride, scale_spread
     (3000, 256, 200, 7, 3, 1, 0),       # N not a multiple of the tile (weight-streamed: padded columns)
     (2500, 64, 32, 11, 5, 1, 4),        # narrow N (weight-streamed 256 x 32 tile), spread operands
     (2000, 128, 64, 7, 1, 1, 12),       # operands spread over 2^+-12
+    (196, 512, 512, 9, 1, 1, 0),        # the U-Net's deepest 1-D analogue: 9 taps, few rows, long K (split-K)
+    (1599, 768, 3072, 1, 1, 1, 0),      # HuBERT FFN at the 30 s (C4) length
 ]
 
 
@@ -49,7 +51,8 @@ def test_split_math_is_fp32_accurate(engine, T, C, N, K, dil, stride, spread):
     errs = {}
     # "wsb": the same split arithmetic on the weight-streamed kernel (conv_wsb.hip), where the shape allows it
     wsb = stride == 1 and C % 32 == 0 and (K - 1) * dil <= 64
-    for mode in ("f32", "split") + (("wsb",) if wsb else ()):
+    gs = C % 32 == 0  # "gs": the gather-streamed kernel (conv_gs.hip: per-step A gather, split-K by the size policy)
+    for mode in ("f32", "split") + (("wsb",) if wsb else ()) + (("gs",) if gs else ()):
         y = engine.conv1d(x, w, bias, dilation=dil, padding=pad, stride=stride, math=mode).cpu().numpy()
         assert y.shape == ref.shape
         errs[mode] = float(np.max(np.abs(y - ref) / (mag + np.abs(bias) + 1e-30)))
@@ -60,6 +63,8 @@ def test_split_math_is_fp32_accurate(engine, T, C, N, K, dil, stride, spread):
     assert errs["split"] <= 1.5 * errs["f32"] + 1e-8, errs
     if wsb:  # one unsplit accumulation chain per output (no split-K partial sums): the fp32 bound only
         assert errs["wsb"] < 1e-6, errs
+    if gs:
+        assert errs["gs"] < 1e-6, errs
 
 
 def test_context_math_mode_switch(engine):
