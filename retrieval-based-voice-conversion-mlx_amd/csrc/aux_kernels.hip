@@ -639,15 +639,17 @@ hipError_t groupnorm_time_gelu(float* x, int T, int C, const float* gamma, const
 
 // ------------------------------------------------------------------ RMVPE front end
 // grid.y = sequence: x rows of stride ldx, y rows of stride ldy
+// (a row stride ldy past the padded length gets its tail zeroed here: no fill launch before)
 __global__ void k_reflect1d(const float* x, int n, int pl, int pr, float* y, long long ldx, long long ldy) {
   const int m = n + pl + pr;
+  const int mz = ldy > m ? (int)ldy : m;
   x += blockIdx.y * ldx;
   y += blockIdx.y * ldy;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < mz; i += gridDim.x * blockDim.x) {
     int j = i - pl;
     if (j < 0) j = -j;
     if (j >= n) j = 2 * (n - 1) - j;
-    y[i] = x[j];
+    y[i] = i < m ? x[j] : 0.f;
   }
 }
 hipError_t reflect_pad_1d(const float* x, int n, int pad_l, int pad_r, float* y, hipStream_t s, int B, long long ldx,
@@ -963,10 +965,14 @@ size_t filtfilt_ws_doubles(long long n, int order) {
   return (size_t)(3 * ne);
 }
 
-// peak normalisation (pipeline.py:550-552): m = max|x| / 0.99 ; if m > 1: x /= m
-// block-reduced, one atomic per block (a per-wave atomic on one address serialised 4096 of them: 49 us)
-__global__ void k_absmax(const float* x, long long n, unsigned* out) {
+// peak normalisation (pipeline.py:550-552): m = max|x| / 0.99 ; if m > 1: x /= m. Fused with the trim copy
+// (pipeline.py:494 audio_opt slices): dst = src / m read from the un-trimmed buffer. Two launches for all B rows
+// and no fill: each absmax block writes its own maximum to ws[row][block], the scale pass reduces those <= 256
+// partials per block before it scales (no atomics, nothing to zero between calls).
+constexpr int PEAK_BLOCKS = 256;
+__global__ void k_absmax(const float* x, long long n, long long ldx, float* part) {
   __shared__ float wm[TB / 64];
+  x += blockIdx.y * ldx;
   float m = 0.f;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
     m = fmaxf(m, fabsf(x[i]));
@@ -975,22 +981,36 @@ __global__ void k_absmax(const float* x, long long n, unsigned* out) {
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int w = 1; w < (int)(blockDim.x >> 6); ++w) m = fmaxf(m, wm[w]);
-    atomicMax(out, __float_as_uint(m));
+    part[blockIdx.y * PEAK_BLOCKS + blockIdx.x] = m;
   }
 }
-__global__ void k_peak_scale(float* x, long long n, const unsigned* mx) {
-  const float m = __uint_as_float(*mx) / 0.99f;
-  if (!(m > 1.f)) return;
+__global__ void k_peak_scale(const float* src, long long lds, float* dst, long long ldd, long long n, const float* part,
+                             int nparts) {
+  __shared__ float wm[TB / 64];
+  src += blockIdx.y * lds;
+  dst += blockIdx.y * ldd;
+  float m = threadIdx.x < nparts ? part[blockIdx.y * PEAK_BLOCKS + threadIdx.x] : 0.f;
+  m = warp_max(m);
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = wm[0];
+  for (int w = 1; w < TB / 64; ++w) m = fmaxf(m, wm[w]);
+  m = m / 0.99f;
+  const bool scale = m > 1.f;
+  if (!scale && src == dst) return;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
-    x[i] = x[i] / m;
+    dst[i] = scale ? src[i] / m : src[i];
 }
-hipError_t peak_normalize(float* x, long long n, unsigned* ws, hipStream_t s) {
-  hipError_t e = hipMemsetAsync(ws, 0, sizeof(unsigned), s);
-  if (e != hipSuccess || n <= 0) return e;
-  hipLaunchKernelGGL(k_absmax, dim3(std::min<long long>(256, (n + TB - 1) / TB)), dim3(TB), 0, s, x, n, ws);
-  hipLaunchKernelGGL(k_peak_scale, dim3(nblocks(n)), dim3(TB), 0, s, x, n, ws);
+hipError_t peak_normalize(const float* src, float* dst, long long n, float* ws, hipStream_t s, int B, long long lds,
+                          long long ldd) {
+  if (n <= 0 || B < 1) return hipSuccess;
+  const int nparts = (int)std::min<long long>(PEAK_BLOCKS, (n + TB - 1) / TB);
+  hipLaunchKernelGGL(k_absmax, dim3(nparts, B), dim3(TB), 0, s, src, n, lds, ws);
+  hipLaunchKernelGGL(k_peak_scale, dim3(std::min(nblocks(n), 4096u), B), dim3(TB), 0, s, src, lds, dst, ldd, n, ws,
+                     nparts);
   return hipGetLastError();
 }
+size_t peak_normalize_ws_floats(int B) { return (size_t)B * PEAK_BLOCKS; }
 
 // ------------------------------------------------------------------ get_f0 adjustments
 // Autotune.autotune_f0 (rvc/infer/pipeline.py:151-162): snap to the nearest of 54 note

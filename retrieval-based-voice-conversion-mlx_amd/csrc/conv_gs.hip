@@ -26,7 +26,10 @@ namespace {
 using namespace splitbf16;
 
 constexpr int GS_WROW = 3 * PLANE;  // bytes of one (chunk, tap, column) row of the pre-split weight image
-constexpr int GS_D = 3;             // prefetch ring depth (steps in flight per operand)
+#ifndef GS_DEPTH
+#define GS_DEPTH 3
+#endif
+constexpr int GS_D = GS_DEPTH;      // prefetch ring depth (steps in flight per operand)
 
 // The accumulator tiles of a wave -> HBM / split-K slab. C layout of a 16x16 tile: lane l holds column l % 16, rows
 // 4 (l / 16) + r, r = 0..3. Rows are output rows (1-D) or flattened output pixels oh * W_out + ow (2-D, OUT_ROWS).
@@ -86,7 +89,8 @@ __device__ __forceinline__ void gs_store(const ConvArgs& a, int m0, int n0, int 
 
 template <int BM, int BN, int WM, int WN, bool TWO_D>
 __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gs16_kernel(const ConvArgs a, const char* __restrict__ wsp,
-                                                                    const int Npad, const int ntn, const int ksplit) {
+                                                                    const int Npad, const int ntn, const int ksplit,
+                                                                    const int mfast) {
   constexpr int NT = CONV_THREADS;
   constexpr int TM16 = BM / (WM * 16);
   constexpr int TN16 = BN / (WN * 16);
@@ -101,6 +105,14 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gs16_kernel(const ConvAr
   const int lc = lane & 15, lg = lane >> 4;
   int bx, by, bz;
   conv_block_coords(ntn, bx, by, bz);
+  if (mfast && ntn > 0) {
+    // each XCD's contiguous run of tiles walks M fastest: it streams only its share of the weight columns (the big
+    // operand of these GEMMs) through its L2 while every XCD re-reads the small activation tile set
+    const int t = bx * ntn + by;
+    const int mt = (int)gridDim.x / ntn;
+    bx = t % mt;
+    by = t / mt;
+  }
   const int zsplit = bz % ksplit;
   const int b = bz / ksplit;
   const int n0 = by * BN;
@@ -249,8 +261,15 @@ hipError_t launch_gs(const ConvArgs& a, int ntn_enable, int ksplit, hipStream_t 
   const int ntn = ntn_enable ? ntiles : 0;
   dim3 grid((unsigned)(ntn ? mtiles * ntiles : mtiles), ntn ? 1 : ntiles, a.batch * ksplit);
   const size_t smem = (size_t)2 * BM * ERS;
+  // M-fastest tile runs when the pre-split weight (6 B per element) outweighs the activation operand (4 B)
+  static const int mf_env = [] {
+    const char* e = std::getenv("RVCX_GS_MFAST");
+    return e ? std::atoi(e) : -1;
+  }();
+  const double wbytes = 6.0 * a.N * a.C_in * a.taps, abytes = 4.0 * (double)Mtot * a.C_in * a.batch;
+  const int mfast = mf_env >= 0 ? mf_env : (wbytes > abytes ? 1 : 0);
   hipLaunchKernelGGL((conv_gs16_kernel<BM, BN, WM, WN, TWO_D>), grid, dim3(CONV_THREADS), smem, s, a,
-                     static_cast<const char*>(a.wsplit), a.wsplit_npad, ntn, ksplit);
+                     static_cast<const char*>(a.wsplit), a.wsplit_npad, ntn, ksplit, mfast);
   return hipGetLastError();
 }
 

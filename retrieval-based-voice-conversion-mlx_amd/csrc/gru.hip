@@ -46,7 +46,8 @@ __device__ __forceinline__ float tanh_g(float v) { return 1.f - 2.f * __frcp_rn(
 __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ gi, const float* whh_f,
                                                      const float* bhh_f, const float* whh_b, const float* bhh_b,
                                                      int T, float* out, unsigned long long* xchg,
-                                                     unsigned* status, unsigned spin_limit, unsigned tag0) {
+                                                     unsigned* status, unsigned spin_limit, unsigned tag0,
+                                                     int adjacent) {
   __shared__ __attribute__((aligned(16))) float h_own[UNITS];
   __shared__ __attribute__((aligned(16))) float h_pw[NT / 64][HALF];  // per-wave copy of its partner columns
   __shared__ float part[2][ROWS];
@@ -57,9 +58,9 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ g
   // Blocks are dealt round-robin to the 8 XCDs (MI355X_MICROARCH.md), so each partner pair shares one XCD and its
   // L2: the per-step hand-off stays inside that L2 instead of crossing XCDs through memory.
   const int w = blockIdx.x & 15;
-  if ((w & 7) > 1) return;
-  const int d = w & 1;   // direction
-  const int q = w >> 3;  // half
+  if (adjacent ? w > 3 : (w & 7) > 1) return;
+  const int d = adjacent ? w >> 1 : w & 1;  // direction
+  const int q = adjacent ? w & 1 : w >> 3;  // half
   const int seq = blockIdx.x >> 4;  // independent sequence (batched streams / utterances of one length)
   gi += (long long)seq * T * 6 * H;
   out += (long long)seq * T * 2 * H;
@@ -200,10 +201,14 @@ hipError_t gru_bidir(const float* gi, const float* whh_f, const float* bhh_f, co
     hipError_t e = hipMemsetAsync(xchg, 0, sizeof(unsigned long long) * gru_xchg_words(B), s);
     if (e != hipSuccess) return e;
   }
+  static const int adj = [] {  // RVCX_GRU_ADJACENT=1: partners in adjacent blocks (different XCDs; A/B aid)
+    const char* e = std::getenv("RVCX_GRU_ADJACENT");
+    return e ? std::atoi(e) : 0;
+  }();
   unsigned spin = SPIN_LIMIT;  // test hook: a tiny RVCX_GRU_SPIN_LIMIT forces the timeout path
   if (const char* e = std::getenv("RVCX_GRU_SPIN_LIMIT")) spin = (unsigned)std::strtoul(e, nullptr, 10);
   hipLaunchKernelGGL(k_gru_bidir, dim3(16 * B), dim3(NT), 0, s, gi, whh_f, bhh_f, whh_b, bhh_b, T, out, xchg, status,
-                     spin, tag0);
+                     spin, tag0, adj);
   return hipGetLastError();
 }
 

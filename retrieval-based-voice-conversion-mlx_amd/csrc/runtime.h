@@ -133,8 +133,15 @@ struct Ctx {
   // Kernels store into it; the host reads it after a synchronisation: every compute entry point checks
   // it on entry (faults of earlier, completed calls), the pipeline at its own sync points, and
   // rvcx_device_status after synchronising the caller's stream.
-  const void* gru_xchg_zeroed = nullptr;  // the BiGRU hand-off buffer last zeroed, and its words (runtime_fe.cpp)
-  size_t gru_xchg_words = 0;
+  // buffers whose zero parts survive from call to call (the BiGRU hand-off tags, the NSF source's pad columns): zeroed
+  // only when the buffer or its layout changes, not by a fill launch every call
+  std::map<std::string, std::pair<const void*, long long>> zero_marks;
+  void zero_once(const std::string& name, void* p, size_t bytes, long long layout, hipStream_t s) {
+    auto& m = zero_marks[name];
+    if (m.first == p && m.second == layout) return;
+    RVCX_HIP(hipMemsetAsync(p, 0, bytes, s));
+    m = {p, layout};
+  }
   unsigned* status_host = nullptr;
   unsigned* status_dev = nullptr;
   unsigned* device_status();

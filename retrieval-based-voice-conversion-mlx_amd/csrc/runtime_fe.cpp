@@ -286,7 +286,9 @@ void hubert_layers(Ctx& c, const HubertRun& run, int l0, int l1, hipStream_t s) 
       f2.res_mode = RES_ADD_POST;
       run1(c, f2, s);
     }
-    check(layernorm_rows(hs2, nullptr, hs, c.W(q + ".ln2.g"), c.W(q + ".ln2.b"), BL, HD, 1e-5f, nullptr, s), "ln2");
+    // v2's output is the last layer's LN itself: written straight into the caller's buffer (no tail copy)
+    float* dst = (run.version != 1 && i == HUBERT_LAYERS - 1) ? run.feats : hs;
+    check(layernorm_rows(hs2, nullptr, dst, c.W(q + ".ln2.g"), c.W(q + ".ln2.b"), BL, HD, 1e-5f, nullptr, s), "ln2");
   }
 }
 
@@ -299,9 +301,8 @@ int64_t hubert_tail(Ctx& c, const HubertRun& run, hipStream_t s) {
   if (version == 1) {
     if (!c.dev.count("hb.final_proj.w")) throw Error(RVCX_E_STATE, "hubert: v1 needs final_proj weights");
     run1(c, lin(hs, HD, BL, HD, c.W("hb.final_proj.w"), 256, c.W("hb.final_proj.b"), feats, 256), s);
-  } else {
-    RVCX_HIP(hipMemcpyAsync(feats, hs, (size_t)BL * outD * sizeof(float), hipMemcpyDeviceToDevice, s));
-  }
+  }  // v2: the last layer wrote feats (hubert_layers)
+  (void)outD;
   return run.L;
 }
 
@@ -660,12 +661,8 @@ static void e2e_chunk(Ctx& c, float* img, int Fc, float* sal, hipStream_t s, int
   run1(c, lin(feat, 3 * NMEL, B * Fc, 3 * NMEL, c.W("rm.gru.wih"), 6 * GRU_H, c.W("rm.gru.bih"), gi, 6 * GRU_H), s);
   float* go = c.buf<float>("rm.gruout", (size_t)B * Fc * 2 * GRU_H, s);
   unsigned long long* xchg = c.buf<unsigned long long>("rm.xchg", gru_xchg_words(B), s);
-  if (xchg != c.gru_xchg_zeroed || gru_xchg_words(B) > c.gru_xchg_words) {
-    // a new (or grown) allocation holds garbage tags: zero it once (gru_bidir never does)
-    RVCX_HIP(hipMemsetAsync(xchg, 0, sizeof(unsigned long long) * gru_xchg_words(B), s));
-    c.gru_xchg_zeroed = xchg;
-    c.gru_xchg_words = gru_xchg_words(B);
-  }
+  // a new (or regrown) allocation holds garbage tags: zeroed once (gru_bidir never zeroes it)
+  c.zero_once("rm.xchg", xchg, sizeof(unsigned long long) * gru_xchg_words(B), (long long)B, s);
   unsigned* status = c.device_status();  // sticky until the host reads it (Ctx::check_device_status)
   // work the caller wants issued beside the BiGRU (which occupies 4 CUs): the gate event marks this point of the
   // stream, the BiGRU goes out first and the hook's (many) launches after it, so the host time spent issuing
@@ -695,7 +692,6 @@ int64_t rmvpe_forward_b(Ctx& c, const float* audio, int64_t n, int64_t lda, int 
   const int64_t np = n + NFFT;
   const int64_t rows = (np + 31) / 32;
   float* xp = c.buf<float>("rm.xp", (size_t)B * rows * 32, s);
-  if (rows * 32 > np) RVCX_HIP(hipMemsetAsync(xp, 0, (size_t)B * rows * 32 * sizeof(float), s));
   check(reflect_pad_1d(audio, (int)n, NFFT / 2, NFFT / 2, xp, s, B, lda, rows * 32), "reflect_pad");
   float* spec = c.buf<float>("rm.spec", (size_t)B * F * 2 * NBIN, s);
   {

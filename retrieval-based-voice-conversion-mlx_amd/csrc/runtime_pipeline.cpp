@@ -319,6 +319,8 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
   const int I = c.scfg.I;
   int64_t written = 0, ez_off = 0, es_off = 0;
   uint64_t cseed = seed;
+  const bool fuse_trim = chunks.size() == 1 && o.volume_envelope == 1.0;
+  const float* trimmed = out;
   for (size_t i = 0; i < chunks.size(); ++i) {
     const Chunk& ch = chunks[i];
     const int64_t len = ch.a1 - ch.a0;
@@ -336,8 +338,11 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
     if (keep <= 0) throw Error(RVCX_E_SHAPE, "pipeline: chunk too short for the padding");
     if (written + keep > cap)
       throw Error(RVCX_E_CAPACITY, "pipeline: output needs more than " + std::to_string(cap) + " samples");
-    RVCX_HIP(hipMemcpyAsync(out + written, vc + o.t_pad_tgt, (size_t)keep * sizeof(float), hipMemcpyDeviceToDevice,
-                            s));
+    if (fuse_trim)
+      trimmed = vc + o.t_pad_tgt;  // one chunk, no envelope: the peak normalisation reads it in place
+    else
+      RVCX_HIP(hipMemcpyAsync(out + written, vc + o.t_pad_tgt, (size_t)keep * sizeof(float), hipMemcpyDeviceToDevice,
+                              s));
     written += keep;
     cseed += 0x9E3779B97F4A7C15ull;
   }
@@ -347,8 +352,8 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
     float* rws = c.buf<float>("pl.rms", (size_t)(n1 + n2), s);
     check(change_rms(filtered, n, 16000, out, written, c.scfg.sr, (float)o.volume_envelope, rws, s), "change_rms");
   }
-  unsigned* mx = c.buf<unsigned>("pl.max", 4, s);
-  check(peak_normalize(out, written, mx, s), "peak_normalize");
+  float* mx = c.buf<float>("pl.max", peak_normalize_ws_floats(1), s);
+  check(peak_normalize(trimmed, out, written, mx, s), "peak_normalize");
   return written;
 }
 
@@ -463,20 +468,21 @@ int64_t pipeline_forward_batch(Ctx& c, const double* audio, int64_t n, int64_t l
   const int64_t keep = nvc - 2 * o.t_pad_tgt;
   if (keep <= 0) throw Error(RVCX_E_SHAPE, "pipeline_batch: utterance too short for the padding");
   if (keep > ldo) throw Error(RVCX_E_CAPACITY, "pipeline_batch: output rows need " + std::to_string(keep));
+  float* mx = c.buf<float>("pb.max", peak_normalize_ws_floats(B), s);
+  if (o.volume_envelope == 1.0) {  // trim + normalise in one pass over all rows
+    check(peak_normalize(vc + o.t_pad_tgt, out, keep, mx, s, B, nvc, ldo), "peak_normalize");
+    return keep;
+  }
   RVCX_HIP(hipMemcpy2DAsync(out, ldo * sizeof(float), vc + o.t_pad_tgt, nvc * sizeof(float), keep * sizeof(float), B,
                             hipMemcpyDeviceToDevice, s));
-  unsigned* mx = c.buf<unsigned>("pb.max", 4, s);
   for (int b = 0; b < B; ++b) {
-    float* ob = out + (size_t)b * ldo;
-    if (o.volume_envelope != 1.0) {
-      const int n1 = rms_frame_count(n, 16000), n2 = rms_frame_count(keep, c.scfg.sr);
-      float* rws = c.buf<float>("pl.rms", (size_t)(n1 + n2), s);
-      check(change_rms(pad64 + (size_t)b * m + o.t_pad, n, 16000, ob, keep, c.scfg.sr, (float)o.volume_envelope, rws,
-                       s),
-            "change_rms");
-    }
-    check(peak_normalize(ob, keep, mx, s), "peak_normalize");
+    const int n1 = rms_frame_count(n, 16000), n2 = rms_frame_count(keep, c.scfg.sr);
+    float* rws = c.buf<float>("pl.rms", (size_t)(n1 + n2), s);
+    check(change_rms(pad64 + (size_t)b * m + o.t_pad, n, 16000, out + (size_t)b * ldo, keep, c.scfg.sr,
+                     (float)o.volume_envelope, rws, s),
+          "change_rms");
   }
+  check(peak_normalize(out, out, keep, mx, s, B, ldo, ldo), "peak_normalize");
   return keep;
 }
 

@@ -318,7 +318,8 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
   float* har = nullptr;
   if (cf.f0) {
     har = c.buf<float>("dec.har", (size_t)(B * har_ld), s);
-    RVCX_HIP(hipMemsetAsync(har, 0, sizeof(float) * (size_t)(B * har_ld), s));
+    // the pad columns stay zero from call to call (the sources write the interior only)
+    c.zero_once("dec.har", har, sizeof(float) * (size_t)(B * har_ld), har_ld * 65536 + B, s);
     const auto& lin_wb = c.host[0].at("__src_lin__").v;
     const uint64_t sseed = splitmix(seed ^ 0x5352434e4f495345ull);
     if (cf.vocoder == 0) {  // NSF SineGen, harmonic_num 0 (hifigan.py:156-228)

@@ -242,7 +242,10 @@ hipError_t filtfilt_pad(const double* x, long long n, const double* b, const dou
                         const double* FL, int order, long long t_pad, double* ws, double* pad64, float* pad32,
                         hipStream_t s);
 size_t filtfilt_ws_doubles(long long n, int order);
-hipError_t peak_normalize(float* x, long long n, unsigned* ws, hipStream_t s);
+// dst row b = src row b / (max|src row b| / 0.99) when that exceeds 1, else a copy (src == dst: in place)
+hipError_t peak_normalize(const float* src, float* dst, long long n, float* ws, hipStream_t s, int B = 1,
+                          long long lds = 0, long long ldd = 0);
+size_t peak_normalize_ws_floats(int B);
 // Pipeline.get_f0 / Pipeline.pipeline host DSP moved on device (aux_kernels.hip)
 hipError_t f0_autotune(double* f0, int F, double strength, int skip_unvoiced, hipStream_t s);
 hipError_t split_points(const double* x, long long n, int window, long long t_center, long long t_query,
