@@ -259,7 +259,9 @@ def bench_c4(args, eng, dev, dist, rank, world):
                     "gain); random-init weights",
             "config": {"workload": f"C4: {len(job)} x 30 s utterances, LPT-sharded over {world} GPU(s), batched "
                                    f"passes of {args.batch}", "utterances_converted": tot["utterances"],
-                       "batch": args.batch, "parallelism": f"dp{world}"}}
+                       "batch": args.batch, "parallelism": f"dp{world}",
+                       # SURVEY §8d's per-utterance speech_like(seed=1000+i) is replaced by c4_audio's pool
+                       "data_substitution": "pool8_shift_gain"}}
 
 
 def bench_c5(args, eng, dev, dist, rank, world):

@@ -323,8 +323,6 @@ int rvcx_finalize(rvcx_ctx* ctx, int model) {
       throw Error(RVCX_E_INVALID, "unknown model");
     }
     RVCX_HIP(hipDeviceSynchronize());
-    ctx->wsplit_cache.clear();  // weights may have been re-packed at new addresses
-    ctx->rb_wsplit_cache.clear();
     ctx->ready[model] = true;
   });
 }

@@ -117,7 +117,8 @@ struct Ctx {
   std::vector<ProfRec> prof_recs;
   std::vector<hipEvent_t> prof_pool;
   std::unique_ptr<IvfIndex> ivf;  // speaker-embedding index (optional)
-  // pre-split weight images of the weight-streamed conv kernel, per (weight, layout); cleared by rvcx_finalize
+  // pre-split weight images of the weight-streamed conv kernel, per (weight, layout); an entry is dropped when its
+  // weight tensor is re-packed (alloc_weight), so finalizing one model keeps the other models' images
   std::map<std::tuple<const void*, int, long long, int, int, int>, std::unique_ptr<DevBuf>> wsplit_cache;
   const void* wsplit_for(const ConvArgs& a, hipStream_t s);
   // pre-split images of the fused ResBlock pair kernel (resblock_fused.hip), per weight tensor
@@ -152,6 +153,8 @@ struct Ctx {
   // address ranges of the packed weights (alloc_weight): a contraction whose B operand lies in one is static
   std::map<uintptr_t, uintptr_t> wranges;
   bool is_weight(const void* p) const;
+  // forget the split images cached for weights in [lo, hi) (a tensor replaced or an address reused)
+  void drop_splits(uintptr_t lo, uintptr_t hi);
   float* alloc_weight(const std::string& name, const std::vector<float>& data);
   template <class T>
   T* buf(const std::string& name, size_t count, hipStream_t s);

@@ -115,10 +115,27 @@ float* Ctx::alloc_weight(const std::string& name, const std::vector<float>& data
   RVCX_HIP(hipMemcpy(b->p, data.data(), data.size() * sizeof(float), hipMemcpyHostToDevice));
   float* p = static_cast<float*>(b->p);
   auto old = dev.find(name);
-  if (old != dev.end()) wranges.erase(reinterpret_cast<uintptr_t>(old->second->p));
-  wranges[reinterpret_cast<uintptr_t>(p)] = reinterpret_cast<uintptr_t>(p) + bytes;
+  if (old != dev.end()) {
+    const uintptr_t o = reinterpret_cast<uintptr_t>(old->second->p);
+    wranges.erase(o);
+    drop_splits(o, o + old->second->bytes);  // the replaced tensor's split images
+  }
+  const uintptr_t u = reinterpret_cast<uintptr_t>(p);
+  drop_splits(u, u + bytes);  // images cached for an earlier tensor at a reused address
+  wranges[u] = u + bytes;
   dev[name] = std::move(b);
   return p;
+}
+
+void Ctx::drop_splits(uintptr_t lo, uintptr_t hi) {
+  for (auto it = wsplit_cache.begin(); it != wsplit_cache.end();) {
+    const uintptr_t u = reinterpret_cast<uintptr_t>(std::get<0>(it->first));
+    it = (u >= lo && u < hi) ? wsplit_cache.erase(it) : std::next(it);
+  }
+  for (auto it = rb_wsplit_cache.begin(); it != rb_wsplit_cache.end();) {
+    const uintptr_t u = reinterpret_cast<uintptr_t>(it->first);
+    it = (u >= lo && u < hi) ? rb_wsplit_cache.erase(it) : std::next(it);
+  }
 }
 
 bool Ctx::is_weight(const void* q) const {
