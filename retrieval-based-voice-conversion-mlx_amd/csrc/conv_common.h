@@ -29,6 +29,17 @@ static __device__ __forceinline__ float act_fn(float v, int act, float slope) {
   return act_fn_slow(v, act, slope);
 }
 
+// Pre-activation chosen at compile time (kernel MODE bits 0-1: 0 none, 1 leaky ReLU, 2 any other via act_fn): a
+// runtime act switch per element put ~30-120 scalar branches into every A staging pass of the streamed kernels
+enum { PA_NONE = 0, PA_LRELU = 1, PA_ANY = 2 };
+template <int PA>
+static __device__ __forceinline__ float pre_fn(float v, int act, float slope) {
+  if constexpr (PA == PA_NONE) return v;
+  else if constexpr (PA == PA_LRELU) return v > 0.f ? v : v * slope;
+  else return act_fn(v, act, slope);
+}
+static inline int pre_mode(int act) { return act == ACT_NONE ? PA_NONE : (act == ACT_LRELU ? PA_LRELU : PA_ANY); }
+
 static __device__ __forceinline__ void epilogue_store(const ConvArgs& a, float v, float bn, long long m, int n, int oh,
                                                       int ow, const float* R, const float* MK, float* Y) {
   if (a.bias) v += bn;

@@ -6,8 +6,8 @@
 // (chunk, tap) steps), so the LDS-staged kernel's one-step register prefetch leaves every step waiting out a full
 // global-load latency (~1-2 us per step against ~0.2 us of MFMA work). Here both operands run a 3-deep register
 // prefetch ring and nothing waits on a load issued less than two steps earlier:
-//   * B: the weights pre-split once into bf16 plane rows in HBM (conv_wsb.hip's image, k_wsplit), per lane one
-//     16-byte fragment per (plane, 16-column tile) straight from L2 into registers -- no LDS, no conversion;
+//   * B: the weights pre-split once into bf16 planes in HBM (conv_wsb.hip's lane-major image, k_wsplit), per lane
+//     one 16-byte fragment per (plane, 16-column tile) straight from L2 into registers -- no LDS, no conversion;
 //   * A: every (chunk, tap) step GATHERS its BM rows x 32 channels from global memory (no halo reuse: the taps of
 //     these convs are 1..9, so re-reading the shifted rows from L2 costs less than a serial halo stage), a
 //     1-D row at m * stride - pad + tap * dil, a 2-D output pixel's input pixel at (oh - padh + kh, ow - padw + kw);
@@ -25,7 +25,8 @@ namespace {
 
 using namespace splitbf16;
 
-constexpr int GS_WROW = 3 * PLANE;  // bytes of one (chunk, tap, column) row of the pre-split weight image
+constexpr int GS_WROW = 3 * PLANE;  // bytes per column of one (chunk, tap) step of the pre-split weight image
+constexpr int GS_BLK = 1024;       // bytes of one (step, 16-column group, plane) block of that image
 #ifndef GS_DEPTH
 #define GS_DEPTH 3
 #endif
@@ -87,7 +88,10 @@ __device__ __forceinline__ void gs_store(const ConvArgs& a, int m0, int n0, int 
   }
 }
 
-template <int BM, int BN, int WM, int WN, bool TWO_D>
+// MODE bits 0-1: the pre-activation (pre_fn: none, leaky ReLU, other), bit 2: a 1-D pre-mask row multiplier --
+// compile-time, so the step loop carries no per-element activation switch and no conditional mask load (both put ~30
+// scalar branches and a load-history merge into every step)
+template <int BM, int BN, int WM, int WN, bool TWO_D, int MODE>
 __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gs16_kernel(const ConvArgs a, const char* __restrict__ wsp,
                                                                     const int Npad, const int ntn, const int ksplit,
                                                                     const int mfast) {
@@ -95,6 +99,8 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gs16_kernel(const ConvAr
   constexpr int TM16 = BM / (WM * 16);
   constexpr int TN16 = BN / (WN * 16);
   constexpr int AV = BM * EC4 / NT;  // float4 groups of the A tile per thread
+  constexpr int PA = MODE & 3;
+  constexpr bool PMASK = !TWO_D && (MODE & 4) != 0;
   static_assert(WM * WN == 4 && TM16 >= 1 && TN16 >= 1 && BM * EC4 % NT == 0, "tile shape");
   extern __shared__ __attribute__((aligned(16))) char smem_gs[];
 
@@ -119,12 +125,19 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gs16_kernel(const ConvAr
   const int m0 = bx * BM;
   const long long Mtot = TWO_D ? (long long)a.T_out * a.W_out : a.T_out;
   const float* X = a.x + (long long)b * a.x_bs;
-  const float* PM = (!TWO_D && a.pre_mask) ? a.pre_mask + (long long)b * a.pre_mask_bs : nullptr;
+  const float* PM = PMASK ? a.pre_mask + (long long)b * a.pre_mask_bs : nullptr;
+
+  // (chunk, tap) steps [it0, it1) of this split-K slice
+  const int taps = a.taps;
+  const int total = (a.C_in / EK) * taps;
+  const int per = (total + ksplit - 1) / ksplit;
+  const int it0 = zsplit * per, it1 = min(total, it0 + per);
+  const int last = it1 - 1;
 
   // ---- A gather: thread rows r_v = v * 32 + arow, channels ac4..ac4+3 of the step's chunk
   const int arow = store_row(tid / EC4), ac4 = (tid % EC4) << 2;
-  int g0[AV];   // 1-D: input row of tap 0 (m * stride - pad); 2-D: oh
-  int w0v[AV];  // 2-D: ow
+  int g0[AV];   // 1-D: input row of tap 0 (m * stride - pad); 2-D: oh - padh
+  int w0v[AV];  // 2-D: ow - padw
   bool rok[AV];
 #pragma unroll
   for (int v = 0; v < AV; ++v) {
@@ -135,42 +148,74 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gs16_kernel(const ConvAr
       w0v[v] = 0;
     } else {
       const int mm = rok[v] ? (int)m : 0;
-      g0[v] = mm / a.W_out;
-      w0v[v] = mm - g0[v] * a.W_out;
+      const int oh = mm / a.W_out;
+      g0[v] = oh - a.padh;
+      w0v[v] = mm - oh * a.W_out - a.padw;
     }
   }
+  // The next step to gather, kept incrementally (no division per load): a_st with its chunk, tap and (2-D) kernel
+  // row / column; loads past the slice's last step reload it (clamped), harmlessly.
+  int a_st = it0, a_ch = it0 / taps, a_tap = it0 - (it0 / taps) * taps, a_kh = 0, a_kw = 0;
+  if constexpr (TWO_D) {
+    a_kh = a_tap / a.KW;
+    a_kw = a_tap - a_kh * a.KW;
+  }
+  // Loads are branch-free: a row outside the input is read at row 0 (always valid) and zeroed when the slot is split
+  // into LDS (its bit in aok clear). A conditional load (`ok ? load : 0`) merges the loaded and the zero value at the
+  // branch join, and the waitcnt pass then waits for the load right there or at the register's next reuse: with it
+  // the ring ran one step ahead instead of GS_D - 1 (every step waited out a load latency).
   f32x4 ar[GS_D][AV];
-  float am[GS_D][AV];
-  auto load_a = [&](int st, f32x4 (&dst)[AV], float (&dm)[AV]) __attribute__((always_inline)) {
-    const int ch = st / a.taps, tap = st - ch * a.taps;
-    const float* src = X + ch * EK + ac4;
+  float am[GS_D][AV];  // pre-mask value of the row (PMASK only)
+  unsigned aok[GS_D];  // bit v: row v of the slot lies inside the input
+  auto load_a = [&](f32x4 (&dst)[AV], float (&dm)[AV], unsigned& okb) __attribute__((always_inline)) {
+    const float* src = X + a_ch * EK + ac4;
+    okb = 0u;
 #pragma unroll
     for (int v = 0; v < AV; ++v) {
-      long long g;
+      int g;
       bool ok;
       if constexpr (!TWO_D) {
-        g = g0[v] + tap * a.dil;
-        ok = rok[v] && g >= 0 && g < a.T_in;
+        g = g0[v] + a_tap * a.dil;
+        ok = rok[v] && (unsigned)g < (unsigned)a.T_in;
       } else {
-        const int kh = tap / a.KW, kw = tap - kh * a.KW;
-        const int ih = g0[v] - a.padh + kh, iw = w0v[v] - a.padw + kw;
-        ok = rok[v] && ih >= 0 && ih < a.T_in && iw >= 0 && iw < a.W_in;
-        g = (long long)ih * a.W_in + iw;
+        const int ih = g0[v] + a_kh, iw = w0v[v] + a_kw;
+        ok = rok[v] && (unsigned)ih < (unsigned)a.T_in && (unsigned)iw < (unsigned)a.W_in;
+        g = ih * a.W_in + iw;
       }
-      dst[v] = ok ? *reinterpret_cast<const f32x4*>(src + g * a.ldx) : f32x4{0.f, 0.f, 0.f, 0.f};
-      dm[v] = ok ? (PM ? PM[g] : 1.f) : 0.f;
+      const unsigned gc = ok ? (unsigned)g : 0u;
+      dst[v] = *reinterpret_cast<const f32x4*>(src + gc * (unsigned)a.ldx);  // conv_gs_eligible: 32-bit offsets
+      if constexpr (PMASK) dm[v] = PM[gc];
+      okb |= ok ? (1u << v) : 0u;
+    }
+    if (a_st < last) {
+      ++a_st;
+      if (++a_tap == taps) {
+        a_tap = 0;
+        ++a_ch;
+        a_kh = 0;
+        a_kw = 0;
+      } else if constexpr (TWO_D) {
+        if (++a_kw == a.KW) {
+          a_kw = 0;
+          ++a_kh;
+        }
+      }
     }
   };
-  auto store_a = [&](char* As, const f32x4 (&src)[AV], const float (&sm)[AV]) __attribute__((always_inline)) {
+  auto store_a = [&](char* As, const f32x4 (&src)[AV], const float (&sm)[AV], unsigned okb) __attribute__((always_inline)) {
 #pragma unroll
     for (int v = 0; v < AV; ++v) {
       f32x4 val = src[v];
-      if (a.pre_act != ACT_NONE) {
+      const bool ok = (okb >> v) & 1u;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) val[j] = act_fn(val[j], a.pre_act, a.pre_slope);  // act(0) = 0
+      for (int j = 0; j < 4; ++j) val[j] = pre_fn<PA>(val[j], a.pre_act, a.pre_slope);
+      if constexpr (PMASK) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) val[j] = ok ? val[j] * sm[v] : 0.f;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) val[j] = ok ? val[j] : 0.f;
       }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) val[j] *= sm[v];
       put_split4(As + (v * (NT / EC4) + arow) * ERS, ac4, val);
     }
   };
@@ -178,14 +223,15 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gs16_kernel(const ConvAr
   // ---- B: pre-split fragments from L2
   typedef bf16x8 BFrag[TN16][3];
   BFrag br[GS_D];
-  const char* bp = wsp + (size_t)(n0 + wn * TN16 * 16 + lc) * GS_WROW + lg * 16;
+  // the image's lane-major blocks (conv_wsb.hip k_wsplit): lane l reads 16-B slot l, one contiguous 1 KB per load
+  const char* bp = wsp + (size_t)((n0 + wn * TN16 * 16) >> 4) * (3 * GS_BLK) + lane * 16;
   const size_t bstep = (size_t)Npad * GS_WROW;
   auto load_b = [&](int st, BFrag& dst) __attribute__((always_inline)) {
     const char* p = bp + (size_t)st * bstep;
 #pragma unroll
     for (int tn = 0; tn < TN16; ++tn)
 #pragma unroll
-      for (int q = 0; q < 3; ++q) dst[tn][q] = *reinterpret_cast<const bf16x8*>(p + (size_t)tn * 16 * GS_WROW + q * PLANE);
+      for (int q = 0; q < 3; ++q) dst[tn][q] = *reinterpret_cast<const bf16x8*>(p + tn * (3 * GS_BLK) + q * GS_BLK);
   };
 
   f32x4 acc[TM16][TN16];
@@ -216,40 +262,49 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gs16_kernel(const ConvAr
     }
   };
 
-  // (chunk, tap) steps [it0, it1) of this split-K slice. Step i: issue B(i + D - 1), MFMAs on A(i) (LDS buffer
-  // i % 2) and B(i), then A(i + 1) -> LDS buffer (i + 1) % 2, issue A(i + D), one barrier (load indices clamped to
-  // the slice: the tail reloads its last step, harmlessly). Ring slots are (step - it0) % D, compile-time after the
-  // D-fold unroll.
-  const int total = (a.C_in / EK) * a.taps;
-  const int per = (total + ksplit - 1) / ksplit;
-  const int it0 = zsplit * per, it1 = min(total, it0 + per);
+  // Step i: issue B(i + D - 1), MFMAs on A(i) (LDS buffer i % 2) and B(i), then A(i + 1) -> LDS buffer (i + 1) % 2,
+  // issue A(i + D), one barrier (load indices clamped to the slice: the tail reloads its last step, harmlessly). Ring
+  // slots are (step - it0) % D, compile-time after the D-fold unroll. The whole groups of D steps run without a
+  // branch inside (a skipped step would merge two load histories at its join and shorten every wait after it to the
+  // skipped path's), the < D remaining steps after them; the prologue issues its loads in the order the steady state
+  // leaves them (B(i), A(i + 1), B(i + 1), ...), so the loop header merges two identical pending-load histories.
   if (it0 < it1) {
-    const int last = it1 - 1;
     auto clampst = [&](int st) { return st < last ? st : last; };
+    load_a(ar[0], am[0], aok[0]);
 #pragma unroll
-    for (int p = 0; p < GS_D; ++p) load_a(clampst(it0 + p), ar[p], am[p]);
-#pragma unroll
-    for (int p = 0; p < GS_D - 1; ++p) load_b(clampst(it0 + p), br[p]);
-    store_a(smem_gs, ar[0], am[0]);
-    __syncthreads();
-    for (int base = it0; base < it1; base += GS_D) {
-#pragma unroll
-      for (int p = 0; p < GS_D; ++p) {
-        const int i = base + p;
-        if (i < it1) {
-          load_b(clampst(i + GS_D - 1), br[(p + GS_D - 1) % GS_D]);
-          __builtin_amdgcn_sched_barrier(0);
-          compute(smem_gs + (size_t)((i - it0) & 1) * BM * ERS, br[p]);
-          // A(i + 1) -> the other LDS buffer (on the last step a harmless copy of A(last) nobody reads), then A(i + D)
-          // into the slot A(i) left
-          store_a(smem_gs + (size_t)((i + 1 - it0) & 1) * BM * ERS, ar[(p + 1) % GS_D], am[(p + 1) % GS_D]);
-          load_a(clampst(i + GS_D), ar[p], am[p]);
-          __syncthreads();
-        }
-      }
+    for (int p = 1; p < GS_D; ++p) {
+      load_b(clampst(it0 + p - 1), br[p - 1]);
+      load_a(ar[p], am[p], aok[p]);
     }
+    store_a(smem_gs, ar[0], am[0], aok[0]);
+    __syncthreads();
+    auto step = [&](int i, int p) __attribute__((always_inline)) {
+      load_b(clampst(i + GS_D - 1), br[(p + GS_D - 1) % GS_D]);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(smem_gs + (size_t)((i - it0) & 1) * BM * ERS, br[p]);
+      // A(i + 1) -> the other LDS buffer (on the last step a harmless copy of A(last) nobody reads), then A(i + D)
+      // into the slot A(i) left
+      store_a(smem_gs + (size_t)((i + 1 - it0) & 1) * BM * ERS, ar[(p + 1) % GS_D], am[(p + 1) % GS_D],
+              aok[(p + 1) % GS_D]);
+      load_a(ar[p], am[p], aok[p]);
+      __syncthreads();
+    };
+    int base = it0;
+    for (; base + GS_D <= it1; base += GS_D) {
+#pragma unroll
+      for (int p = 0; p < GS_D; ++p) step(base + p, p);
+    }
+#pragma unroll
+    for (int p = 0; p < GS_D - 1; ++p)
+      if (base + p < it1) step(base + p, p);
   }
   gs_store<TM16, TN16, WM, WN>(a, m0, n0, b, zsplit, ksplit, Mtot, acc);
+}
+
+template <int BM, int BN, int WM, int WN, bool TWO_D, int MODE>
+void launch_gs_mode(const ConvArgs& a, dim3 grid, size_t smem, int ntn, int ksplit, int mfast, hipStream_t s) {
+  hipLaunchKernelGGL((conv_gs16_kernel<BM, BN, WM, WN, TWO_D, MODE>), grid, dim3(CONV_THREADS), smem, s, a,
+                     static_cast<const char*>(a.wsplit), a.wsplit_npad, ntn, ksplit, mfast);
 }
 
 template <int BM, int BN, int WM, int WN, bool TWO_D>
@@ -268,8 +323,15 @@ hipError_t launch_gs(const ConvArgs& a, int ntn_enable, int ksplit, hipStream_t 
   }();
   const double wbytes = 6.0 * a.N * a.C_in * a.taps, abytes = 4.0 * (double)Mtot * a.C_in * a.batch;
   const int mfast = mf_env >= 0 ? mf_env : (wbytes > abytes ? 1 : 0);
-  hipLaunchKernelGGL((conv_gs16_kernel<BM, BN, WM, WN, TWO_D>), grid, dim3(CONV_THREADS), smem, s, a,
-                     static_cast<const char*>(a.wsplit), a.wsplit_npad, ntn, ksplit, mfast);
+  const int mode = pre_mode(a.pre_act) | (!TWO_D && a.pre_mask ? 4 : 0);
+  switch (mode) {
+    case 0: launch_gs_mode<BM, BN, WM, WN, TWO_D, 0>(a, grid, smem, ntn, ksplit, mfast, s); break;
+    case 1: launch_gs_mode<BM, BN, WM, WN, TWO_D, 1>(a, grid, smem, ntn, ksplit, mfast, s); break;
+    case 2: launch_gs_mode<BM, BN, WM, WN, TWO_D, 2>(a, grid, smem, ntn, ksplit, mfast, s); break;
+    case 4: launch_gs_mode<BM, BN, WM, WN, TWO_D, 4>(a, grid, smem, ntn, ksplit, mfast, s); break;
+    case 5: launch_gs_mode<BM, BN, WM, WN, TWO_D, 5>(a, grid, smem, ntn, ksplit, mfast, s); break;
+    default: launch_gs_mode<BM, BN, WM, WN, TWO_D, 6>(a, grid, smem, ntn, ksplit, mfast, s); break;
+  }
   return hipGetLastError();
 }
 
@@ -280,6 +342,9 @@ bool conv_gs_eligible(const ConvArgs& a, bool two_d) {
   const bool common = a.batch_inner == 1 && !a.b_kn && a.C_in % EK == 0 && a.C_in > 0 && a.taps >= 1 && vec_a &&
                       a.out_map == OUT_ROWS && a.stride >= 1 && a.dil >= 1;
   if (!common) return false;
+  // 32-bit element offsets within one batch entry (the A gather)
+  const long long rows_in = two_d ? (long long)a.T_in * a.W_in : a.T_in;
+  if (rows_in * a.ldx + a.C_in >= INT32_MAX) return false;
   if (!two_d) return (long long)a.T_out * a.stride < INT32_MAX / 2 && a.T_in < INT32_MAX / 2;
   return a.taps == a.KH * a.KW && !a.pre_mask && a.stride == 1 && a.W_out >= 1 && a.W_in >= 1;
 }

@@ -33,8 +33,12 @@ constexpr int WROW = 3 * PLANE;  // bytes of one (chunk, tap, column) row of spl
 constexpr int WSB_HALO = 64;     // max (taps - 1) * dil: the A prefetch registers cover BM + 64 rows
 constexpr int WSB_ROWS_2D = 224;  // 2-D: pixel-window rows the A prefetch registers cover (3x3 windows of 128 px)
 
-// w [tap][n][c] (ldw, w_ts) -> out rows ((ch * taps + tap) * Npad + n) of [hi | mid | lo] x 32 bf16; zero
-// beyond N and C_in. The plane arithmetic is put_split1's.
+// w [tap][n][c] (ldw, w_ts) -> the pre-split image: per (chunk, tap) step, per 16-column group and plane a 1 KB
+// block laid out lane-major for the 16x16x32 MFMA B operand: 16-B slot g * 16 + j holds channels 8g..8g+7 of column
+// 16 * group + j, so one wave's fragment load of a plane is one contiguous 1 KB (8 whole 128-B lines) -- the earlier
+// [column][hi | mid | lo] rows made every such load touch 16-24 lines for 64-B pieces of each. Zero beyond N and
+// C_in. The plane arithmetic is put_split1's.
+constexpr int WBLK = 1024;  // bytes of one (step, 16-column group, plane) block
 __global__ void k_wsplit(const float* __restrict__ w, int ldw, long long w_ts, int N, int C_in, int taps, int nchunks,
                          int Npad, unsigned short* __restrict__ out) {
   const long long total = (long long)nchunks * taps * Npad * EK;
@@ -51,10 +55,11 @@ __global__ void k_wsplit(const float* __restrict__ w, int ldw, long long w_ts, i
     const float rr = v - lo_f(h);
     const unsigned m = pk_bf16(rr, 0.f);
     const unsigned l = pk_bf16(rr - lo_f(m), 0.f);
-    unsigned short* o = out + r * (3 * EK);
-    o[c] = (unsigned short)h;
-    o[EK + c] = (unsigned short)m;
-    o[2 * EK + c] = (unsigned short)l;
+    const long long blk = (ct * (Npad / 16) + n / 16) * 3;
+    unsigned short* o = out + blk * (WBLK / 2) + ((c >> 3) * 16 + (n & 15)) * 8 + (c & 7);
+    o[0] = (unsigned short)h;
+    o[WBLK / 2] = (unsigned short)m;
+    o[WBLK] = (unsigned short)l;
   }
 }
 
@@ -103,9 +108,11 @@ __global__ __launch_bounds__(CONV_THREADS, (BM == 128 && BN == 64 && !TWO_D) ? W
     const int r = !TWO_D ? ml : ((ml < rh * rw) ? (ml / rw) * aw + (ml % rw) : 0);
     aoff[tm] = r * ERS + hk * 16;
   }
+  // lane (column li, k-half hk): in the image block of its 16-column group, 16-B slot (2 s + hk) * 16 + li % 16
   const char* bp[TN];
 #pragma unroll
-  for (int tn = 0; tn < TN; ++tn) bp[tn] = wsp + (size_t)(n0 + wn * TN * 32 + tn * 32 + li) * WROW + hk * 16;
+  for (int tn = 0; tn < TN; ++tn)
+    bp[tn] = wsp + (size_t)((n0 + wn * TN * 32 + tn * 32 + li) >> 4) * (3 * WBLK) + hk * 256 + (li & 15) * 16;
   const size_t bstep = (size_t)Npad * WROW;  // one (chunk, tap) iteration
 
   f32x16 acc[TM][TN];
@@ -119,11 +126,14 @@ __global__ __launch_bounds__(CONV_THREADS, (BM == 128 && BN == 64 && !TWO_D) ? W
   // ---- A: the chunk's nrows_a x 32 halo tile (1-D rows / 2-D pixel window), prefetched into registers one chunk
   // ahead
   constexpr int AP = ((TWO_D ? WSB_ROWS_2D : BM + WSB_HALO) * EC4 + NT - 1) / NT;
+  // branch-free prefetch (conv_gs.hip load_a): rows outside the input read row 0 and are zeroed when split into LDS
   f32x4 apre[AP];
   float apm[AP];
+  unsigned long long aok = 0ull;
   const int arow = store_row(tid / EC4), ac4 = (tid % EC4) << 2;
   auto load_a_regs = [&](int c0) __attribute__((always_inline)) {
     const float* src0 = X + c0 + ac4;
+    aok = 0ull;
 #pragma unroll
     for (int v = 0; v < AP; ++v) {
       const int r = v * (NT / EC4) + arow;
@@ -138,8 +148,10 @@ __global__ __launch_bounds__(CONV_THREADS, (BM == 128 && BN == 64 && !TWO_D) ? W
         ok = r < nrows_a && gh >= 0 && gh < a.T_in && gw >= 0 && gw < a.W_in;
         g = (long long)gh * a.W_in + gw;
       }
-      apre[v] = ok ? *reinterpret_cast<const f32x4*>(src0 + g * a.ldx) : f32x4{0.f, 0.f, 0.f, 0.f};
-      apm[v] = ok ? (PM ? PM[g] : 1.f) : 0.f;
+      const long long gc = ok ? g : 0;
+      apre[v] = *reinterpret_cast<const f32x4*>(src0 + gc * a.ldx);
+      apm[v] = PM ? PM[gc] : 1.f;
+      aok |= ok ? (1ull << v) : 0ull;
     }
   };
   auto write_a_regs = [&]() __attribute__((always_inline)) {
@@ -148,12 +160,13 @@ __global__ __launch_bounds__(CONV_THREADS, (BM == 128 && BN == 64 && !TWO_D) ? W
       const int r = v * (NT / EC4) + arow;
       if (r < nrows_a) {
         f32x4 val = apre[v];
+        const bool ok = (aok >> v) & 1ull;
         if (a.pre_act != ACT_NONE) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) val[j] = act_fn(val[j], a.pre_act, a.pre_slope);  // act(0) = 0
+          for (int j = 0; j < 4; ++j) val[j] = act_fn(val[j], a.pre_act, a.pre_slope);
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) val[j] *= apm[v];
+        for (int j = 0; j < 4; ++j) val[j] = ok ? val[j] * apm[v] : 0.f;
         put_split4(As + r * ERS, ac4, val);
       }
     }
@@ -169,7 +182,7 @@ __global__ __launch_bounds__(CONV_THREADS, (BM == 128 && BN == 64 && !TWO_D) ? W
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int q = 0; q < 3; ++q)
-          dst[tn][s * 3 + q] = *reinterpret_cast<const bf16x8*>(bp[tn] + o + q * PLANE + s * 32);
+          dst[tn][s * 3 + q] = *reinterpret_cast<const bf16x8*>(bp[tn] + o + q * WBLK + s * 512);
   };
   auto compute = [&](int tap, const BFrag& bf) __attribute__((always_inline)) {
     const int toff = (TWO_D ? (tap / a.KW) * aw + (tap % a.KW) : tap * a.dil) * ERS;
@@ -319,11 +332,14 @@ __device__ __forceinline__ void conv_store_tile16(const ConvArgs& a, const TileP
   }
 }
 
-template <int BM, int BN, int WM, int WN>
+// MODE: bits 0-1 the pre-activation (pre_fn), bit 2 a pre-mask row multiplier (conv_gs.hip's MODE)
+template <int BM, int BN, int WM, int WN, int MODE>
 __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 : 3) void conv_wsb16_kernel(const ConvArgs a, const char* __restrict__ wsp,
                                                                      const int Npad, const int nrows_a, const int ntn,
                                                                      const int ksplit) {
   constexpr int NT = CONV_THREADS;
+  constexpr int PA = MODE & 3;
+  constexpr bool PMASK = (MODE & 4) != 0;
   constexpr int TM16 = BM / (WM * 16);
   constexpr int TN16 = BN / (WN * 16);
   static_assert(WM * WN == 4 && TM16 >= 1 && TN16 >= 1, "4 waves, whole 16x16 sub-tiles");
@@ -342,15 +358,15 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
   const int n0 = by * BN;
   const int m0 = bx * BM;
   const float* X = a.x + (long long)b * a.x_bs;
-  const float* PM = a.pre_mask ? a.pre_mask + (long long)b * a.pre_mask_bs : nullptr;
+  const float* PM = PMASK ? a.pre_mask + (long long)b * a.pre_mask_bs : nullptr;
   const int row0 = m0 - a.pad;
 
   int aoff[TM16];
 #pragma unroll
   for (int tm = 0; tm < TM16; ++tm) aoff[tm] = (wm * TM16 * 16 + tm * 16 + lc) * ERS + lg * 16;
-  const char* bp[TN16];
+  const char* bp[TN16];  // lane l reads 16-B slot l of each block: one contiguous 1 KB per wave load
 #pragma unroll
-  for (int tn = 0; tn < TN16; ++tn) bp[tn] = wsp + (size_t)(n0 + wn * TN16 * 16 + tn * 16 + lc) * WROW + lg * 16;
+  for (int tn = 0; tn < TN16; ++tn) bp[tn] = wsp + (size_t)((n0 + wn * TN16 * 16 + tn * 16) >> 4) * (3 * WBLK) + lane * 16;
   const size_t bstep = (size_t)Npad * WROW;
 
   f32x4 acc[TM16][TN16];
@@ -362,16 +378,20 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
   constexpr int AP = ((BM + WSB_HALO) * EC4 + NT - 1) / NT;
   f32x4 apre[AP];
   float apm[AP];
+  unsigned aok = 0u;  // branch-free prefetch, as conv_wsb_kernel's
   const int arow = store_row(tid / EC4), ac4 = (tid % EC4) << 2;
   auto load_a_regs = [&](int c0) __attribute__((always_inline)) {
     const float* src0 = X + c0 + ac4;
+    aok = 0u;
 #pragma unroll
     for (int v = 0; v < AP; ++v) {
       const int r = v * (NT / EC4) + arow;
       const long long g = row0 + r;
       const bool ok = r < nrows_a && g >= 0 && g < a.T_in;
-      apre[v] = ok ? *reinterpret_cast<const f32x4*>(src0 + g * a.ldx) : f32x4{0.f, 0.f, 0.f, 0.f};
-      apm[v] = ok ? (PM ? PM[g] : 1.f) : 0.f;
+      const long long gc = ok ? g : 0;
+      apre[v] = *reinterpret_cast<const f32x4*>(src0 + gc * a.ldx);
+      if constexpr (PMASK) apm[v] = PM[gc];
+      aok |= ok ? (1u << v) : 0u;
     }
   };
   auto write_a_regs = [&]() __attribute__((always_inline)) {
@@ -380,12 +400,16 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
       const int r = v * (NT / EC4) + arow;
       if (r < nrows_a) {
         f32x4 val = apre[v];
-        if (a.pre_act != ACT_NONE) {
+        const bool ok = (aok >> v) & 1u;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) val[j] = act_fn(val[j], a.pre_act, a.pre_slope);
+        for (int j = 0; j < 4; ++j) val[j] = pre_fn<PA>(val[j], a.pre_act, a.pre_slope);
+        if constexpr (PMASK) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) val[j] = ok ? val[j] * apm[v] : 0.f;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) val[j] = ok ? val[j] : 0.f;
         }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) val[j] *= apm[v];
         put_split4(As + r * ERS, ac4, val);
       }
     }
@@ -396,7 +420,7 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
 #pragma unroll
     for (int tn = 0; tn < TN16; ++tn)
 #pragma unroll
-      for (int q = 0; q < 3; ++q) dst[tn][q] = *reinterpret_cast<const bf16x8*>(bp[tn] + o + q * PLANE);
+      for (int q = 0; q < 3; ++q) dst[tn][q] = *reinterpret_cast<const bf16x8*>(bp[tn] + o + q * WBLK);
   };
   auto compute = [&](int tap, const BFrag& bf) __attribute__((always_inline)) {
     const int toff = tap * a.dil * ERS;
@@ -461,13 +485,20 @@ hipError_t launch_wsb16(const ConvArgs& a, int ntn_enable, int ksplit, hipStream
   const int ntiles = (a.N + BN - 1) / BN;
   const int ntn = ntn_enable ? ntiles : 0;
   dim3 grid(ntn ? mtiles * ntiles : mtiles, ntn ? 1 : ntiles, a.batch * ksplit);
-  auto kern = conv_wsb16_kernel<BM, BN, WM, WN>;
-  static size_t smem_set = 64 * 1024;
-  if (smem > smem_set) {
+  const int mode = pre_mode(a.pre_act) | (a.pre_mask ? 4 : 0);
+  auto kern = mode == 0   ? conv_wsb16_kernel<BM, BN, WM, WN, 0>
+              : mode == 1 ? conv_wsb16_kernel<BM, BN, WM, WN, 1>
+              : mode == 2 ? conv_wsb16_kernel<BM, BN, WM, WN, 2>
+              : mode == 4 ? conv_wsb16_kernel<BM, BN, WM, WN, 4>
+              : mode == 5 ? conv_wsb16_kernel<BM, BN, WM, WN, 5>
+                          : conv_wsb16_kernel<BM, BN, WM, WN, 6>;
+  // per instantiation: raise the dynamic-LDS limit once, not per launch
+  static size_t smem_set[8] = {64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024};
+  if (smem > smem_set[mode & 7]) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
-    smem_set = smem;
+    smem_set[mode & 7] = smem;
   }
   hipLaunchKernelGGL(kern, grid, dim3(CONV_THREADS), smem, s, a, static_cast<const char*>(a.wsplit), a.wsplit_npad,
                      nrows_a, ntn, ksplit);
