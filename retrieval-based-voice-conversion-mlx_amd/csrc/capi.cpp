@@ -43,7 +43,19 @@ namespace rvcx {
 hipStream_t Ctx::aux_stream() {
   if (!aux) {
     RVCX_HIP(hipSetDevice(device));
-    RVCX_HIP(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
+    // RVCX_AUX_PRIO=1: the aux stream (HuBERT beside RMVPE) at the device's least priority, so the critical RMVPE
+    // chain's workgroups are dispatched first when both queues have work
+    static const int low = [] {
+      const char* e = std::getenv("RVCX_AUX_PRIO");
+      return e ? std::atoi(e) : 0;
+    }();
+    int least = 0, greatest = 0;
+    if (low && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && least != greatest) {
+      RVCX_HIP(hipStreamCreateWithPriority(&aux, hipStreamNonBlocking, least));
+    } else {
+      (void)hipGetLastError();
+      RVCX_HIP(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
+    }
     RVCX_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     RVCX_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
     RVCX_HIP(hipEventCreateWithFlags(&ev_gate, hipEventDisableTiming));

@@ -62,6 +62,110 @@ static __device__ __forceinline__ void epilogue_store(const ConvArgs& a, float v
   *dst = v;
 }
 
+// The 16x16 accumulator tiles of a wave (v_mfma_f32_16x16x32 C layout: lane l holds column l % 16, rows 4 (l / 16) + r)
+// -> HBM or the split-K slab, with the shared epilogue (epilogue_store's order of operations, bit-identical). The
+// epilogue switches are uniform and tested once per 4-element group, each around its group-wide operation: tested
+// per element (as epilogue_store does) they cost ~25 scalar branches per output, as much as a short tile's MMA loop.
+template <int TM16, int TN16, int WM, int WN>
+__device__ __forceinline__ void store_tile16(const ConvArgs& a, int m0, int n0, int b, int zsplit, int ksplit,
+                                             long long Mtot, f32x4 (&acc)[TM16][TN16]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int lc = lane & 15, lg = lane >> 4;
+  if (ksplit > 1) {
+#pragma unroll
+    for (int tn = 0; tn < TN16; ++tn) {
+      const int n = n0 + wn * TN16 * 16 + tn * 16 + lc;
+#pragma unroll
+      for (int tm = 0; tm < TM16; ++tm) {
+        const long long mb = (long long)m0 + wm * TM16 * 16 + tm * 16 + 4 * lg;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (n < a.N && mb + r < Mtot) a.ws[(((long long)b * ksplit + zsplit) * a.ws_rows + mb + r) * a.N + n] = acc[tm][tn][r];
+      }
+    }
+    return;
+  }
+  const float* bias = a.bias ? a.bias + (long long)b * a.bias_bs : nullptr;
+  const float* R = a.res ? a.res + (long long)b * a.res_bs : nullptr;
+  const float* MK = a.mask ? a.mask + (long long)b * a.mask_bs : nullptr;
+  float* Y = a.y + (long long)b * a.y_bs;
+  const bool need_r = R && a.res_mode != RES_NONE;
+  const bool need_d = a.acc_mode != ACC_STORE;
+  const int act = a.act;
+#pragma unroll
+  for (int tn = 0; tn < TN16; ++tn) {
+    const int n = n0 + wn * TN16 * 16 + tn * 16 + lc;
+    const bool n_ok = n < a.N;
+    const float bn = (bias && n_ok) ? bias[n] : 0.f;
+#pragma unroll
+    for (int tm = 0; tm < TM16; ++tm) {
+      const long long mb = (long long)m0 + wm * TM16 * 16 + tm * 16 + 4 * lg;
+      bool ok[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ok[r] = n_ok && mb + r < Mtot;
+      f32x4 v = acc[tm][tn];
+      f32x4 rv = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f}, mv = {1.f, 1.f, 1.f, 1.f};
+      // gather first (residual / accumulate / mask operands), then the arithmetic, then the stores
+      if (need_r) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rv[r] = ok[r] ? R[(mb + r) * a.ldr + n] : 0.f;
+      }
+      if (need_d) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dv[r] = ok[r] ? Y[(mb + r) * a.ldy + n] : 0.f;
+      }
+      if (MK) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mv[r] = ok[r] ? MK[mb + r] : 1.f;
+      }
+      if (bias) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += bn;
+      }
+      if (a.res_mode == RES_ADD_PRE) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = v[r] + rv[r];
+      }
+      if (a.alpha != 1.f) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] *= a.alpha;
+      }
+      if (act == ACT_LRELU) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope;
+      } else if (act == ACT_RELU) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
+      } else if (act != ACT_NONE) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = act_fn_slow(v[r], act, a.slope);
+      }
+      if (a.res_mode == RES_ADD_POST) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = v[r] + rv[r];
+      } else if (a.res_mode == RES_RSUB_POST) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = rv[r] - v[r];
+      }
+      if (a.acc_mode == ACC_ADD) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = dv[r] + v[r];
+      } else if (a.acc_mode == ACC_ADD_DIV) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (dv[r] + v[r]) / a.acc_div;
+      }
+      if (MK) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] *= mv[r];
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (ok[r]) Y[(mb + r) * a.ldy + n] = v[r];
+    }
+  }
+}
+
 // Where a block tile sits: output rows m0.. (1-D) or the rh x rw pixel window at (h0, w0) (2-D), output channels
 // n0.., outer/inner batch (b, bi), split-K slice zsplit of ksplit for batch entry zb.
 struct TilePos {

@@ -32,62 +32,6 @@ constexpr int GS_BLK = 1024;       // bytes of one (step, 16-column group, plane
 #endif
 constexpr int GS_D = GS_DEPTH;      // prefetch ring depth (steps in flight per operand)
 
-// The accumulator tiles of a wave -> HBM / split-K slab. C layout of a 16x16 tile: lane l holds column l % 16, rows
-// 4 (l / 16) + r, r = 0..3. Rows are output rows (1-D) or flattened output pixels oh * W_out + ow (2-D, OUT_ROWS).
-template <int TM16, int TN16, int WM, int WN>
-__device__ __forceinline__ void gs_store(const ConvArgs& a, int m0, int n0, int b, int zsplit, int ksplit, long long Mtot,
-                                         f32x4 (&acc)[TM16][TN16]) {
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  const int lc = lane & 15, lg = lane >> 4;
-  const float* bias = a.bias ? a.bias + (long long)b * a.bias_bs : nullptr;
-  const float* R = a.res ? a.res + (long long)b * a.res_bs : nullptr;
-  const float* MK = a.mask ? a.mask + (long long)b * a.mask_bs : nullptr;
-  float* Y = a.y + (long long)b * a.y_bs;
-  const bool need_r = R && a.res_mode != RES_NONE;
-  const bool need_d = a.acc_mode != ACC_STORE;
-#pragma unroll
-  for (int tn = 0; tn < TN16; ++tn) {
-    const int n = n0 + wn * TN16 * 16 + tn * 16 + lc;
-    const bool n_ok = n < a.N;
-    const float bn = (bias && n_ok) ? bias[n] : 0.f;
-#pragma unroll
-    for (int tm = 0; tm < TM16; ++tm) {
-      const long long mb = (long long)m0 + wm * TM16 * 16 + tm * 16 + 4 * lg;
-      if (ksplit > 1) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (n_ok && mb + r < Mtot) a.ws[(((long long)b * ksplit + zsplit) * a.ws_rows + mb + r) * a.N + n] = acc[tm][tn][r];
-        continue;
-      }
-      float rv[4], dv[4], mv[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const bool ok = n_ok && mb + r < Mtot;
-        rv[r] = (ok && need_r) ? R[(mb + r) * a.ldr + n] : 0.f;
-        dv[r] = (ok && need_d) ? Y[(mb + r) * a.ldy + n] : 0.f;
-        mv[r] = (ok && MK) ? MK[mb + r] : 1.f;
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (!(n_ok && mb + r < Mtot)) continue;
-        float v = acc[tm][tn][r];
-        if (a.bias) v += bn;
-        if (a.res_mode == RES_ADD_PRE) v = v + rv[r];
-        if (a.alpha != 1.f) v *= a.alpha;
-        v = act_fn(v, a.act, a.slope);
-        if (a.res_mode == RES_ADD_POST) v = v + rv[r];
-        else if (a.res_mode == RES_RSUB_POST) v = rv[r] - v;
-        if (a.acc_mode == ACC_ADD) v = dv[r] + v;
-        else if (a.acc_mode == ACC_ADD_DIV) v = (dv[r] + v) / a.acc_div;
-        if (MK) v *= mv[r];
-        Y[(mb + r) * a.ldy + n] = v;
-      }
-    }
-  }
-}
-
 // MODE bits 0-1: the pre-activation (pre_fn: none, leaky ReLU, other), bit 2: a 1-D pre-mask row multiplier --
 // compile-time, so the step loop carries no per-element activation switch and no conditional mask load (both put ~30
 // scalar branches and a load-history merge into every step)
@@ -298,7 +242,7 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gs16_kernel(const ConvAr
     for (int p = 0; p < GS_D - 1; ++p)
       if (base + p < it1) step(base + p, p);
   }
-  gs_store<TM16, TN16, WM, WN>(a, m0, n0, b, zsplit, ksplit, Mtot, acc);
+  store_tile16<TM16, TN16, WM, WN>(a, m0, n0, b, zsplit, ksplit, Mtot, acc);
 }
 
 template <int BM, int BN, int WM, int WN, bool TWO_D, int MODE>

@@ -277,61 +277,6 @@ __global__ __launch_bounds__(CONV_THREADS, (BM == 128 && BN == 64 && !TWO_D) ? W
 // cycles per step as the 32x32x16 form at the same wave tile. The chip sustains a higher clock on this shape under
 // power-limited load (MI355X_MICROARCH.md "DVFS give-back" item 7), which is the point.
 // C layout of a 16x16 tile: lane l holds column l % 16, rows 4 (l / 16) + r, r = 0..3.
-template <int TM16, int TN16, int WM, int WN>
-__device__ __forceinline__ void conv_store_tile16(const ConvArgs& a, const TilePos& p, f32x4 (&acc)[TM16][TN16]) {
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  const int lc = lane & 15, lg = lane >> 4;
-  const float* bias = a.bias ? a.bias + (long long)p.b * a.bias_bs : nullptr;
-  const float* R = a.res ? a.res + (long long)p.b * a.res_bs : nullptr;
-  const float* MK = a.mask ? a.mask + (long long)p.b * a.mask_bs : nullptr;
-  float* Y = a.y + (long long)p.b * a.y_bs;
-  const bool need_r = R && a.res_mode != RES_NONE;
-  const bool need_d = a.acc_mode != ACC_STORE;
-#pragma unroll
-  for (int tn = 0; tn < TN16; ++tn) {
-    const int n = p.n0 + wn * TN16 * 16 + tn * 16 + lc;
-    const bool n_ok = n < a.N;
-    const float bn = (bias && n_ok) ? bias[n] : 0.f;
-#pragma unroll
-    for (int tm = 0; tm < TM16; ++tm) {
-      const int mb = p.m0 + wm * TM16 * 16 + tm * 16 + 4 * lg;
-      if (p.ksplit > 1) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (n_ok && mb + r < a.T_out)
-            a.ws[(((long long)p.zb * p.ksplit + p.zsplit) * a.ws_rows + mb + r) * a.N + n] = acc[tm][tn][r];
-        continue;
-      }
-      // gather first (residual / accumulate / mask operands of the lane's 4 outputs), then store
-      float rv[4], dv[4], mv[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const bool ok = n_ok && mb + r < a.T_out;
-        rv[r] = (ok && need_r) ? R[(long long)(mb + r) * a.ldr + n] : 0.f;
-        dv[r] = (ok && need_d) ? Y[(long long)(mb + r) * a.ldy + n] : 0.f;
-        mv[r] = (ok && MK) ? MK[mb + r] : 1.f;
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (!(n_ok && mb + r < a.T_out)) continue;
-        float v = acc[tm][tn][r];
-        if (a.bias) v += bn;
-        if (a.res_mode == RES_ADD_PRE) v = v + rv[r];
-        if (a.alpha != 1.f) v *= a.alpha;
-        v = act_fn(v, a.act, a.slope);
-        if (a.res_mode == RES_ADD_POST) v = v + rv[r];
-        else if (a.res_mode == RES_RSUB_POST) v = rv[r] - v;
-        if (a.acc_mode == ACC_ADD) v = dv[r] + v;
-        else if (a.acc_mode == ACC_ADD_DIV) v = (dv[r] + v) / a.acc_div;
-        if (MK) v *= mv[r];
-        Y[(long long)(mb + r) * a.ldy + n] = v;
-      }
-    }
-  }
-}
-
 // MODE: bits 0-1 the pre-activation (pre_fn), bit 2 a pre-mask row multiplier (conv_gs.hip's MODE)
 template <int BM, int BN, int WM, int WN, int MODE>
 __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 : 3) void conv_wsb16_kernel(const ConvArgs a, const char* __restrict__ wsp,
@@ -473,7 +418,7 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
       if (it + 1 < it1) step(it + 1, b1, b0);
     }
   }
-  conv_store_tile16<TM16, TN16, WM, WN>(a, TilePos{m0, 0, 0, 0, 0, n0, b, 0, b, zsplit, ksplit}, acc);
+  store_tile16<TM16, TN16, WM, WN>(a, m0, n0, b, zsplit, ksplit, (long long)a.T_out, acc);
 }
 
 template <int BM, int BN, int WM, int WN>

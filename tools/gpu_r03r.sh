@@ -1,0 +1,12 @@
+#!/bin/bash
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+TAG=${1:-r}
+timeout -k 10 600 python -u -m pytest -m gpu -x -v -s --timeout 120 --timeout-method thread tests/test_gpu_conv_math.py tests/test_gpu_c2_parity.py tests/test_gpu_models.py tests/test_gpu_resblock_fused.py tests/test_gpu_sizes.py > gpurun_out/gt_$TAG.log 2>&1 || { echo "tests failed"; grep -E "FAILED|Error|^E " gpurun_out/gt_$TAG.log | head -30; exit 1; }
+grep -E "passed|failed" gpurun_out/gt_$TAG.log | tail -1
+bash tools/ab_lib.sh build/ab/librvcx_base.so 2 || exit 1
+rm -f gpurun_out/convdump_$TAG.csv
+RVCX_PROF_DUMP=gpurun_out/convdump_$TAG.csv timeout -k 10 200 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --roofline-pass after > gpurun_out/dump_$TAG.json 2> gpurun_out/dump_$TAG.err || { echo "dump failed"; tail gpurun_out/dump_$TAG.err; exit 1; }
+python tools/convdump_summary.py gpurun_out/convdump_$TAG.csv 40 > gpurun_out/convdump_$TAG.txt
+head -30 gpurun_out/convdump_$TAG.txt
