@@ -20,11 +20,6 @@ namespace rvcx {
 namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ float act_small(float v, int act, float slope) {
-  if (act == ACT_RELU) return v > 0.f ? v : 0.f;
-  if (act == ACT_LRELU) return v > 0.f ? v : v * slope;
-  return v;
-}
 }  // namespace
 
 constexpr int SIT = 17;  // staging rounds of 256 float4 per block: (RH + 2) x (W + 2) x CIN / 4 <= 17 x 256 (all U-Net levels)
@@ -120,27 +115,53 @@ __global__ __launch_bounds__(256) void k_conv2d_small(const ConvArgs a, const in
       }
     }
   }
-  // ---- epilogue: lane holds rows (pixels) 4*kq + i of fragment p, column (channel) li of fragment t
+  // ---- epilogue: lane holds rows (pixels) 4*kq + i of fragment p, column (channel) li of fragment t. The uniform
+  // switches (alpha, act, residual) are tested once per 4-pixel group around the group-wide operation (per element
+  // they were ~10 scalar branches per output, as in store_tile16)
   float* Y = a.y + (long long)b * a.y_bs;
   const float* R = a.res ? a.res + (long long)b * a.res_bs : nullptr;
+  const bool res = a.res_mode == RES_ADD_POST;
+  const int act = a.act;
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int n = t * 16 + li;
     const float bn = a.bias ? a.bias[n] : 0.f;
 #pragma unroll
     for (int p = 0; p < TPW; ++p) {
+      long long m[4];
+      bool ok[4];
+      f32x4 v = acc[p][t], rv = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int pix = wave * (PIX / 4) + p * 16 + 4 * kq + i;
         const int gh = h0 + pix / W, gw = pix % W;
-        if (gh >= H) continue;
-        const long long m = (long long)gh * W + gw;
-        float v = acc[p][t][i] + bn;
-        if (a.alpha != 1.f) v *= a.alpha;
-        v = act_small(v, a.act, a.slope);
-        if (a.res_mode == RES_ADD_POST) v = v + R[m * a.ldr + n];
-        Y[m * a.ldy + n] = v;
+        ok[i] = gh < H;
+        m[i] = (long long)(ok[i] ? gh : 0) * W + gw;
       }
+      if (res) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rv[i] = R[m[i] * a.ldr + n];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] += bn;
+      if (a.alpha != 1.f) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] *= a.alpha;
+      }
+      if (act == ACT_RELU) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = v[i] > 0.f ? v[i] : 0.f;
+      } else if (act == ACT_LRELU) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = v[i] > 0.f ? v[i] : v[i] * a.slope;
+      }
+      if (res) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = v[i] + rv[i];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (ok[i]) Y[m[i] * a.ldy + n] = v[i];
     }
   }
 }

@@ -244,22 +244,54 @@ __device__ __forceinline__ void conv_store_tile(const ConvArgs& a, const TilePos
             dv[i] = (ok && need_d) ? Yl[ro * a.ldy] : 0.f;
             mv[i] = (ok && MK) ? Ml[ro] : 1.f;
           }
+          // the uniform switches once per 8-element half, each around its half-wide operation (store_tile16)
+          float v[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) v[i] = acc[tm][tn][8 * h + i];
+          if (a.bias) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] += bn;
+          }
+          if (a.res_mode == RES_ADD_PRE) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = v[i] + rv[i];
+          }
+          if (a.alpha != 1.f) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] *= a.alpha;
+          }
+          if (a.act == ACT_LRELU) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = v[i] > 0.f ? v[i] : v[i] * a.slope;
+          } else if (a.act == ACT_RELU) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = v[i] > 0.f ? v[i] : 0.f;
+          } else if (a.act != ACT_NONE) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = act_fn_slow(v[i], a.act, a.slope);
+          }
+          if (a.res_mode == RES_ADD_POST) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = v[i] + rv[i];
+          } else if (a.res_mode == RES_RSUB_POST) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = rv[i] - v[i];
+          }
+          if (a.acc_mode == ACC_ADD) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = dv[i] + v[i];
+          } else if (a.acc_mode == ACC_ADD_DIV) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = (dv[i] + v[i]) / a.acc_div;
+          }
+          if (MK) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] *= mv[i];
+          }
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             const int r = 8 * h + i;
-            if (!row_ok(r)) continue;
-            const int ro = (r & 3) + 8 * (r >> 2);
-            float v = acc[tm][tn][r];
-            if (a.bias) v += bn;
-            if (a.res_mode == RES_ADD_PRE) v = v + rv[i];
-            if (a.alpha != 1.f) v *= a.alpha;
-            v = act_fn(v, a.act, a.slope);
-            if (a.res_mode == RES_ADD_POST) v = v + rv[i];
-            else if (a.res_mode == RES_RSUB_POST) v = rv[i] - v;
-            if (a.acc_mode == ACC_ADD) v = dv[i] + v;
-            else if (a.acc_mode == ACC_ADD_DIV) v = (dv[i] + v) / a.acc_div;
-            if (MK) v *= mv[i];
-            Yl[ro * a.ldy] = v;
+            if (row_ok(r)) Yl[((r & 3) + 8 * (r >> 2)) * a.ldy] = v[i];
           }
         }
       }

@@ -82,8 +82,10 @@ __device__ __forceinline__ void split8(const float (&v)[8], uint4& h, uint4& m, 
 
 __device__ __forceinline__ float lrelu01(float v) { return v > 0.f ? v : v * 0.1f; }
 
-// C channels, NBT 32-row time blocks per workgroup tile, TN time blocks per wave unit
-template <int C, int NBT, int TN>
+// C channels, NBT 32-row time blocks per workgroup tile, TN time blocks per wave unit, ACCM the output's accumulate
+// mode (ACC_STORE / ACC_ADD / ACC_ADD_DIV: compile-time, so the accumulate target's loads are not a uniform branch
+// whose join would cost the weight ring its depth)
+template <int C, int NBT, int TN, int ACCM>
 __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, const int ntiles) {
   constexpr int NCH = RbGeo<C>::NCH, ROW = RbGeo<C>::ROW, OB = C / 32;
   constexpr int UNITS = OB * NBT / TN;  // wave work units per conv: (out-channel block, TN time blocks)
@@ -106,9 +108,8 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
   const int total = ntiles * a.B;
 
   // ---- the wave's jobs: UPW conv1 units, then UPW conv2 units. A unit is one 32-channel output block x TN time
-  // blocks; one (tap, chunk) step of it is 3 A fragments (weights, global/L2, a PF-deep register ring issued PF
-  // steps ahead and across job boundaries), 3 * TN B fragments (LDS, one step ahead) and 6 * TN MFMAs.
-  constexpr int PF = 2;
+  // blocks; one (tap, chunk) step of it is 3 A fragments (weights, global/L2, two steps ahead), 3 * TN B fragments
+  // (LDS, one step ahead) and 6 * TN MFMAs.
   constexpr size_t QS = (size_t)C * 32;  // bytes of one plane of one (tap, chunk) step of the weight image
   typedef bf16x8 AFrag[3];
   typedef bf16x8 BFrag[TN][3];
@@ -145,31 +146,36 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
       acc[tn] = c;
     }
   };
-  AFrag ring[PF];
-  auto prefetch_ring = [&](const char* wl) __attribute__((always_inline)) {
-#pragma unroll
-    for (int p = 0; p < PF; ++p)
-      if (p < nsteps) load_a(wl, p, ring[p]);
-  };
-  // acc[tn] = sum over steps; ring[] holds steps 0..PF-1 on entry
+  // Weight fragments run a 3-slot register ring two steps ahead, LDS fragments one step ahead (their own 3 slots, so
+  // every slot index is compile-time in the 3-fold unrolled loop). Every load is unconditional (indices clamped to
+  // the last step: the tail reloads it, harmlessly) and issued at the top of its step, pinned there: a conditional
+  // load's join made the waitcnt pass wait for the ring at every step (vmcnt(0) before each MFMA group), and the
+  // scheduler sank the loads below the MFMAs.
+  AFrag ring[3];
+  BFrag bring[3];
   auto run_conv = [&](const char* wl, const char* bl, int dil, f32x16(&acc)[TN]) __attribute__((always_inline)) {
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[tn][r] = 0.f;
-    BFrag b0, b1;
-    load_b(bl, dil, 0, b0);
-    for (int st = 0; st < nsteps; st += PF) {
+    const int last = nsteps - 1;
+    load_a(wl, 0, ring[0]);
+    load_a(wl, 1 < last ? 1 : last, ring[1]);
+    load_b(bl, dil, 0, bring[0]);
+    auto step = [&](int i, int p) __attribute__((always_inline)) {
+      load_a(wl, i + 2 < last ? i + 2 : last, ring[(p + 2) % 3]);
+      load_b(bl, dil, i + 1 < last ? i + 1 : last, bring[(p + 1) % 3]);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(ring[p], bring[p], acc);
+    };
+    int cur = 0;
+    for (; cur + 3 <= nsteps; cur += 3) {
 #pragma unroll
-      for (int p = 0; p < PF; ++p) {
-        const int cur = st + p;
-        if (cur < nsteps) {
-          if (cur + 1 < nsteps) load_b(bl, dil, cur + 1, (p & 1) ? b0 : b1);
-          mma(ring[p], (p & 1) ? b1 : b0, acc);
-          if (cur + PF < nsteps) load_a(wl, cur + PF, ring[p]);
-        }
-      }
+      for (int p = 0; p < 3; ++p) step(cur + p, p);
     }
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      if (cur + p < nsteps) step(cur + p, p);
   };
 
   // ---- x tile -> XS = split(lrelu(x)); row r <-> time t0 - h2 - h1 + r, zero outside [0, T) (conv1's padding)
@@ -225,7 +231,6 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
   if (tile >= tile_end) return;
   // the first job's weights and the first tile's x are in flight together
   const bool pre = (a.flags & 1) != 0;  // contiguous runs: the next tile mostly sits in L2 already (A/B: off 22.19, on 22.30 ms)
-  prefetch_ring(wl_of(0));
   if (pre) load_x(tile);
 #pragma unroll 1
   for (; tile < tile_end; ++tile) {
@@ -260,17 +265,14 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
         const bool ok = o < TT && t < a.T;
         const long long off = (long long)(ok ? t : 0) * C + ob * 32 + 4 * hk;
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          rv[tn][m] = ok ? *reinterpret_cast<const f32x4*>(X + off + 8 * m) : f32x4{0.f, 0.f, 0.f, 0.f};
-          dv[tn][m] = (ok && a.acc_mode != ACC_STORE) ? *reinterpret_cast<const f32x4*>(Y + off + 8 * m)
-                                                      : f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int m = 0; m < 4; ++m) {  // branch-free: rows past the tile read row 0 (their results are not stored)
+          rv[tn][m] = *reinterpret_cast<const f32x4*>(X + off + 8 * m);
+          if constexpr (ACCM != ACC_STORE) dv[tn][m] = *reinterpret_cast<const f32x4*>(Y + off + 8 * m);
         }
       }
     }
     f32x16 acc[TN];
     run_conv(wl_of(job), (second ? TS : XS) + (size_t)(tg * TN * 32 + li) * ROW + hk * 16, second ? 1 : a.d, acc);
-    if (job + 1 < 2 * UPW) prefetch_ring(wl_of(job + 1));
-    else if (tile + 1 < tile_end) prefetch_ring(wl_of(0));
     if (!second) {
       // conv1 -> TS = split(lrelu(conv1 + b1)); TS row p <-> time t0 - h2 + p, zero outside [0, T)
 #pragma unroll
@@ -311,8 +313,8 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
             for (int e = 0; e < 4; ++e) {
               float v = acc[tn][4 * m + e] + bv[m][e];
               v = v + rv[tn][m][e];
-              if (a.acc_mode == ACC_ADD) v = dv[tn][m][e] + v;
-              else if (a.acc_mode == ACC_ADD_DIV) v = (dv[tn][m][e] + v) / a.acc_div;
+              if constexpr (ACCM == ACC_ADD) v = dv[tn][m][e] + v;
+              else if constexpr (ACCM == ACC_ADD_DIV) v = (dv[tn][m][e] + v) / a.acc_div;
               o4[e] = v;
             }
             *reinterpret_cast<f32x4*>(Y + off + 8 * m) = o4;
@@ -324,13 +326,13 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
   }  // tiles
 }
 
-template <int C, int NBT, int TN>
-hipError_t launch_rb(const RbPairArgs& a, hipStream_t s) {
+template <int C, int NBT, int TN, int ACCM>
+hipError_t launch_rb_acc(const RbPairArgs& a, hipStream_t s) {
   constexpr int ROW = RbGeo<C>::ROW;
   const int h2 = (a.k - 1) / 2, h1 = h2 * a.d;
   const int TT = NBT * 32 - 2 * h2;
   const size_t smem = (size_t)(NBT * 32 + 2 * h1) * ROW + (size_t)(NBT * 32 + 2 * h2) * ROW;
-  auto kern = k_rb_pair<C, NBT, TN>;
+  auto kern = k_rb_pair<C, NBT, TN, ACCM>;
   static size_t smem_set = 64 * 1024;
   if (smem > smem_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -352,6 +354,16 @@ hipError_t launch_rb(const RbPairArgs& a, hipStream_t s) {
   const int grid = (int)std::min<long long>(tiles, (long long)ncu * per_cu);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(RB_THREADS), smem, s, a, ntiles);
   return hipGetLastError();
+}
+
+template <int C, int NBT, int TN>
+hipError_t launch_rb(const RbPairArgs& a, hipStream_t s) {
+  switch (a.acc_mode) {
+    case ACC_STORE: return launch_rb_acc<C, NBT, TN, ACC_STORE>(a, s);
+    case ACC_ADD: return launch_rb_acc<C, NBT, TN, ACC_ADD>(a, s);
+    case ACC_ADD_DIV: return launch_rb_acc<C, NBT, TN, ACC_ADD_DIV>(a, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 }  // namespace
