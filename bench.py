@@ -32,7 +32,8 @@ BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense BF16 MFMA (no sparsity)
 # algorithmic fp32 FLOP/s is the dense bf16 peak / 6. A few launches still take the native f32 MFMA (ceiling
 # 157.3); pricing every FLOP against the higher ceiling keeps frac a lower bound.
 SPLIT_PEAK_TFLOPS = round(BF16_PEAK_TFLOPS / 6.0, 1)
-CONV_KERNEL = ("conv_emu_kernel / conv_wsb_kernel / k_rb_pair / conv_gemm_kernel / conv_tiny_kernel / k_conv2d_small "
+CONV_KERNEL = ("conv_wsb16_kernel / conv_gs16_kernel / conv_gsw16_kernel / k_rb_pair / conv_emu_kernel / conv_gemm_kernel / "
+               "conv_tiny_kernel / k_conv2d_small "
                "(+ splitk_reduce): every conv, linear and matmul launch of the step, Σ algorithmic fp32 FLOPs / Σ "
                "HIP-event kernel time")
 SR_IN = 16000
@@ -144,7 +145,11 @@ def _pmc_traffic():
     tree = source_tree_hash()
     if rec.get("tree") != tree:
         return None, f"profiles/pmc_traffic.json is from tree {rec.get('tree')}, not this tree {tree}"
-    return round(rec["traffic_bytes_per_launch"]), f"profiles/pmc_traffic.json (tree {tree}, {rec.get('file')})"
+    step = None
+    if rec.get("step_hbm_bytes") and rec.get("step_alg_bytes"):
+        step = {"hbm_bytes": round(rec["step_hbm_bytes"]), "alg_bytes": round(rec["step_alg_bytes"]),
+                "ratio": round(rec["step_hbm_bytes"] / rec["step_alg_bytes"], 3)}
+    return (round(rec["traffic_bytes_per_launch"]), step), f"profiles/pmc_traffic.json (tree {tree}, {rec.get('file')})"
 
 
 def _timed(step, args, dev, dist):
@@ -453,11 +458,15 @@ def main():
 
     achieved_tflops = k_flops / (k_ms / 1000.0) / 1e12 if k_ms > 0 else 0.0
     traffic, traffic_src = _pmc_traffic()
+    traffic, traffic_step = traffic if traffic else (None, None)
     roofline = {"bound": "mfma", "achieved": round(achieved_tflops, 3), "peak": SPLIT_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved_tflops / SPLIT_PEAK_TFLOPS, 4), "traffic": traffic,
                 "peak_basis": "dense bf16 MFMA 2500 TF / 6 plane products (fp32-accurate 3-way split); "
                               f"native f32 MFMA peak {FP32_PEAK_TFLOPS}",
                 "traffic_unit": "HBM bytes per conv launch", "traffic_source": traffic_src,
+                # the conv family's measured HBM bytes per C2 step against its algorithmic bytes (operands read once,
+                # result written once), the same PMC record
+                "traffic_step": traffic_step,
                 "kernel": CONV_KERNEL,
                 "launches_per_step": k_launches // max(1, args.steps),
                 "kernel_ms_per_step": round(k_ms / args.steps, 3),

@@ -516,10 +516,13 @@ __global__ void conv_tiny_kernel(const ConvArgs a) {
 namespace {
 
 constexpr int TINY_MAX_CIN = 4;
+// also the few-output contractions (N <= 4: RMVPE's final 16 -> 3 3x3 conv, 144 MACs per output), which an MFMA tile
+// runs at N / 32 of its width and C_in / 32 of its depth (200704 pixels: 131 us on the 128x32 tile, 1.3 TF)
 inline bool tiny_fits(const ConvArgs& a) {
   const long long rows = a.W_out > 0 ? (long long)a.T_out * a.W_out : a.T_out;
-  return a.C_in <= TINY_MAX_CIN && a.C_in * a.taps <= 16 && a.force_cfg < 0 &&
-         rows * a.N * a.batch * a.batch_inner < (1LL << 30);
+  const bool few_in = a.C_in <= TINY_MAX_CIN && a.C_in * a.taps <= 16;
+  const bool few_out = a.N <= 4 && a.C_in * a.taps <= 160;
+  return (few_in || few_out) && a.force_cfg < 0 && rows * a.N * a.batch * a.batch_inner < (1LL << 30);
 }
 
 hipError_t launch_tiny(const ConvArgs& a, bool two_d, hipStream_t s) {
@@ -815,8 +818,17 @@ long long conv_plan_splitk(ConvArgs& a, bool two_d) {
   static const int min_iters = env_cfg("RVCX_SPLITK_MINITERS", 4);  // shortest contraction worth a split
   if (tiles >= min_tiles || iters < min_iters || (flops < 1.0e8 && iters < 16)) return 0;
   int ks = (int)((target + tiles - 1) / tiles);
-  ks = std::min(ks, iters / 2);
+  // the gather-streamed kernels keep >= 8 (chunk, tap) steps per slice: below that a slice is all prologue and
+  // epilogue and the extra slab + combine launch cost more than the parallelism gains (bench_gs r03s, cold: HuBERT
+  // 768 -> 768 ks 1 22.1 us vs ks 4 27.6, TextEncoder 1x1 ks 1 11.6 vs ks 3 14.4, U-Net 196 px ks 8 19.8 vs ks 16
+  // 21.8, 3136 px ks 2 20.2 vs ks 6 27.3; the 3072 -> 768 linear keeps ks 4: 48.6 vs 62.8 unsplit)
+  static const int gs_min_steps = env_cfg("RVCX_GS_MINSTEPS", 8);  // same-box C2: 2 17.73, 8 17.72, 16 17.86, 24 17.97 ms
+  ks = std::min(ks, a.wsb == 2 ? iters / gs_min_steps : iters / 2);
   ks = std::min(ks, 32);
+  // the windowed 2-D gather-streamed kernel splits by whole 32-channel chunks (bench_gs: U-Net 784 px ks 8 and 3136 px
+  // ks 4 beat the 10 and 6 the step count would give)
+  if (a.wsb == 2 && two_d && (a.force_cfg < 0 || a.force_cfg == 30) && conv_gsw_eligible(a))
+    ks = std::min(ks, (a.C_in + CK - 1) / CK);
   if (ks < 2) return 0;
   a.ksplit = ks;
   a.ws_rows = two_d ? (long long)a.T_out * a.W_out : a.T_out;

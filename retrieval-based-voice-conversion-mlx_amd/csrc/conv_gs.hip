@@ -279,6 +279,185 @@ hipError_t launch_gs(const ConvArgs& a, int ntn_enable, int ksplit, hipStream_t 
   return hipGetLastError();
 }
 
+// ---- 3x3 / pad-1 2-D convs on images at most 32 pixels wide (the RMVPE U-Net's deep levels, 4..32 wide):
+// "windowed" gather-streamed kernel. A 64-pixel tile is rh = 64 / W whole image rows, so its outputs are 64
+// consecutive flattened pixels (the 1-D store_tile16 and split-K slab apply unchanged). Per 32-channel chunk the
+// tile's (rh + 2) x (W + 2) input window is split into LDS ONCE and all 9 taps read their shifted A fragments from
+// it (the per-tap gather of conv_gs16_kernel re-loaded and re-split every input pixel 9 times: ~90 VALU of its ~200
+// instructions per step); the next chunk's window is prefetched into registers during the current chunk's taps.
+// B streams from the lane-major image through the same 3-deep register ring. Split-K slices are whole chunks, so
+// chunk switches fall on 3-step group boundaries and the 9 unrolled taps per chunk carry no branch.
+constexpr int GSW_MAXW = 32;
+constexpr int GSW_WROWS = (64 / GSW_MAXW + 2) * (GSW_MAXW + 2);  // largest window: rh = 2 (4 x 34 = 136 pixels)
+
+template <int MODE>
+__global__ __launch_bounds__(CONV_THREADS, 2) void conv_gsw16_kernel(const ConvArgs a, const char* __restrict__ wsp,
+                                                                     const int Npad, const int ntn, const int ksplit,
+                                                                     const int mfast) {
+  constexpr int BM = 64, BN = 64, WM = 2, WN = 2;
+  constexpr int NT = CONV_THREADS;
+  constexpr int TM16 = BM / (WM * 16), TN16 = BN / (WN * 16);
+  constexpr int PA = MODE & 3;
+  constexpr int WV = (GSW_WROWS * EC4 + NT - 1) / NT;  // float4 groups of the window per thread
+  extern __shared__ __attribute__((aligned(16))) char smem_gsw[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int lc = lane & 15, lg = lane >> 4;
+  int bx, by, bz;
+  conv_block_coords(ntn, bx, by, bz);
+  if (mfast && ntn > 0) {
+    const int t = bx * ntn + by;
+    const int mt = (int)gridDim.x / ntn;
+    bx = t % mt;
+    by = t / mt;
+  }
+  const int zsplit = bz % ksplit;
+  const int b = bz / ksplit;
+  const int n0 = by * BN;
+  const int W = a.W_out, H = a.T_out;
+  const int rh = BM / W, aw = W + 2;
+  const int h0 = bx * rh;
+  const int nwin = (rh + 2) * aw;
+  const float* X = a.x + (long long)b * a.x_bs;
+  const int nch = a.C_in / EK;
+  const int pc = (nch + ksplit - 1) / ksplit;  // whole chunks per split-K slice
+  const int c0 = zsplit * pc, c1 = min(nch, c0 + pc);
+
+  // ---- window staging: thread rows v * 32 + arow (window pixel (wr / aw, wr % aw)), channels ac4..ac4+3
+  const int arow = store_row(tid / EC4), ac4 = (tid % EC4) << 2;
+  f32x4 wr_[WV];
+  unsigned wok = 0u;
+  auto load_win = [&](int ch) __attribute__((always_inline)) {
+    const float* src = X + ch * EK + ac4;
+    wok = 0u;
+#pragma unroll
+    for (int v = 0; v < WV; ++v) {
+      const int r = v * (NT / EC4) + arow;
+      const int wh = r / aw, wc = r - wh * aw;
+      const int ih = h0 - 1 + wh, iw = wc - 1;
+      const bool ok = r < nwin && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      const unsigned g = ok ? (unsigned)(ih * W + iw) : 0u;
+      wr_[v] = *reinterpret_cast<const f32x4*>(src + g * (unsigned)a.ldx);  // branch-free (conv_gs16_kernel)
+      wok |= ok ? (1u << v) : 0u;
+    }
+  };
+  auto store_win = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int v = 0; v < WV; ++v) {
+      const int r = v * (NT / EC4) + arow;
+      if (r < nwin) {
+        f32x4 val = wr_[v];
+        const bool ok = (wok >> v) & 1u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) val[j] = ok ? pre_fn<PA>(val[j], a.pre_act, a.pre_slope) : 0.f;
+        put_split4(smem_gsw + r * ERS, ac4, val);
+      }
+    }
+  };
+
+  // ---- B ring (conv_gs16_kernel's)
+  typedef bf16x8 BFrag[TN16][3];
+  BFrag br[GS_D];
+  const char* bp = wsp + (size_t)((n0 + wn * TN16 * 16) >> 4) * (3 * GS_BLK) + lane * 16;
+  const size_t bstep = (size_t)Npad * GS_WROW;
+  auto load_b = [&](int st, BFrag& dst) __attribute__((always_inline)) {
+    const char* p = bp + (size_t)st * bstep;
+#pragma unroll
+    for (int tn = 0; tn < TN16; ++tn)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) dst[tn][q] = *reinterpret_cast<const bf16x8*>(p + tn * (3 * GS_BLK) + q * GS_BLK);
+  };
+
+  f32x4 acc[TM16][TN16];
+#pragma unroll
+  for (int tm = 0; tm < TM16; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < TN16; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // A fragment rows: tile pixel ml = (r, c) -> window pixel (r + kh, c + kw)
+  int aoff[TM16];
+#pragma unroll
+  for (int tm = 0; tm < TM16; ++tm) {
+    const int ml = wm * TM16 * 16 + tm * 16 + lc;
+    const int r = ml / W, c = ml - r * W;
+    aoff[tm] = (r * aw + c) * ERS + lg * 16;
+  }
+  auto compute = [&](int tap, const BFrag& bf) __attribute__((always_inline)) {
+    const int toff = ((tap / 3) * aw + (tap % 3)) * ERS;
+#pragma unroll
+    for (int tm = 0; tm < TM16; ++tm) {
+      bf16x8 af[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) af[q] = *reinterpret_cast<const bf16x8*>(smem_gsw + aoff[tm] + toff + q * PLANE);
+#pragma unroll
+      for (int tn = 0; tn < TN16; ++tn) {
+        f32x4 cc = acc[tm][tn];
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], bf[tn][0], cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[tn][1], cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[tn][2], cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[tn][0], cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[tn][1], cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[tn][0], cc, 0, 0, 0);
+        acc[tm][tn] = cc;
+      }
+    }
+  };
+
+  if (c0 < c1) {
+    const int it0 = c0 * 9, last = c1 * 9 - 1;
+    auto clampst = [&](int st) { return st < last ? st : last; };
+    load_win(c0);
+#pragma unroll
+    for (int p = 0; p < GS_D - 1; ++p) load_b(clampst(it0 + p), br[p]);
+    store_win();
+    if (c0 + 1 < c1) load_win(c0 + 1);
+    __syncthreads();
+    for (int ch = c0; ch < c1; ++ch) {
+      const int base = ch * 9;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int p = tap % GS_D;  // ring slot: (step - it0) % 3 = tap % 3 (whole chunks of 9 steps)
+        load_b(clampst(base + tap + GS_D - 1), br[(p + GS_D - 1) % GS_D]);
+        __builtin_amdgcn_sched_barrier(0);
+        compute(tap, br[p]);
+      }
+      if (ch + 1 < c1) {
+        __syncthreads();  // every wave is done with this chunk's window
+        store_win();
+        if (ch + 2 < c1) load_win(ch + 2);
+        __syncthreads();
+      }
+    }
+  }
+  store_tile16<TM16, TN16, WM, WN>(a, h0 * W, n0, b, zsplit, ksplit, (long long)H * W, acc);
+}
+
+template <int MODE>
+void launch_gsw_mode(const ConvArgs& a, dim3 grid, size_t smem, int ntn, int ksplit, int mfast, hipStream_t s) {
+  hipLaunchKernelGGL((conv_gsw16_kernel<MODE>), grid, dim3(CONV_THREADS), smem, s, a,
+                     static_cast<const char*>(a.wsplit), a.wsplit_npad, ntn, ksplit, mfast);
+}
+
+hipError_t launch_gsw(const ConvArgs& a, int ntn_enable, int ksplit, hipStream_t s) {
+  const int W = a.W_out, rh = 64 / W;
+  const long long mtiles = (a.T_out + rh - 1) / rh;
+  if (a.wsplit_npad % 64 != 0 || ksplit < 1 || (ksplit > 1 && !a.ws) || mtiles > INT32_MAX / 64) return hipErrorInvalidValue;
+  const int ntiles = (a.N + 63) / 64;
+  const int ntn = ntn_enable ? ntiles : 0;
+  dim3 grid((unsigned)(ntn ? mtiles * ntiles : mtiles), ntn ? 1 : ntiles, a.batch * ksplit);
+  const size_t smem = (size_t)(rh + 2) * (W + 2) * ERS;
+  const double wbytes = 6.0 * a.N * a.C_in * 9, abytes = 4.0 * (double)a.T_out * W * a.C_in * a.batch;
+  const int mfast = wbytes > abytes ? 1 : 0;
+  switch (pre_mode(a.pre_act)) {
+    case 0: launch_gsw_mode<0>(a, grid, smem, ntn, ksplit, mfast, s); break;
+    case 1: launch_gsw_mode<1>(a, grid, smem, ntn, ksplit, mfast, s); break;
+    default: launch_gsw_mode<2>(a, grid, smem, ntn, ksplit, mfast, s); break;
+  }
+  return hipGetLastError();
+}
+
 }  // namespace
 
 bool conv_gs_eligible(const ConvArgs& a, bool two_d) {
@@ -302,8 +481,19 @@ bool conv_gs_tile(int cfg, int& BM, int& BN) {
   return true;
 }
 
+// the windowed 2-D kernel: 3x3 / pad 1 / stride 1, same-size images at most 32 pixels wide with 32 % W == 0
+bool conv_gsw_eligible(const ConvArgs& a) {
+  static const bool on = [] {
+    const char* e = std::getenv("RVCX_NO_GSW");
+    return !(e && std::atoi(e) != 0);
+  }();
+  return on && conv_gs_eligible(a, true) && a.KH == 3 && a.KW == 3 && a.padh == 1 && a.padw == 1 &&
+         a.T_in == a.T_out && a.W_in == a.W_out && a.W_out <= GSW_MAXW && GSW_MAXW % a.W_out == 0 && a.W_out >= 4;
+}
+
 hipError_t conv_gs_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream_t s, bool two_d, int ksplit) {
   if (!a.wsplit || !conv_gs_eligible(a, two_d)) return hipErrorInvalidValue;
+  if (two_d && cfg == 30 && conv_gsw_eligible(a)) return launch_gsw(a, ntn_enable, ksplit, s);
   if (two_d) {
     switch (cfg) {
       case 30: return launch_gs<64, 64, 2, 2, true>(a, ntn_enable, ksplit, s);

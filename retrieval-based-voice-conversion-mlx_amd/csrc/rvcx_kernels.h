@@ -144,6 +144,7 @@ bool conv_wsb_tile(int cfg, int& BM, int& BN);  // cfg 20..26 -> tile
 // register ring, A gathered per (chunk, tap) step; 1-D (any stride / dilation) and 2-D (stride 1, OUT_ROWS), C_in % 32
 // == 0, split-K capable. cfg 30..32 -> tile
 bool conv_gs_eligible(const ConvArgs& a, bool two_d);
+bool conv_gsw_eligible(const ConvArgs& a);  // the windowed 2-D form (split-K slices of whole 32-channel chunks)
 bool conv_gs_tile(int cfg, int& BM, int& BN);
 hipError_t conv_gs_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream_t s, bool two_d, int ksplit);
 int conv_wsplit_npad(int N);

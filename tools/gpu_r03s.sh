@@ -4,6 +4,7 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 TAG=${1:-s}; shift
+[ -x build/bench_gs ] && timeout -k 10 300 ./build/bench_gs 10 1 > gpurun_out/bench_gs_$TAG.txt 2>&1
 timeout -k 10 600 python -u -m pytest -m gpu -x -v -s --timeout 120 --timeout-method thread tests/test_gpu_conv_math.py tests/test_gpu_c2_parity.py tests/test_gpu_models.py tests/test_gpu_resblock_fused.py tests/test_gpu_sizes.py > gpurun_out/gt_$TAG.log 2>&1 || { echo "tests failed"; grep -E "FAILED|Error|^E " gpurun_out/gt_$TAG.log | head -30; exit 1; }
 grep -E "passed|failed" gpurun_out/gt_$TAG.log | tail -1
 run() {  # run LIB ENV...

@@ -14,7 +14,8 @@ import glob
 import os
 import sys
 
-FAMILY = ("conv_emu_kernel", "conv_wsb_kernel", "k_rb_pair", "conv_gemm_kernel", "conv_tiny_kernel", "k_conv2d_small")
+FAMILY = ("conv_emu_kernel", "conv_wsb_kernel", "conv_wsb16_kernel", "conv_gs16_kernel", "conv_gsw16_kernel", "k_rb_pair",
+          "conv_gemm_kernel", "conv_tiny_kernel", "k_conv2d_small")
 
 
 def dispatches(d, tag):

@@ -34,7 +34,8 @@ def load(d, counter):
 def main():
     d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
     keys = (sys.argv[2] if len(sys.argv) > 2 else
-            "conv_emu_kernel,conv_wsb_kernel,k_rb_pair,conv_gemm_kernel,conv_tiny_kernel,k_conv2d_small").split(",")
+            "conv_emu_kernel,conv_wsb_kernel,conv_wsb16_kernel,conv_gs16_kernel,conv_gsw16_kernel,k_rb_pair,conv_gemm_kernel,"
+            "conv_tiny_kernel,k_conv2d_small").split(",")
     key = ",".join(keys)
     fam = lambda k: any(s in k for s in keys)  # noqa: E731
     bytes_fam = lambda k: fam(k) or "splitk_reduce" in k  # noqa: E731
@@ -50,6 +51,17 @@ def main():
     all_f = sum(sum(v) for v in fe.values()) * 2 * 1024
     all_w = sum(sum(v) for v in wr.values()) * 1024
     rec["all_kernels_bytes"] = all_f + all_w
+    # per step: the conv family's measured HBM bytes (each kernel ran once per pipeline call: warm-up + the timed
+    # step) against the algorithmic bytes of the timed step's launches (operands read once, result written once:
+    # the RVCX_PROF_DUMP csv of the same pass, last column)
+    dump = glob.glob(os.path.join(d, "convdump_FETCH_SIZE.csv"))
+    if dump:
+        lines = [r for r in open(dump[0]) if r.strip()]
+        calls = max(1, round(n / max(1, len(lines))))
+        alg = sum(float(r.split(",")[-1]) for r in lines)
+        rec["step_hbm_bytes"] = (2.0 * tot_f + tot_w) * 1024 / calls
+        rec["step_alg_bytes"] = alg
+        rec["step_ratio"] = rec["step_hbm_bytes"] / alg if alg > 0 else None
     from rvcx.provenance import source_tree_hash
 
     rec["tree"] = source_tree_hash()
