@@ -65,8 +65,12 @@ __global__ __launch_bounds__(256) void k_conv2d_small(const ConvArgs a, const in
       const int q = idx % (CIN / 4);
       const int tn = idx / (CIN / 4);  // tap * NOUT + n
       const int tap = tn / NOUT, n = tn % NOUT;
-      if (NW % 256 == 0 || idx < NW)
-        wv[it] = *reinterpret_cast<const f32x4*>(a.w + (long long)tap * a.w_ts + (long long)n * a.ldw + 4 * q);
+      // N < NOUT (RMVPE's 16 -> 3 output conv on the 16-wide tile): the missing weight rows read row 0, zeroed below
+      if (NW % 256 == 0 || idx < NW) {
+        wv[it] = *reinterpret_cast<const f32x4*>(a.w + (long long)tap * a.w_ts + (long long)(n < a.N ? n : 0) * a.ldw +
+                                                 4 * q);
+        if (n >= a.N) wv[it] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     }
 #pragma unroll
     for (int it = 0; it < SIT; ++it) {
@@ -95,24 +99,31 @@ __global__ __launch_bounds__(256) void k_conv2d_small(const ConvArgs a, const in
     pr[p] = pix / W;
     pc[p] = pix % W;
   }
-#pragma unroll 1
+  // per (tap, channel group): every A and B fragment read first (one exposed LDS latency), then the MFMAs k-slice
+  // major so consecutive ones feed TPW x NT independent accumulators (v_mfma_f32_16x16x4_f32 issues every 32 cycles
+  // but a dependent one waits 40; the pixel-major order chained 4 dependent MFMAs per fragment and read A one
+  // fragment at a time: 2x the MFMA time)
+  int abase[TPW];
+#pragma unroll
+  for (int p = 0; p < TPW; ++p) abase[p] = (pr[p] * AW + pc[p]) * CP + 4 * kq;
+#pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
     const int dh = tap / 3, dw = tap % 3;
 #pragma unroll
     for (int g = 0; g < CG; ++g) {
-      f32x4 bf[NT];
+      f32x4 bf[NT], af[TPW];
 #pragma unroll
       for (int t = 0; t < NT; ++t)
         bf[t] = *reinterpret_cast<const f32x4*>(Bs + (size_t)(tap * NOUT + t * 16 + li) * CP + g * 16 + 4 * kq);
 #pragma unroll
-      for (int p = 0; p < TPW; ++p) {
-        const f32x4 af = *reinterpret_cast<const f32x4*>(
-            As + ((size_t)(pr[p] + dh) * AW + pc[p] + dw) * CP + g * 16 + 4 * kq);
+      for (int p = 0; p < TPW; ++p)
+        af[p] = *reinterpret_cast<const f32x4*>(As + abase[p] + (dh * AW + dw) * CP + g * 16);
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int t = 0; t < NT; ++t) acc[p][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[j], bf[t][j], acc[p][t], 0, 0, 0);
-      }
+        for (int p = 0; p < TPW; ++p)
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[p][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[p][j], bf[t][j], acc[p][t], 0, 0, 0);
     }
   }
   // ---- epilogue: lane holds rows (pixels) 4*kq + i of fragment p, column (channel) li of fragment t. The uniform
@@ -125,7 +136,8 @@ __global__ __launch_bounds__(256) void k_conv2d_small(const ConvArgs a, const in
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int n = t * 16 + li;
-    const float bn = a.bias ? a.bias[n] : 0.f;
+    const bool n_ok = n < a.N;
+    const float bn = (a.bias && n_ok) ? a.bias[n] : 0.f;
 #pragma unroll
     for (int p = 0; p < TPW; ++p) {
       long long m[4];
@@ -135,12 +147,12 @@ __global__ __launch_bounds__(256) void k_conv2d_small(const ConvArgs a, const in
       for (int i = 0; i < 4; ++i) {
         const int pix = wave * (PIX / 4) + p * 16 + 4 * kq + i;
         const int gh = h0 + pix / W, gw = pix % W;
-        ok[i] = gh < H;
-        m[i] = (long long)(ok[i] ? gh : 0) * W + gw;
+        ok[i] = gh < H && n_ok;
+        m[i] = (long long)(gh < H ? gh : 0) * W + gw;
       }
       if (res) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) rv[i] = R[m[i] * a.ldr + n];
+        for (int i = 0; i < 4; ++i) rv[i] = R[m[i] * a.ldr + (n_ok ? n : 0)];
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] += bn;
@@ -189,7 +201,7 @@ hipError_t launch_small(const ConvArgs& a, hipStream_t s) {
 
 bool conv2d_small_fits(const ConvArgs& a) {
   const bool shape = a.KH == 3 && a.KW == 3 && a.taps == 9 && a.padh == 1 && a.padw == 1 && a.T_in == a.T_out &&
-                     a.W_in == a.W_out && (a.C_in == 16 || a.C_in == 32) && (a.N == 16 || a.N == 32);
+                     a.W_in == a.W_out && (a.C_in == 16 || a.C_in == 32) && (a.N == 32 || (a.N >= 1 && a.N <= 16));
   if (!shape) return false;
   const int pix = a.C_in == 16 ? 512 : 256;
   if (a.W_out < 16 || pix % a.W_out) return false;
@@ -205,9 +217,9 @@ bool conv2d_small_fits(const ConvArgs& a) {
 }
 
 hipError_t conv2d_small(const ConvArgs& a, hipStream_t s) {
-  if (a.C_in == 16 && a.N == 16) return launch_small<16, 16, 512>(a, s);
+  if (a.C_in == 16 && a.N <= 16) return launch_small<16, 16, 512>(a, s);
   if (a.C_in == 16 && a.N == 32) return launch_small<16, 32, 512>(a, s);
-  if (a.C_in == 32 && a.N == 16) return launch_small<32, 16, 256>(a, s);
+  if (a.C_in == 32 && a.N <= 16) return launch_small<32, 16, 256>(a, s);
   if (a.C_in == 32 && a.N == 32) return launch_small<32, 32, 256>(a, s);
   return hipErrorInvalidValue;
 }

@@ -516,13 +516,10 @@ __global__ void conv_tiny_kernel(const ConvArgs a) {
 namespace {
 
 constexpr int TINY_MAX_CIN = 4;
-// also the few-output contractions (N <= 4: RMVPE's final 16 -> 3 3x3 conv, 144 MACs per output), which an MFMA tile
-// runs at N / 32 of its width and C_in / 32 of its depth (200704 pixels: 131 us on the 128x32 tile, 1.3 TF)
 inline bool tiny_fits(const ConvArgs& a) {
   const long long rows = a.W_out > 0 ? (long long)a.T_out * a.W_out : a.T_out;
-  const bool few_in = a.C_in <= TINY_MAX_CIN && a.C_in * a.taps <= 16;
-  const bool few_out = a.N <= 4 && a.C_in * a.taps <= 160;
-  return (few_in || few_out) && a.force_cfg < 0 && rows * a.N * a.batch * a.batch_inner < (1LL << 30);
+  return a.C_in <= TINY_MAX_CIN && a.C_in * a.taps <= 16 && a.force_cfg < 0 &&
+         rows * a.N * a.batch * a.batch_inner < (1LL << 30);
 }
 
 hipError_t launch_tiny(const ConvArgs& a, bool two_d, hipStream_t s) {

@@ -274,28 +274,42 @@ __global__ __launch_bounds__(64) void k_flash_attn(const float* __restrict__ qkv
 }
 
 // out[b][i][h*DK + d] = sum_s O_s[d] e^(m_s - M) / sum_s l_s e^(m_s - M)
-__global__ void k_flash_combine(const float* __restrict__ part_o, const float* __restrict__ part_ml, int nsplit,
-                                int BH, int T, int DK, int nh, float* __restrict__ out, int ldo) {
-  const long long n = (long long)BH * T * DK;
-  for (long long x = blockIdx.x * (long long)blockDim.x + threadIdx.x; x < n; x += (long long)gridDim.x * blockDim.x) {
-    const int d = (int)(x % DK);
-    const long long bt = x / DK;
-    const int i = (int)(bt % T);
-    const int bh = (int)(bt / T);
-    float M = -INFINITY;
-    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, part_ml[2 * (((long long)s * BH + bh) * T + i)]);
-    float L = 0.f, acc = 0.f;
-    for (int s = 0; s < nsplit; ++s) {
-      const long long row = ((long long)s * BH + bh) * T + i;
-      const float ms = part_ml[2 * row];
-      if (ms == -INFINITY) continue;  // an empty split
-      const float e = expf(ms - M);
-      L += part_ml[2 * row + 1] * e;
-      acc += part_o[row * DK + d] * e;
-    }
-    const int b = bh / nh, h = bh % nh;
-    out[((long long)b * T + i) * ldo + h * DK + d] = acc / L;
+// Merges the key splits: one row (bh, query i) per DK/4 lanes, each lane a float4 of the head dimension. The split
+// weights exp(m_s - M) are computed per lane group (was: per output element, with 64-bit index divisions per element),
+// every load is a 16-B vector or a broadcast, and the sum runs over the splits in order (same arithmetic as before).
+template <int DK>
+__global__ __launch_bounds__(256) void k_flash_combine(const float* __restrict__ part_o,
+                                                       const float* __restrict__ part_ml, int nsplit, int BH, int T,
+                                                       int nh, float* __restrict__ out, int ldo) {
+  constexpr int LPR = DK / 4;          // lanes per row
+  constexpr int RPW = 64 / LPR;        // rows per wave
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int sub = lane / LPR, d4 = (lane - sub * LPR) * 4;
+  if (sub >= RPW) return;  // DK = 96: lanes 48..63 idle
+  const int rows = BH * T;
+  const int row = (blockIdx.x * 4 + wave) * RPW + sub;
+  if (row >= rows) return;
+  const unsigned split_rows = (unsigned)rows;  // rows per split slab
+  float M = -INFINITY;
+  for (int sp = 0; sp < nsplit; ++sp) M = fmaxf(M, part_ml[2u * (sp * split_rows + (unsigned)row)]);
+  float L = 0.f;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int sp = 0; sp < nsplit; ++sp) {
+    const unsigned r = sp * split_rows + (unsigned)row;
+    const float ms = part_ml[2u * r];
+    if (ms == -INFINITY) continue;  // an empty split
+    const float e = expf(ms - M);
+    L += part_ml[2u * r + 1] * e;
+    const f32x4 o = *reinterpret_cast<const f32x4*>(part_o + r * (unsigned)DK + d4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] += o[j] * e;
   }
+  const int bh = row / T, i = row - bh * T;
+  const int b = bh / nh, h = bh - b * nh;
+  f32x4 res;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) res[j] = acc[j] / L;
+  *reinterpret_cast<f32x4*>(out + ((long long)b * T + i) * ldo + h * DK + d4) = res;
 }
 
 }  // namespace
@@ -328,10 +342,15 @@ hipError_t flash_attn(const float* qkv, int ldq, int B, int T, int nh, int dk, f
                        mask, part_o, part_ml);
   else
     return hipErrorInvalidValue;
-  const long long n = (long long)B * nh * T * dk;
-  const long long nb = std::min<long long>((n + 255) / 256, 1 << 20);
-  hipLaunchKernelGGL(k_flash_combine, dim3((unsigned)nb), dim3(256), 0, s, part_o, part_ml, nsplit, B * nh, T, dk, nh,
-                     out, ldo);
+  const long long rows = (long long)B * nh * T;
+  if (rows * nsplit * dk >= (1LL << 31) || (ldo & 3) != 0 || (reinterpret_cast<uintptr_t>(out) & 15) != 0)
+    return hipErrorInvalidValue;  // 32-bit slab offsets, float4 output rows
+  const int rpb = 4 * (64 / (dk / 4));  // rows per 256-thread block
+  const unsigned nb = (unsigned)((rows + rpb - 1) / rpb);
+  if (dk == 64)
+    hipLaunchKernelGGL(k_flash_combine<64>, dim3(nb), dim3(256), 0, s, part_o, part_ml, nsplit, B * nh, T, nh, out, ldo);
+  else
+    hipLaunchKernelGGL(k_flash_combine<96>, dim3(nb), dim3(256), 0, s, part_o, part_ml, nsplit, B * nh, T, nh, out, ldo);
   return hipGetLastError();
 }
 
