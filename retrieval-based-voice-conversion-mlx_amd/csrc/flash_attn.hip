@@ -11,6 +11,7 @@
 // conv_emu.hip (fp32 accurate). Key splits write unnormalised partials (O, running max, running sum) that
 // k_flash_combine merges; the relative-value band is folded into each split's O before it is written.
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 
 #include "split_bf16.h"
@@ -314,11 +315,15 @@ __global__ __launch_bounds__(256) void k_flash_combine(const float* __restrict__
 
 }  // namespace
 
-// key splits: enough waves for two per SIMD (the kernel is latency-bound per key block), at least 2 key blocks
+// key splits: ~4096 query-block x split waves (the kernel is latency-bound per key block), at least 2 key blocks
 // per split
 int flash_attn_splits(int B, int nh, int T) {
+  static const int waves = [] {  // RVCX_FA_WAVES: target query-block x split waves (A/B aid)
+    const char* e = std::getenv("RVCX_FA_WAVES");
+    return e ? std::max(1, std::atoi(e)) : 4096;  // same-box C2: 512 18.12, 1024 17.91, 2048 17.98, 4096 17.84 ms
+  }();
   const int qb = (T + FA_Q - 1) / FA_Q, kb = (T + FA_K - 1) / FA_K;
-  int ns = (2048 + qb * B * nh - 1) / (qb * B * nh);
+  int ns = (waves + qb * B * nh - 1) / (qb * B * nh);
   ns = std::max(1, std::min(ns, std::max(1, kb / 2)));
   return ns;
 }
