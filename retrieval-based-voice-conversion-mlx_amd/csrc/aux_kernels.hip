@@ -588,17 +588,28 @@ __global__ void k_gn_stats(const float* x, int T, int C, int chunk, double* ws) 
 // per-channel statistics -> affine form y = x * scale + shift (torch GroupNorm's ApplyScaleBias:
 // scale = rstd * gamma, shift = beta - mean * scale), once per channel instead of per element.
 // grid (C/256, B): sequence b's partials at ws + b*nchunks*C*2, its scale/shift at ss + b*2C
+// grid (C/64, B), block 256 = 64 channels x 4 chunk lanes: lane r sums chunks r, r + 4, ... (coalesced over the 64
+// channels), the 4 lane sums are added in order (one thread per channel looping over all 256 chunks took 66 us)
 __global__ void k_gn_finalize(const double* ws, int nchunks, int T, int C, const float* gamma, const float* beta,
                               float eps, float* ss) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;
   ws += (long long)blockIdx.y * nchunks * C * 2;
   ss += (long long)blockIdx.y * 2 * C;
   double s = 0.0, q = 0.0;
-  for (int k = 0; k < nchunks; ++k) {
-    s += ws[((long long)k * C + c) * 2];
-    q += ws[((long long)k * C + c) * 2 + 1];
+  if (c < C) {
+    for (int k = rl; k < nchunks; k += 4) {
+      s += ws[((long long)k * C + c) * 2];
+      q += ws[((long long)k * C + c) * 2 + 1];
+    }
   }
+  __shared__ double sp[4][64], qp[4][64];
+  sp[rl][threadIdx.x & 63] = s;
+  qp[rl][threadIdx.x & 63] = q;
+  __syncthreads();
+  if (rl != 0 || c >= C) return;
+  s = ((sp[0][threadIdx.x] + sp[1][threadIdx.x]) + sp[2][threadIdx.x]) + sp[3][threadIdx.x];
+  q = ((qp[0][threadIdx.x] + qp[1][threadIdx.x]) + qp[2][threadIdx.x]) + qp[3][threadIdx.x];
   const double mean = s / T;
   double var = q / T - mean * mean;
   if (var < 0) var = 0;
@@ -608,11 +619,12 @@ __global__ void k_gn_finalize(const double* ws, int nchunks, int T, int C, const
   ss[C + c] = beta[c] - (float)mean * scale;
 }
 // x: B sequences of T rows back to back; n4_per = T*C/4 float4 per sequence
-__global__ void k_gn_apply(float* __restrict__ x, long long n4, long long n4_per, int C4, const float* __restrict__ ss,
+// (32-bit indices: the launch checks n4 < 2^31; the 64-bit % and / per float4 were most of its instructions)
+__global__ void k_gn_apply(float* __restrict__ x, unsigned n4, unsigned n4_per, unsigned C4, const float* __restrict__ ss,
                            int C) {
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
     const int c = (int)(i % C4) * 4;
-    const float* sb = ss + (i / n4_per) * 2 * C;
+    const float* sb = ss + (size_t)(i / n4_per) * 2 * C;
     f32x4v v = reinterpret_cast<f32x4v*>(x)[i];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -630,10 +642,12 @@ hipError_t groupnorm_time_gelu(float* x, int T, int C, const float* gamma, const
   if (C % 4 || B < 1) return hipErrorInvalidValue;
   float* ss = reinterpret_cast<float*>(ws + (size_t)B * nchunks * C * 2);
   hipLaunchKernelGGL(k_gn_stats, dim3((C + 63) / 64, nchunks, B), dim3(256), 0, s, x, T, C, chunk, ws);
-  hipLaunchKernelGGL(k_gn_finalize, dim3((C + 255) / 256, B), dim3(256), 0, s, ws, nchunks, T, C, gamma, beta, eps,
+  hipLaunchKernelGGL(k_gn_finalize, dim3((C + 63) / 64, B), dim3(256), 0, s, ws, nchunks, T, C, gamma, beta, eps,
                      ss);
   const long long n4p = (long long)T * C / 4;
-  hipLaunchKernelGGL(k_gn_apply, dim3(nblocks(n4p * B)), dim3(TB), 0, s, x, n4p * B, n4p, C / 4, ss, C);
+  if (n4p * B >= (1LL << 31)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_gn_apply, dim3(nblocks(n4p * B)), dim3(TB), 0, s, x, (unsigned)(n4p * B), (unsigned)n4p,
+                     (unsigned)(C / 4), ss, C);
   return hipGetLastError();
 }
 
