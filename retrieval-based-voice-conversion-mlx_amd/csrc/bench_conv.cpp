@@ -76,7 +76,7 @@ int main(int argc, char** argv) {
                        pad, 1);
     std::vector<float> ref((size_t)T * N), out((size_t)T * N);
     CK_(hipMemcpy(ref.data(), yr, ref.size() * 4, hipMemcpyDeviceToHost));
-    for (int cfg : {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 20, 21, 22, 23, 24, 25, 26})
+    for (int cfg : {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 20, 21, 22, 23, 24, 25, 26, 27, 28})
       for (int pipe : {-1}) {
         ConvArgs a;
         a.x = x; a.ldx = C; a.T_in = T; a.C_in = C;
@@ -187,7 +187,7 @@ int main(int argc, char** argv) {
     const double flops = 2.0 * cs.T * cs.N * (double)cs.Cin * cs.taps;
     // variants: (cfg, math, pipe); cfg -1 = the library's policy for that math
     struct V { int cfg, math, pipe; };
-    std::vector<V> vars = {{-1, 2, 0}, {20, 2, -1}, {21, 2, -1}, {22, 2, -1}, {23, 2, -1}, {24, 2, -1}, {25, 2, -1}, {26, 2, -1}, {10, 2, -1}, {11, 2, -1}, {12, 2, -1}, {13, 2, -1}, {14, 2, -1}, {15, 2, -1},
+    std::vector<V> vars = {{-1, 2, 0}, {20, 2, -1}, {21, 2, -1}, {22, 2, -1}, {23, 2, -1}, {24, 2, -1}, {25, 2, -1}, {26, 2, -1}, {27, 2, -1}, {28, 2, -1}, {10, 2, -1}, {11, 2, -1}, {12, 2, -1}, {13, 2, -1}, {14, 2, -1}, {15, 2, -1},
                            {16, 2, -1}, {-1, 1, 0}, {1, 1, -1}, {3, 1, -1}};
     if (cs.taps == 1)
       for (int c : {10, 12, 13, 14, 15}) vars.push_back({c, 2, 1});

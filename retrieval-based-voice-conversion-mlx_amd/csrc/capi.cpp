@@ -606,7 +606,7 @@ int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const floa
     if (math == 3) {  // the weight-streamed split kernel (conv_wsb.hip) whatever the size policy would pick
       if (!conv_wsb_eligible(a)) throw Error(RVCX_E_SHAPE, "rvcx_conv1d: shape not eligible for the weight-streamed kernel");
       a.w_static = 1;
-      a.force_cfg = N <= 32 ? 24 : 23;  // the tiles the pipeline's policy picks (pick_wsb)
+      a.force_cfg = conv_wsb_pick(a);  // the tile the pipeline's policy picks for this shape
       a.no_splitk = 1;
       // a fresh split image every call, never the address-keyed cache: the caller may reuse d_w (or torch's
       // allocator may hand the address back) with new weights of the same shape

@@ -702,15 +702,31 @@ inline bool small2d_enabled() {
 // Round 3: the same tiles on v_mfma_f32_16x16x32_bf16 (cfg 24 / 23) hold a higher clock under the power-limited load
 // (bench_conv r03h, same box, 32x32x16 -> 16x16x32 TF/s: C128 k11 198 -> 214, k7 181 -> 194, k3 124 -> 131, C256 k11
 // 171 -> 182, C64 k11 177 -> 190, ConvTranspose phases 108 / 125 / 94 -> 114 / 129 / 99).
+// Round 3, wave layout per shape (cfg 23 = 2 x 2 waves of 64 x 32, 27 = 1 x 4 waves of 128 x 16, 28 = 256 x 64 as
+// 2 x 2 waves of 128 x 32). bench_conv r03bc (warm, TF/s): short taps (k = 3 ResBlock convs, ConvTranspose phases)
+// gain on 27 (C128 k3+res 141 -> 159, C64 k3+res 90 -> 109, up3 152 -> 159: a wave's 3 B loads per step feed 8 row
+// blocks), k = 7 / 11 at C_in <= 128 a little on 28 (C128 k11 244 -> 252), C256 k11 loses on 28 (208 -> 171). In the
+// C2 step (rocprof r03ab, weight-streamed time per step): 27 for k <= 3 7969 -> 7919 us, 28 for k = 7 / 11 +147 us
+// (cold activations, 2 workgroups per CU), so the long convs stay on 23 (RVCX_WCFG_LONG=28 to compare)
 inline int pick_wsb(const ConvArgs& a) {
   static const int c_narrow = env_cfg("RVCX_WCFG_NARROW", 24);
-  static const int c_mid = env_cfg("RVCX_WCFG_MID", 23);
+  static const int c_short = env_cfg("RVCX_WCFG_SHORT", 27);
+  static const int c_long = env_cfg("RVCX_WCFG_LONG", 23);
   static const int c_wide = env_cfg("RVCX_WCFG_WIDE", 23);
   static const int c_gs = env_cfg("RVCX_GCFG", 30);
   if (a.wsb == 2) return c_gs;  // gather-streamed (conv_gs.hip): the short contractions
-  return a.N <= 32 ? c_narrow : (a.N <= 64 ? c_mid : c_wide);
+  if (a.N <= 32) return c_narrow;
+  if (a.taps <= 3) return c_short;
+  return a.C_in >= 256 ? c_wide : c_long;
 }
 inline bool cfg_is_gs(int cfg) { return cfg >= 30; }
+}  // namespace
+int conv_wsb_pick(const ConvArgs& a) {
+  ConvArgs b = a;
+  b.wsb = 1;
+  return pick_wsb(b);
+}
+namespace {
 
 template <bool TWO_D>
 hipError_t dispatch(const ConvArgs& a, hipStream_t s) {

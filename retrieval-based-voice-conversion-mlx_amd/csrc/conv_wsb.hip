@@ -514,13 +514,15 @@ hipError_t conv_wsplit_build(const ConvArgs& a, void* out, hipStream_t s) {
 
 // cfg 20: 256 x 32 (4 x 1 waves of 64 x 32), 21: 128 x 64 (2 x 2 waves of 64 x 32), 22: 128 x 128 (2 x 2 of 64 x 64);
 // cfg 23 / 24: the 21 / 20 tiles on v_mfma_f32_16x16x32_bf16 (1-D); 25: 128 x 128 (2 x 2 waves of 64 x 64), 26: 256 x 64
-// (4 x 1 waves of 64 x 64) on 16x16x32. A persistent form of the 16x16x32
+// (4 x 1 waves of 64 x 64) on 16x16x32; 27: 128 x 64 as 1 x 4 waves of 128 x 16, 28: 256 x 64 as 2 x 2 waves of 128 x 32
+// (16x16x32). A persistent form of the 16x16x32
 // kernel (contiguous tile runs per workgroup, A halos and B prefetched across tile boundaries) measured slower on every
 // shape (bench_conv r03k: C128 k3 118 vs 129 TF, k11 198 vs 219, up-phases 88-111 vs 97-128): three independent
 // one-tile workgroups per CU already overlap each other's prologue and epilogue
 bool conv_wsb_tile(int cfg, int& BM, int& BN) {
-  static const int t[7][2] = {{256, 32}, {128, 64}, {128, 128}, {128, 64}, {256, 32}, {128, 128}, {256, 64}};
-  if (cfg < 20 || cfg > 26) return false;
+  static const int t[9][2] = {{256, 32}, {128, 64}, {128, 128}, {128, 64}, {256, 32}, {128, 128}, {256, 64},
+                              {128, 64}, {256, 64}};
+  if (cfg < 20 || cfg > 28) return false;
   BM = t[cfg - 20][0];
   BN = t[cfg - 20][1];
   return true;
@@ -537,6 +539,8 @@ hipError_t conv_wsb_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream
     case 24: return launch_wsb16<256, 32, 4, 1>(a, ntn_enable, ksplit, s);
     case 25: return launch_wsb16<128, 128, 2, 2>(a, ntn_enable, ksplit, s);
     case 26: return launch_wsb16<256, 64, 4, 1>(a, ntn_enable, ksplit, s);
+    case 27: return launch_wsb16<128, 64, 1, 4>(a, ntn_enable, ksplit, s);
+    case 28: return launch_wsb16<256, 64, 2, 2>(a, ntn_enable, ksplit, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -139,7 +139,8 @@ bool conv_wsb_wants(const ConvArgs& a);
 // behind RVCX_WSB_SPLIT / RVCX_WSB_2D the small 1-D grids (with split-K) and the 3x3 2-D convs with >= 64 channels
 // 0: not routed (conv_emu / conv_gemm), 1: conv_wsb.hip, 2: conv_gs.hip
 int conv_wsb_route(const ConvArgs& a, bool two_d);
-bool conv_wsb_tile(int cfg, int& BM, int& BN);  // cfg 20..26 -> tile
+bool conv_wsb_tile(int cfg, int& BM, int& BN);  // cfg 20..28 -> tile
+int conv_wsb_pick(const ConvArgs& a);  // the weight-streamed tile cfg the size policy picks for a
 // gather-streamed split conv (conv_gs.hip) for the short contractions: pre-split weights (the conv_wsb image) in a
 // register ring, A gathered per (chunk, tap) step; 1-D (any stride / dilation) and 2-D (stride 1, OUT_ROWS), C_in % 32
 // == 0, split-K capable. cfg 30..32 -> tile
