@@ -260,14 +260,34 @@ __global__ __launch_bounds__(64) void k_flash_attn(const float* __restrict__ qkv
       }
     }
   }
-  if (!qok) return;
-  const long long row = ((long long)split * BH + bh) * T + i;
-  float* po = part_o + row * DK;
+  // O^T leaves the registers one query per lane column: stored directly, every store instruction would write 64
+  // scattered 4-B words (one per query row, 48 instructions for DK = 96). Each 32-dim tile goes through LDS instead
+  // (relq's 32 x 33 floats, free once the band is folded in) and out as float4 rows: 4 instructions of 8 whole 128-B
+  // row segments each.
+  float* ot = &relq[0][0];
+  const long long slab = ((long long)split * BH + bh) * T;
 #pragma unroll
-  for (int t = 0; t < NT; ++t)
+  for (int t = 0; t < NT; ++t) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-    for (int r = 0; r < 16; ++r) po[32 * t + crow(r, hk)] = o[t][r];
-  if (hk == 0) {
+    for (int r = 0; r < 16; ++r) ot[li * (FA_NW + 1) + crow(r, hk)] = o[t][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int idx = k * 64 + lane, rr = idx >> 3, c4 = (idx & 7) * 4;
+      if (q0 + rr < T) {
+        const float* src = ot + rr * (FA_NW + 1) + c4;
+        const f32x4 v = {src[0], src[1], src[2], src[3]};
+        *reinterpret_cast<f32x4*>(part_o + (slab + q0 + rr) * DK + 32 * t + c4) = v;
+      }
+    }
+  }
+  if (qok && hk == 0) {
+    const long long row = slab + i;
     part_ml[2 * row] = m_run;
     part_ml[2 * row + 1] = l_run;
   }
