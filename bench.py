@@ -51,6 +51,9 @@ def parse():
                     help="c2 (default, the headline line): full pipeline, 13.5 s utterance per step; c3: HiFiGAN-NSF "
                          "generator alone, B=32 x 400 frames per step; c5: 16 realtime streams, one 256 ms hop per step")
     ap.add_argument("--streams", type=int, default=16, help="c5: concurrent streams")
+    ap.add_argument("--gen-precision", choices=["fp32", "bf16"], default="fp32",
+                    help="c5: the generator's weight-streamed convs on bf16 operands (opt-in, BASELINE C5 is fp16; "
+                         "gated by tests/test_gpu_stream_ref.py at spectrogram corr >= 0.986)")
     ap.add_argument("--batch", type=int, default=8, help="c4: 30 s utterances per batched pipeline pass")
     ap.add_argument("--c4-utterances", type=int, default=512, help="c4: job size (BASELINE configs[3]: 512)")
     ap.add_argument("--selftest-launch", action="store_true",
@@ -94,7 +97,13 @@ def cpu_baseline(n_samples: int, reps: int = 2):
     from rvcx.weights import normalize_state
 
     model, ncpu, avail = _host_cpu()
-    threads = max(1, min(16, avail))
+    # one GPU's share of the host: the GPU box gives each 1-GPU job 16 CPUs (OMP_NUM_THREADS=16 there); the host's
+    # 256 logical CPUs serve every GPU slot, so os.cpu_count() would oversubscribe them
+    try:
+        share = int(os.environ.get("OMP_NUM_THREADS", "16"))
+    except ValueError:
+        share = 16
+    threads = max(1, min(share if share > 0 else 16, avail))
     torch.set_num_threads(threads)
     sw = normalize_state(synthetic.synth_state(2))
     hw = normalize_state(synthetic.hubert_state(4))
@@ -123,6 +132,7 @@ def cpu_baseline(n_samples: int, reps: int = 2):
             "sample": f"oracle Pipeline.pipeline (torch-CPU fp32, {threads} threads) on the C2 clip itself "
                       f"({sec:.2f} s, x_pad=1), median of {reps} after a 2 s warm-up ({med:.2f} s/run)",
             "host_cpu": model, "host_logical_cpus": ncpu, "host_cpus_available": avail,
+            "threads_basis": "OMP_NUM_THREADS (16 on the GPU box: one GPU's CPU share), capped by the CPUs available",
             "c1": {"value": round(5.0 / c1m, 3), "unit": "audio-sec/sec", "sec_per_clip": round(c1m, 4),
                    "sample": "C1: oracle RMVPE0Predictor.infer_from_audio on the 5 s benchmark_rmvpe.py clip, "
                              "median of 5"}}
@@ -277,6 +287,7 @@ def bench_c5(args, eng, dev, dist, rank, world):
     from rvcx.sharding import reduce_throughput
 
     S = args.streams
+    eng.set_generator_precision(args.gen_precision)
     grp = StreamGroup(eng, S, read_chunk_size=96, cross_fade_overlap_size=0.1, extra_convert_size=0.5,
                       silent_threshold=-90.0)
     block = grp.block_frame
@@ -302,9 +313,12 @@ def bench_c5(args, eng, dev, dist, rank, world):
     return {"metric": "audio-sec/sec streaming VC (C5), hop latency p50/p99", "value": round(tot["value"], 3),
             "unit": "audio-sec/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(tot["elapsed"] / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "fp32", "data": "synthetic speech-like 48 kHz streams; random-init weights",
+            "vs_baseline": None,
+            "dtype": "fp32" if args.gen_precision == "fp32" else "fp32 (generator weight-streamed convs bf16)",
+            "data": "synthetic speech-like 48 kHz streams; random-init weights",
             "config": {"workload": f"C5: {S} streams x 256 ms hop (block 12288 @48k, convert buffer 13920 @16k, "
-                                   "87 frames) per step", "streams": S, "parallelism": f"dp{world}"},
+                                   "87 frames) per step", "streams": S, "parallelism": f"dp{world}",
+                       "generator_precision": args.gen_precision},
             "latency_ms": {"p50": round(float(np.percentile(lat, 50)), 3),
                            "p99": round(float(np.percentile(lat, 99)), 3), "budget": round(hop_sec * 1e3, 1)}}
 

@@ -320,6 +320,13 @@ int rvcx_rt_process(rvcx_ctx* ctx, rvcx_rt* rt, const float* d_in, const int32_t
  * MFMA rate). Env RVCX_CONV_MATH=f32 sets the process default to 1. */
 int rvcx_set_conv_math(rvcx_ctx* ctx, int mode);
 
+/* Opt-in reduced precision for the GENERATOR (HiFi-GAN-NSF decoder) only: 1 = its weight-streamed convs (ResBlocks of
+ * the 64-512-channel stages, the ConvTranspose phases) take bf16 operands with fp32 accumulation, one MFMA product
+ * instead of the exact split's six; 0 (default) = fp32-accurate everywhere. RMVPE, HuBERT, the TextEncoder, the flow
+ * and the 32-channel fused ResBlock pairs stay fp32-accurate. For streaming (BASELINE C5 computes in fp16); no
+ * parity claim rests on it. */
+int rvcx_set_generator_precision(rvcx_ctx* ctx, int bf16);
+
 /* One Conv1d forward, time-major: d_x [T][C_in], d_w [taps][N][C_in] (torch weight [N][C_in][taps] permuted),
  * d_bias [N] (optional), d_y [T_out][N]; y[t] = bias + sum_k W[k] x[t*stride - pad + k*dilation] (zero outside).
  * The kernel family behind every contraction of the path, exposed for numerics tests; replaces

@@ -585,6 +585,13 @@ int rvcx_set_conv_math(rvcx_ctx* ctx, int mode) {
   });
 }
 
+int rvcx_set_generator_precision(rvcx_ctx* ctx, int bf16) {
+  return guard(ctx, [&] {
+    if (bf16 < 0 || bf16 > 1) throw Error(RVCX_E_INVALID, "generator precision must be 0 (fp32) or 1 (bf16)");
+    ctx->gen_lowp = bf16;
+  });
+}
+
 int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const float* d_w, const float* d_bias, int N,
                 int taps, int dilation, int pad, int stride, int math, float* d_y, int64_t T_out, void* stream) {
   return guard(ctx, [&] {

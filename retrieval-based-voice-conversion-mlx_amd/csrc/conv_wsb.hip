@@ -285,6 +285,9 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
   constexpr int NT = CONV_THREADS;
   constexpr int PA = MODE & 3;
   constexpr bool PMASK = (MODE & 4) != 0;
+  // bit 3: the opt-in reduced-precision generator (ConvArgs::lowp): bf16 operands, the hi planes' product only
+  constexpr bool LOWP = (MODE & 8) != 0;
+  constexpr int NQ = LOWP ? 1 : 3;
   constexpr int TM16 = BM / (WM * 16);
   constexpr int TN16 = BN / (WN * 16);
   static_assert(WM * WN == 4 && TM16 >= 1 && TN16 >= 1, "4 waves, whole 16x16 sub-tiles");
@@ -359,29 +362,35 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
       }
     }
   };
-  typedef bf16x8 BFrag[TN16][3];
+  typedef bf16x8 BFrag[TN16][NQ];
   auto load_b = [&](int it, BFrag& dst) __attribute__((always_inline)) {
     const size_t o = (size_t)it * bstep;
 #pragma unroll
     for (int tn = 0; tn < TN16; ++tn)
 #pragma unroll
-      for (int q = 0; q < 3; ++q) dst[tn][q] = *reinterpret_cast<const bf16x8*>(bp[tn] + o + q * WBLK);
+      for (int q = 0; q < NQ; ++q) dst[tn][q] = *reinterpret_cast<const bf16x8*>(bp[tn] + o + q * WBLK);
   };
   auto compute = [&](int tap, const BFrag& bf) __attribute__((always_inline)) {
     const int toff = tap * a.dil * ERS;
 #pragma unroll
     for (int tm = 0; tm < TM16; ++tm) {
-      bf16x8 af[3];
+      bf16x8 af[NQ];
 #pragma unroll
-      for (int q = 0; q < 3; ++q) af[q] = *reinterpret_cast<const bf16x8*>(As + aoff[tm] + toff + q * PLANE);
+      for (int q = 0; q < NQ; ++q) af[q] = *reinterpret_cast<const bf16x8*>(As + aoff[tm] + toff + q * PLANE);
+      if constexpr (LOWP) {
+#pragma unroll
+        for (int tn = 0; tn < TN16; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[tn][0], acc[tm][tn], 0, 0, 0);
+        continue;
+      }
 #pragma unroll
       for (int tn = 0; tn < TN16; ++tn) {
         f32x4 c = acc[tm][tn];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], bf[tn][0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[tn][1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[tn][2], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], bf[tn][0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[tn][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[NQ - 1], bf[tn][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[NQ / 2], bf[tn][NQ / 2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[tn][NQ - 1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[NQ / 2], bf[tn][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[tn][NQ / 2], c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[tn][0], c, 0, 0, 0);
         acc[tm][tn] = c;
       }
@@ -430,20 +439,24 @@ hipError_t launch_wsb16(const ConvArgs& a, int ntn_enable, int ksplit, hipStream
   const int ntiles = (a.N + BN - 1) / BN;
   const int ntn = ntn_enable ? ntiles : 0;
   dim3 grid(ntn ? mtiles * ntiles : mtiles, ntn ? 1 : ntiles, a.batch * ksplit);
-  const int mode = pre_mode(a.pre_act) | (a.pre_mask ? 4 : 0);
+  // the reduced-precision opt-in only without a pre-mask (the generator's convs)
+  const int mode = pre_mode(a.pre_act) | (a.pre_mask ? 4 : (a.lowp ? 8 : 0));
   auto kern = mode == 0   ? conv_wsb16_kernel<BM, BN, WM, WN, 0>
               : mode == 1 ? conv_wsb16_kernel<BM, BN, WM, WN, 1>
               : mode == 2 ? conv_wsb16_kernel<BM, BN, WM, WN, 2>
               : mode == 4 ? conv_wsb16_kernel<BM, BN, WM, WN, 4>
               : mode == 5 ? conv_wsb16_kernel<BM, BN, WM, WN, 5>
-                          : conv_wsb16_kernel<BM, BN, WM, WN, 6>;
+              : mode == 6 ? conv_wsb16_kernel<BM, BN, WM, WN, 6>
+              : mode == 8 ? conv_wsb16_kernel<BM, BN, WM, WN, 8>
+              : mode == 9 ? conv_wsb16_kernel<BM, BN, WM, WN, 9>
+                          : conv_wsb16_kernel<BM, BN, WM, WN, 10>;
   // per instantiation: raise the dynamic-LDS limit once, not per launch
-  static size_t smem_set[8] = {64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024, 64 * 1024};
-  if (smem > smem_set[mode & 7]) {
+  static size_t smem_set[16] = {};
+  if (smem > 64 * 1024 && smem > smem_set[mode & 15]) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
-    smem_set[mode & 7] = smem;
+    smem_set[mode & 15] = smem;
   }
   hipLaunchKernelGGL(kern, grid, dim3(CONV_THREADS), smem, s, a, static_cast<const char*>(a.wsplit), a.wsplit_npad,
                      nrows_a, ntn, ksplit);

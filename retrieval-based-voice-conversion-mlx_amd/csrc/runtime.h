@@ -107,6 +107,7 @@ struct Ctx {
   uint64_t call_counter = 0;
   // kernel timing (rvcx_profile): event pairs around every conv-GEMM launch, on its stream
   bool prof = false;
+  int gen_lowp = 0;  // rvcx_set_generator_precision: the generator's weight-streamed convs on bf16 operands
   int conv_math = 0;  // ConvArgs::math of every conv launch (rvcx_set_conv_math): 0 default, 1 fp32 MFMA, 2 split
   struct ProfRec {
     hipEvent_t a, b;

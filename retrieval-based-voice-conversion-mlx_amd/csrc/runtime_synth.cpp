@@ -388,6 +388,7 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
     // LeakyReLU(0.1) -> ConvTranspose1d (polyphase) ; output [B][curT][u*C] == [B][Ti][C]
     ConvArgs a = conv(cur, Cin, curT, Cin, L.w, u * C, L.taps, 1, L.pad, L.b, y, u * C, curT, B);
     a.w_static = 1;
+    a.lowp = c.gen_lowp;
     a.pre_act = ACT_LRELU;
     a.pre_slope = 0.1f;
     run(c, a, s, 2.0 * B * curT * (double)Cin * C * L.k);
@@ -470,6 +471,7 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
         const std::string n2 = rb + ".convs2." + std::to_string(m);
         ConvArgs a1 = conv(r_in, C, Ti, C, c.W(n1 + ".w"), C, k, d, (k * d - d) / 2, c.W(n1 + ".b"), T1, C, Ti, B);
         a1.w_static = 1;
+        a1.lowp = c.gen_lowp;
         a1.pre_act = ACT_LRELU;
         a1.pre_slope = 0.1f;
         a1.act = ACT_LRELU;
@@ -479,6 +481,7 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
         float* dst = last ? S : RR;
         ConvArgs a2 = conv(T1, C, Ti, C, c.W(n2 + ".w"), C, k, 1, (k - 1) / 2, c.W(n2 + ".b"), dst, C, Ti, B);
         a2.w_static = 1;
+        a2.lowp = c.gen_lowp;
         a2.res = r_in;
         a2.ldr = C;
         a2.res_bs = (long long)Ti * C;

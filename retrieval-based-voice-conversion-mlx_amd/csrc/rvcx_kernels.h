@@ -100,6 +100,9 @@ struct ConvArgs {
   int wsb = 0;  // set by the runtime (conv_wsb_route on a static weight): 1 weight-streamed kernel, 2 gather-streamed
   int ksplit = 1;
   int no_splitk = 0;
+  // opt-in reduced precision (the generator's weight-streamed convs only, Ctx::gen_lowp): bf16 operands, one MFMA
+  // product instead of the exact split's six. Never set on the parity path.
+  int lowp = 0;
   long long ws_rows = 0;
   float* ws = nullptr;
 };

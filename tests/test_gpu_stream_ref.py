@@ -75,3 +75,47 @@ def test_stream_group_16_matches_reference(engine):
     engine.check_device_status()
     assert same >= 0.95 * voiced, (same, voiced)
     grp.close()
+
+
+def test_stream_group_16_generator_bf16_gate(engine):
+    """The opt-in reduced-precision generator (rvcx_set_generator_precision: bf16 operands in the generator's
+    weight-streamed convs, RMVPE / HuBERT / TextEncoder / flow fp32-accurate) for BASELINE C5's fp16 streaming, against
+    the same fp32 reference fixture: gate v of SURVEY §8(d), per-hop spectrogram correlation >= 0.986 on every voiced
+    hop; volumes (front end, fp32) stay exact."""
+    from oracle.metrics import spectrogram_correlation
+    from rvcx.config import SYNTH_48K_V2
+    from rvcx.realtime import StreamGroup
+
+    g = golden("stream_c5_16.npz")
+    S, H, blk = int(g["n_streams"]), int(g["hops"]), int(g["block"])
+    x = _inputs(g)
+    engine.set_generator_precision("bf16")
+    try:
+        grp = StreamGroup(engine, S, read_chunk_size=96, cross_fade_overlap_size=0.1, extra_convert_size=0.5,
+                          silent_threshold=-90.0, sid=[int(v) for v in g["sids"]])
+        T, I, upp = grp.geometry["frames"], SYNTH_48K_V2.inter_channels, SYNTH_48K_V2.upp
+        rngs = [np.random.Generator(np.random.PCG64(int(g["noise_seed0"]) + s)) for s in range(S)]
+        opts = grp.opts(f0_up_key=float(g["f0_up_key"]), protect=float(g["protect"]), index_rate=0.0)
+        corrs = []
+        for h in range(H):
+            ez = np.empty((S, I, T), np.float32)
+            es = np.empty((S, T * upp), np.float32)
+            for s in range(S):
+                ez[s] = rngs[s].standard_normal((1, I, T)).astype(np.float32)[0]
+                es[s] = rngs[s].standard_normal((1, T * upp, 1)).astype(np.float32).reshape(-1)
+            out, vol = grp.process(x[:, h * blk:(h + 1) * blk], opts, eps_z=ez, eps_src=es)
+            torch.cuda.synchronize()
+            out, vol = out.cpu().numpy(), vol.cpu().numpy()
+            for s in range(S):
+                rv = float(g["vol"][s, h])
+                assert abs(float(vol[s]) - rv) <= 1e-5 * max(rv, 1e-12), (h, s, vol[s], rv)
+                if rv == 0.0:
+                    continue
+                c = spectrogram_correlation(out[s], g["out16"][s, h].astype(np.float32))
+                corrs.append(c)
+                assert c >= 0.986, (h, s, c)
+        engine.check_device_status()
+        grp.close()
+        print(f"\ngenerator bf16: {len(corrs)} voiced hops, spec corr min {min(corrs):.5f} mean {np.mean(corrs):.5f}")
+    finally:
+        engine.set_generator_precision("fp32")
