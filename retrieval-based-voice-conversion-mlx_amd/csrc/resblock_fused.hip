@@ -85,8 +85,13 @@ __device__ __forceinline__ float lrelu01(float v) { return v > 0.f ? v : v * 0.1
 // C channels, NBT 32-row time blocks per workgroup tile, TN time blocks per wave unit, ACCM the output's accumulate
 // mode (ACC_STORE / ACC_ADD / ACC_ADD_DIV: compile-time, so the accumulate target's loads are not a uniform branch
 // whose join would cost the weight ring its depth)
-template <int C, int NBT, int TN, int ACCM>
+// MODE: bits 0-1 the accumulate mode ACCM; bit 2 the opt-in reduced precision (RbPairArgs::lowp: bf16 operands, the
+// hi planes' product only; the LDS images and the weight image keep their three planes, only plane 0 is read)
+template <int C, int NBT, int TN, int MODE>
 __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, const int ntiles) {
+  constexpr int ACCM = MODE & 3;
+  constexpr bool LOWP = (MODE & 4) != 0;
+  constexpr int NQ = LOWP ? 1 : 3;
   constexpr int NCH = RbGeo<C>::NCH, ROW = RbGeo<C>::ROW, OB = C / 32;
   constexpr int UNITS = OB * NBT / TN;  // wave work units per conv: (out-channel block, TN time blocks)
   static_assert(UNITS % 4 == 0, "whole units per wave");
@@ -111,8 +116,8 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
   // blocks; one (tap, chunk) step of it is 3 A fragments (weights, global/L2, two steps ahead), 3 * TN B fragments
   // (LDS, one step ahead) and 6 * TN MFMAs.
   constexpr size_t QS = (size_t)C * 32;  // bytes of one plane of one (tap, chunk) step of the weight image
-  typedef bf16x8 AFrag[3];
-  typedef bf16x8 BFrag[TN][3];
+  typedef bf16x8 AFrag[NQ];
+  typedef bf16x8 BFrag[TN][NQ];
   const int nsteps = k * NCH;
   auto unit_ob = [&](int job) { return (wave + 4 * (job % UPW)) % OB; };
   auto unit_tg = [&](int job) { return (wave + 4 * (job % UPW)) / OB; };
@@ -123,7 +128,7 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
   auto load_a = [&](const char* wl, int st, AFrag& f) __attribute__((always_inline)) {
     const char* p = wl + (size_t)st * 3 * QS;
 #pragma unroll
-    for (int q = 0; q < 3; ++q) f[q] = *reinterpret_cast<const bf16x8*>(p + q * QS);
+    for (int q = 0; q < NQ; ++q) f[q] = *reinterpret_cast<const bf16x8*>(p + q * QS);
   };
   auto load_b = [&](const char* bl, int dil, int st, BFrag& f) __attribute__((always_inline)) {
     const int tap = st / NCH, s = st - tap * NCH;
@@ -131,17 +136,19 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
-      for (int q = 0; q < 3; ++q) f[tn][q] = *reinterpret_cast<const bf16x8*>(bp + (size_t)tn * 32 * ROW + q * 32);
+      for (int q = 0; q < NQ; ++q) f[tn][q] = *reinterpret_cast<const bf16x8*>(bp + (size_t)tn * 32 * ROW + q * 32);
   };
   auto mma = [&](const AFrag& af, const BFrag& bf, f32x16(&acc)[TN]) __attribute__((always_inline)) {
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
       f32x16 c = acc[tn];
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2], bf[tn][0], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bf[tn][1], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bf[tn][2], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1], bf[tn][0], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bf[tn][1], c, 0, 0, 0);
+      if constexpr (!LOWP) {
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[NQ - 1], bf[tn][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[NQ / 2], bf[tn][NQ / 2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bf[tn][NQ - 1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[NQ / 2], bf[tn][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bf[tn][NQ / 2], c, 0, 0, 0);
+      }
       c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bf[tn][0], c, 0, 0, 0);
       acc[tn] = c;
     }
@@ -326,13 +333,13 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
   }  // tiles
 }
 
-template <int C, int NBT, int TN, int ACCM>
+template <int C, int NBT, int TN, int MODE>
 hipError_t launch_rb_acc(const RbPairArgs& a, hipStream_t s) {
   constexpr int ROW = RbGeo<C>::ROW;
   const int h2 = (a.k - 1) / 2, h1 = h2 * a.d;
   const int TT = NBT * 32 - 2 * h2;
   const size_t smem = (size_t)(NBT * 32 + 2 * h1) * ROW + (size_t)(NBT * 32 + 2 * h2) * ROW;
-  auto kern = k_rb_pair<C, NBT, TN, ACCM>;
+  auto kern = k_rb_pair<C, NBT, TN, MODE>;
   static size_t smem_set = 64 * 1024;
   if (smem > smem_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -358,10 +365,13 @@ hipError_t launch_rb_acc(const RbPairArgs& a, hipStream_t s) {
 
 template <int C, int NBT, int TN>
 hipError_t launch_rb(const RbPairArgs& a, hipStream_t s) {
-  switch (a.acc_mode) {
+  switch (a.acc_mode | (a.lowp ? 4 : 0)) {
     case ACC_STORE: return launch_rb_acc<C, NBT, TN, ACC_STORE>(a, s);
     case ACC_ADD: return launch_rb_acc<C, NBT, TN, ACC_ADD>(a, s);
     case ACC_ADD_DIV: return launch_rb_acc<C, NBT, TN, ACC_ADD_DIV>(a, s);
+    case 4 | ACC_STORE: return launch_rb_acc<C, NBT, TN, 4 | ACC_STORE>(a, s);
+    case 4 | ACC_ADD: return launch_rb_acc<C, NBT, TN, 4 | ACC_ADD>(a, s);
+    case 4 | ACC_ADD_DIV: return launch_rb_acc<C, NBT, TN, 4 | ACC_ADD_DIV>(a, s);
     default: return hipErrorInvalidValue;
   }
 }

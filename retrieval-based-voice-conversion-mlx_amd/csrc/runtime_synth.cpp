@@ -456,6 +456,7 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
           p.B = B;
           p.y = dst;
           p.y_bs = (long long)Ti * C;
+          p.lowp = c.gen_lowp;
           if (last) {
             p.acc_mode = (j == 0) ? ACC_STORE : ((j + 1 == nk) ? ACC_ADD_DIV : ACC_ADD);
             p.acc_div = (float)nk;

@@ -172,6 +172,7 @@ struct RbPairArgs {
   int acc_mode = ACC_STORE;
   float acc_div = 1.f;
   int flags = 0;  // bit 0: next-tile x prefetch into registers (measurement aid, RVCX_RB_FLAGS)
+  int lowp = 0;   // opt-in reduced precision (Ctx::gen_lowp): bf16 operands, one MFMA product per step
 };
 bool rb_pair_fits(int C, int k, int d);
 long long rb_wsplit_bytes(int C, int k);
