@@ -5,7 +5,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 TAG=${1:-bc}; shift
 timeout -k 10 400 ./build/bench_conv 20 > gpurun_out/bench_conv_$TAG.txt 2>&1 || { echo "bench_conv failed"; tail gpurun_out/bench_conv_$TAG.txt; exit 1; }
-grep -E "^check cfg=2[3-8]" gpurun_out/bench_conv_$TAG.txt
+grep -E "^check cfg=2[3-9]" gpurun_out/bench_conv_$TAG.txt
 grep -v "^check" gpurun_out/bench_conv_$TAG.txt | grep gen | sed -E 's/ [ef](1[0-6]|2[0-2]|-1|1|3)p?: *[0-9.]+\*?//g'
 for rep in 1 2; do
   for e in X=0 "$@"; do
