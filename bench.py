@@ -51,8 +51,8 @@ def parse():
                     help="c2 (default, the headline line): full pipeline, 13.5 s utterance per step; c3: HiFiGAN-NSF "
                          "generator alone, B=32 x 400 frames per step; c5: 16 realtime streams, one 256 ms hop per step")
     ap.add_argument("--streams", type=int, default=16, help="c5: concurrent streams")
-    ap.add_argument("--gen-precision", choices=["fp32", "bf16"], default="fp32",
-                    help="c5: the generator's weight-streamed convs on bf16 operands (opt-in, BASELINE C5 is fp16; "
+    ap.add_argument("--gen-precision", choices=["fp32", "fp16"], default="fp32",
+                    help="c5: each hop's generator on fp16 operands (rvcx_rt_opts.gen_precision, BASELINE C5's fp16; "
                          "gated by tests/test_gpu_stream_ref.py at spectrogram corr >= 0.986)")
     ap.add_argument("--batch", type=int, default=8, help="c4: 30 s utterances per batched pipeline pass")
     ap.add_argument("--c4-utterances", type=int, default=512, help="c4: job size (BASELINE configs[3]: 512)")
@@ -86,10 +86,12 @@ def _host_cpu():
     return model, os.cpu_count() or 1, avail
 
 
-def cpu_baseline(n_samples: int, reps: int = 2):
+def cpu_baseline(n_samples: int, reps: int = 3):
     """Time the CPU oracle (test infrastructure: oracle/) on the SAME C2 workload: the 13.5 s clip through
-    Pipeline.pipeline (x_pad = 1), after a 2 s warm-up call; plus C1 (RMVPE f0 of the 5 s
-    benchmark_rmvpe.py clip, BASELINE configs[0]). torch-CPU fp32 with min(16, available) threads."""
+    Pipeline.pipeline (x_pad = 1), median of 3 after a 2 s warm-up call; plus C1 (RMVPE f0 of the
+    5 s benchmark_rmvpe.py clip, BASELINE configs[0]). torch-CPU fp32 on every CPU this process may run on
+    (sched_getaffinity), capped at the GPU box's per-GPU CPU share (OMP_NUM_THREADS: 16 there; the box's rules
+    forbid sizing a pool by os.cpu_count(), which counts the whole 256-CPU host that every GPU slot shares)."""
     from oracle import rmvpe as ormvpe
     from oracle.pipeline import OraclePipeline
     from rvcx import synthetic
@@ -287,7 +289,6 @@ def bench_c5(args, eng, dev, dist, rank, world):
     from rvcx.sharding import reduce_throughput
 
     S = args.streams
-    eng.set_generator_precision(args.gen_precision)
     grp = StreamGroup(eng, S, read_chunk_size=96, cross_fade_overlap_size=0.1, extra_convert_size=0.5,
                       silent_threshold=-90.0)
     block = grp.block_frame
@@ -295,7 +296,7 @@ def bench_c5(args, eng, dev, dist, rank, world):
     audio = np.stack([synthetic.speech_like(block * nh, seed=500 + 100 * rank + s, sr=48000).astype(np.float32)
                       for s in range(S)])
     x = torch.as_tensor(audio, device=dev)
-    opts = grp.opts(protect=0.5)
+    opts = grp.opts(protect=0.5, gen_precision=args.gen_precision)
     lat = []
 
     def step(i):
@@ -314,7 +315,7 @@ def bench_c5(args, eng, dev, dist, rank, world):
             "unit": "audio-sec/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(tot["elapsed"] / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32" if args.gen_precision == "fp32" else "fp32 (generator weight-streamed convs bf16)",
+            "dtype": "fp32" if args.gen_precision == "fp32" else "fp16 generator (fp32 front end, TextEncoder, flow)",
             "data": "synthetic speech-like 48 kHz streams; random-init weights",
             "config": {"workload": f"C5: {S} streams x 256 ms hop (block 12288 @48k, convert buffer 13920 @16k, "
                                    "87 frames) per step", "streams": S, "parallelism": f"dp{world}",
@@ -428,17 +429,26 @@ def main():
         return
 
     n = args.samples
-    audio = torch.as_tensor(synthetic.speech_like(n, seed=1000 + rank), dtype=torch.float64, device=dev)
+    # the utterance in pinned host memory and resident in HBM; the output buffer in HBM and pinned on the host
+    audio_host = torch.as_tensor(synthetic.speech_like(n, seed=1000 + rank), dtype=torch.float64).pin_memory()
+    audio = audio_host.to(dev)
     t_pad, t_pad_tgt = SR_IN * 1, 48000 * 1
     cap = ((n + 2 * t_pad) // 160) * eng.upp
     out = torch.empty((cap,), dtype=torch.float32, device=dev)
+    out_host = torch.empty((cap,), dtype=torch.float32).pin_memory()
 
-    def step(i):
-        return eng.pipeline(audio, sid=0, semitones=0.0, protect=0.33, t_pad=t_pad, t_pad_tgt=t_pad_tgt,
-                            seed=1234 + i, out=out)
+    def step(i, host_io=False):
+        # host_io: SURVEY §8(d)'s host audio-in -> audio-out, the H2D and D2H copies on the compute stream
+        if host_io:
+            audio.copy_(audio_host, non_blocking=True)
+        y = eng.pipeline(audio, sid=0, semitones=0.0, protect=0.33, t_pad=t_pad, t_pad_tgt=t_pad_tgt,
+                         seed=1234 + i, out=out)
+        if host_io:
+            out_host[: y.numel()].copy_(y, non_blocking=True)
+        return y
 
     for i in range(args.warmup):
-        step(i)
+        step(i, host_io=True)
     torch.cuda.synchronize(dev)
     eng.profile_read()  # drop anything recorded so far
     eng.profile(args.roofline_pass == "inline")
@@ -453,6 +463,17 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     eng.profile(False)
+    # the same K steps from pinned host input to pinned host output (PCIe-inclusive; reported beside value)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    th0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i, host_io=True)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    th1 = time.perf_counter()
     if args.roofline_pass == "after":
         eng.profile(True)
         for i in range(args.steps):
@@ -465,6 +486,7 @@ def main():
     audio_sec = n / SR_IN
     # whole job: audio-seconds summed over ranks / wall time maxed over ranks
     tot = reduce_throughput(dist, args.steps * audio_sec, t1 - t0, device=dev)
+    tot_io = reduce_throughput(dist, args.steps * audio_sec, th1 - th0, device=dev)
     elapsed = tot["elapsed"]
     ms_per_step = elapsed / args.steps * 1000.0
     value = tot["value"]
@@ -502,6 +524,11 @@ def main():
                        "samples_16k": n, "audio_sec_per_step_per_gpu": round(audio_sec, 5), "x_pad": 1,
                        "f0_method": "rmvpe", "index_rate": 0, "protect": 0.33, "parallelism": f"dp{world}"},
             "roofline": roofline, "cpu_baseline": cpu,
+            # SURVEY §8(d)'s definition: pinned host audio in -> pinned host audio out, the H2D (1.7 MB fp64) and
+            # D2H (2.6 MB fp32) copies on the compute stream inside the timed loop; value above is HBM-resident
+            "host_io": {"value": round(tot_io["value"], 3), "unit": "audio-sec/sec",
+                        "ms_per_step": round(tot_io["elapsed"] / args.steps * 1000.0, 3),
+                        "timed": "pinned host input -> H2D -> pipeline -> D2H -> pinned host output, same K steps"},
         }
         print(json.dumps(rec))
     if dist:

@@ -294,6 +294,11 @@ typedef struct {                  /* per-hop options of VoiceChanger.on_request 
   double f0_autotune_strength;
   int proposed_pitch;             /* one host sync per hop */
   double proposed_pitch_threshold;
+  int gen_precision;              /* 0 (default) fp32-accurate everywhere; 1 = this hop's GENERATOR (HiFi-GAN-NSF
+                                   * decoder: its weight-streamed convs and 32-channel fused ResBlock pairs) on fp16
+                                   * operands with fp32 accumulation, one MFMA product per step: BASELINE C5's fp16
+                                   * streaming. RMVPE, HuBERT, the TextEncoder and the flow stay fp32-accurate, and no
+                                   * other entry point is affected (the setting travels with the hop, not the ctx). */
 } rvcx_rt_opts;
 
 int rvcx_rt_default_desc(rvcx_rt_desc* desc);
@@ -317,15 +322,10 @@ int rvcx_rt_process(rvcx_ctx* ctx, rvcx_rt* rt, const float* d_in, const int32_t
  * the reference; torch's fp32 CPU conv is what both modes reproduce): 0 = default (2), 1 = fp32-input MFMA
  * (v_mfma_f32_32x32x2_f32, an exact fp32 fma chain at 157 TF), 2 = fp32 through an exact 3-way bf16 split of both
  * operands with the six significant plane products on bf16 MFMA (error below fp32's own rounding, 2.67x the
- * MFMA rate). Env RVCX_CONV_MATH=f32 sets the process default to 1. */
+ * MFMA rate), 3 = as 2, except that the generator-sized weight-streamed convs split both operands into two fp16
+ * planes (22 significand bits each) with three plane products (csrc/split_bf16.h). Env RVCX_CONV_MATH=f32 | h16
+ * sets the process default to 1 | 3. */
 int rvcx_set_conv_math(rvcx_ctx* ctx, int mode);
-
-/* Opt-in reduced precision for the GENERATOR (HiFi-GAN-NSF decoder) only: 1 = its weight-streamed convs (ResBlocks of
- * the 64-512-channel stages, the ConvTranspose phases) take bf16 operands with fp32 accumulation, one MFMA product
- * instead of the exact split's six; 0 (default) = fp32-accurate everywhere. RMVPE, HuBERT, the TextEncoder, the flow
- * and the 32-channel fused ResBlock pairs stay fp32-accurate. For streaming (BASELINE C5 computes in fp16); no
- * parity claim rests on it. */
-int rvcx_set_generator_precision(rvcx_ctx* ctx, int bf16);
 
 /* One Conv1d forward, time-major: d_x [T][C_in], d_w [taps][N][C_in] (torch weight [N][C_in][taps] permuted),
  * d_bias [N] (optional), d_y [T_out][N]; y[t] = bias + sum_k W[k] x[t*stride - pad + k*dilation] (zero outside).

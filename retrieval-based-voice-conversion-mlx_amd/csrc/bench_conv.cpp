@@ -76,8 +76,11 @@ int main(int argc, char** argv) {
                        pad, 1);
     std::vector<float> ref((size_t)T * N), out((size_t)T * N);
     CK_(hipMemcpy(ref.data(), yr, ref.size() * 4, hipMemcpyDeviceToHost));
+    // fmt 1: the two-plane fp16 image (math 3), fmt 2: its reduced-precision hi-plane mode
     for (int cfg : {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 20, 21, 22, 23, 24, 25, 26, 27, 28})
-      for (int pipe : {-1}) {
+      for (int fmt : {0, 1, 2}) {
+        if (fmt && cfg != 23 && cfg != 24 && cfg != 27) continue;
+        const int pipe = -1;
         ConvArgs a;
         a.x = x; a.ldx = C; a.T_in = T; a.C_in = C;
         a.w = w; a.ldw = C; a.w_ts = (long long)N * C; a.taps = taps; a.dil = dil; a.pad = pad;
@@ -86,22 +89,27 @@ int main(int argc, char** argv) {
         a.force_cfg = cfg; a.pipe = pipe;
         void* wsb = nullptr;
         if (cfg >= 20) {  // weight-streamed split kernel: pre-split weight image
+          a.wsplit_fmt = fmt ? WSPLIT_H16 : WSPLIT_BF16;
+          a.lowp = fmt == 2;
           CK_(hipMalloc(&wsb, conv_wsplit_bytes(a)));
           CK_(conv_wsplit_build(a, wsb, 0));
-          a.wsplit = wsb; a.wsplit_npad = conv_wsplit_npad(a.N); a.math = 2; a.wsb = 1;
+          a.wsplit = wsb; a.wsplit_npad = conv_wsplit_npad(a.N); a.math = fmt ? 3 : 2; a.wsb = 1;
         }
         CK_(hipMemset(y, 0, (size_t)T * N * 4));
         CK_(conv1d(a, 0));
         if (wsb) (void)hipFree(wsb);
         CK_(hipDeviceSynchronize());
         CK_(hipMemcpy(out.data(), y, out.size() * 4, hipMemcpyDeviceToHost));
-        double md = 0, mr = 0;
+        double md = 0, mr = 0, se = 0;
         for (size_t i = 0; i < out.size(); ++i) {
           md = std::max(md, (double)fabsf(out[i] - ref[i]));
           mr = std::max(mr, (double)fabsf(ref[i]));
+          se += (double)(out[i] - ref[i]) * (out[i] - ref[i]);
         }
-        printf("check cfg=%d (%s) pipe=%d max|diff|/max|ref| = %.3e %s\n", cfg, cfg >= 10 ? "split" : "f32", pipe,
-               md / mr, md / mr < 1e-5 ? "OK" : "FAIL");
+        const double tol = fmt == 2 ? 2e-2 : 1e-5;
+        printf("check cfg=%d (%s) pipe=%d max|diff|/max|ref| = %.3e rms diff %.3e %s\n", cfg,
+               fmt == 2 ? "h16 lowp" : (fmt ? "h16x2" : (cfg >= 10 ? "split" : "f32")), pipe, md / mr,
+               std::sqrt(se / out.size()), md / mr < tol ? "OK" : "FAIL");
       }
   }
   // split-K correctness on small-M shapes
@@ -187,8 +195,8 @@ int main(int argc, char** argv) {
     const double flops = 2.0 * cs.T * cs.N * (double)cs.Cin * cs.taps;
     // variants: (cfg, math, pipe); cfg -1 = the library's policy for that math
     struct V { int cfg, math, pipe; };
-    std::vector<V> vars = {{-1, 2, 0}, {20, 2, -1}, {21, 2, -1}, {22, 2, -1}, {23, 2, -1}, {24, 2, -1}, {25, 2, -1}, {26, 2, -1}, {27, 2, -1}, {28, 2, -1}, {10, 2, -1}, {11, 2, -1}, {12, 2, -1}, {13, 2, -1}, {14, 2, -1}, {15, 2, -1},
-                           {16, 2, -1}, {-1, 1, 0}, {1, 1, -1}, {3, 1, -1}};
+    std::vector<V> vars = {{-1, 2, 0}, {23, 2, -1}, {24, 2, -1}, {27, 2, -1}, {28, 2, -1}, {23, 3, -1}, {24, 3, -1},
+                           {27, 3, -1}, {23, 4, -1}, {27, 4, -1}, {13, 2, -1}, {1, 1, -1}};
     if (cs.taps == 1)
       for (int c : {10, 12, 13, 14, 15}) vars.push_back({c, 2, 1});
     printf("%-28s", cs.name);
@@ -208,7 +216,9 @@ int main(int argc, char** argv) {
           a.act = ACT_NONE;
           a.res = rb; a.ldr = cs.N; a.res_mode = RES_ADD_POST; a.acc_mode = ACC_ADD;
         }
-        a.force_cfg = vv.cfg; a.pipe = vv.pipe; a.math = vv.math;
+        a.force_cfg = vv.cfg; a.pipe = vv.pipe; a.math = vv.math == 4 ? 3 : vv.math;
+        a.wsplit_fmt = vv.math >= 3 ? WSPLIT_H16 : WSPLIT_BF16;
+        a.lowp = vv.math == 4;
         float* wsp = nullptr;
         void* wsb = nullptr;
         if (vv.cfg >= 20) {
@@ -244,7 +254,8 @@ int main(int argc, char** argv) {
         if (wsp) (void)hipFree(wsp);
         if (wsb) (void)hipFree(wsb);
       }
-      printf(" %s%d%s:%6.1f%s", vv.math == 2 ? "e" : "f", vv.cfg, vv.pipe > 0 ? "p" : "", best, ksp > 1 ? "*" : " ");
+      printf(" %s%d%s:%6.1f%s", vv.math == 2 ? "e" : (vv.math == 3 ? "h" : (vv.math == 4 ? "l" : "f")), vv.cfg,
+             vv.pipe > 0 ? "p" : "", best, ksp > 1 ? "*" : " ");
     }
     printf("\n");
     fflush(stdout);

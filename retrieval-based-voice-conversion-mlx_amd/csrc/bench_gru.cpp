@@ -43,13 +43,14 @@ int main(int argc, char** argv) {
   CK_(hipMemcpy(gi, hgi.data(), hgi.size() * 4, hipMemcpyHostToDevice));
   CK_(hipMemcpy(w, hw.data(), hw.size() * 4, hipMemcpyHostToDevice));
   CK_(hipMemcpy(b, hb.data(), hb.size() * 4, hipMemcpyHostToDevice));
-  CK_(gru_bidir(gi, w, b, w, b, T, out, xchg, status, 0, B));
+  unsigned tag = 0;
+  CK_(gru_bidir(gi, w, b, w, b, T, out, xchg, status, &tag, 0, B));
   CK_(hipDeviceSynchronize());
   hipEvent_t e0, e1;
   CK_(hipEventCreate(&e0));
   CK_(hipEventCreate(&e1));
   CK_(hipEventRecord(e0, 0));
-  for (int i = 0; i < iters; ++i) CK_(gru_bidir(gi, w, b, w, b, T, out, xchg, status, 0, B));
+  for (int i = 0; i < iters; ++i) CK_(gru_bidir(gi, w, b, w, b, T, out, xchg, status, &tag, 0, B));
   CK_(hipEventRecord(e1, 0));
   CK_(hipEventSynchronize(e1));
   float ms = 0;

@@ -119,7 +119,7 @@ void join_aux(Ctx& c, hipStream_t s, hipStream_t ax) {
 // the weight tensor's pre-split image (built once on first use; the stream then synchronises so a later use on
 // another stream never races the build)
 const void* Ctx::wsplit_for(const ConvArgs& a, hipStream_t s) {
-  const auto key = std::make_tuple(static_cast<const void*>(a.w), a.ldw, a.w_ts, a.N, a.C_in, a.taps);
+  const auto key = std::make_tuple(static_cast<const void*>(a.w), a.ldw, a.w_ts, a.N, a.C_in, a.taps, a.wsplit_fmt);
   auto& slot = wsplit_cache[key];
   if (!slot) {
     std::unique_ptr<DevBuf> b(new DevBuf());
@@ -199,6 +199,8 @@ void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double
              : (a.force_cfg >= 20 && !two_d) ? 1 : (a.force_cfg < 0 ? conv_wsb_route(a, two_d) : 0));
   const long long need = conv_plan_splitk(a, two_d);
   if (a.wsb) {
+    // the weight-streamed kernel's fp16 image: the two-plane fp16 arithmetic (math 3) or the reduced-precision mode
+    if (!a.wsplit) a.wsplit_fmt = (a.wsb == 1 && (a.lowp || conv_math_of(a) == 3)) ? WSPLIT_H16 : WSPLIT_BF16;
     if (!a.wsplit) a.wsplit = c.wsplit_for(a, s);  // a caller-built image (rvcx_conv1d) is used as given
     a.wsplit_npad = conv_wsplit_npad(a.N);
   }
@@ -580,15 +582,8 @@ int rvcx_index_parse(const void* bytes, int64_t nbytes, int64_t* d, int64_t* nto
 
 int rvcx_set_conv_math(rvcx_ctx* ctx, int mode) {
   return guard(ctx, [&] {
-    if (mode < 0 || mode > 2) throw Error(RVCX_E_INVALID, "conv math mode must be 0, 1 or 2");
+    if (mode < 0 || mode > 3) throw Error(RVCX_E_INVALID, "conv math mode must be 0, 1, 2 or 3");
     ctx->conv_math = mode;
-  });
-}
-
-int rvcx_set_generator_precision(rvcx_ctx* ctx, int bf16) {
-  return guard(ctx, [&] {
-    if (bf16 < 0 || bf16 > 1) throw Error(RVCX_E_INVALID, "generator precision must be 0 (fp32) or 1 (bf16)");
-    ctx->gen_lowp = bf16;
   });
 }
 

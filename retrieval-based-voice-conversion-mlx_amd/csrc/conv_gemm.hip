@@ -637,11 +637,13 @@ inline int env_cfg(const char* name, int dflt) {
   return e ? std::atoi(e) : dflt;
 }
 // contraction arithmetic: 1 = native fp32 MFMA (conv_gemm_kernel), 2 = fp32 through the 3-way bf16 split
-// (conv_emu.hip, the default); ConvArgs::math overrides RVCX_CONV_MATH (f32 | split)
+// (conv_emu.hip, the default), 3 = as 2 except the weight-streamed kernel, which takes the two-plane fp16 split
+// (the WSPLIT_H16 image); ConvArgs::math overrides RVCX_CONV_MATH (f32 | split | h16)
 inline int conv_math(const ConvArgs& a) {
   static const int env = [] {
     const char* e = std::getenv("RVCX_CONV_MATH");
     if (e && (std::string(e) == "f32" || std::string(e) == "1")) return 1;
+    if (e && (std::string(e) == "h16" || std::string(e) == "3")) return 3;
     return 2;
   }();
   return a.math > 0 ? a.math : env;
@@ -670,7 +672,7 @@ int pick_emu(const ConvArgs& a) {
 template <bool TWO_D>
 int pick_cfg(const ConvArgs& a) {
   if (a.force_cfg >= 0) return a.force_cfg;
-  if (conv_math(a) == 2) return pick_emu<TWO_D>(a);
+  if (conv_math(a) >= 2) return pick_emu<TWO_D>(a);
   static const int c_long = env_cfg("RVCX_CFG_LONG", 1);      // 1-D, taps >= 5, N > 32 (A/B: 32.8 vs 33.6 ms)
   static const int c_short = env_cfg("RVCX_CFG_SHORT", 3);    // everything else with N > 32
   static const int c_narrow = env_cfg("RVCX_CFG_NARROW", 1);  // N <= 32
@@ -733,14 +735,14 @@ hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
   if (a.N <= 0 || a.T_out <= 0 || a.batch <= 0) return hipSuccess;
   if (a.C_in <= 0 || a.taps <= 0) return hipErrorInvalidValue;
   if (tiny_fits(a)) return launch_tiny(a, TWO_D, s);
-  if (a.wsb == 2 && a.wsplit && conv_math(a) == 2 && conv_gs_eligible(a, TWO_D)) {
+  if (a.wsb == 2 && a.wsplit && conv_math(a) >= 2 && conv_gs_eligible(a, TWO_D)) {
     const int ks = (a.ws && a.ksplit > 1) ? a.ksplit : 1;
     const int cfg = a.force_cfg >= 30 ? a.force_cfg : pick_wsb(a);
     hipError_t e = conv_gs_launch(a, cfg, xcd_enabled() ? 1 : 0, s, TWO_D, ks);
     if (e == hipSuccess && ks > 1) e = launch_splitk_reduce(a, ks, TWO_D, s);
     if (e != hipErrorInvalidValue) return e;
   }
-  if (a.wsb == 1 && a.wsplit && conv_math(a) == 2 && conv_wsb_eligible(a, TWO_D)) {
+  if (a.wsb == 1 && a.wsplit && conv_math(a) >= 2 && conv_wsb_eligible(a, TWO_D)) {
     const int ks = (a.ws && a.ksplit > 1) ? a.ksplit : 1;
     const int cfg = TWO_D ? 21 : (a.force_cfg >= 20 ? a.force_cfg : pick_wsb(a));
     hipError_t e = conv_wsb_launch(a, cfg, xcd_enabled() ? 1 : 0, s, TWO_D, ks);
@@ -853,7 +855,7 @@ bool conv_wsb_wants(const ConvArgs& a) {
     const char* e = std::getenv("RVCX_NO_WSB");
     return e && std::atoi(e) != 0;
   }();
-  if (off || conv_math(a) != 2 || !conv_wsb_eligible(a)) return false;
+  if (off || conv_math(a) < 2 || !conv_wsb_eligible(a)) return false;
   // where it measured faster (bench_conv, profiles/r02i_bench_conv.txt: 128 x 64 tiles of 2 x 2 waves of 64 x 32
   // with the register epilogue; C2 A/B): N >= 64 with >= 2 taps (ResBlock convs at 64-256 channels incl. k = 3, the
   // polyphase ConvTranspose phases), on a grid that fills the chip (RVCX_WSB_MINN / _MINTAPS / _MINTILES: A/B aid)
@@ -870,7 +872,7 @@ int conv_wsb_route(const ConvArgs& a, bool two_d) {
   static const bool route_2d = env_cfg("RVCX_WSB_2D", 0) != 0;     // 3x3 2-D convs, >= 64 channels
   static const bool gs_on = env_cfg("RVCX_NO_GS", 0) == 0;         // the gather-streamed kernel (A/B aid)
   static const int gs_min_n = env_cfg("RVCX_GS_MINN", 64);
-  if (conv_math(a) != 2 || tiny_fits(a)) return 0;
+  if (conv_math(a) < 2 || tiny_fits(a)) return 0;
   if (two_d && small2d_enabled() && conv2d_small_fits(a)) return 0;
   if (conv_wsb_eligible(a, two_d)) {
     if (two_d && route_2d && a.N >= 64 && a.C_in >= 64) return 1;
@@ -882,6 +884,7 @@ int conv_wsb_route(const ConvArgs& a, bool two_d) {
   return 0;
 }
 
+int conv_math_of(const ConvArgs& a) { return conv_math(a); }
 hipError_t conv1d(const ConvArgs& a, hipStream_t s) { return dispatch<false>(a, s); }
 hipError_t conv2d(const ConvArgs& a, hipStream_t s) { return dispatch<true>(a, s); }
 

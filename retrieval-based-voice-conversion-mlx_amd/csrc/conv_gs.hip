@@ -492,7 +492,7 @@ bool conv_gsw_eligible(const ConvArgs& a) {
 }
 
 hipError_t conv_gs_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream_t s, bool two_d, int ksplit) {
-  if (!a.wsplit || !conv_gs_eligible(a, two_d)) return hipErrorInvalidValue;
+  if (!a.wsplit || !conv_gs_eligible(a, two_d) || a.wsplit_fmt != WSPLIT_BF16) return hipErrorInvalidValue;
   if (two_d && cfg == 30 && conv_gsw_eligible(a)) return launch_gsw(a, ntn_enable, ksplit, s);
   if (two_d) {
     switch (cfg) {

@@ -63,6 +63,58 @@ __global__ void k_wsplit(const float* __restrict__ w, int ldw, long long w_ts, i
   }
 }
 
+// The two-plane fp16 image (split_bf16.h put_h16x4 arithmetic) of the same weights: per (chunk, tap) step and 16-column
+// group two 1 KB blocks [h | l], lane-major as k_wsplit's. The weights are scaled by a power of two s (max |w| s in
+// [128, 256): small weights stay normal fp16) and the activations by 2^-4 (inputs up to 2^20 stay finite); the image's
+// tail holds {s, 1 / (s 2^-4)}, which the kernel's epilogue multiplies back in exactly.
+constexpr int WROW_H = 2 * PLANE;  // bytes of one (chunk, tap, column) row of the fp16 image
+constexpr float H16_XS = 1.f / 16.f;
+__global__ void k_wmax_scale(const float* __restrict__ w, int ldw, long long w_ts, int N, int C_in, int taps,
+                             float* __restrict__ tail) {
+  __shared__ float red[1024 / 64];
+  float m = 0.f;
+  const long long total = (long long)taps * N * C_in;
+  for (long long i = threadIdx.x; i < total; i += blockDim.x) {
+    const int c = (int)(i % C_in);
+    const long long r = i / C_in;
+    const int n = (int)(r % N), tap = (int)(r / N);
+    m = fmaxf(m, fabsf(w[tap * w_ts + (long long)n * ldw + c]));
+  }
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) m = fmaxf(m, red[i]);
+    red[0] = m;
+    int e = 0;
+    (void)frexpf(m, &e);  // m = f 2^e, f in [0.5, 1)
+    const float sc = m > 0.f ? ldexpf(1.f, 8 - e) : 1.f;
+    tail[0] = sc;
+    tail[1] = 1.f / (sc * H16_XS);
+  }
+}
+__global__ void k_wsplit_h16(const float* __restrict__ w, int ldw, long long w_ts, int N, int C_in, int taps,
+                             int nchunks, int Npad, unsigned short* __restrict__ out, const float* __restrict__ tail) {
+  const float sc = tail[0];
+  const long long total = (long long)nchunks * taps * Npad * EK;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % EK);
+    const long long r = i / EK;
+    const int n = (int)(r % Npad);
+    const long long ct = r / Npad;
+    const int tap = (int)(ct % taps), ch = (int)(ct / taps);
+    const int cc = ch * EK + c;
+    const float v = (n < N && cc < C_in) ? w[tap * w_ts + (long long)n * ldw + cc] * sc : 0.f;
+    const unsigned h = pk_f16(v, 0.f);
+    const unsigned l = pk_f16((v - f16lo_f(h)) * H16_LO, 0.f);
+    const long long blk = (ct * (Npad / 16) + n / 16) * 2;
+    unsigned short* o = out + blk * (WBLK / 2) + ((c >> 3) * 16 + (n & 15)) * 8 + (c & 7);
+    o[0] = (unsigned short)h;
+    o[WBLK / 2] = (unsigned short)l;
+  }
+}
+
 #ifndef WSB_WAVES_128x64
 #define WSB_WAVES_128x64 3
 #endif
@@ -277,7 +329,9 @@ __global__ __launch_bounds__(CONV_THREADS, (BM == 128 && BN == 64 && !TWO_D) ? W
 // cycles per step as the 32x32x16 form at the same wave tile. The chip sustains a higher clock on this shape under
 // power-limited load (MI355X_MICROARCH.md "DVFS give-back" item 7), which is the point.
 // C layout of a 16x16 tile: lane l holds column l % 16, rows 4 (l / 16) + r, r = 0..3.
-// MODE: bits 0-1 the pre-activation (pre_fn), bit 2 a pre-mask row multiplier (conv_gs.hip's MODE)
+// MODE: bits 0-1 the pre-activation (pre_fn), bit 2 a pre-mask row multiplier (conv_gs.hip's MODE), bit 4 the
+// two-plane fp16 arithmetic (split_bf16.h put_h16x4; weights from the k_wsplit_h16 image), bit 3 (with bit 4) the
+// opt-in reduced precision: the fp16 hi planes' product alone
 template <int BM, int BN, int WM, int WN, int MODE>
 __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 : 3) void conv_wsb16_kernel(const ConvArgs a, const char* __restrict__ wsp,
                                                                      const int Npad, const int nrows_a, const int ntn,
@@ -285,9 +339,11 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
   constexpr int NT = CONV_THREADS;
   constexpr int PA = MODE & 3;
   constexpr bool PMASK = (MODE & 4) != 0;
-  // bit 3: the opt-in reduced-precision generator (ConvArgs::lowp): bf16 operands, the hi planes' product only
-  constexpr bool LOWP = (MODE & 8) != 0;
-  constexpr int NQ = LOWP ? 1 : 3;
+  constexpr bool H16 = (MODE & 16) != 0;
+  constexpr bool LOWP = H16 && (MODE & 8) != 0;
+  constexpr int NQ = LOWP ? 1 : (H16 ? 2 : 3);  // planes an MFMA step reads
+  constexpr int NQI = H16 ? 2 : 3;               // planes of the weight image
+  constexpr int RS = H16 ? ERS_H : ERS;          // LDS row stride
   constexpr int TM16 = BM / (WM * 16);
   constexpr int TN16 = BN / (WN * 16);
   static_assert(WM * WN == 4 && TM16 >= 1 && TN16 >= 1, "4 waves, whole 16x16 sub-tiles");
@@ -311,17 +367,21 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
 
   int aoff[TM16];
 #pragma unroll
-  for (int tm = 0; tm < TM16; ++tm) aoff[tm] = (wm * TM16 * 16 + tm * 16 + lc) * ERS + lg * 16;
+  for (int tm = 0; tm < TM16; ++tm) aoff[tm] = (wm * TM16 * 16 + tm * 16 + lc) * RS + lg * 16;
   const char* bp[TN16];  // lane l reads 16-B slot l of each block: one contiguous 1 KB per wave load
 #pragma unroll
-  for (int tn = 0; tn < TN16; ++tn) bp[tn] = wsp + (size_t)((n0 + wn * TN16 * 16 + tn * 16) >> 4) * (3 * WBLK) + lane * 16;
-  const size_t bstep = (size_t)Npad * WROW;
+  for (int tn = 0; tn < TN16; ++tn)
+    bp[tn] = wsp + (size_t)((n0 + wn * TN16 * 16 + tn * 16) >> 4) * (NQI * WBLK) + lane * 16;
+  const size_t bstep = (size_t)Npad * NQI * PLANE;
 
-  f32x4 acc[TM16][TN16];
+  f32x4 acc[TM16][TN16], acc2[H16 && !LOWP ? TM16 : 1][H16 && !LOWP ? TN16 : 1];
 #pragma unroll
   for (int tm = 0; tm < TM16; ++tm)
 #pragma unroll
-    for (int tn = 0; tn < TN16; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int tn = 0; tn < TN16; ++tn) {
+      acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (H16 && !LOWP) acc2[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
 
   constexpr int AP = ((BM + WSB_HALO) * EC4 + NT - 1) / NT;
   f32x4 apre[AP];
@@ -358,7 +418,13 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
 #pragma unroll
           for (int j = 0; j < 4; ++j) val[j] = ok ? val[j] : 0.f;
         }
-        put_split4(As + r * ERS, ac4, val);
+        if constexpr (H16) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) val[j] *= H16_XS;
+          put_h16x4<NQ>(As + r * RS, ac4, val);
+        } else {
+          put_split4(As + r * RS, ac4, val);
+        }
       }
     }
   };
@@ -371,16 +437,25 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
       for (int q = 0; q < NQ; ++q) dst[tn][q] = *reinterpret_cast<const bf16x8*>(bp[tn] + o + q * WBLK);
   };
   auto compute = [&](int tap, const BFrag& bf) __attribute__((always_inline)) {
-    const int toff = tap * a.dil * ERS;
+    const int toff = tap * a.dil * RS;
 #pragma unroll
     for (int tm = 0; tm < TM16; ++tm) {
       bf16x8 af[NQ];
 #pragma unroll
       for (int q = 0; q < NQ; ++q) af[q] = *reinterpret_cast<const bf16x8*>(As + aoff[tm] + toff + q * PLANE);
-      if constexpr (LOWP) {
+      if constexpr (H16) {
+        const f16x8 ah = __builtin_bit_cast(f16x8, af[0]);
 #pragma unroll
-        for (int tn = 0; tn < TN16; ++tn)
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[tn][0], acc[tm][tn], 0, 0, 0);
+        for (int tn = 0; tn < TN16; ++tn) {
+          const f16x8 bh = __builtin_bit_cast(f16x8, bf[tn][0]);
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc[tm][tn], 0, 0, 0);
+          if constexpr (!LOWP) {
+            f32x4 c = acc2[tm][tn];
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, af[NQ - 1]), bh, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, __builtin_bit_cast(f16x8, bf[tn][NQ - 1]), c, 0, 0, 0);
+            acc2[tm][tn] = c;
+          }
+        }
         continue;
       }
 #pragma unroll
@@ -427,36 +502,54 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
       if (it + 1 < it1) step(it + 1, b1, b0);
     }
   }
+  if constexpr (H16) {
+    // acc + 2^-11 acc2, times 1 / (weight scale x activation scale) from the image tail: exact powers of two
+    const float inv = *reinterpret_cast<const float*>(wsp + (size_t)total * bstep + sizeof(float));
+#pragma unroll
+    for (int tm = 0; tm < TM16; ++tm)
+#pragma unroll
+      for (int tn = 0; tn < TN16; ++tn)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[tm][tn][r];
+          if constexpr (!LOWP) v += acc2[tm][tn][r] * H16_LO_INV;
+          acc[tm][tn][r] = v * inv;
+        }
+  }
   store_tile16<TM16, TN16, WM, WN>(a, m0, n0, b, zsplit, ksplit, (long long)a.T_out, acc);
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, bool H16OK = false>
 hipError_t launch_wsb16(const ConvArgs& a, int ntn_enable, int ksplit, hipStream_t s) {
   const int nrows_a = BM + (a.taps - 1) * a.dil;
   const int mtiles = (a.T_out + BM - 1) / BM;
-  const size_t smem = (size_t)nrows_a * ERS;
+  const bool h16 = a.wsplit_fmt == WSPLIT_H16;
+  const size_t smem = (size_t)nrows_a * (h16 ? ERS_H : ERS);
   if (a.wsplit_npad % BN != 0 || ksplit < 1 || (ksplit > 1 && !a.ws)) return hipErrorInvalidValue;
+  if (a.lowp && !h16) return hipErrorInvalidValue;  // the reduced-precision mode reads the fp16 image's hi plane
+  if (h16 && !H16OK) return hipErrorInvalidValue;   // fp16 instantiations only for the tiles the policy picks
   const int ntiles = (a.N + BN - 1) / BN;
   const int ntn = ntn_enable ? ntiles : 0;
   dim3 grid(ntn ? mtiles * ntiles : mtiles, ntn ? 1 : ntiles, a.batch * ksplit);
   // the reduced-precision opt-in only without a pre-mask (the generator's convs)
-  const int mode = pre_mode(a.pre_act) | (a.pre_mask ? 4 : (a.lowp ? 8 : 0));
-  auto kern = mode == 0   ? conv_wsb16_kernel<BM, BN, WM, WN, 0>
-              : mode == 1 ? conv_wsb16_kernel<BM, BN, WM, WN, 1>
-              : mode == 2 ? conv_wsb16_kernel<BM, BN, WM, WN, 2>
-              : mode == 4 ? conv_wsb16_kernel<BM, BN, WM, WN, 4>
-              : mode == 5 ? conv_wsb16_kernel<BM, BN, WM, WN, 5>
-              : mode == 6 ? conv_wsb16_kernel<BM, BN, WM, WN, 6>
-              : mode == 8 ? conv_wsb16_kernel<BM, BN, WM, WN, 8>
-              : mode == 9 ? conv_wsb16_kernel<BM, BN, WM, WN, 9>
-                          : conv_wsb16_kernel<BM, BN, WM, WN, 10>;
+  const int mode = pre_mode(a.pre_act) | (a.pre_mask ? 4 : 0) | (h16 ? 16 : 0) | (h16 && a.lowp && !a.pre_mask ? 8 : 0);
+  void (*kern)(const ConvArgs, const char*, int, int, int, int);
+  switch (mode) {
+#define WSB16_CASE(M) \
+  case M: kern = conv_wsb16_kernel<BM, BN, WM, WN, (H16OK || M < 16) ? M : 0>; break;
+    WSB16_CASE(0) WSB16_CASE(1) WSB16_CASE(2) WSB16_CASE(4) WSB16_CASE(5) WSB16_CASE(6)
+    WSB16_CASE(16) WSB16_CASE(17) WSB16_CASE(18) WSB16_CASE(20) WSB16_CASE(21) WSB16_CASE(22)
+    WSB16_CASE(24) WSB16_CASE(25) WSB16_CASE(26)
+#undef WSB16_CASE
+    default: return hipErrorInvalidValue;
+  }
   // per instantiation: raise the dynamic-LDS limit once, not per launch
-  static size_t smem_set[16] = {};
-  if (smem > 64 * 1024 && smem > smem_set[mode & 15]) {
+  static size_t smem_set[32] = {};
+  if (smem > 64 * 1024 && smem > smem_set[mode & 31]) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
-    smem_set[mode & 15] = smem;
+    smem_set[mode & 31] = smem;
   }
   hipLaunchKernelGGL(kern, grid, dim3(CONV_THREADS), smem, s, a, static_cast<const char*>(a.wsplit), a.wsplit_npad,
                      nrows_a, ntn, ksplit);
@@ -510,9 +603,10 @@ bool conv_wsb_eligible(const ConvArgs& a, bool two_d) {
 
 int conv_wsplit_npad(int N) { return (N + 127) / 128 * 128; }
 
-// chunks of 32 input channels, the last one zero-padded
+// chunks of 32 input channels, the last one zero-padded; the fp16 image carries a 256-B tail (its scales)
 long long conv_wsplit_bytes(const ConvArgs& a) {
-  return (long long)((a.C_in + EK - 1) / EK) * a.taps * conv_wsplit_npad(a.N) * WROW;
+  const long long steps = (long long)((a.C_in + EK - 1) / EK) * a.taps * conv_wsplit_npad(a.N);
+  return a.wsplit_fmt == WSPLIT_H16 ? steps * WROW_H + 256 : steps * WROW;
 }
 
 hipError_t conv_wsplit_build(const ConvArgs& a, void* out, hipStream_t s) {
@@ -520,6 +614,13 @@ hipError_t conv_wsplit_build(const ConvArgs& a, void* out, hipStream_t s) {
   if (nch < 1 || a.taps < 1 || a.N < 1) return hipErrorInvalidValue;
   const long long total = (long long)nch * a.taps * Npad * EK;
   const long long nb = std::min<long long>((total + 255) / 256, 1 << 20);
+  if (a.wsplit_fmt == WSPLIT_H16) {
+    float* tail = reinterpret_cast<float*>(static_cast<char*>(out) + (long long)nch * a.taps * Npad * WROW_H);
+    hipLaunchKernelGGL(k_wmax_scale, dim3(1), dim3(1024), 0, s, a.w, a.ldw, a.w_ts, a.N, a.C_in, a.taps, tail);
+    hipLaunchKernelGGL(k_wsplit_h16, dim3((unsigned)nb), dim3(256), 0, s, a.w, a.ldw, a.w_ts, a.N, a.C_in, a.taps, nch,
+                       Npad, static_cast<unsigned short*>(out), static_cast<const float*>(tail));
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_wsplit, dim3((unsigned)nb), dim3(256), 0, s, a.w, a.ldw, a.w_ts, a.N, a.C_in, a.taps, nch, Npad,
                      static_cast<unsigned short*>(out));
   return hipGetLastError();
@@ -543,16 +644,18 @@ bool conv_wsb_tile(int cfg, int& BM, int& BN) {
 
 hipError_t conv_wsb_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream_t s, bool two_d, int ksplit) {
   if (!a.wsplit || !conv_wsb_eligible(a, two_d)) return hipErrorInvalidValue;
+  // the fp16 image only on the 16x16x32 kernel (1-D)
+  if (a.wsplit_fmt == WSPLIT_H16 && (two_d || cfg < 23)) return hipErrorInvalidValue;
   if (two_d) return cfg == 21 ? launch_wsb<128, 64, 2, 2, true>(a, ntn_enable, ksplit, s) : hipErrorInvalidValue;
   switch (cfg) {
     case 20: return launch_wsb<256, 32, 4, 1, false>(a, ntn_enable, ksplit, s);
     case 21: return launch_wsb<128, 64, 2, 2, false>(a, ntn_enable, ksplit, s);
     case 22: return launch_wsb<128, 128, 2, 2, false>(a, ntn_enable, ksplit, s);
-    case 23: return launch_wsb16<128, 64, 2, 2>(a, ntn_enable, ksplit, s);
-    case 24: return launch_wsb16<256, 32, 4, 1>(a, ntn_enable, ksplit, s);
+    case 23: return launch_wsb16<128, 64, 2, 2, true>(a, ntn_enable, ksplit, s);
+    case 24: return launch_wsb16<256, 32, 4, 1, true>(a, ntn_enable, ksplit, s);
     case 25: return launch_wsb16<128, 128, 2, 2>(a, ntn_enable, ksplit, s);
     case 26: return launch_wsb16<256, 64, 4, 1>(a, ntn_enable, ksplit, s);
-    case 27: return launch_wsb16<128, 64, 1, 4>(a, ntn_enable, ksplit, s);
+    case 27: return launch_wsb16<128, 64, 1, 4, true>(a, ntn_enable, ksplit, s);
     case 28: return launch_wsb16<256, 64, 2, 2>(a, ntn_enable, ksplit, s);
     default: return hipErrorInvalidValue;
   }

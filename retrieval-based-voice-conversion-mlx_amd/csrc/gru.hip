@@ -43,6 +43,10 @@ __device__ __forceinline__ float sigm(float v) { return __frcp_rn(1.f + __expf(-
 __device__ __forceinline__ float tanh_g(float v) { return 1.f - 2.f * __frcp_rn(1.f + __expf(2.f * v)); }
 }  // namespace
 
+// MODE (measurement aid, RVCX_GRU_MODE; bench_gru): 0 the recurrence; 1 the hand-off alone (no W_hh dots: the
+// partner poll, the gates and the publish of every step); 2 the math alone (the dots and gates, no poll: partner
+// values read as published by nobody)
+template <int MODE>
 __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ gi, const float* whh_f,
                                                      const float* bhh_f, const float* whh_b, const float* bhh_b,
                                                      int T, float* out, unsigned long long* xchg,
@@ -122,12 +126,12 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ g
     // ---- phase A: own columns from h_own(s-1) right away, then each wave fetches the 64 partner values of
     // h(s-1) it needs (one granule per lane) and takes its partner columns. (One polling wave + a barrier
     // measured slower: 2.4 vs 1.9 us/step.)
-    float own, par;
-    RVCX_GRU_DOT(wo, h_own + j * HALF, own);
+    float own = 0.f, par = 0.f;
+    if constexpr (MODE != 1) RVCX_GRU_DOT(wo, h_own + j * HALF, own);
     asm volatile("" : "+v"(own));  // finish the own-column dot before polling (else it is sunk past the spin)
     {
       float* hp = h_pw[wave];
-      if (s > 0) {
+      if (MODE != 2 && s > 0) {
         const unsigned epoch = tag0 + (unsigned)s;
         const unsigned long long* slot = theirs + ((s - 1) & 1) * UNITS + j * HALF;
         unsigned long long gv = 0;
@@ -150,7 +154,7 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ g
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      RVCX_GRU_DOT(wp, hp, par);
+      if constexpr (MODE != 1) RVCX_GRU_DOT(wp, hp, par);
     }
     part[j][r] = own + par;
     __syncthreads();
@@ -183,32 +187,34 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ g
 
 hipError_t gru_bidir(const float* gi, const float* whh_f, const float* bhh_f, const float* whh_b,
                      const float* bhh_b, int T, float* out, unsigned long long* xchg, unsigned* status,
-                     hipStream_t s, int B) {
+                     unsigned* next_tag, hipStream_t s, int B) {
   // the two halves of a direction spin on each other: all 4B working workgroups (1 per CU) must be co-resident;
   // the 12B idle ones exit at once
-  if (B < 1 || B > 16) return hipErrorInvalidValue;
-  // granule tags run on across launches (tag0 advances by T + 1 per launch), so whatever a buffer holds from an
-  // earlier launch never matches a tag this launch waits for and no per-launch zeroing is needed; the buffer is
-  // zeroed only when the 32-bit tag space wraps
-  static unsigned next_tag = 1u << 31;
-  const unsigned tag0 = next_tag;
-  if ((unsigned long long)tag0 + (unsigned)T + 1 >= (1ull << 32)) {
-    next_tag = 0;
-    return gru_bidir(gi, whh_f, bhh_f, whh_b, bhh_b, T, out, xchg, status, s, B);
-  }
-  next_tag = tag0 + (unsigned)T + 1;
-  if (tag0 == 0) {
+  if (B < 1 || B > 16 || !next_tag) return hipErrorInvalidValue;
+  // granule tags run on across launches on the same buffer (tag0 advances by T + 1 per launch; *next_tag is the
+  // caller's counter OF THIS BUFFER, starting at 0 for a zeroed one), so whatever the buffer holds from an earlier
+  // launch never matches a tag this launch waits for and no per-launch zeroing is needed. When the 32-bit tag space
+  // would wrap, the buffer is zeroed and the count restarts at 1: no stale tag can equal a new one.
+  unsigned tag0 = *next_tag;
+  if ((unsigned long long)tag0 + (unsigned)T + 1 >= (1ull << 32) || tag0 == 0) {
     hipError_t e = hipMemsetAsync(xchg, 0, sizeof(unsigned long long) * gru_xchg_words(B), s);
     if (e != hipSuccess) return e;
+    tag0 = 1;
   }
+  *next_tag = tag0 + (unsigned)T + 1;
   static const int adj = [] {  // RVCX_GRU_ADJACENT=1: partners in adjacent blocks (different XCDs; A/B aid)
     const char* e = std::getenv("RVCX_GRU_ADJACENT");
     return e ? std::atoi(e) : 0;
   }();
   unsigned spin = SPIN_LIMIT;  // test hook: a tiny RVCX_GRU_SPIN_LIMIT forces the timeout path
   if (const char* e = std::getenv("RVCX_GRU_SPIN_LIMIT")) spin = (unsigned)std::strtoul(e, nullptr, 10);
-  hipLaunchKernelGGL(k_gru_bidir, dim3(16 * B), dim3(NT), 0, s, gi, whh_f, bhh_f, whh_b, bhh_b, T, out, xchg, status,
-                     spin, tag0, adj);
+  static const int mode = [] {
+    const char* e = std::getenv("RVCX_GRU_MODE");
+    return e ? std::atoi(e) : 0;
+  }();
+  auto kern = mode == 1 ? k_gru_bidir<1> : (mode == 2 ? k_gru_bidir<2> : k_gru_bidir<0>);
+  hipLaunchKernelGGL(kern, dim3(16 * B), dim3(NT), 0, s, gi, whh_f, bhh_f, whh_b, bhh_b, T, out, xchg, status, spin,
+                     tag0, adj);
   return hipGetLastError();
 }
 

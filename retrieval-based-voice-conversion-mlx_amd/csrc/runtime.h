@@ -107,7 +107,6 @@ struct Ctx {
   uint64_t call_counter = 0;
   // kernel timing (rvcx_profile): event pairs around every conv-GEMM launch, on its stream
   bool prof = false;
-  int gen_lowp = 0;  // rvcx_set_generator_precision: the generator's weight-streamed convs on bf16 operands
   int conv_math = 0;  // ConvArgs::math of every conv launch (rvcx_set_conv_math): 0 default, 1 fp32 MFMA, 2 split
   struct ProfRec {
     hipEvent_t a, b;
@@ -120,7 +119,7 @@ struct Ctx {
   std::unique_ptr<IvfIndex> ivf;  // speaker-embedding index (optional)
   // pre-split weight images of the weight-streamed conv kernel, per (weight, layout); an entry is dropped when its
   // weight tensor is re-packed (alloc_weight), so finalizing one model keeps the other models' images
-  std::map<std::tuple<const void*, int, long long, int, int, int>, std::unique_ptr<DevBuf>> wsplit_cache;
+  std::map<std::tuple<const void*, int, long long, int, int, int, int>, std::unique_ptr<DevBuf>> wsplit_cache;
   const void* wsplit_for(const ConvArgs& a, hipStream_t s);
   // pre-split images of the fused ResBlock pair kernel (resblock_fused.hip), per weight tensor
   std::map<const void*, std::unique_ptr<DevBuf>> rb_wsplit_cache;
@@ -138,12 +137,16 @@ struct Ctx {
   // buffers whose zero parts survive from call to call (the BiGRU hand-off tags, the NSF source's pad columns): zeroed
   // only when the buffer or its layout changes, not by a fill launch every call
   std::map<std::string, std::pair<const void*, long long>> zero_marks;
-  void zero_once(const std::string& name, void* p, size_t bytes, long long layout, hipStream_t s) {
+  // returns true when it zeroed
+  bool zero_once(const std::string& name, void* p, size_t bytes, long long layout, hipStream_t s) {
     auto& m = zero_marks[name];
-    if (m.first == p && m.second == layout) return;
+    if (m.first == p && m.second == layout) return false;
     RVCX_HIP(hipMemsetAsync(p, 0, bytes, s));
     m = {p, layout};
+    return true;
   }
+  // the BiGRU hand-off tag counter of each zeroed xchg slice (gru_bidir), reset whenever the buffer is re-zeroed
+  std::map<const void*, unsigned> gru_tags;
   unsigned* status_host = nullptr;
   unsigned* status_dev = nullptr;
   unsigned* device_status();
@@ -216,9 +219,11 @@ int64_t rmvpe_forward_b(Ctx& c, const float* audio, int64_t n, int64_t lda, int 
                         int64_t cap, float* hidden, hipStream_t s);
 void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* lengths, const int32_t* pitch,
                    const float* pitchf, const int32_t* sid, const float* eps_z, const float* eps_src, uint64_t seed,
-                   float* out, float* zp_out, float* z_out, hipStream_t s);
+                   float* out, float* zp_out, float* z_out, hipStream_t s, int gen_lowp = 0);
+// gen_lowp: the generator's weight-streamed convs and fused ResBlock pairs on fp16 operands (one MFMA product per
+// step): the realtime hop's opt-in (rvcx_rt_opts::gen_precision), never set by an offline entry point
 void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, const float* f0, const float* g,
-                 const float* eps_src, uint64_t seed, float* out, hipStream_t s);
+                 const float* eps_src, uint64_t seed, float* out, hipStream_t s, int gen_lowp = 0);
 
 void set_highpass(Ctx& c, const double* b, const double* a, const double* zi, int order);
 void set_highpass_sos(Ctx& c, const double* sos, int nsec);

@@ -661,8 +661,9 @@ static void e2e_chunk(Ctx& c, float* img, int Fc, float* sal, hipStream_t s, int
   run1(c, lin(feat, 3 * NMEL, B * Fc, 3 * NMEL, c.W("rm.gru.wih"), 6 * GRU_H, c.W("rm.gru.bih"), gi, 6 * GRU_H), s);
   float* go = c.buf<float>("rm.gruout", (size_t)B * Fc * 2 * GRU_H, s);
   unsigned long long* xchg = c.buf<unsigned long long>("rm.xchg", gru_xchg_words(B), s);
-  // a new (or regrown) allocation holds garbage tags: zeroed once (gru_bidir never zeroes it)
-  c.zero_once("rm.xchg", xchg, sizeof(unsigned long long) * gru_xchg_words(B), (long long)B, s);
+  // a new (or regrown) allocation holds garbage tags: zeroed once, and the tag counters of its slices restart
+  if (c.zero_once("rm.xchg", xchg, sizeof(unsigned long long) * gru_xchg_words(B), (long long)B, s))
+    c.gru_tags.clear();
   unsigned* status = c.device_status();  // sticky until the host reads it (Ctx::check_device_status)
   // work the caller wants issued beside the BiGRU (which occupies 4 CUs): the gate event marks this point of the
   // stream, the BiGRU goes out first and the hook's (many) launches after it, so the host time spent issuing
@@ -672,8 +673,8 @@ static void e2e_chunk(Ctx& c, float* img, int Fc, float* sal, hipStream_t s, int
   if (hook && c.ev_gate) RVCX_HIP(hipEventRecord(c.ev_gate, s));
   for (int g0 = 0; g0 < B; g0 += 16)  // at most 16 sequences per launch (16 x 4 working workgroups co-resident)
     check(gru_bidir(gi + (size_t)g0 * Fc * 6 * GRU_H, c.W("rm.gru.whh_f"), c.W("rm.gru.bhh_f"), c.W("rm.gru.whh_b"),
-                    c.W("rm.gru.bhh_b"), Fc, go + (size_t)g0 * Fc * 2 * GRU_H, xchg + gru_xchg_words(g0), status, s,
-                    std::min(16, B - g0)),
+                    c.W("rm.gru.bhh_b"), Fc, go + (size_t)g0 * Fc * 2 * GRU_H, xchg + gru_xchg_words(g0), status,
+                    &c.gru_tags[xchg + gru_xchg_words(g0)], s, std::min(16, B - g0)),
           "gru");
   if (hook) hook(s);
   ConvArgs f = lin(go, 2 * GRU_H, B * Fc, 2 * GRU_H, c.W("rm.fc.w"), NCLS, c.W("rm.fc.b"), sal, NCLS);
@@ -733,11 +734,21 @@ int64_t rmvpe_forward_b(Ctx& c, const float* audio, int64_t n, int64_t lda, int 
       e2e_chunk(c, img + (size_t)b0 * Fp * NMEL, Fp, sal + (size_t)b0 * Fp * NCLS, s, nb);
     }
   } else {
-    for (int b = 0; b < B; ++b)
-      for (int st = 0; st < Fp; st += chunk) {
-        const int Fc = std::min(chunk, Fp - st);
-        e2e_chunk(c, img + ((size_t)b * Fp + st) * NMEL, Fc, sal + ((size_t)b * Fp + st) * NCLS, s);
+    // every chunk is an independent E2E pass (RMVPE.py:459-481: the U-Net pads each chunk's edges, the BiGRU
+    // restarts); a sequence's full 32000-frame chunks lie back to back, so they go through as one batch (as the
+    // short branch batches sequences), the shorter tail chunk as a second pass
+    const int nfull = Fp / chunk, tail = Fp - nfull * chunk;
+    for (int b = 0; b < B; ++b) {
+      for (int k0 = 0; k0 < nfull; k0 += 8) {  // <= 8 chunks per pass: ~13 GB of U-Net activations
+        const int nb = std::min(8, nfull - k0);
+        const size_t r0 = (size_t)b * Fp + (size_t)k0 * chunk;
+        e2e_chunk(c, img + r0 * NMEL, chunk, sal + r0 * NCLS, s, nb);
       }
+      if (tail > 0) {
+        const size_t r0 = (size_t)b * Fp + (size_t)nfull * chunk;
+        e2e_chunk(c, img + r0 * NMEL, tail, sal + r0 * NCLS, s);
+      }
+    }
   }
   if (hidden)
     for (int b = 0; b < B; ++b)

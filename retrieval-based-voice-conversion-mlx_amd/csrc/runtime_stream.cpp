@@ -203,6 +203,8 @@ void rt_process(Ctx& c, RtState& s, const float* in48, const int32_t* sids, cons
   for (int b = 0; b < B; ++b)
     if (sids[b] < 0 || sids[b] >= c.scfg.n_spk) throw Error(RVCX_E_INVALID, "stream: sid out of range");
   if (o.index_rate > 0 && !c.ivf) throw Error(RVCX_E_STATE, "stream: index_rate > 0 but no feature index loaded");
+  if (o.gen_precision < 0 || o.gen_precision > 1)
+    throw Error(RVCX_E_INVALID, "stream: gen_precision must be 0 (fp32) or 1 (fp16 generator)");
   if (o.index_rate > 0 && c.ivf->view.d != E) throw Error(RVCX_E_SHAPE, "stream: index dimension mismatch");
   const int nxt = 1 - s.cur;
   // 1. input resample 48k -> 16k, circular buffers, RMS gate (core.py:227-267)
@@ -283,7 +285,7 @@ void rt_process(Ctx& c, RtState& s, const float* in48, const int32_t* sids, cons
   const int64_t n_model = (int64_t)T * upp;
   float* model = c.buf<float>("rt.model", (size_t)B * n_model, st);
   synth_forward(c, B, T, phone, dmeta, guided ? pitch : nullptr, guided ? pitchf : nullptr, dmeta + B, eps_z, eps_src,
-                seed, model, nullptr, nullptr, st);
+                seed, model, nullptr, nullptr, st, o.gen_precision);
   (void)I;
   check(rt_clip(model, n_model, (int)n_model, B, st), "rt_clip");
   if (o.volume_envelope != 1.0) {  // pipeline.py:299-307 (source = the 16 kHz convert buffer)

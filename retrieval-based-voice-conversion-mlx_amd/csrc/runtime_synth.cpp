@@ -321,7 +321,7 @@ void finalize_synth(Ctx& c) {
 // ------------------------------------------------------------------ generator
 // HiFiGANNSFGenerator.forward (generators/hifigan_nsf.py:173-212); z_btc [B][T][I] time-major.
 void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, const float* f0, const float* g,
-                 const float* eps_src, uint64_t seed, float* out, hipStream_t s) {
+                 const float* eps_src, uint64_t seed, float* out, hipStream_t s, int gen_lowp) {
   const SynthCfg& cf = c.scfg;
   if (cf.f0 && cf.vocoder == 2) {
     refinegan_forward(c, B, T, z_btc, mask, f0, g, eps_src, seed, out, s);
@@ -388,7 +388,7 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
     // LeakyReLU(0.1) -> ConvTranspose1d (polyphase) ; output [B][curT][u*C] == [B][Ti][C]
     ConvArgs a = conv(cur, Cin, curT, Cin, L.w, u * C, L.taps, 1, L.pad, L.b, y, u * C, curT, B);
     a.w_static = 1;
-    a.lowp = c.gen_lowp;
+    a.lowp = gen_lowp;
     a.pre_act = ACT_LRELU;
     a.pre_slope = 0.1f;
     run(c, a, s, 2.0 * B * curT * (double)Cin * C * L.k);
@@ -456,7 +456,7 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
           p.B = B;
           p.y = dst;
           p.y_bs = (long long)Ti * C;
-          p.lowp = c.gen_lowp;
+          p.lowp = gen_lowp;
           if (last) {
             p.acc_mode = (j == 0) ? ACC_STORE : ((j + 1 == nk) ? ACC_ADD_DIV : ACC_ADD);
             p.acc_div = (float)nk;
@@ -472,7 +472,7 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
         const std::string n2 = rb + ".convs2." + std::to_string(m);
         ConvArgs a1 = conv(r_in, C, Ti, C, c.W(n1 + ".w"), C, k, d, (k * d - d) / 2, c.W(n1 + ".b"), T1, C, Ti, B);
         a1.w_static = 1;
-        a1.lowp = c.gen_lowp;
+        a1.lowp = gen_lowp;
         a1.pre_act = ACT_LRELU;
         a1.pre_slope = 0.1f;
         a1.act = ACT_LRELU;
@@ -482,7 +482,7 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
         float* dst = last ? S : RR;
         ConvArgs a2 = conv(T1, C, Ti, C, c.W(n2 + ".w"), C, k, 1, (k - 1) / 2, c.W(n2 + ".b"), dst, C, Ti, B);
         a2.w_static = 1;
-        a2.lowp = c.gen_lowp;
+        a2.lowp = gen_lowp;
         a2.res = r_in;
         a2.ldr = C;
         a2.res_bs = (long long)Ti * C;
@@ -507,7 +507,7 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
 // ------------------------------------------------------------------ Synthesizer.infer
 void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* lengths, const int32_t* pitch,
                    const float* pitchf, const int32_t* sid, const float* eps_z, const float* eps_src, uint64_t seed,
-                   float* out, float* zp_out, float* z_out, hipStream_t s) {
+                   float* out, float* zp_out, float* z_out, hipStream_t s, int gen_lowp) {
   const SynthCfg& cf = c.scfg;
   const int H = cf.H, I = cf.I, F = cf.F, E = cf.emb_dim, nh = cf.n_heads, dk = H / nh, nw = 2 * cf.window + 1;
   const long long BT = (long long)B * T;
@@ -692,7 +692,7 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
   }
   if (z_out) RVCX_HIP(hipMemcpyAsync(z_out, z, BT * I * sizeof(float), hipMemcpyDeviceToDevice, s));
   // ---- dec(z * mask, nsff0, g)
-  dec_forward(c, B, T, z, mask, pitchf, g, eps_src, seed, out, s);
+  dec_forward(c, B, T, z, mask, pitchf, g, eps_src, seed, out, s, gen_lowp);
 }
 
 }  // namespace rvcx

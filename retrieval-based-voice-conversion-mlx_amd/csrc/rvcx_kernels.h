@@ -38,6 +38,8 @@ enum OutMap : int {
 };
 
 // Implicit-GEMM convolution:  y[b][m][n] = epi( sum_tap sum_c pre(X[b][row(m,tap)][c]) * W[tap][n][c] )
+enum WsplitFmt : int { WSPLIT_BF16 = 0, WSPLIT_H16 = 1 };
+
 struct ConvArgs {
   // A operand (activations)
   const float* x = nullptr;
@@ -98,16 +100,20 @@ struct ConvArgs {
   const void* wsplit = nullptr;  // ((chunk * taps + tap) * wsplit_npad + n) rows of [hi|mid|lo] x 32 bf16
   int wsplit_npad = 0;
   int wsb = 0;  // set by the runtime (conv_wsb_route on a static weight): 1 weight-streamed kernel, 2 gather-streamed
+  int wsplit_fmt = 0;  // WSPLIT_BF16: three bf16 planes (every streamed kernel); WSPLIT_H16: two fp16 planes + scale tail
+                       // (conv_wsb16_kernel only: the two-plane fp16 arithmetic and the reduced-precision mode)
   int ksplit = 1;
   int no_splitk = 0;
-  // opt-in reduced precision (the generator's weight-streamed convs only, Ctx::gen_lowp): bf16 operands, one MFMA
-  // product instead of the exact split's six. Never set on the parity path.
+  // opt-in reduced precision (the generator's weight-streamed convs of a realtime hop, rvcx_rt_opts::gen_precision):
+  // fp16 operands (the WSPLIT_H16 image's hi plane), one MFMA product per step. Never set on the parity path.
   int lowp = 0;
   long long ws_rows = 0;
   float* ws = nullptr;
 };
 
 hipError_t conv1d(const ConvArgs& a, hipStream_t s);
+// the contraction arithmetic a launch gets: ConvArgs::math, else RVCX_CONV_MATH (1 fp32 MFMA, 2 bf16 split, 3 fp16 split)
+int conv_math_of(const ConvArgs& a);
 hipError_t conv2d(const ConvArgs& a, hipStream_t s);
 // 3x3/pad-1 2-D convs with C_in, N in {16, 32} on 16x16x4 MFMA fragments (conv2d_small.hip); conv2d routes
 // the shapes conv2d_small_fits accepts there (RVCX_NO_SMALL2D=1 disables)
@@ -172,7 +178,7 @@ struct RbPairArgs {
   int acc_mode = ACC_STORE;
   float acc_div = 1.f;
   int flags = 0;  // bit 0: next-tile x prefetch into registers (measurement aid, RVCX_RB_FLAGS)
-  int lowp = 0;   // opt-in reduced precision (Ctx::gen_lowp): bf16 operands, one MFMA product per step
+  int lowp = 0;   // opt-in reduced precision (rvcx_rt_opts::gen_precision): fp16 operands, one MFMA product per step
 };
 bool rb_pair_fits(int C, int k, int d);
 long long rb_wsplit_bytes(int C, int k);
@@ -231,10 +237,11 @@ hipError_t stft_magnitude(const float* spec, int F, int nbins, float* mag, int l
 hipError_t affine_inplace(float* x, long long n, float a, float b, hipStream_t s);
 hipError_t avgpool2(const float* x, int H, int W, int C, int ldx, float* y, hipStream_t s);
 hipError_t nhwc_to_hcw(const float* x, int H, int W, int C, float* y, hipStream_t s);
-// B independent sequences (gi [B][T][1536], out [B][T][512], xchg gru_xchg_words(B) words)
+// B independent sequences (gi [B][T][1536], out [B][T][512], xchg gru_xchg_words(B) words); next_tag: the
+// hand-off tag counter of this xchg buffer, owned by the caller (0 = buffer state unknown: zeroed first)
 hipError_t gru_bidir(const float* gi, const float* whh_f, const float* bhh_f, const float* whh_b,
                      const float* bhh_b, int T, float* out, unsigned long long* xchg, unsigned* status,
-                     hipStream_t s, int B = 1);
+                     unsigned* next_tag, hipStream_t s, int B = 1);
 inline size_t gru_xchg_words(int B) { return (size_t)B * 4 * 2 * 128; }
 // B sequences: sal rows of sequence b start at b*Fs (Fs = F when 0), f0 [B][F]
 hipError_t rmvpe_decode(const float* sal, int F, int ncls, float thred, double* f0, hipStream_t s, int B = 1,

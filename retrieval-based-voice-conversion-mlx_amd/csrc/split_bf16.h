@@ -53,6 +53,37 @@ __device__ __forceinline__ void put_split1(char* row, int c, float v) {
   *reinterpret_cast<unsigned short*>(row + 2 * PLANE + c * 2) = (unsigned short)l;
 }
 
+// ---- fp32 operands as two fp16 planes (x = h + 2^-11 l): h = f16(x), l = f16((x - h) * 2^11). Each plane carries 11
+// significand bits, so x is held to 2^-22 |x| (the residual scaled by 2^11 stays a normal fp16 wherever h is one); the
+// MFMA sums h*h' in one accumulator and h*l' + l*h' in a second, combined as acc + 2^-11 acc2 (the dropped l*l' term is
+// below 2^-22 |x y|). Three MFMA products per step instead of the bf16 split's six.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+constexpr int ERS_H = 2 * PLANE + 16;  // LDS row stride of the two-plane image: 36 dwords, 16 rows -> 16 bank groups
+constexpr float H16_LO = 2048.f, H16_LO_INV = 1.f / 2048.f;
+
+__device__ __forceinline__ unsigned pk_f16(float x, float y) {
+  const f16x2 h = __builtin_convertvector((f32x2){x, y}, f16x2);  // RNE
+  return __builtin_bit_cast(unsigned, h);
+}
+__device__ __forceinline__ float f16lo_f(unsigned p) { return (float)__builtin_bit_cast(f16x2, p)[0]; }
+__device__ __forceinline__ float f16hi_f(unsigned p) { return (float)__builtin_bit_cast(f16x2, p)[1]; }
+
+// 4 consecutive channels of one LDS row as the two fp16 planes (NPL = 1: the hi plane alone, the reduced-precision mode)
+template <int NPL>
+__device__ __forceinline__ void put_h16x4(char* row, int c4, f32x4 v) {
+  uint2 h;
+  h.x = pk_f16(v[0], v[1]);
+  h.y = pk_f16(v[2], v[3]);
+  *reinterpret_cast<uint2*>(row + c4 * 2) = h;
+  if constexpr (NPL > 1) {
+    uint2 l;
+    l.x = pk_f16((v[0] - f16lo_f(h.x)) * H16_LO, (v[1] - f16hi_f(h.x)) * H16_LO);
+    l.y = pk_f16((v[2] - f16lo_f(h.y)) * H16_LO, (v[3] - f16hi_f(h.y)) * H16_LO);
+    *reinterpret_cast<uint2*>(row + PLANE + c4 * 2) = l;
+  }
+}
+
 // row order of a store: the 8 rows written by one 64-lane store instruction (8 lanes per 32-channel row) go as
 // 0,4,1,5,2,6,3,7 so each 16-lane group writes two rows 4 apart: 4 x 52 dwords = 16 mod 32 banks, disjoint halves
 __device__ __forceinline__ int store_row(int w) { return (w & ~7) | (((w & 7) >> 1) + 4 * (w & 1)); }

@@ -468,17 +468,11 @@ class Engine:
 
     # ------------------------------------------------------------------ kernel timing
     def set_conv_math(self, mode: str):
-        """Contraction arithmetic of this context: "split" (default; fp32 via three bf16 planes on bf16 MFMA) or
-        "f32" (fp32-input MFMA). Both reproduce torch's fp32 conv to fp32 rounding (rvcx_set_conv_math)."""
-        m = {"default": 0, "f32": 1, "split": 2}[mode]
+        """Contraction arithmetic of this context: "split" (default; fp32 via three bf16 planes on bf16 MFMA),
+        "f32" (fp32-input MFMA) or "h16" (as split, with the generator's weight-streamed convs on two fp16 planes)
+        (rvcx_set_conv_math)."""
+        m = {"default": 0, "f32": 1, "split": 2, "h16": 3}[mode]
         self._check(self.lib.rvcx_set_conv_math(self.ctx, m), "set_conv_math")
-
-    def set_generator_precision(self, precision: str):
-        """"fp32" (default: fp32-accurate everywhere) or "bf16": the generator's weight-streamed convs take bf16
-        operands with fp32 accumulation (rvcx_set_generator_precision). An opt-in for streaming (BASELINE C5's fp16);
-        the f0 / feature front end, TextEncoder and flow stay fp32-accurate."""
-        m = {"fp32": 0, "bf16": 1}[precision]
-        self._check(self.lib.rvcx_set_generator_precision(self.ctx, m), "set_generator_precision")
 
     def conv1d(self, x, w, bias=None, dilation: int = 1, padding: int = 0, stride: int = 1, math: str = "default"):
         """torch.nn.functional.conv1d(x.T[None], w, bias, stride, padding, dilation)[0].T on the device kernel:

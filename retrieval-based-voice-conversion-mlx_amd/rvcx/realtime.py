@@ -74,7 +74,10 @@ class StreamGroup:
                            "rt_reset")
 
     def opts(self, f0_up_key=0, index_rate=0.5, protect=0.5, volume_envelope=1.0, f0_autotune=False,
-             f0_autotune_strength=1.0, proposed_pitch=False, proposed_pitch_threshold=155.0) -> _lib.RtOpts:
+             f0_autotune_strength=1.0, proposed_pitch=False, proposed_pitch_threshold=155.0,
+             gen_precision: str = "fp32") -> _lib.RtOpts:
+        """Per-hop options (rvcx_rt_opts). gen_precision "fp16" runs this hop's generator on fp16 operands (BASELINE
+        C5's half precision); the f0 / feature front end, TextEncoder and flow stay fp32-accurate either way."""
         o = _lib.RtOpts()
         self.engine.lib.rvcx_rt_default_opts(ctypes.byref(o))
         # rvc/realtime only retrieves when an index is loaded (pipeline.py:264); index_rate alone does not
@@ -83,6 +86,7 @@ class StreamGroup:
         o.volume_envelope, o.f0_autotune = float(volume_envelope), int(bool(f0_autotune))
         o.f0_autotune_strength, o.proposed_pitch = float(f0_autotune_strength), int(bool(proposed_pitch))
         o.proposed_pitch_threshold = float(proposed_pitch_threshold)
+        o.gen_precision = {"fp32": 0, "fp16": 1}[gen_precision]
         return o
 
     def process(self, audio_in, opts: Optional[_lib.RtOpts] = None, eps_z=None, eps_src=None, seed: int = 0):
