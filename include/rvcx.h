@@ -239,6 +239,10 @@ int rvcx_profile(rvcx_ctx* ctx, int enable);
  * (Replaces nothing in the reference, whose computations cannot fail this way; it never prints and continues.) */
 int rvcx_device_status(rvcx_ctx* ctx, void* stream);
 int rvcx_profile_read(rvcx_ctx* ctx, double* total_ms, double* total_flops, int64_t* launches);
+/* As rvcx_profile_read, plus the launches' time at their arithmetic's MFMA ceiling (ms): sum of flops / ceiling,
+ * with the ceiling 2500 / 6 TF for the exact bf16 split, 2500 / 3 for the two-plane fp16 split and 2500 for the fp16
+ * reduced-precision mode (the dense bf16 / fp16 MFMA peak over the MFMA products per fp32 product). */
+int rvcx_profile_read_ex(rvcx_ctx* ctx, double* total_ms, double* total_flops, int64_t* launches, double* ceiling_ms);
 
 /* ---------------------------------------------------------------- feature index (FAISS IndexIVFFlat)
  * The bytes of a faiss .index file (IndexIVFFlat over IndexFlatL2, METRIC_L2, ArrayInvertedLists;
@@ -319,12 +323,13 @@ int rvcx_rt_process(rvcx_ctx* ctx, rvcx_rt* rt, const float* d_in, const int32_t
                     int32_t* d_offs, void* stream);
 
 /* Contraction arithmetic of every convolution / linear / attention matmul of this context (replaces nothing in
- * the reference; torch's fp32 CPU conv is what both modes reproduce): 0 = default (2), 1 = fp32-input MFMA
+ * the reference; torch's fp32 CPU conv is what every mode reproduces): 0 = default (3), 1 = fp32-input MFMA
  * (v_mfma_f32_32x32x2_f32, an exact fp32 fma chain at 157 TF), 2 = fp32 through an exact 3-way bf16 split of both
  * operands with the six significant plane products on bf16 MFMA (error below fp32's own rounding, 2.67x the
- * MFMA rate), 3 = as 2, except that the generator-sized weight-streamed convs split both operands into two fp16
- * planes (22 significand bits each) with three plane products (csrc/split_bf16.h). Env RVCX_CONV_MATH=f32 | h16
- * sets the process default to 1 | 3. */
+ * MFMA rate), 3 = as 2, except that the generator's weight-streamed convs and fused ResBlock pairs split both
+ * operands into two fp16 planes (x = h + 2^-11 l, 11 significand bits each) with three plane products into two
+ * fp32 accumulators (csrc/split_bf16.h; error against fp64 measured at or below the fp32-input MFMA's, 5.3x the
+ * fp32 MFMA rate). Env RVCX_CONV_MATH=f32 | split | h16 sets the process default. */
 int rvcx_set_conv_math(rvcx_ctx* ctx, int mode);
 
 /* One Conv1d forward, time-major: d_x [T][C_in], d_w [taps][N][C_in] (torch weight [N][C_in][taps] permuted),
@@ -333,7 +338,9 @@ int rvcx_set_conv_math(rvcx_ctx* ctx, int mode);
  * torch.nn.Conv1d.forward as used throughout rvc/lib/algorithm (e.g. residuals.py:34-80). math as above, plus
  * 3 = the split arithmetic on the weight-streamed kernel (weights pre-split in HBM; 1-D stride-1 convs with
  * C_in % 32 == 0 and (taps - 1) * dilation <= 64, else RVCX_E_SHAPE), 4 = the split arithmetic on the gather-streamed
- * kernel (weights pre-split in HBM, A gathered per step, split-K by the size policy; C_in % 32 == 0). */
+ * kernel (weights pre-split in HBM, A gathered per step, split-K by the size policy; C_in % 32 == 0), 5 = the
+ * two-plane fp16 split on the weight-streamed kernel (rvcx_set_conv_math mode 3's generator arithmetic), 6 = its fp16
+ * hi planes alone (the realtime reduced-precision mode); 5 and 6 take the shapes 3 does. */
 int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const float* d_w, const float* d_bias, int N,
                 int taps, int dilation, int pad, int stride, int math, float* d_y, int64_t T_out, void* stream);
 
@@ -343,8 +350,9 @@ int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const floa
  *     acc_mode 0: y = out; 1: y = y + out; 2: y = (y + out) / acc_div
  * Replaces one iteration of ResBlock.forward (rvc/lib/algorithm/residuals.py:71-80) and MRFLayer.forward
  * (generators/hifigan_mrf.py:45-50), plus the ResBlock mean of HiFiGANNSFGenerator.forward (hifigan_nsf.py:190-207)
- * on the last pair. C in {32, 64}, odd k, (k - 1) / 2 * dilation <= 30, else RVCX_E_SHAPE. cfg 0 = default
- * tile (RVCX_RB_CFG in the pipeline). Exposed for numerics tests and A/B timing. */
+ * on the last pair. C in {32, 64}, odd k, (k - 1) / 2 * dilation <= 30, else RVCX_E_SHAPE. cfg bits 0-3: the tile
+ * (0 = default, RVCX_RB_CFG in the pipeline); bits 4-5 the arithmetic: 0 the exact 3-plane bf16 split, 1 the two-plane
+ * fp16 split, 2 fp16 hi planes alone (the realtime reduced-precision mode). Exposed for numerics tests and A/B timing. */
 int rvcx_resblock_pair(rvcx_ctx* ctx, const float* d_x, int B, int64_t T, int C, const float* d_w1, const float* d_b1,
                        const float* d_w2, const float* d_b2, int k, int dilation, int acc_mode, float acc_div, int cfg,
                        float* d_y, void* stream);

@@ -136,17 +136,17 @@ const void* Ctx::wsplit_for(const ConvArgs& a, hipStream_t s) {
   return slot->p;
 }
 
-const void* Ctx::rb_wsplit_for(const float* w, int C, int k, hipStream_t s) {
-  auto& slot = rb_wsplit_cache[static_cast<const void*>(w)];
+const void* Ctx::rb_wsplit_for(const float* w, int C, int k, int wfmt, hipStream_t s) {
+  auto& slot = rb_wsplit_cache[{static_cast<const void*>(w), wfmt}];
   if (!slot) {
     std::unique_ptr<DevBuf> b(new DevBuf());
-    const size_t bytes = (size_t)rb_wsplit_bytes(C, k);
+    const size_t bytes = (size_t)rb_wsplit_bytes(C, k, wfmt);
     if (hipMalloc(&b->p, bytes) != hipSuccess) {
       (void)hipGetLastError();
       throw Error(RVCX_E_OOM, "split-weight allocation failed");
     }
     b->bytes = bytes;
-    check(rb_wsplit_build(w, C, k, b->p, s), "rb_wsplit_build");
+    check(rb_wsplit_build(w, C, k, b->p, s, wfmt), "rb_wsplit_build");
     RVCX_HIP(hipStreamSynchronize(s));
     slot = std::move(b);
   }
@@ -181,7 +181,8 @@ void launch_rb_pair(Ctx& c, const RbPairArgs& a_in, hipStream_t s) {
   const double flops = 2.0 * 2.0 * a.B * (double)a.T * a.C * a.C * a.k;
   // x read, y written (+ read when accumulating), both weight tensors
   const double bytes = 4.0 * ((double)a.B * a.T * a.C * (2 + (a.acc_mode != ACC_STORE ? 1 : 0)) + 2.0 * a.k * a.C * a.C);
-  Ctx::ProfRec r{ev[0], ev[1], flops, 0, a.T, a.C, a.C, -a.k, a.B, 1, bytes};
+  Ctx::ProfRec r{ev[0], ev[1], flops, 0, a.T, a.C, a.C, -a.k, a.B, 1, bytes,
+                 a.wfmt == RB_WF16 ? (a.lowp ? Ctx::PEAK_F16 : Ctx::PEAK_F16X2) : Ctx::PEAK_SPLIT};
   RVCX_HIP(hipEventRecord(r.a, s));
   check(rb_pair(a, cfg, s), "rb_pair");
   RVCX_HIP(hipEventRecord(r.b, s));
@@ -200,7 +201,8 @@ void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double
   const long long need = conv_plan_splitk(a, two_d);
   if (a.wsb) {
     // the weight-streamed kernel's fp16 image: the two-plane fp16 arithmetic (math 3) or the reduced-precision mode
-    if (!a.wsplit) a.wsplit_fmt = (a.wsb == 1 && (a.lowp || conv_math_of(a) == 3)) ? WSPLIT_H16 : WSPLIT_BF16;
+    if (!a.wsplit)
+      a.wsplit_fmt = ((a.wsb == 1 && a.lowp) || conv_math_of(a) == 3) ? WSPLIT_H16 : WSPLIT_BF16;
     if (!a.wsplit) a.wsplit = c.wsplit_for(a, s);  // a caller-built image (rvcx_conv1d) is used as given
     a.wsplit_npad = conv_wsplit_npad(a.N);
   }
@@ -230,8 +232,12 @@ void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double
   const double alg_bytes = 4.0 * (in_rows * a.C_in * a.batch * a.batch_inner + (double)a.taps * a.N * a.C_in +
                                   out_el * (1 + (a.res && a.res_mode != RES_NONE ? 1 : 0) +
                                             (a.acc_mode != ACC_STORE ? 1 : 0)));
+  // the launch's arithmetic ceiling (the rest of the family is priced at the bf16 split's, a lower bound for the few
+  // launches on the fp32-input MFMA)
+  const double peak = (a.wsb && a.wsplit_fmt == WSPLIT_H16) ? ((a.lowp && a.wsb == 1) ? Ctx::PEAK_F16 : Ctx::PEAK_F16X2)
+                                                            : Ctx::PEAK_SPLIT;
   Ctx::ProfRec r{get_ev(), get_ev(), flops, two_d ? 1 : 0, two_d ? a.T_out * a.W_out : a.T_out, a.N, a.C_in,
-                 a.taps, a.batch * a.batch_inner, a.ksplit, alg_bytes};
+                 a.taps, a.batch * a.batch_inner, a.ksplit, alg_bytes, peak};
   RVCX_HIP(hipEventRecord(r.a, s));
   check(two_d ? conv2d(a, s) : conv1d(a, s), two_d ? "conv2d" : "conv1d");
   RVCX_HIP(hipEventRecord(r.b, s));
@@ -593,7 +599,7 @@ int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const floa
     set_device(ctx);
     ctx->check_device_status();
     if (!d_x || !d_w || !d_y || T <= 0 || C_in <= 0 || N <= 0 || taps <= 0 || dilation <= 0 || stride <= 0 ||
-        pad < 0 || T_out <= 0 || math < 0 || math > 4)
+        pad < 0 || T_out <= 0 || math < 0 || math > 6)
       throw Error(RVCX_E_INVALID, "rvcx_conv1d: bad argument");
     if ((T_out - 1) * stride + (int64_t)(taps - 1) * dilation + 1 > T + 2 * (int64_t)pad)
       throw Error(RVCX_E_SHAPE, "rvcx_conv1d: T_out exceeds the padded input");
@@ -604,8 +610,12 @@ int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const floa
     a.w = d_w; a.ldw = C_in; a.w_ts = (long long)N * C_in; a.taps = taps; a.dil = dilation; a.pad = pad;
     a.stride = stride;
     a.y = d_y; a.ldy = N; a.T_out = (int)T_out; a.N = N; a.bias = d_bias;
-    a.math = math >= 3 ? 2 : math;
-    if (math == 3) {  // the weight-streamed split kernel (conv_wsb.hip) whatever the size policy would pick
+    a.math = math >= 5 ? 3 : (math >= 3 ? 2 : math);
+    if (math == 5 || math == 6) {  // the two-plane fp16 arithmetic / its hi plane alone on the weight-streamed kernel
+      a.wsplit_fmt = WSPLIT_H16;
+      a.lowp = math == 6;
+    }
+    if (math == 3 || math >= 5) {  // the weight-streamed split kernel (conv_wsb.hip) whatever the size policy would pick
       if (!conv_wsb_eligible(a)) throw Error(RVCX_E_SHAPE, "rvcx_conv1d: shape not eligible for the weight-streamed kernel");
       a.w_static = 1;
       a.force_cfg = conv_wsb_pick(a);  // the tile the pipeline's policy picks for this shape
@@ -640,12 +650,18 @@ int rvcx_resblock_pair(rvcx_ctx* ctx, const float* d_x, int B, int64_t T, int C,
     if (!rb_pair_fits(C, k, dilation) || T > INT32_MAX / C)
       throw Error(RVCX_E_SHAPE, "rvcx_resblock_pair: shape not supported by the fused kernel");
     hipStream_t s = static_cast<hipStream_t>(stream);
+    const int fmt = (cfg >> 4) & 3;
+    if (fmt > 2) throw Error(RVCX_E_INVALID, "rvcx_resblock_pair: arithmetic (cfg bits 4-5) must be 0, 1 or 2");
+    cfg &= 15;
+    const int wfmt = fmt ? RB_WF16 : RB_WBF16;
     // fresh split images every call (test entry: the weight pointers may be reused by the caller)
-    void* w1s = ctx->buf<char>("rb.test.w1s", (size_t)rb_wsplit_bytes(C, k), s);
-    void* w2s = ctx->buf<char>("rb.test.w2s", (size_t)rb_wsplit_bytes(C, k), s);
-    check(rb_wsplit_build(d_w1, C, k, w1s, s), "rb_wsplit_build");
-    check(rb_wsplit_build(d_w2, C, k, w2s, s), "rb_wsplit_build");
+    void* w1s = ctx->buf<char>("rb.test.w1s", (size_t)rb_wsplit_bytes(C, k, wfmt), s);
+    void* w2s = ctx->buf<char>("rb.test.w2s", (size_t)rb_wsplit_bytes(C, k, wfmt), s);
+    check(rb_wsplit_build(d_w1, C, k, w1s, s, wfmt), "rb_wsplit_build");
+    check(rb_wsplit_build(d_w2, C, k, w2s, s, wfmt), "rb_wsplit_build");
     RbPairArgs a;
+    a.wfmt = wfmt;
+    a.lowp = fmt == 2;
     a.x = d_x;
     a.x_bs = T * C;
     a.w1s = w1s;
@@ -670,9 +686,13 @@ int rvcx_profile(rvcx_ctx* ctx, int enable) {
 }
 
 int rvcx_profile_read(rvcx_ctx* ctx, double* total_ms, double* total_flops, int64_t* launches) {
+  return rvcx_profile_read_ex(ctx, total_ms, total_flops, launches, nullptr);
+}
+
+int rvcx_profile_read_ex(rvcx_ctx* ctx, double* total_ms, double* total_flops, int64_t* launches, double* ceiling_ms) {
   return guard(ctx, [&] {
     set_device(ctx);
-    double ms = 0.0, fl = 0.0;
+    double ms = 0.0, fl = 0.0, cms = 0.0;
     const char* dump = std::getenv("RVCX_PROF_DUMP");  // append one CSV line per conv launch
     FILE* fd = dump ? std::fopen(dump, "a") : nullptr;
     for (auto& r : ctx->prof_recs) {
@@ -680,10 +700,11 @@ int rvcx_profile_read(rvcx_ctx* ctx, double* total_ms, double* total_flops, int6
       float t = 0.f;
       RVCX_HIP(hipEventElapsedTime(&t, r.a, r.b));
       if (fd)
-        std::fprintf(fd, "%d,%d,%d,%d,%d,%d,%d,%.6f,%.0f,%.0f\n", r.two_d, r.M, r.N, r.C_in, r.taps, r.batch, r.ksplit, t,
-                     r.flops, r.bytes);
+        std::fprintf(fd, "%d,%d,%d,%d,%d,%d,%d,%.6f,%.0f,%.0f,%.1f\n", r.two_d, r.M, r.N, r.C_in, r.taps, r.batch, r.ksplit,
+                     t, r.flops, r.bytes, r.peak_tf);
       ms += t;
       fl += r.flops;
+      cms += r.flops / (r.peak_tf * 1e9);
       ctx->prof_pool.push_back(r.a);
       ctx->prof_pool.push_back(r.b);
     }
@@ -691,6 +712,7 @@ int rvcx_profile_read(rvcx_ctx* ctx, double* total_ms, double* total_flops, int6
     if (total_ms) *total_ms = ms;
     if (total_flops) *total_flops = fl;
     if (launches) *launches = (int64_t)ctx->prof_recs.size();
+    if (ceiling_ms) *ceiling_ms = cms;
     ctx->prof_recs.clear();
   });
 }

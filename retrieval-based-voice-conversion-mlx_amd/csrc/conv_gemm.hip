@@ -541,7 +541,40 @@ bool xcd_enabled() {
   return v;
 }
 
+// the split-K combine of a gated WaveNet in_layer (ConvArgs::gate_h): the pair (c, c + H) of one output row per thread
+// (k_gate's arithmetic, aux_kernels.hip), acts [rows][ldy]
+__global__ void splitk_reduce_gate_kernel(const ConvArgs a, const int ksplit) {
+  const unsigned H = (unsigned)a.gate_h;
+  const unsigned per_b = (unsigned)(a.ws_rows * a.N), per_o = (unsigned)a.ws_rows * H;
+  const int b = blockIdx.y;
+  const float* g = a.gate_g + (long long)b * a.gate_g_bs;
+  float* Y = a.y + (long long)b * a.y_bs;
+  const float* base = a.ws + (long long)b * ksplit * per_b;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < per_o; i += gridDim.x * blockDim.x) {
+    const unsigned m = i / H, c = i - m * H;
+    const float* p = base + (size_t)m * a.N + c;
+    float u = 0.f, v = 0.f;
+    for (int s = 0; s < ksplit; ++s) {
+      u += p[(long long)s * per_b];
+      v += p[(long long)s * per_b + H];
+    }
+    if (a.bias) {
+      u += a.bias[c];
+      v += a.bias[c + H];
+    }
+    const float ta = u + g[c], sb = v + g[c + H];
+    Y[(long long)m * a.ldy + c] = tanhf(ta) * (1.f / (1.f + expf(-sb)));
+  }
+}
+
 hipError_t launch_splitk_reduce(const ConvArgs& a, int ksplit, bool two_d, hipStream_t s) {
+  if (a.gate_h > 0) {
+    if (two_d || a.batch_inner != 1 || a.N != 2 * a.gate_h || !a.gate_g) return hipErrorInvalidValue;
+    const long long per_o = a.ws_rows * a.gate_h;
+    hipLaunchKernelGGL(splitk_reduce_gate_kernel, dim3((unsigned)std::min<long long>((per_o + 255) / 256, 4096),
+                                                       (unsigned)a.batch), dim3(256), 0, s, a, ksplit);
+    return hipGetLastError();
+  }
   const long long per_b = (long long)a.ws_rows * a.N;
   const int nz = a.batch * a.batch_inner;
   if (per_b >= (1LL << 31) || nz > 65535) return hipErrorInvalidValue;  // 32-bit element index, grid y
@@ -636,15 +669,17 @@ inline int env_cfg(const char* name, int dflt) {
   const char* e = std::getenv(name);
   return e ? std::atoi(e) : dflt;
 }
-// contraction arithmetic: 1 = native fp32 MFMA (conv_gemm_kernel), 2 = fp32 through the 3-way bf16 split
-// (conv_emu.hip, the default), 3 = as 2 except the weight-streamed kernel, which takes the two-plane fp16 split
-// (the WSPLIT_H16 image); ConvArgs::math overrides RVCX_CONV_MATH (f32 | split | h16)
+// contraction arithmetic: 1 = native fp32 MFMA (conv_gemm_kernel), 2 = fp32 through the 3-way bf16 split everywhere
+// (conv_emu.hip), 3 (the default) = as 2 except the weight-streamed kernel and the fused ResBlock pairs (the generator),
+// which take the two-plane fp16 split (the WSPLIT_H16 / RB_WF16 images: three MFMA products per step instead of six,
+// measured as accurate as native fp32, bench_conv / tests/test_gpu_conv_math.py); ConvArgs::math overrides
+// RVCX_CONV_MATH (f32 | split | h16)
 inline int conv_math(const ConvArgs& a) {
   static const int env = [] {
     const char* e = std::getenv("RVCX_CONV_MATH");
     if (e && (std::string(e) == "f32" || std::string(e) == "1")) return 1;
-    if (e && (std::string(e) == "h16" || std::string(e) == "3")) return 3;
-    return 2;
+    if (e && (std::string(e) == "split" || std::string(e) == "2")) return 2;
+    return 3;
   }();
   return a.math > 0 ? a.math : env;
 }
@@ -734,6 +769,7 @@ template <bool TWO_D>
 hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
   if (a.N <= 0 || a.T_out <= 0 || a.batch <= 0) return hipSuccess;
   if (a.C_in <= 0 || a.taps <= 0) return hipErrorInvalidValue;
+  if (a.gate_h > 0 && !(a.ws && a.ksplit > 1)) return hipErrorInvalidValue;  // the gate is applied by the combine
   if (tiny_fits(a)) return launch_tiny(a, TWO_D, s);
   if (a.wsb == 2 && a.wsplit && conv_math(a) >= 2 && conv_gs_eligible(a, TWO_D)) {
     const int ks = (a.ws && a.ksplit > 1) ? a.ksplit : 1;
@@ -831,7 +867,8 @@ long long conv_plan_splitk(ConvArgs& a, bool two_d) {
   static const int target = env_cfg("RVCX_SPLITK_TARGET", 512);   // workgroups a split launch aims for
   static const int min_tiles = env_cfg("RVCX_SPLITK_TILES", 192);  // grids with at least this many tiles stay unsplit
   static const int min_iters = env_cfg("RVCX_SPLITK_MINITERS", 4);  // shortest contraction worth a split
-  if (tiles >= min_tiles || iters < min_iters || (flops < 1.0e8 && iters < 16)) return 0;
+  // a gated WaveNet in_layer always splits: its gate lives in the combine (ConvArgs::gate_h)
+  if (a.gate_h == 0 && (tiles >= min_tiles || iters < min_iters || (flops < 1.0e8 && iters < 16))) return 0;
   int ks = (int)((target + tiles - 1) / tiles);
   // the gather-streamed kernels keep >= 8 (chunk, tap) steps per slice: below that a slice is all prologue and
   // epilogue and the extra slab + combine launch cost more than the parallelism gains (bench_gs r03s, cold: HuBERT
@@ -844,6 +881,7 @@ long long conv_plan_splitk(ConvArgs& a, bool two_d) {
   // ks 4 beat the 10 and 6 the step count would give)
   if (a.wsb == 2 && two_d && (a.force_cfg < 0 || a.force_cfg == 30) && conv_gsw_eligible(a))
     ks = std::min(ks, (a.C_in + CK - 1) / CK);
+  if (a.gate_h > 0 && iters >= 2) ks = std::max(ks, 2);
   if (ks < 2) return 0;
   a.ksplit = ks;
   a.ws_rows = two_d ? (long long)a.T_out * a.W_out : a.T_out;

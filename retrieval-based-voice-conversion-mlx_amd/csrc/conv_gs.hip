@@ -32,9 +32,38 @@ constexpr int GS_BLK = 1024;       // bytes of one (step, 16-column group, plane
 #endif
 constexpr int GS_D = GS_DEPTH;      // prefetch ring depth (steps in flight per operand)
 
+// one (tm) row block of 16x16x32 fp16 MFMAs of the two-plane arithmetic: acc += h*h', acc2 += l*h' + h*l'
+template <int TN16>
+__device__ __forceinline__ void mma_h16(const bf16x8 (&af)[2], const bf16x8 (&bf)[TN16][2], f32x4 (&acc)[TN16],
+                                        f32x4 (&acc2)[TN16]) {
+  const f16x8 ah = __builtin_bit_cast(f16x8, af[0]), al = __builtin_bit_cast(f16x8, af[1]);
+#pragma unroll
+  for (int tn = 0; tn < TN16; ++tn) {
+    const f16x8 bh = __builtin_bit_cast(f16x8, bf[tn][0]);
+    acc[tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc[tn], 0, 0, 0);
+    f32x4 c = acc2[tn];
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, __builtin_bit_cast(f16x8, bf[tn][1]), c, 0, 0, 0);
+    acc2[tn] = c;
+  }
+}
+// acc + 2^-11 acc2, times 1 / (weight scale x activation scale) from the fp16 image's tail (at tail_off bytes)
+template <int TM16, int TN16>
+__device__ __forceinline__ void h16_finish(const char* wsp, size_t tail_off, f32x4 (&acc)[TM16][TN16],
+                                           const f32x4 (&acc2)[TM16][TN16]) {
+  const float inv = *reinterpret_cast<const float*>(wsp + tail_off + sizeof(float));
+#pragma unroll
+  for (int tm = 0; tm < TM16; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < TN16; ++tn)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[tm][tn][r] = (acc[tm][tn][r] + acc2[tm][tn][r] * H16_LO_INV) * inv;
+}
+
 // MODE bits 0-1: the pre-activation (pre_fn: none, leaky ReLU, other), bit 2: a 1-D pre-mask row multiplier --
 // compile-time, so the step loop carries no per-element activation switch and no conditional mask load (both put ~30
-// scalar branches and a load-history merge into every step)
+// scalar branches and a load-history merge into every step); bit 4: the two-plane fp16 arithmetic (split_bf16.h
+// put_h16x4, the WSPLIT_H16 image: three MFMA products into two accumulators instead of six)
 template <int BM, int BN, int WM, int WN, bool TWO_D, int MODE>
 __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gs16_kernel(const ConvArgs a, const char* __restrict__ wsp,
                                                                     const int Npad, const int ntn, const int ksplit,
@@ -45,6 +74,9 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gs16_kernel(const ConvAr
   constexpr int AV = BM * EC4 / NT;  // float4 groups of the A tile per thread
   constexpr int PA = MODE & 3;
   constexpr bool PMASK = !TWO_D && (MODE & 4) != 0;
+  constexpr bool H16 = (MODE & 16) != 0;
+  constexpr int NQ = H16 ? 2 : 3;            // planes per operand
+  constexpr int RS = H16 ? ERS_H : ERS;      // LDS row stride
   static_assert(WM * WN == 4 && TM16 >= 1 && TN16 >= 1 && BM * EC4 % NT == 0, "tile shape");
   extern __shared__ __attribute__((aligned(16))) char smem_gs[];
 
@@ -160,38 +192,51 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gs16_kernel(const ConvAr
 #pragma unroll
         for (int j = 0; j < 4; ++j) val[j] = ok ? val[j] : 0.f;
       }
-      put_split4(As + (v * (NT / EC4) + arow) * ERS, ac4, val);
+      if constexpr (H16) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) val[j] *= H16_XS;
+        put_h16x4<2>(As + (v * (NT / EC4) + arow) * RS, ac4, val);
+      } else {
+        put_split4(As + (v * (NT / EC4) + arow) * RS, ac4, val);
+      }
     }
   };
 
   // ---- B: pre-split fragments from L2
-  typedef bf16x8 BFrag[TN16][3];
+  typedef bf16x8 BFrag[TN16][NQ];
   BFrag br[GS_D];
   // the image's lane-major blocks (conv_wsb.hip k_wsplit): lane l reads 16-B slot l, one contiguous 1 KB per load
-  const char* bp = wsp + (size_t)((n0 + wn * TN16 * 16) >> 4) * (3 * GS_BLK) + lane * 16;
-  const size_t bstep = (size_t)Npad * GS_WROW;
+  const char* bp = wsp + (size_t)((n0 + wn * TN16 * 16) >> 4) * (NQ * GS_BLK) + lane * 16;
+  const size_t bstep = (size_t)Npad * NQ * PLANE;
   auto load_b = [&](int st, BFrag& dst) __attribute__((always_inline)) {
     const char* p = bp + (size_t)st * bstep;
 #pragma unroll
     for (int tn = 0; tn < TN16; ++tn)
 #pragma unroll
-      for (int q = 0; q < 3; ++q) dst[tn][q] = *reinterpret_cast<const bf16x8*>(p + tn * (3 * GS_BLK) + q * GS_BLK);
+      for (int q = 0; q < NQ; ++q) dst[tn][q] = *reinterpret_cast<const bf16x8*>(p + tn * (NQ * GS_BLK) + q * GS_BLK);
   };
 
-  f32x4 acc[TM16][TN16];
+  f32x4 acc[TM16][TN16], acc2[H16 ? TM16 : 1][H16 ? TN16 : 1];
 #pragma unroll
   for (int tm = 0; tm < TM16; ++tm)
 #pragma unroll
-    for (int tn = 0; tn < TN16; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int tn = 0; tn < TN16; ++tn) {
+      acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (H16) acc2[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   int aoff[TM16];
 #pragma unroll
-  for (int tm = 0; tm < TM16; ++tm) aoff[tm] = (wm * TM16 * 16 + tm * 16 + lc) * ERS + lg * 16;
+  for (int tm = 0; tm < TM16; ++tm) aoff[tm] = (wm * TM16 * 16 + tm * 16 + lc) * RS + lg * 16;
   auto compute = [&](const char* As, const BFrag& bf) __attribute__((always_inline)) {
 #pragma unroll
     for (int tm = 0; tm < TM16; ++tm) {
-      bf16x8 af[3];
+      bf16x8 af[NQ];
 #pragma unroll
-      for (int q = 0; q < 3; ++q) af[q] = *reinterpret_cast<const bf16x8*>(As + aoff[tm] + q * PLANE);
+      for (int q = 0; q < NQ; ++q) af[q] = *reinterpret_cast<const bf16x8*>(As + aoff[tm] + q * PLANE);
+      if constexpr (H16) {
+        mma_h16(af, bf, acc[tm], acc2[tm]);
+        continue;
+      }
 #pragma unroll
       for (int tn = 0; tn < TN16; ++tn) {
         f32x4 c = acc[tm][tn];
@@ -225,10 +270,10 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gs16_kernel(const ConvAr
     auto step = [&](int i, int p) __attribute__((always_inline)) {
       load_b(clampst(i + GS_D - 1), br[(p + GS_D - 1) % GS_D]);
       __builtin_amdgcn_sched_barrier(0);
-      compute(smem_gs + (size_t)((i - it0) & 1) * BM * ERS, br[p]);
+      compute(smem_gs + (size_t)((i - it0) & 1) * BM * RS, br[p]);
       // A(i + 1) -> the other LDS buffer (on the last step a harmless copy of A(last) nobody reads), then A(i + D)
       // into the slot A(i) left
-      store_a(smem_gs + (size_t)((i + 1 - it0) & 1) * BM * ERS, ar[(p + 1) % GS_D], am[(p + 1) % GS_D],
+      store_a(smem_gs + (size_t)((i + 1 - it0) & 1) * BM * RS, ar[(p + 1) % GS_D], am[(p + 1) % GS_D],
               aok[(p + 1) % GS_D]);
       load_a(ar[p], am[p], aok[p]);
       __syncthreads();
@@ -242,6 +287,7 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gs16_kernel(const ConvAr
     for (int p = 0; p < GS_D - 1; ++p)
       if (base + p < it1) step(base + p, p);
   }
+  if constexpr (H16) h16_finish(wsp, (size_t)total * bstep, acc, acc2);
   store_tile16<TM16, TN16, WM, WN>(a, m0, n0, b, zsplit, ksplit, Mtot, acc);
 }
 
@@ -259,7 +305,8 @@ hipError_t launch_gs(const ConvArgs& a, int ntn_enable, int ksplit, hipStream_t 
   const int ntiles = (a.N + BN - 1) / BN;
   const int ntn = ntn_enable ? ntiles : 0;
   dim3 grid((unsigned)(ntn ? mtiles * ntiles : mtiles), ntn ? 1 : ntiles, a.batch * ksplit);
-  const size_t smem = (size_t)2 * BM * ERS;
+  const bool h16 = a.wsplit_fmt == WSPLIT_H16;
+  const size_t smem = (size_t)2 * BM * (h16 ? ERS_H : ERS);
   // M-fastest tile runs when the pre-split weight (6 B per element) outweighs the activation operand (4 B)
   static const int mf_env = [] {
     const char* e = std::getenv("RVCX_GS_MFAST");
@@ -267,14 +314,23 @@ hipError_t launch_gs(const ConvArgs& a, int ntn_enable, int ksplit, hipStream_t 
   }();
   const double wbytes = 6.0 * a.N * a.C_in * a.taps, abytes = 4.0 * (double)Mtot * a.C_in * a.batch;
   const int mfast = mf_env >= 0 ? mf_env : (wbytes > abytes ? 1 : 0);
-  const int mode = pre_mode(a.pre_act) | (!TWO_D && a.pre_mask ? 4 : 0);
+  const int mode = pre_mode(a.pre_act) | (!TWO_D && a.pre_mask ? 4 : 0) | (h16 ? 16 : 0);
+  if (h16 && !(BM == 64 && BN == 64)) return hipErrorInvalidValue;  // the fp16 instantiations: the policy's tile only
+  constexpr bool HI = BM == 64 && BN == 64;
   switch (mode) {
     case 0: launch_gs_mode<BM, BN, WM, WN, TWO_D, 0>(a, grid, smem, ntn, ksplit, mfast, s); break;
     case 1: launch_gs_mode<BM, BN, WM, WN, TWO_D, 1>(a, grid, smem, ntn, ksplit, mfast, s); break;
     case 2: launch_gs_mode<BM, BN, WM, WN, TWO_D, 2>(a, grid, smem, ntn, ksplit, mfast, s); break;
     case 4: launch_gs_mode<BM, BN, WM, WN, TWO_D, 4>(a, grid, smem, ntn, ksplit, mfast, s); break;
     case 5: launch_gs_mode<BM, BN, WM, WN, TWO_D, 5>(a, grid, smem, ntn, ksplit, mfast, s); break;
-    default: launch_gs_mode<BM, BN, WM, WN, TWO_D, 6>(a, grid, smem, ntn, ksplit, mfast, s); break;
+    case 6: launch_gs_mode<BM, BN, WM, WN, TWO_D, 6>(a, grid, smem, ntn, ksplit, mfast, s); break;
+    case 16: launch_gs_mode<BM, BN, WM, WN, TWO_D, HI ? 16 : 0>(a, grid, smem, ntn, ksplit, mfast, s); break;
+    case 17: launch_gs_mode<BM, BN, WM, WN, TWO_D, HI ? 17 : 0>(a, grid, smem, ntn, ksplit, mfast, s); break;
+    case 18: launch_gs_mode<BM, BN, WM, WN, TWO_D, HI ? 18 : 0>(a, grid, smem, ntn, ksplit, mfast, s); break;
+    case 20: launch_gs_mode<BM, BN, WM, WN, TWO_D, HI && !TWO_D ? 20 : 0>(a, grid, smem, ntn, ksplit, mfast, s); break;
+    case 21: launch_gs_mode<BM, BN, WM, WN, TWO_D, HI && !TWO_D ? 21 : 0>(a, grid, smem, ntn, ksplit, mfast, s); break;
+    case 22: launch_gs_mode<BM, BN, WM, WN, TWO_D, HI && !TWO_D ? 22 : 0>(a, grid, smem, ntn, ksplit, mfast, s); break;
+    default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
@@ -290,6 +346,7 @@ hipError_t launch_gs(const ConvArgs& a, int ntn_enable, int ksplit, hipStream_t 
 constexpr int GSW_MAXW = 32;
 constexpr int GSW_WROWS = (64 / GSW_MAXW + 2) * (GSW_MAXW + 2);  // largest window: rh = 2 (4 x 34 = 136 pixels)
 
+// MODE bits 0-1 the pre-activation, bit 4 the two-plane fp16 arithmetic (as conv_gs16_kernel)
 template <int MODE>
 __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gsw16_kernel(const ConvArgs a, const char* __restrict__ wsp,
                                                                      const int Npad, const int ntn, const int ksplit,
@@ -298,6 +355,9 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gsw16_kernel(const ConvA
   constexpr int NT = CONV_THREADS;
   constexpr int TM16 = BM / (WM * 16), TN16 = BN / (WN * 16);
   constexpr int PA = MODE & 3;
+  constexpr bool H16 = (MODE & 16) != 0;
+  constexpr int NQ = H16 ? 2 : 3;
+  constexpr int RS = H16 ? ERS_H : ERS;
   constexpr int WV = (GSW_WROWS * EC4 + NT - 1) / NT;  // float4 groups of the window per thread
   extern __shared__ __attribute__((aligned(16))) char smem_gsw[];
 
@@ -353,44 +413,57 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gsw16_kernel(const ConvA
         const bool ok = (wok >> v) & 1u;
 #pragma unroll
         for (int j = 0; j < 4; ++j) val[j] = ok ? pre_fn<PA>(val[j], a.pre_act, a.pre_slope) : 0.f;
-        put_split4(smem_gsw + r * ERS, ac4, val);
+        if constexpr (H16) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) val[j] *= H16_XS;
+          put_h16x4<2>(smem_gsw + r * RS, ac4, val);
+        } else {
+          put_split4(smem_gsw + r * RS, ac4, val);
+        }
       }
     }
   };
 
   // ---- B ring (conv_gs16_kernel's)
-  typedef bf16x8 BFrag[TN16][3];
+  typedef bf16x8 BFrag[TN16][NQ];
   BFrag br[GS_D];
-  const char* bp = wsp + (size_t)((n0 + wn * TN16 * 16) >> 4) * (3 * GS_BLK) + lane * 16;
-  const size_t bstep = (size_t)Npad * GS_WROW;
+  const char* bp = wsp + (size_t)((n0 + wn * TN16 * 16) >> 4) * (NQ * GS_BLK) + lane * 16;
+  const size_t bstep = (size_t)Npad * NQ * PLANE;
   auto load_b = [&](int st, BFrag& dst) __attribute__((always_inline)) {
     const char* p = bp + (size_t)st * bstep;
 #pragma unroll
     for (int tn = 0; tn < TN16; ++tn)
 #pragma unroll
-      for (int q = 0; q < 3; ++q) dst[tn][q] = *reinterpret_cast<const bf16x8*>(p + tn * (3 * GS_BLK) + q * GS_BLK);
+      for (int q = 0; q < NQ; ++q) dst[tn][q] = *reinterpret_cast<const bf16x8*>(p + tn * (NQ * GS_BLK) + q * GS_BLK);
   };
 
-  f32x4 acc[TM16][TN16];
+  f32x4 acc[TM16][TN16], acc2[H16 ? TM16 : 1][H16 ? TN16 : 1];
 #pragma unroll
   for (int tm = 0; tm < TM16; ++tm)
 #pragma unroll
-    for (int tn = 0; tn < TN16; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int tn = 0; tn < TN16; ++tn) {
+      acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (H16) acc2[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   // A fragment rows: tile pixel ml = (r, c) -> window pixel (r + kh, c + kw)
   int aoff[TM16];
 #pragma unroll
   for (int tm = 0; tm < TM16; ++tm) {
     const int ml = wm * TM16 * 16 + tm * 16 + lc;
     const int r = ml / W, c = ml - r * W;
-    aoff[tm] = (r * aw + c) * ERS + lg * 16;
+    aoff[tm] = (r * aw + c) * RS + lg * 16;
   }
   auto compute = [&](int tap, const BFrag& bf) __attribute__((always_inline)) {
-    const int toff = ((tap / 3) * aw + (tap % 3)) * ERS;
+    const int toff = ((tap / 3) * aw + (tap % 3)) * RS;
 #pragma unroll
     for (int tm = 0; tm < TM16; ++tm) {
-      bf16x8 af[3];
+      bf16x8 af[NQ];
 #pragma unroll
-      for (int q = 0; q < 3; ++q) af[q] = *reinterpret_cast<const bf16x8*>(smem_gsw + aoff[tm] + toff + q * PLANE);
+      for (int q = 0; q < NQ; ++q) af[q] = *reinterpret_cast<const bf16x8*>(smem_gsw + aoff[tm] + toff + q * PLANE);
+      if constexpr (H16) {
+        mma_h16(af, bf, acc[tm], acc2[tm]);
+        continue;
+      }
 #pragma unroll
       for (int tn = 0; tn < TN16; ++tn) {
         f32x4 cc = acc[tm][tn];
@@ -431,6 +504,7 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gsw16_kernel(const ConvA
       }
     }
   }
+  if constexpr (H16) h16_finish(wsp, (size_t)nch * 9 * bstep, acc, acc2);
   store_tile16<TM16, TN16, WM, WN>(a, h0 * W, n0, b, zsplit, ksplit, (long long)H * W, acc);
 }
 
@@ -447,13 +521,17 @@ hipError_t launch_gsw(const ConvArgs& a, int ntn_enable, int ksplit, hipStream_t
   const int ntiles = (a.N + 63) / 64;
   const int ntn = ntn_enable ? ntiles : 0;
   dim3 grid((unsigned)(ntn ? mtiles * ntiles : mtiles), ntn ? 1 : ntiles, a.batch * ksplit);
-  const size_t smem = (size_t)(rh + 2) * (W + 2) * ERS;
+  const bool h16 = a.wsplit_fmt == WSPLIT_H16;
+  const size_t smem = (size_t)(rh + 2) * (W + 2) * (h16 ? ERS_H : ERS);
   const double wbytes = 6.0 * a.N * a.C_in * 9, abytes = 4.0 * (double)a.T_out * W * a.C_in * a.batch;
   const int mfast = wbytes > abytes ? 1 : 0;
-  switch (pre_mode(a.pre_act)) {
+  switch (pre_mode(a.pre_act) | (h16 ? 16 : 0)) {
     case 0: launch_gsw_mode<0>(a, grid, smem, ntn, ksplit, mfast, s); break;
     case 1: launch_gsw_mode<1>(a, grid, smem, ntn, ksplit, mfast, s); break;
-    default: launch_gsw_mode<2>(a, grid, smem, ntn, ksplit, mfast, s); break;
+    case 2: launch_gsw_mode<2>(a, grid, smem, ntn, ksplit, mfast, s); break;
+    case 16: launch_gsw_mode<16>(a, grid, smem, ntn, ksplit, mfast, s); break;
+    case 17: launch_gsw_mode<17>(a, grid, smem, ntn, ksplit, mfast, s); break;
+    default: launch_gsw_mode<18>(a, grid, smem, ntn, ksplit, mfast, s); break;
   }
   return hipGetLastError();
 }
@@ -492,7 +570,7 @@ bool conv_gsw_eligible(const ConvArgs& a) {
 }
 
 hipError_t conv_gs_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream_t s, bool two_d, int ksplit) {
-  if (!a.wsplit || !conv_gs_eligible(a, two_d) || a.wsplit_fmt != WSPLIT_BF16) return hipErrorInvalidValue;
+  if (!a.wsplit || !conv_gs_eligible(a, two_d) || a.lowp) return hipErrorInvalidValue;
   if (two_d && cfg == 30 && conv_gsw_eligible(a)) return launch_gsw(a, ntn_enable, ksplit, s);
   if (two_d) {
     switch (cfg) {

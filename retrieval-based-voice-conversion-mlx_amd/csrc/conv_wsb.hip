@@ -68,7 +68,6 @@ __global__ void k_wsplit(const float* __restrict__ w, int ldw, long long w_ts, i
 // [128, 256): small weights stay normal fp16) and the activations by 2^-4 (inputs up to 2^20 stay finite); the image's
 // tail holds {s, 1 / (s 2^-4)}, which the kernel's epilogue multiplies back in exactly.
 constexpr int WROW_H = 2 * PLANE;  // bytes of one (chunk, tap, column) row of the fp16 image
-constexpr float H16_XS = 1.f / 16.f;
 __global__ void k_wmax_scale(const float* __restrict__ w, int ldw, long long w_ts, int N, int C_in, int taps,
                              float* __restrict__ tail) {
   __shared__ float red[1024 / 64];

@@ -8,8 +8,10 @@
 // output. Per pair that is one read and one write of the [T][C] activation instead of five passes (x, t written,
 // t read, x re-read as the residual, out), and one launch instead of two latency-bound ones at 32/64 channels.
 //
-// Arithmetic: the exact 3-plane bf16 split of conv_emu.hip (x = x0 + x1 + x2, six plane products with i + j <= 2
-// summed smallest first into one fp32 accumulator per output).
+// Arithmetic (FMT): the exact 3-plane bf16 split of conv_emu.hip (x = x0 + x1 + x2, six plane products with i + j <= 2
+// summed smallest first into one fp32 accumulator per output); or the two-plane fp16 split of split_bf16.h
+// (put_h16x4: three products into two accumulators, weights and activations scaled by powers of two); or its hi plane
+// alone (the realtime hop's reduced-precision generator, rvcx_rt_opts::gen_precision).
 //
 // Orientation: D[out channel][time] = W[out ch][in ch] * X^T[in ch][time] on v_mfma_f32_32x32x16_bf16, so a lane
 // of the accumulator holds 16 output channels of ONE time step. Inside each 16-channel chunk the contraction slots
@@ -33,10 +35,15 @@ constexpr int RB_MAXH1 = 30;  // conv1 halo rows per side supported: (k - 1) / 2
 
 __host__ __device__ constexpr int rb_pi(int j) { return (j & 3) | (((j >> 3) & 1) << 2) | (((j >> 2) & 1) << 3); }
 
-template <int C>
+// activation / weight formats: planes per value and element type
+enum RbFmt : int { RB_BF16X3 = 0, RB_F16X2 = 1, RB_F16X1 = 2 };
+__host__ __device__ constexpr int rb_planes(int fmt) { return fmt == RB_BF16X3 ? 3 : (fmt == RB_F16X2 ? 2 : 1); }
+
+template <int C, int FMT = RB_BF16X3>
 struct RbGeo {
-  static constexpr int NCH = C / 16;               // 16-channel contraction chunks
-  static constexpr int ROW = NCH * 3 * 32 + 16;    // LDS bytes per time row: [chunk][plane][16 slots] + pad
+  static constexpr int NCH = C / 16;                           // 16-channel contraction chunks
+  static constexpr int NP = rb_planes(FMT);
+  static constexpr int ROW = NCH * NP * 32 + 16;  // LDS bytes per time row: [chunk][plane][16 slots] + pad
 };
 
 // w [tap][C_out][C_in] fp32 -> ((tap * NCH + s) * 3 + q) planes of [C_out][16 slots] bf16, slot j = channel
@@ -63,6 +70,46 @@ __global__ void k_rb_wsplit(const float* __restrict__ w, int C, int k, unsigned 
   }
 }
 
+// the fp16 images: ((tap * NCH + s) * NP + q) planes of [C_out][16 slots] fp16 (q = 0 hi, 1 the 2^11-scaled residual:
+// put_h16x4's arithmetic) of w * sc, sc a power of two with max |w| sc in [128, 256); the image's tail (after the
+// planes) holds {sc, 1 / (sc * RB_XS)}. Activations are split at RB_XS = 2^-4.
+constexpr float RB_XS = 1.f / 16.f;
+__global__ void k_rb_wmax(const float* __restrict__ w, long long n, float* __restrict__ tail) {
+  __shared__ float red[16];
+  float m = 0.f;
+  for (long long i = threadIdx.x; i < n; i += blockDim.x) m = fmaxf(m, fabsf(w[i]));
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) m = fmaxf(m, red[i]);
+    int e = 0;
+    (void)frexpf(m, &e);
+    const float sc = m > 0.f ? ldexpf(1.f, 8 - e) : 1.f;
+    tail[0] = sc;
+    tail[1] = 1.f / (sc * RB_XS);
+  }
+}
+__global__ void k_rb_wsplit_h16(const float* __restrict__ w, int C, int k, int NP, unsigned short* __restrict__ out,
+                                const float* __restrict__ tail) {
+  const float sc = tail[0];
+  const int NCH = C / 16;
+  const long long total = (long long)k * NCH * C * 16;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int j = (int)(i & 15);
+    long long r = i >> 4;
+    const int och = (int)(r % C);
+    r /= C;
+    const int s = (int)(r % NCH), tap = (int)(r / NCH);
+    const float v = w[((long long)tap * C + och) * C + 16 * s + rb_pi(j)] * sc;
+    const unsigned h = pk_f16(v, 0.f);
+    const long long base = (((long long)(tap * NCH + s) * NP) * C + och) * 16 + j;
+    out[base] = (unsigned short)h;
+    if (NP > 1) out[base + (long long)C * 16] = (unsigned short)pk_f16((v - f16lo_f(h)) * H16_LO, 0.f);
+  }
+}
+
 // 8 fp32 values -> three 16-byte planes (hi, mid, lo)
 __device__ __forceinline__ void split8(const float (&v)[8], uint4& h, uint4& m, uint4& l) {
   unsigned hh[4], mm[4], ll[4];
@@ -80,19 +127,34 @@ __device__ __forceinline__ void split8(const float (&v)[8], uint4& h, uint4& m, 
   l = make_uint4(ll[0], ll[1], ll[2], ll[3]);
 }
 
+// 8 fp32 values (already scaled by RB_XS) -> the fp16 hi plane and the 2^11-scaled residual plane
+__device__ __forceinline__ void split8_h16(const float (&v)[8], uint4& h, uint4& l) {
+  unsigned hh[4], ll[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    hh[p] = pk_f16(v[2 * p], v[2 * p + 1]);
+    ll[p] = pk_f16((v[2 * p] - f16lo_f(hh[p])) * H16_LO, (v[2 * p + 1] - f16hi_f(hh[p])) * H16_LO);
+  }
+  h = make_uint4(hh[0], hh[1], hh[2], hh[3]);
+  l = make_uint4(ll[0], ll[1], ll[2], ll[3]);
+}
+
 __device__ __forceinline__ float lrelu01(float v) { return v > 0.f ? v : v * 0.1f; }
 
 // C channels, NBT 32-row time blocks per workgroup tile, TN time blocks per wave unit, ACCM the output's accumulate
 // mode (ACC_STORE / ACC_ADD / ACC_ADD_DIV: compile-time, so the accumulate target's loads are not a uniform branch
 // whose join would cost the weight ring its depth)
-// MODE: bits 0-1 the accumulate mode ACCM; bit 2 the opt-in reduced precision (RbPairArgs::lowp: bf16 operands, the
-// hi planes' product only; the LDS images and the weight image keep their three planes, only plane 0 is read)
+// MODE: bits 0-1 the accumulate mode ACCM; bits 2-3 the arithmetic FMT (RbFmt: the exact bf16 split, the two-plane
+// fp16 split, or the realtime hop's reduced-precision fp16 hi planes)
 template <int C, int NBT, int TN, int MODE>
 __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, const int ntiles) {
   constexpr int ACCM = MODE & 3;
-  constexpr bool LOWP = (MODE & 4) != 0;
-  constexpr int NQ = LOWP ? 1 : 3;
-  constexpr int NCH = RbGeo<C>::NCH, ROW = RbGeo<C>::ROW, OB = C / 32;
+  constexpr int FMT = (MODE >> 2) & 3;
+  constexpr bool H16 = FMT != RB_BF16X3;
+  constexpr int NQ = rb_planes(FMT);              // planes of the activations in LDS and of an MFMA step
+  constexpr int NQI = H16 ? 2 : 3;               // planes of the weight image (the fp16 image always holds two)
+  constexpr int CB = NQ * 32;  // LDS bytes of one 16-channel chunk of a row
+  constexpr int NCH = RbGeo<C, FMT>::NCH, ROW = RbGeo<C, FMT>::ROW, OB = C / 32;
   constexpr int UNITS = OB * NBT / TN;  // wave work units per conv: (out-channel block, TN time blocks)
   static_assert(UNITS % 4 == 0, "whole units per wave");
   constexpr int UPW = UNITS / 4;
@@ -126,23 +188,35 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
     return w + (size_t)(unit_ob(job) * 32 + li) * 32 + hk * 16;
   };
   auto load_a = [&](const char* wl, int st, AFrag& f) __attribute__((always_inline)) {
-    const char* p = wl + (size_t)st * 3 * QS;
+    const char* p = wl + (size_t)st * NQI * QS;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) f[q] = *reinterpret_cast<const bf16x8*>(p + q * QS);
   };
   auto load_b = [&](const char* bl, int dil, int st, BFrag& f) __attribute__((always_inline)) {
     const int tap = st / NCH, s = st - tap * NCH;
-    const char* bp = bl + (size_t)tap * dil * ROW + s * 96;
+    const char* bp = bl + (size_t)tap * dil * ROW + s * CB;
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
       for (int q = 0; q < NQ; ++q) f[tn][q] = *reinterpret_cast<const bf16x8*>(bp + (size_t)tn * 32 * ROW + q * 32);
   };
-  auto mma = [&](const AFrag& af, const BFrag& bf, f32x16(&acc)[TN]) __attribute__((always_inline)) {
+  typedef _Float16 f16x8_ __attribute__((ext_vector_type(8)));
+  auto mma = [&](const AFrag& af, const BFrag& bf, f32x16(&acc)[TN], f32x16(&acc2)[TN]) __attribute__((always_inline)) {
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
+      if constexpr (H16) {
+        const f16x8_ ah = __builtin_bit_cast(f16x8_, af[0]), bh = __builtin_bit_cast(f16x8_, bf[tn][0]);
+        acc[tn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[tn], 0, 0, 0);
+        if constexpr (NQ > 1) {
+          f32x16 c2 = acc2[tn];
+          c2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_, af[1]), bh, c2, 0, 0, 0);
+          c2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, __builtin_bit_cast(f16x8_, bf[tn][1]), c2, 0, 0, 0);
+          acc2[tn] = c2;
+        }
+        continue;
+      }
       f32x16 c = acc[tn];
-      if constexpr (!LOWP) {
+      {
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[NQ - 1], bf[tn][0], c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[NQ / 2], bf[tn][NQ / 2], c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0], bf[tn][NQ - 1], c, 0, 0, 0);
@@ -160,11 +234,12 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
   // scheduler sank the loads below the MFMAs.
   AFrag ring[3];
   BFrag bring[3];
-  auto run_conv = [&](const char* wl, const char* bl, int dil, f32x16(&acc)[TN]) __attribute__((always_inline)) {
+  auto run_conv = [&](const char* wl, const char* bl, int dil, f32x16(&acc)[TN], f32x16(&acc2)[TN])
+                      __attribute__((always_inline)) {
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[tn][r] = 0.f;
+      for (int r = 0; r < 16; ++r) acc[tn][r] = acc2[tn][r] = 0.f;
     const int last = nsteps - 1;
     load_a(wl, 0, ring[0]);
     load_a(wl, 1 < last ? 1 : last, ring[1]);
@@ -173,7 +248,7 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
       load_a(wl, i + 2 < last ? i + 2 : last, ring[(p + 2) % 3]);
       load_b(bl, dil, i + 1 < last ? i + 1 : last, bring[(p + 1) % 3]);
       __builtin_amdgcn_sched_barrier(0);
-      mma(ring[p], bring[p], acc);
+      mma(ring[p], bring[p], acc, acc2);
     };
     int cur = 0;
     for (; cur + 3 <= nsteps; cur += 3) {
@@ -208,9 +283,22 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
         // channels 16 s + 8 p + 4 q + e sit at slots 8 q + 4 p + e
         const int s = c4 >> 4, o = c4 & 15;
         const int slot = ((o >> 2) & 1) * 8 + (o >> 3) * 4;
-        char* row = XS + (size_t)r * ROW + s * 96 + slot * 2;
+        char* row = XS + (size_t)r * ROW + s * CB + slot * 2;
         const float x0 = lrelu01(xv[it][0]), x1 = lrelu01(xv[it][1]), x2 = lrelu01(xv[it][2]),
                     x3 = lrelu01(xv[it][3]);
+        if constexpr (H16) {
+          uint2 hh, ll;
+          const float y0 = x0 * RB_XS, y1 = x1 * RB_XS, y2 = x2 * RB_XS, y3 = x3 * RB_XS;
+          hh.x = pk_f16(y0, y1);
+          hh.y = pk_f16(y2, y3);
+          *reinterpret_cast<uint2*>(row) = hh;
+          if constexpr (NQ > 1) {
+            ll.x = pk_f16((y0 - f16lo_f(hh.x)) * H16_LO, (y1 - f16hi_f(hh.x)) * H16_LO);
+            ll.y = pk_f16((y2 - f16lo_f(hh.y)) * H16_LO, (y3 - f16hi_f(hh.y)) * H16_LO);
+            *reinterpret_cast<uint2*>(row + 32) = ll;
+          }
+          continue;
+        }
         uint2 hh, mm, ll;
         hh.x = pk_bf16(x0, x1);
         hh.y = pk_bf16(x2, x3);
@@ -278,8 +366,17 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
         }
       }
     }
-    f32x16 acc[TN];
-    run_conv(wl_of(job), (second ? TS : XS) + (size_t)(tg * TN * 32 + li) * ROW + hk * 16, second ? 1 : a.d, acc);
+    f32x16 acc[TN], acc2[TN];
+    run_conv(wl_of(job), (second ? TS : XS) + (size_t)(tg * TN * 32 + li) * ROW + hk * 16, second ? 1 : a.d, acc, acc2);
+    if constexpr (H16) {
+      // acc + 2^-11 acc2, times 1 / (weight scale x activation scale) from the weight image's tail
+      const float inv = *reinterpret_cast<const float*>(static_cast<const char*>(second ? a.w2s : a.w1s) +
+                                                        (size_t)nsteps * NQI * QS + sizeof(float));
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[tn][r] = (NQ > 1 ? acc[tn][r] + acc2[tn][r] * H16_LO_INV : acc[tn][r]) * inv;
+    }
     if (!second) {
       // conv1 -> TS = split(lrelu(conv1 + b1)); TS row p <-> time t0 - h2 + p, zero outside [0, T)
 #pragma unroll
@@ -295,14 +392,21 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
           for (int i = 0; i < 8; ++i) {
             const int r = 8 * hh + i;
             const float x = lrelu01(acc[tn][r] + bv[r >> 2][r & 3]);
-            v[i] = ok ? x : 0.f;
+            v[i] = ok ? (H16 ? x * RB_XS : x) : 0.f;
           }
-          uint4 H, M, L;
-          split8(v, H, M, L);
-          char* dst = row + (2 * ob + hh) * 96;
-          *reinterpret_cast<uint4*>(dst) = H;
-          *reinterpret_cast<uint4*>(dst + 32) = M;
-          *reinterpret_cast<uint4*>(dst + 64) = L;
+          char* dst = row + (2 * ob + hh) * CB;
+          if constexpr (H16) {
+            uint4 Hh, Ll;
+            split8_h16(v, Hh, Ll);
+            *reinterpret_cast<uint4*>(dst) = Hh;
+            if constexpr (NQ > 1) *reinterpret_cast<uint4*>(dst + 32) = Ll;
+          } else {
+            uint4 H, M, L;
+            split8(v, H, M, L);
+            *reinterpret_cast<uint4*>(dst) = H;
+            *reinterpret_cast<uint4*>(dst + 32) = M;
+            *reinterpret_cast<uint4*>(dst + 64) = L;
+          }
         }
       }
     } else {
@@ -335,7 +439,7 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
 
 template <int C, int NBT, int TN, int MODE>
 hipError_t launch_rb_acc(const RbPairArgs& a, hipStream_t s) {
-  constexpr int ROW = RbGeo<C>::ROW;
+  constexpr int ROW = RbGeo<C, (MODE >> 2) & 3>::ROW;
   const int h2 = (a.k - 1) / 2, h1 = h2 * a.d;
   const int TT = NBT * 32 - 2 * h2;
   const size_t smem = (size_t)(NBT * 32 + 2 * h1) * ROW + (size_t)(NBT * 32 + 2 * h2) * ROW;
@@ -365,13 +469,14 @@ hipError_t launch_rb_acc(const RbPairArgs& a, hipStream_t s) {
 
 template <int C, int NBT, int TN>
 hipError_t launch_rb(const RbPairArgs& a, hipStream_t s) {
-  switch (a.acc_mode | (a.lowp ? 4 : 0)) {
-    case ACC_STORE: return launch_rb_acc<C, NBT, TN, ACC_STORE>(a, s);
-    case ACC_ADD: return launch_rb_acc<C, NBT, TN, ACC_ADD>(a, s);
-    case ACC_ADD_DIV: return launch_rb_acc<C, NBT, TN, ACC_ADD_DIV>(a, s);
-    case 4 | ACC_STORE: return launch_rb_acc<C, NBT, TN, 4 | ACC_STORE>(a, s);
-    case 4 | ACC_ADD: return launch_rb_acc<C, NBT, TN, 4 | ACC_ADD>(a, s);
-    case 4 | ACC_ADD_DIV: return launch_rb_acc<C, NBT, TN, 4 | ACC_ADD_DIV>(a, s);
+  // the weight images' format decides the arithmetic; the reduced-precision mode reads the fp16 image's hi plane
+  const int fmt = a.wfmt == RB_WF16 ? (a.lowp ? RB_F16X1 : RB_F16X2) : RB_BF16X3;
+  if (a.lowp && a.wfmt != RB_WF16) return hipErrorInvalidValue;
+  switch (a.acc_mode | (fmt << 2)) {
+#define RB_CASE(M) \
+  case M: return launch_rb_acc<C, NBT, TN, M>(a, s);
+    RB_CASE(0) RB_CASE(1) RB_CASE(2) RB_CASE(4) RB_CASE(5) RB_CASE(6) RB_CASE(8) RB_CASE(9) RB_CASE(10)
+#undef RB_CASE
     default: return hipErrorInvalidValue;
   }
 }
@@ -385,12 +490,22 @@ bool rb_pair_fits(int C, int k, int d) {
   return h2 * d <= RB_MAXH1 && 2 * h2 < 32;
 }
 
-long long rb_wsplit_bytes(int C, int k) { return (long long)k * (C / 16) * 3 * C * 32; }
+// the fp16 image: two planes + a 256-B tail (its scales)
+long long rb_wsplit_bytes(int C, int k, int wfmt) {
+  return wfmt == RB_WF16 ? (long long)k * (C / 16) * 2 * C * 32 + 256 : (long long)k * (C / 16) * 3 * C * 32;
+}
 
-hipError_t rb_wsplit_build(const float* w, int C, int k, void* out, hipStream_t s) {
+hipError_t rb_wsplit_build(const float* w, int C, int k, void* out, hipStream_t s, int wfmt) {
   if (C % 16 != 0 || k < 1) return hipErrorInvalidValue;
   const long long total = (long long)k * (C / 16) * C * 16;
   const long long nb = std::min<long long>((total + 255) / 256, 1 << 20);
+  if (wfmt == RB_WF16) {
+    float* tail = reinterpret_cast<float*>(static_cast<char*>(out) + (long long)k * (C / 16) * 2 * C * 32);
+    hipLaunchKernelGGL(k_rb_wmax, dim3(1), dim3(1024), 0, s, w, (long long)k * C * C, tail);
+    hipLaunchKernelGGL(k_rb_wsplit_h16, dim3((unsigned)nb), dim3(256), 0, s, w, C, k, 2,
+                       static_cast<unsigned short*>(out), static_cast<const float*>(tail));
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_rb_wsplit, dim3((unsigned)nb), dim3(256), 0, s, w, C, k, static_cast<unsigned short*>(out));
   return hipGetLastError();
 }

@@ -108,11 +108,19 @@ struct Ctx {
   // kernel timing (rvcx_profile): event pairs around every conv-GEMM launch, on its stream
   bool prof = false;
   int conv_math = 0;  // ConvArgs::math of every conv launch (rvcx_set_conv_math): 0 default, 1 fp32 MFMA, 2 split
+  // the arithmetic a launch without ConvArgs::math gets: rvcx_set_conv_math, else RVCX_CONV_MATH
+  int conv_math_default() const {
+    ConvArgs a;
+    a.math = conv_math;
+    return conv_math_of(a);
+  }
+  static constexpr double PEAK_SPLIT = 2500.0 / 6.0, PEAK_F16X2 = 2500.0 / 3.0, PEAK_F16 = 2500.0;
   struct ProfRec {
     hipEvent_t a, b;
     double flops;
     int two_d, M, N, C_in, taps, batch, ksplit;  // shape, for RVCX_PROF_DUMP
     double bytes;  // algorithmic HBM bytes: operands read once, result written once (RVCX_PROF_DUMP)
+    double peak_tf;  // the MFMA ceiling of the launch's arithmetic, algorithmic fp32 TFLOP/s
   };
   std::vector<ProfRec> prof_recs;
   std::vector<hipEvent_t> prof_pool;
@@ -122,8 +130,8 @@ struct Ctx {
   std::map<std::tuple<const void*, int, long long, int, int, int, int>, std::unique_ptr<DevBuf>> wsplit_cache;
   const void* wsplit_for(const ConvArgs& a, hipStream_t s);
   // pre-split images of the fused ResBlock pair kernel (resblock_fused.hip), per weight tensor
-  std::map<const void*, std::unique_ptr<DevBuf>> rb_wsplit_cache;
-  const void* rb_wsplit_for(const float* w, int C, int k, hipStream_t s);
+  std::map<std::pair<const void*, int>, std::unique_ptr<DevBuf>> rb_wsplit_cache;
+  const void* rb_wsplit_for(const float* w, int C, int k, int wfmt, hipStream_t s);
   // second stream for work independent of the caller's stream (HuBERT beside RMVPE), created lazily
   hipStream_t aux = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_gate = nullptr;

@@ -133,7 +133,7 @@ void Ctx::drop_splits(uintptr_t lo, uintptr_t hi) {
     it = (u >= lo && u < hi) ? wsplit_cache.erase(it) : std::next(it);
   }
   for (auto it = rb_wsplit_cache.begin(); it != rb_wsplit_cache.end();) {
-    const uintptr_t u = reinterpret_cast<uintptr_t>(it->first);
+    const uintptr_t u = reinterpret_cast<uintptr_t>(it->first.first);
     it = (u >= lo && u < hi) ? rb_wsplit_cache.erase(it) : std::next(it);
   }
 }
@@ -184,15 +184,23 @@ void finalize_synth(Ctx& c) {
   }
   c.alloc_weight("te.proj.w", get(c, M, "enc_p.proj.weight", {2 * I, H, 1}).v);
   c.alloc_weight("te.proj.b", get(c, M, "enc_p.proj.bias", {2 * I}).v);
-  // flow (residuals.py:103-258, modules.py:5-117)
+  // flow (residuals.py:103-258, modules.py:5-117). A coupling's WaveNet state lives in one [T][2H] buffer: the
+  // residual stream h in columns [0, H), the skip sum in [H, 2H). `pre` is packed with H zero rows appended, so its
+  // launch also clears the skip sum; the cond layers of all couplings are one [flow_n * cl][gin] GEMM.
+  std::vector<float> condw, condb;
   for (int f = 0; f < g.flow_n; ++f) {
     const std::string p = "flow.flows." + std::to_string(2 * f);
     const std::string q = "flow." + std::to_string(f);
-    c.alloc_weight(q + ".pre.w", get(c, M, p + ".pre.weight", {H, I / 2, 1}).v);
-    c.alloc_weight(q + ".pre.b", get(c, M, p + ".pre.bias", {H}).v);
+    std::vector<float> prew = get(c, M, p + ".pre.weight", {H, I / 2, 1}).v, preb = get(c, M, p + ".pre.bias", {H}).v;
+    prew.resize((size_t)2 * H * (I / 2), 0.f);
+    preb.resize((size_t)2 * H, 0.f);
+    c.alloc_weight(q + ".pre.w", prew);
+    c.alloc_weight(q + ".pre.b", preb);
     const int cl = 2 * H * g.flow_layers;
-    c.alloc_weight(q + ".cond.w", get(c, M, p + ".enc.cond_layer.weight", {cl, g.gin, 1}).v);
-    c.alloc_weight(q + ".cond.b", get(c, M, p + ".enc.cond_layer.bias", {cl}).v);
+    const auto& cw = get(c, M, p + ".enc.cond_layer.weight", {cl, g.gin, 1}).v;
+    const auto& cb = get(c, M, p + ".enc.cond_layer.bias", {cl}).v;
+    condw.insert(condw.end(), cw.begin(), cw.end());
+    condb.insert(condb.end(), cb.begin(), cb.end());
     for (int L = 0; L < g.flow_layers; ++L) {
       const std::string l = std::to_string(L);
       c.alloc_weight(q + ".in" + l + ".w",
@@ -205,6 +213,8 @@ void finalize_synth(Ctx& c) {
     c.alloc_weight(q + ".post.w", get(c, M, p + ".post.weight", {I / 2, H, 1}).v);
     c.alloc_weight(q + ".post.b", get(c, M, p + ".post.bias", {I / 2}).v);
   }
+  c.alloc_weight("flow.cond.w", condw);
+  c.alloc_weight("flow.cond.b", condb);
   c.alloc_weight("emb_g", get(c, M, "emb_g.weight", {g.n_spk, g.gin}).v);
   if (g.f0 && g.vocoder == 2) {  // RefineGAN (generators/refinegan.py), its own weight tree
     finalize_refinegan(c);
@@ -445,9 +455,10 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
           RbPairArgs p;
           p.x = r_in;
           p.x_bs = (long long)Ti * C;
-          p.w1s = c.rb_wsplit_for(c.W(n1 + ".w"), C, k, s);
+          p.wfmt = (gen_lowp || c.conv_math_default() == 3) ? RB_WF16 : RB_WBF16;
+          p.w1s = c.rb_wsplit_for(c.W(n1 + ".w"), C, k, p.wfmt, s);
           p.b1 = c.W(n1 + ".b");
-          p.w2s = c.rb_wsplit_for(c.W(n2 + ".w"), C, k, s);
+          p.w2s = c.rb_wsplit_for(c.W(n2 + ".w"), C, k, p.wfmt, s);
           p.b2 = c.W(n2 + ".b");
           p.C = C;
           p.k = k;
@@ -640,48 +651,44 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
   check(zp_sample(stats, B, T, I, eps_z, splitmix(seed ^ 0x5a505f4e4f495345ull), mask, z, s), "zp_sample");
   if (zp_out) RVCX_HIP(hipMemcpyAsync(zp_out, z, BT * I * sizeof(float), hipMemcpyDeviceToDevice, s));
   // ---- flow reverse (residuals.py:151-164, 233-258; modules.py:78-109)
-  float* hb = c.buf<float>("flow.h", BT * H, s);
-  float* outb = c.buf<float>("flow.out", BT * H, s);
-  float* xin = c.buf<float>("flow.xin", BT * 2 * H, s);
+  // hs [BT][2H]: the WaveNet residual stream h (columns [0, H)) and its skip sum (columns [H, 2H))
+  float* hs = c.buf<float>("flow.hs", BT * 2 * H, s);
   float* acts = c.buf<float>("flow.acts", BT * H, s);
   const int cl = 2 * H * cf.flow_layers;
-  float* gc = c.buf<float>("flow.gc", (size_t)B * cl, s);
+  float* gc = c.buf<float>("flow.gc", (size_t)B * cf.flow_n * cl, s);
+  // g -> every coupling's cond_layer(g) in one GEMM (modules.py:32-35, :92-93)
+  run(c, lin(g, cf.gin, B, cf.gin, c.W("flow.cond.w"), cf.flow_n * cl, c.W("flow.cond.b"), gc, cf.flow_n * cl), s);
   for (int f = cf.flow_n - 1; f >= 0; --f) {
     const std::string q = "flow." + std::to_string(f);
     check(channel_flip(z, xf, (int)BT, I, s), "flip");
-    {
-      ConvArgs a = lin(xf, I, (int)BT, I / 2, c.W(q + ".pre.w"), H, c.W(q + ".pre.b"), hb, H);
+    {  // h = pre(x0) * mask, and the skip sum cleared (the zero rows of the packed pre weight)
+      ConvArgs a = lin(xf, I, (int)BT, I / 2, c.W(q + ".pre.w"), 2 * H, c.W(q + ".pre.b"), hs, 2 * H);
       a.mask = mask;
       run(c, a, s);
     }
-    run(c, lin(g, cf.gin, B, cf.gin, c.W(q + ".cond.w"), cl, c.W(q + ".cond.b"), gc, cl), s);
     for (int L = 0; L < cf.flow_layers; ++L) {
       const std::string l = std::to_string(L);
-      run(c, conv(hb, H, T, H, c.W(q + ".in" + l + ".w"), 2 * H, cf.flow_k, 1, (cf.flow_k - 1) / 2,
-               c.W(q + ".in" + l + ".b"), xin, 2 * H, T, B),
-          s);
-      check(gate_tanh_sigmoid(xin, 2 * H, gc + L * 2 * H, cl, acts, B, T, H, s), "gate");
-      const float* wrs = c.W(q + ".rs" + l + ".w");
-      const float* brs = c.W(q + ".rs" + l + ".b");
-      if (L < cf.flow_layers - 1) {
-        ConvArgs a = lin(acts, H, (int)BT, H, wrs, H, brs, hb, H);
-        a.res = hb;
-        a.ldr = H;
-        a.res_mode = RES_ADD_POST;
-        a.mask = mask;
-        run(c, a, s);
-        ConvArgs b = lin(acts, H, (int)BT, H, wrs + (size_t)H * H, H, brs + H, outb, H);
-        b.acc_mode = (L == 0) ? ACC_STORE : ACC_ADD;
-        run(c, b, s);
-      } else {
-        ConvArgs a = lin(acts, H, (int)BT, H, wrs, H, brs, outb, H);
-        a.acc_mode = (L == 0) ? ACC_STORE : ACC_ADD;
-        a.mask = mask;
+      {  // acts = tanh(in(h)[:H] + g_l[:H]) * sigmoid(in(h)[H:] + g_l[H:])  (commons.py:88-103), in the split-K combine
+        ConvArgs a = conv(hs, 2 * H, T, H, c.W(q + ".in" + l + ".w"), 2 * H, cf.flow_k, 1, (cf.flow_k - 1) / 2,
+                          c.W(q + ".in" + l + ".b"), acts, H, T, B);
+        a.x_bs = (long long)T * 2 * H;
+        a.gate_h = H;
+        a.gate_g = gc + (size_t)f * cl + (size_t)L * 2 * H;
+        a.gate_g_bs = (long long)cf.flow_n * cl;
         run(c, a, s);
       }
+      const float* wrs = c.W(q + ".rs" + l + ".w");
+      const float* brs = c.W(q + ".rs" + l + ".b");
+      // h = (h + res(acts)) * mask and skip += skip(acts) as one GEMM over both halves (modules.py:95-107); the skip
+      // sum is masked at every layer instead of once at the end: the same values, the mask being exactly 0 / 1
+      const bool last = L == cf.flow_layers - 1;
+      ConvArgs a = lin(acts, H, (int)BT, H, wrs, last ? H : 2 * H, brs, last ? hs + H : hs, 2 * H);
+      a.acc_mode = ACC_ADD;
+      a.mask = mask;
+      run(c, a, s);
     }
     {  // x1 = (x1 - m) * mask, m = post(h) * mask
-      ConvArgs a = lin(outb, H, (int)BT, H, c.W(q + ".post.w"), I / 2, c.W(q + ".post.b"), xf + I / 2, I);
+      ConvArgs a = lin(hs + H, 2 * H, (int)BT, H, c.W(q + ".post.w"), I / 2, c.W(q + ".post.b"), xf + I / 2, I);
       a.res = xf + I / 2;
       a.ldr = I;
       a.res_mode = RES_RSUB_POST;

@@ -85,6 +85,12 @@ struct ConvArgs {
   long long mask_bs = 0;
   int acc_mode = ACC_STORE;
   float acc_div = 1.f;
+  // WaveNet gate (commons.py:88-103) in the split-K combine: N = 2 gate_h columns; y[m][c] (c < gate_h) =
+  // tanh(v[c] + g[c]) * sigmoid(v[c + gate_h] + g[c + gate_h]), v = acc + bias, g = gate_g + b * gate_g_bs. Forces a
+  // split (ksplit >= 2); no other epilogue field may be set.
+  int gate_h = 0;
+  const float* gate_g = nullptr;
+  long long gate_g_bs = 0;
   // grid z = batch * batch_inner; pointer offset = zo * *_bs + zi * *_bs2 (mask: zo only)
   int batch = 1;
   int batch_inner = 1;
@@ -178,11 +184,13 @@ struct RbPairArgs {
   int acc_mode = ACC_STORE;
   float acc_div = 1.f;
   int flags = 0;  // bit 0: next-tile x prefetch into registers (measurement aid, RVCX_RB_FLAGS)
-  int lowp = 0;   // opt-in reduced precision (rvcx_rt_opts::gen_precision): fp16 operands, one MFMA product per step
+  int wfmt = 0;   // RB_WBF16: w1s / w2s are three-plane bf16 images (the exact split); RB_WF16: two-plane fp16 images
+  int lowp = 0;   // opt-in reduced precision (rvcx_rt_opts::gen_precision): the fp16 images' hi planes alone
 };
+enum RbWfmt : int { RB_WBF16 = 0, RB_WF16 = 1 };
 bool rb_pair_fits(int C, int k, int d);
-long long rb_wsplit_bytes(int C, int k);
-hipError_t rb_wsplit_build(const float* w, int C, int k, void* out, hipStream_t s);
+long long rb_wsplit_bytes(int C, int k, int wfmt = RB_WBF16);
+hipError_t rb_wsplit_build(const float* w, int C, int k, void* out, hipStream_t s, int wfmt = RB_WBF16);
 hipError_t rb_pair(const RbPairArgs& a, int cfg, hipStream_t s);
 // fused attention (flash_attn.hip): qkv [B][T][ldq] (q | k | v, heads of dk inside each), optional relative
 // window (rel_k / rel_v [2w+1][dk]) and key/query mask [B][T]; partials part_o [nsplit][B*nh][T][dk], part_ml

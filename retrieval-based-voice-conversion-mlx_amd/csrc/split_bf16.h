@@ -61,6 +61,9 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 constexpr int ERS_H = 2 * PLANE + 16;  // LDS row stride of the two-plane image: 36 dwords, 16 rows -> 16 bank groups
 constexpr float H16_LO = 2048.f, H16_LO_INV = 1.f / 2048.f;
+// activations are split at this scale (weights at a power of two chosen per tensor, conv_wsb.hip k_wmax_scale):
+// inputs up to 2^20 stay finite fp16
+constexpr float H16_XS = 1.f / 16.f;
 
 __device__ __forceinline__ unsigned pk_f16(float x, float y) {
   const f16x2 h = __builtin_convertvector((f32x2){x, y}, f16x2);  // RNE

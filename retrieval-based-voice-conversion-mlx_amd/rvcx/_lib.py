@@ -23,7 +23,7 @@ EXPORTS = [
     "rvcx_create", "rvcx_destroy", "rvcx_last_error", "rvcx_set_synth_config", "rvcx_upload", "rvcx_finalize",
     "rvcx_hubert", "rvcx_rmvpe", "rvcx_f0_post", "rvcx_synth_infer", "rvcx_dec_only", "rvcx_voice_conversion",
     "rvcx_synth_upp", "rvcx_set_highpass", "rvcx_pipeline", "rvcx_pipeline_default_opts", "rvcx_pipeline_ex",
-    "rvcx_f0_autotune", "rvcx_rmvpe_decode", "rvcx_profile", "rvcx_profile_read", "rvcx_index_load",
+    "rvcx_f0_autotune", "rvcx_rmvpe_decode", "rvcx_profile", "rvcx_profile_read", "rvcx_profile_read_ex", "rvcx_index_load",
     "rvcx_index_unload", "rvcx_index_info", "rvcx_index_set_nprobe", "rvcx_index_search", "rvcx_index_reconstruct_n",
     "rvcx_index_retrieve", "rvcx_rt_default_desc", "rvcx_rt_default_opts", "rvcx_rt_create", "rvcx_rt_destroy",
     "rvcx_rt_geometry", "rvcx_rt_reset", "rvcx_rt_process", "rvcx_hubert_batch", "rvcx_rmvpe_batch",
@@ -121,6 +121,7 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "rvcx_set_highpass": (i32, [vp, vp, vp, vp, i32]),
         "rvcx_profile": (i32, [vp, i32]),
         "rvcx_profile_read": (i32, [vp, P(f64), P(f64), P(i64)]),
+        "rvcx_profile_read_ex": (i32, [vp, P(f64), P(f64), P(i64), P(f64)]),
         "rvcx_pipeline": (i32, [vp, vp, i64, i32, f64, f32, i64, i64, vp, vp, u64, vp, i64, P(i64), vp, vp]),
         "rvcx_pipeline_default_opts": (i32, [P(PipelineOpts)]),
         "rvcx_pipeline_ex": (i32, [vp, vp, i64, P(PipelineOpts), vp, vp, u64, vp, i64, P(i64), vp, vp]),

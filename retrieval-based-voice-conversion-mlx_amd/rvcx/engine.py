@@ -468,9 +468,9 @@ class Engine:
 
     # ------------------------------------------------------------------ kernel timing
     def set_conv_math(self, mode: str):
-        """Contraction arithmetic of this context: "split" (default; fp32 via three bf16 planes on bf16 MFMA),
-        "f32" (fp32-input MFMA) or "h16" (as split, with the generator's weight-streamed convs on two fp16 planes)
-        (rvcx_set_conv_math)."""
+        """Contraction arithmetic of this context: "h16" (the default: fp32 via three bf16 planes on bf16 MFMA, the
+        generator's weight-streamed convs and fused ResBlock pairs via two fp16 planes), "split" (three bf16 planes
+        everywhere) or "f32" (fp32-input MFMA) (rvcx_set_conv_math)."""
         m = {"default": 0, "f32": 1, "split": 2, "h16": 3}[mode]
         self._check(self.lib.rvcx_set_conv_math(self.ctx, m), "set_conv_math")
 
@@ -486,7 +486,7 @@ class Engine:
         T = int(x.shape[0])
         T_out = (T + 2 * padding - dilation * (K - 1) - 1) // stride + 1
         y = torch.empty((T_out, N), dtype=torch.float32, device=self.device)
-        m = {"default": 0, "f32": 1, "split": 2, "wsb": 3, "gs": 4}[math]
+        m = {"default": 0, "f32": 1, "split": 2, "wsb": 3, "gs": 4, "h16": 5, "f16": 6}[math]
         self._check(self.lib.rvcx_conv1d(self.ctx, _ptr(x), T, C, _ptr(wk), _ptr(b), N, K, dilation, padding, stride,
                                          m, _ptr(y), T_out, self.stream()), "conv1d")
         return y
@@ -513,9 +513,10 @@ class Engine:
     def profile(self, enable: bool):
         self._check(self.lib.rvcx_profile(self.ctx, 1 if enable else 0), "profile")
 
-    def profile_read(self):
-        """(summed conv-GEMM kernel ms, summed algorithmic FLOPs, launches) since the last read."""
-        ms, fl, n = ctypes.c_double(0), ctypes.c_double(0), ctypes.c_int64(0)
-        self._check(self.lib.rvcx_profile_read(self.ctx, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(n)),
-                    "profile_read")
-        return ms.value, fl.value, n.value
+    def profile_read(self, with_ceiling: bool = False):
+        """(summed conv-GEMM kernel ms, summed algorithmic FLOPs, launches) since the last read; with_ceiling adds
+        the same launches' time at their arithmetic's MFMA ceiling (ms, rvcx_profile_read_ex)."""
+        ms, fl, n, cm = ctypes.c_double(0), ctypes.c_double(0), ctypes.c_int64(0), ctypes.c_double(0)
+        self._check(self.lib.rvcx_profile_read_ex(self.ctx, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(n),
+                                                  ctypes.byref(cm)), "profile_read")
+        return (ms.value, fl.value, n.value, cm.value) if with_ceiling else (ms.value, fl.value, n.value)

@@ -51,6 +51,12 @@ def test_c2_pipeline_vs_reference(engine, clip):
     vc = engine.voice_conversion(p32, coarse[:p_len], pitchf[:p_len], 0, 0.33, eps_z=ez, eps_src=es).cpu().numpy()
     cons = rel_err(out, trim_normalize(vc))
     assert cons <= 1e-6, cons
+    # sample-level bar where f0 cannot have drifted yet: the output up to 20 frames (the generator's
+    # receptive field) before the first frame whose f0 may legitimately differ, at the round-2 bar rel <= 2e-3
+    end = out.shape[0] if r["first_flip"] is None else max(0, (r["first_flip"] - 20) * 480 - 48000)
+    if end >= 48000:
+        pre = float(np.abs(out[:end] - g["out"][:end]).max() / (np.abs(g["out"]).max() + 1e-12))
+        assert pre <= 2e-3, (pre, end)
     print(f"\nC2 {clip}: salience err {r['err']:.2e} (bound {3 * float(g['sal_fp32_noise']):.2e}), {r['n_near']} "
           f"near-tied frames, flips {list(r['flips'])}, spec corr {c:.6f}, rel to reference {rel_err(out, g['out']):.2e}, "
           f"pipeline vs staged {cons:.1e}")

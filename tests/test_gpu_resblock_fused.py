@@ -94,6 +94,23 @@ def test_fused_pair_matches_two_launch_path(engine):
     assert float(np.abs(y - o).max() / np.abs(o).max()) < 2e-6
 
 
+@pytest.mark.parametrize("B,T,C,k,d,cfg", [c for c in CASES if c[5] == 0])
+def test_fused_pair_fp16_arithmetic(engine, B, T, C, k, d, cfg):
+    """cfg bits 4-5: the two-plane fp16 split (fp32-class: within 3x the exact split's bound) and the fp16 hi planes
+    alone (the realtime reduced-precision mode: fp16 rounding)."""
+    rng = np.random.Generator(np.random.PCG64(1000 * C + 10 * k + d + T))
+    x = rng.standard_normal((B, T, C)).astype(np.float32)
+    w1, b1, w2, b2 = _weights(rng, C, k)
+    ref = _ref(x, w1, b1, w2, b2, d)
+    e = {}
+    for fmt in (1, 2):
+        y = engine.resblock_pair(x, w1, b1, w2, b2, d, cfg=cfg | (fmt << 4)).cpu().numpy()
+        e[fmt] = float(np.abs(y - ref).max() / np.abs(ref).max())
+    assert e[1] < 6e-6, e
+    assert e[2] < 3e-3, e
+    print(f"\nfused pair B{B} T{T} C{C} k{k} d{d}: h16x2 {e[1]:.2e} f16 {e[2]:.2e}")
+
+
 def test_fused_pair_rejects_unsupported(engine):
     from rvcx._lib import RvcxError
 

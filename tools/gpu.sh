@@ -46,7 +46,7 @@ for step in "$@"; do
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$TAG -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ${arg//,/ } > $O/prof_$TAG.log 2>&1 || { tail -20 $O/prof_$TAG.log; exit 1; }
       DB=$(find $O/prof_$TAG -name "*.db" | head -1)
-      python3 tools/timeline.py "$DB" 2 > $O/timeline_$TAG.txt 2>&1
+      python3 tools/timeline.py "$DB" 2 -v > $O/timeline_$TAG.txt 2>&1
       python3 tools/prof_summary.py "$DB" 7 > $O/kstats_$TAG.txt 2>&1
       python3 tools/kfamily.py "$DB" 7 > $O/kfamily_$TAG.txt 2>&1
       head -30 $O/kstats_$TAG.txt ;;
