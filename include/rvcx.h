@@ -340,7 +340,8 @@ int rvcx_set_conv_math(rvcx_ctx* ctx, int mode);
  * C_in % 32 == 0 and (taps - 1) * dilation <= 64, else RVCX_E_SHAPE), 4 = the split arithmetic on the gather-streamed
  * kernel (weights pre-split in HBM, A gathered per step, split-K by the size policy; C_in % 32 == 0), 5 = the
  * two-plane fp16 split on the weight-streamed kernel (rvcx_set_conv_math mode 3's generator arithmetic), 6 = its fp16
- * hi planes alone (the realtime reduced-precision mode); 5 and 6 take the shapes 3 does. */
+ * hi planes alone (the realtime reduced-precision mode); 5 and 6 take the shapes 3 does; 7 = the two-plane fp16 split
+ * on the gather-streamed kernel (the shapes 4 takes). */
 int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const float* d_w, const float* d_bias, int N,
                 int taps, int dilation, int pad, int stride, int math, float* d_y, int64_t T_out, void* stream);
 

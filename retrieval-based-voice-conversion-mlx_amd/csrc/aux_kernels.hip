@@ -2,7 +2,9 @@
 // softmax with relative-position bands, layout transforms, RNG, RMVPE front/back end.
 // Elementwise / reduction work here is HBM- or latency-bound; every kernel keeps channels
 // contiguous (time-major rows) so a wave reads whole 128-B lines.
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "dd_math.h"
 #include "rvcx_kernels.h"
@@ -960,6 +962,11 @@ hipError_t filtfilt_sos_pad(const SosPlan& p, int order, const double* x, long l
   double* yb = yf + ne;
   double* sw = yb + ne;
   hipLaunchKernelGGL(k_odd_ext, dim3(nblocks(ne)), dim3(TB), 0, s, x, n, padlen, ext);
+  static const bool per_section = [] {  // RVCX_SOS_PER_SECTION=1: one local / carry / fix round per section (A/B aid)
+    const char* e = std::getenv("RVCX_SOS_PER_SECTION");
+    return e && std::atoi(e) != 0;
+  }();
+  if (p.casc && !per_section) return casc_filtfilt_pad(p, ext, ne, padlen, n, t_pad, yf, pad64, pad32, s);
   hipError_t e = sos_pass(p, ext, ne, 0, yf, sw, s);  // forward, x0 = ext[0]
   if (e != hipSuccess) return e;
   e = sos_pass(p, yf, ne, 1, yb, sw, s);  // backward over reversed yf, x0 = yf[ne - 1]
@@ -971,7 +978,7 @@ hipError_t filtfilt_sos_pad(const SosPlan& p, int order, const double* x, long l
 
 size_t filtfilt_sos_ws_doubles(long long n, int order, int L) {
   const long long ne = n + 2 * 3 * (order + 1);
-  return (size_t)(3 * ne) + sos_ws_doubles(ne, L);
+  return (size_t)(3 * ne) + std::max(sos_ws_doubles(ne, L), casc_ws_doubles(ne, 64));
 }
 
 size_t filtfilt_ws_doubles(long long n, int order) {

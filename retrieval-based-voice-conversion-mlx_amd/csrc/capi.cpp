@@ -599,7 +599,7 @@ int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const floa
     set_device(ctx);
     ctx->check_device_status();
     if (!d_x || !d_w || !d_y || T <= 0 || C_in <= 0 || N <= 0 || taps <= 0 || dilation <= 0 || stride <= 0 ||
-        pad < 0 || T_out <= 0 || math < 0 || math > 6)
+        pad < 0 || T_out <= 0 || math < 0 || math > 7)
       throw Error(RVCX_E_INVALID, "rvcx_conv1d: bad argument");
     if ((T_out - 1) * stride + (int64_t)(taps - 1) * dilation + 1 > T + 2 * (int64_t)pad)
       throw Error(RVCX_E_SHAPE, "rvcx_conv1d: T_out exceeds the padded input");
@@ -611,11 +611,12 @@ int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const floa
     a.stride = stride;
     a.y = d_y; a.ldy = N; a.T_out = (int)T_out; a.N = N; a.bias = d_bias;
     a.math = math >= 5 ? 3 : (math >= 3 ? 2 : math);
+    if (math == 7) a.wsplit_fmt = WSPLIT_H16;  // the two-plane fp16 arithmetic on the gather-streamed kernel
     if (math == 5 || math == 6) {  // the two-plane fp16 arithmetic / its hi plane alone on the weight-streamed kernel
       a.wsplit_fmt = WSPLIT_H16;
       a.lowp = math == 6;
     }
-    if (math == 3 || math >= 5) {  // the weight-streamed split kernel (conv_wsb.hip) whatever the size policy would pick
+    if (math == 3 || math == 5 || math == 6) {  // the weight-streamed split kernel (conv_wsb.hip) whatever the size policy would pick
       if (!conv_wsb_eligible(a)) throw Error(RVCX_E_SHAPE, "rvcx_conv1d: shape not eligible for the weight-streamed kernel");
       a.w_static = 1;
       a.force_cfg = conv_wsb_pick(a);  // the tile the pipeline's policy picks for this shape
@@ -626,7 +627,7 @@ int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const floa
       check(conv_wsplit_build(a, img, static_cast<hipStream_t>(stream)), "conv_wsplit_build");
       a.wsplit = img;
     }
-    if (math == 4) {  // the gather-streamed split kernel (conv_gs.hip), split-K by the size policy
+    if (math == 4 || math == 7) {  // the gather-streamed split kernel (conv_gs.hip), split-K by the size policy
       if (!conv_gs_eligible(a, false)) throw Error(RVCX_E_SHAPE, "rvcx_conv1d: shape not eligible for the gather-streamed kernel");
       a.w_static = 1;
       a.force_cfg = 30;

@@ -513,7 +513,78 @@ __global__ void conv_tiny_kernel(const ConvArgs a) {
   }
 }
 
+// The tiny contractions whose epilogue is only bias + activation + store (the RMVPE U-Net's first ConvBlockRes on the
+// 1-channel mel image: the 3x3 1 -> 16 conv and the 1x1 shortcut), one thread per output ROW computing all N <= 32
+// outputs: the weights and bias in LDS, the <= 16 inputs read once instead of once per output, the activation a
+// compile-time choice, float4 stores. (conv_tiny_kernel's per-element index math, activation switch and shared epilogue
+// took 100-135 us for these two 3.2 M-output convs.)
+template <bool TWO_D, int N, int ACT>
+__global__ __launch_bounds__(256) void conv_tiny_rows_kernel(const ConvArgs a) {
+  __shared__ float ws[16 * 32], bs[32];
+  const int ck = a.C_in * a.taps;  // <= 16
+  for (int i = threadIdx.x; i < ck * N; i += blockDim.x) {
+    const int tap = i / (a.C_in * N), r = i - tap * (a.C_in * N);
+    const int n = r / a.C_in, c = r - n * a.C_in;
+    ws[(tap * a.C_in + c) * N + n] = a.w[(long long)tap * a.w_ts + (long long)n * a.ldw + c];
+  }
+  if (threadIdx.x < N) bs[threadIdx.x] = a.bias ? a.bias[threadIdx.x] : 0.f;
+  __syncthreads();
+  const int rows = TWO_D ? a.T_out * a.W_out : a.T_out;
+  const int total = rows * a.batch;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int b = i / rows, m = i - b * rows;
+    const float* X = a.x + (long long)b * a.x_bs;
+    float acc[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) acc[n] = 0.f;
+    int oh = 0, ow = m;
+    if (TWO_D) {
+      oh = m / a.W_out;
+      ow = m - oh * a.W_out;
+    }
+    for (int tap = 0; tap < a.taps; ++tap) {
+      int g;
+      if (!TWO_D) {
+        g = m * a.stride - a.pad + tap * a.dil;
+        if (g < 0 || g >= a.T_in) continue;
+      } else {
+        const int kh = tap / a.KW;
+        const int gh = oh - a.padh + kh, gw = ow - a.padw + (tap - kh * a.KW);
+        if (gh < 0 || gh >= a.T_in || gw < 0 || gw >= a.W_in) continue;
+        g = gh * a.W_in + gw;
+      }
+      for (int c = 0; c < a.C_in; ++c) {
+        const float v = X[(long long)g * a.ldx + c];
+        const float* wr = ws + (tap * a.C_in + c) * N;
+#pragma unroll
+        for (int n = 0; n < N; ++n) acc[n] = fmaf(v, wr[n], acc[n]);
+      }
+    }
+    float* Y = a.y + (long long)b * a.y_bs + (long long)m * a.ldy;
+#pragma unroll
+    for (int n = 0; n < N; n += 4) {
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = acc[n + e] + bs[n + e];  // conv_tiny_kernel's order: the fma chain, then the bias
+        if (ACT == ACT_RELU) v = v > 0.f ? v : 0.f;
+        else if (ACT == ACT_LRELU) v = v > 0.f ? v : v * a.slope;
+        o[e] = v;
+      }
+      *reinterpret_cast<f32x4*>(Y + n) = o;
+    }
+  }
+}
+
 namespace {
+
+// conv_tiny_rows_kernel's shapes: only bias + activation in the epilogue, N in {16, 32}, 16-B aligned output rows
+inline bool tiny_rows_fits(const ConvArgs& a) {
+  return (a.N == 16 || a.N == 32) && a.pre_act == ACT_NONE && !a.pre_mask && !a.b_kn && a.batch_inner == 1 &&
+         a.out_map == OUT_ROWS && a.res_mode == RES_NONE && !a.mask && a.acc_mode == ACC_STORE && a.alpha == 1.f &&
+         (a.act == ACT_NONE || a.act == ACT_RELU || a.act == ACT_LRELU) && (a.ldy & 3) == 0 && (a.y_bs & 3) == 0 &&
+         (reinterpret_cast<uintptr_t>(a.y) & 15) == 0 && a.gate_h == 0;
+}
 
 constexpr int TINY_MAX_CIN = 4;
 inline bool tiny_fits(const ConvArgs& a) {
@@ -526,6 +597,21 @@ hipError_t launch_tiny(const ConvArgs& a, bool two_d, hipStream_t s) {
   const long long rows = two_d ? (long long)a.T_out * a.W_out : a.T_out;
   const long long total = rows * a.N * a.batch * a.batch_inner;
   if (total >= (1LL << 31) - 65536LL * 256) return hipErrorInvalidValue;  // 32-bit indexing in the kernel
+  if (tiny_rows_fits(a)) {
+    const long long nr = total / a.N;
+    const unsigned nbr = (unsigned)std::min<long long>((nr + 255) / 256, 65536);
+#define TINY_ROWS(TD, NN, AC) hipLaunchKernelGGL((conv_tiny_rows_kernel<TD, NN, AC>), dim3(nbr), dim3(256), 0, s, a)
+    const int act = a.act;
+    if (two_d) {
+      if (a.N == 16) { if (act == ACT_RELU) TINY_ROWS(true, 16, ACT_RELU); else if (act == ACT_LRELU) TINY_ROWS(true, 16, ACT_LRELU); else TINY_ROWS(true, 16, ACT_NONE); }
+      else { if (act == ACT_RELU) TINY_ROWS(true, 32, ACT_RELU); else if (act == ACT_LRELU) TINY_ROWS(true, 32, ACT_LRELU); else TINY_ROWS(true, 32, ACT_NONE); }
+    } else {
+      if (a.N == 16) { if (act == ACT_RELU) TINY_ROWS(false, 16, ACT_RELU); else if (act == ACT_LRELU) TINY_ROWS(false, 16, ACT_LRELU); else TINY_ROWS(false, 16, ACT_NONE); }
+      else { if (act == ACT_RELU) TINY_ROWS(false, 32, ACT_RELU); else if (act == ACT_LRELU) TINY_ROWS(false, 32, ACT_LRELU); else TINY_ROWS(false, 32, ACT_NONE); }
+    }
+#undef TINY_ROWS
+    return hipGetLastError();
+  }
   long long nb = (total + 255) / 256;
   if (nb > 65536) nb = 65536;
   if (two_d) hipLaunchKernelGGL(conv_tiny_kernel<true>, dim3((unsigned)nb), dim3(256), 0, s, a);

@@ -25,7 +25,6 @@ namespace {
 
 using namespace splitbf16;
 
-constexpr int GS_WROW = 3 * PLANE;  // bytes per column of one (chunk, tap) step of the pre-split weight image
 constexpr int GS_BLK = 1024;       // bytes of one (step, 16-column group, plane) block of that image
 #ifndef GS_DEPTH
 #define GS_DEPTH 3

@@ -68,33 +68,27 @@ __global__ void k_wsplit(const float* __restrict__ w, int ldw, long long w_ts, i
 // [128, 256): small weights stay normal fp16) and the activations by 2^-4 (inputs up to 2^20 stay finite); the image's
 // tail holds {s, 1 / (s 2^-4)}, which the kernel's epilogue multiplies back in exactly.
 constexpr int WROW_H = 2 * PLANE;  // bytes of one (chunk, tap, column) row of the fp16 image
+// max |w| over the grid into tail word 2 (zeroed before; a single 1024-thread workgroup took 0.2-0.5 ms per tensor)
 __global__ void k_wmax_scale(const float* __restrict__ w, int ldw, long long w_ts, int N, int C_in, int taps,
                              float* __restrict__ tail) {
-  __shared__ float red[1024 / 64];
   float m = 0.f;
   const long long total = (long long)taps * N * C_in;
-  for (long long i = threadIdx.x; i < total; i += blockDim.x) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(i % C_in);
     const long long r = i / C_in;
     const int n = (int)(r % N), tap = (int)(r / N);
     m = fmaxf(m, fabsf(w[tap * w_ts + (long long)n * ldw + c]));
   }
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) m = fmaxf(m, red[i]);
-    red[0] = m;
-    int e = 0;
-    (void)frexpf(m, &e);  // m = f 2^e, f in [0.5, 1)
-    const float sc = m > 0.f ? ldexpf(1.f, 8 - e) : 1.f;
+  absmax_wave_publish(m, reinterpret_cast<unsigned*>(tail) + 2);
+}
+__global__ void k_wsplit_h16(const float* __restrict__ w, int ldw, long long w_ts, int N, int C_in, int taps,
+                             int nchunks, int Npad, unsigned short* __restrict__ out, float* __restrict__ tail) {
+  const float sc = h16_weight_scale(reinterpret_cast<const unsigned*>(tail)[2]);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     tail[0] = sc;
     tail[1] = 1.f / (sc * H16_XS);
   }
-}
-__global__ void k_wsplit_h16(const float* __restrict__ w, int ldw, long long w_ts, int N, int C_in, int taps,
-                             int nchunks, int Npad, unsigned short* __restrict__ out, const float* __restrict__ tail) {
-  const float sc = tail[0];
   const long long total = (long long)nchunks * taps * Npad * EK;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
@@ -330,7 +324,9 @@ __global__ __launch_bounds__(CONV_THREADS, (BM == 128 && BN == 64 && !TWO_D) ? W
 // C layout of a 16x16 tile: lane l holds column l % 16, rows 4 (l / 16) + r, r = 0..3.
 // MODE: bits 0-1 the pre-activation (pre_fn), bit 2 a pre-mask row multiplier (conv_gs.hip's MODE), bit 4 the
 // two-plane fp16 arithmetic (split_bf16.h put_h16x4; weights from the k_wsplit_h16 image), bit 3 (with bit 4) the
-// opt-in reduced precision: the fp16 hi planes' product alone
+// opt-in reduced precision: the fp16 hi planes' product alone, bit 5 (with bit 4) two A halo buffers in LDS: the next
+// chunk's halo is written into the idle buffer, so a chunk switch is one barrier instead of write-between-two (the
+// fp16 rows are 144 B, so two halos of the generator's widest tap span, 178 rows, still fit three workgroups per CU)
 template <int BM, int BN, int WM, int WN, int MODE>
 __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 : 3) void conv_wsb16_kernel(const ConvArgs a, const char* __restrict__ wsp,
                                                                      const int Npad, const int nrows_a, const int ntn,
@@ -340,6 +336,7 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
   constexpr bool PMASK = (MODE & 4) != 0;
   constexpr bool H16 = (MODE & 16) != 0;
   constexpr bool LOWP = H16 && (MODE & 8) != 0;
+  constexpr bool DBUF = H16 && (MODE & 32) != 0;
   constexpr int NQ = LOWP ? 1 : (H16 ? 2 : 3);  // planes an MFMA step reads
   constexpr int NQI = H16 ? 2 : 3;               // planes of the weight image
   constexpr int RS = H16 ? ERS_H : ERS;          // LDS row stride
@@ -347,7 +344,7 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
   constexpr int TN16 = BN / (WN * 16);
   static_assert(WM * WN == 4 && TM16 >= 1 && TN16 >= 1, "4 waves, whole 16x16 sub-tiles");
   extern __shared__ __attribute__((aligned(16))) char smem_w16[];
-  char* const As = smem_w16;
+  char* As = smem_w16;  // the halo being read (DBUF: one of two, alternating per chunk)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -474,9 +471,11 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
   const int taps = a.taps, total = (a.C_in / EK) * taps;
   const int per = (total + ksplit - 1) / ksplit;
   const int it0 = zsplit * per, it1 = min(total, it0 + per);
+  const size_t hbytes = (size_t)nrows_a * RS;  // one halo image
   if (it0 < it1) {
     BFrag b0, b1;
     int ch = it0 / taps, tap = it0 - ch * taps;
+    if constexpr (DBUF) As = smem_w16 + (ch & 1) * hbytes;
     load_a_regs(ch * EK);
     write_a_regs();
     if ((ch + 1) * taps < it1) load_a_regs((ch + 1) * EK);
@@ -489,10 +488,18 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
       if (++tap == taps) {
         tap = 0;
         if (++ch * taps < it1) {
-          __syncthreads();
-          write_a_regs();
-          if ((ch + 1) * taps < it1) load_a_regs((ch + 1) * EK);
-          __syncthreads();
+          if constexpr (DBUF) {
+            // the idle buffer was last read in chunk ch - 2, before the barrier that ended chunk ch - 1
+            As = smem_w16 + (ch & 1) * hbytes;
+            write_a_regs();
+            if ((ch + 1) * taps < it1) load_a_regs((ch + 1) * EK);
+            __syncthreads();
+          } else {
+            __syncthreads();
+            write_a_regs();
+            if ((ch + 1) * taps < it1) load_a_regs((ch + 1) * EK);
+            __syncthreads();
+          }
         }
       }
     };
@@ -523,7 +530,14 @@ hipError_t launch_wsb16(const ConvArgs& a, int ntn_enable, int ksplit, hipStream
   const int nrows_a = BM + (a.taps - 1) * a.dil;
   const int mtiles = (a.T_out + BM - 1) / BM;
   const bool h16 = a.wsplit_fmt == WSPLIT_H16;
-  const size_t smem = (size_t)nrows_a * (h16 ? ERS_H : ERS);
+  // RVCX_WSB_DBUF=1: two halo buffers in the fp16 modes (one barrier per chunk). Off by default: -0.13 ms in the C2
+  // step without it (r04f, same box), the conv family's kernel time unchanged
+  static const bool dbuf_env = [] {
+    const char* e = std::getenv("RVCX_WSB_DBUF");
+    return e && std::atoi(e) == 1;
+  }();
+  const bool dbuf = h16 && dbuf_env && 3 * 2 * (size_t)nrows_a * ERS_H <= 160 * 1024;
+  const size_t smem = (size_t)nrows_a * (h16 ? ERS_H : ERS) * (dbuf ? 2 : 1);
   if (a.wsplit_npad % BN != 0 || ksplit < 1 || (ksplit > 1 && !a.ws)) return hipErrorInvalidValue;
   if (a.lowp && !h16) return hipErrorInvalidValue;  // the reduced-precision mode reads the fp16 image's hi plane
   if (h16 && !H16OK) return hipErrorInvalidValue;   // fp16 instantiations only for the tiles the policy picks
@@ -531,7 +545,8 @@ hipError_t launch_wsb16(const ConvArgs& a, int ntn_enable, int ksplit, hipStream
   const int ntn = ntn_enable ? ntiles : 0;
   dim3 grid(ntn ? mtiles * ntiles : mtiles, ntn ? 1 : ntiles, a.batch * ksplit);
   // the reduced-precision opt-in only without a pre-mask (the generator's convs)
-  const int mode = pre_mode(a.pre_act) | (a.pre_mask ? 4 : 0) | (h16 ? 16 : 0) | (h16 && a.lowp && !a.pre_mask ? 8 : 0);
+  const int mode = pre_mode(a.pre_act) | (a.pre_mask ? 4 : 0) | (h16 ? 16 : 0) | (h16 && a.lowp && !a.pre_mask ? 8 : 0) |
+                   (dbuf && !a.pre_mask ? 32 : 0);
   void (*kern)(const ConvArgs, const char*, int, int, int, int);
   switch (mode) {
 #define WSB16_CASE(M) \
@@ -539,16 +554,17 @@ hipError_t launch_wsb16(const ConvArgs& a, int ntn_enable, int ksplit, hipStream
     WSB16_CASE(0) WSB16_CASE(1) WSB16_CASE(2) WSB16_CASE(4) WSB16_CASE(5) WSB16_CASE(6)
     WSB16_CASE(16) WSB16_CASE(17) WSB16_CASE(18) WSB16_CASE(20) WSB16_CASE(21) WSB16_CASE(22)
     WSB16_CASE(24) WSB16_CASE(25) WSB16_CASE(26)
+    WSB16_CASE(48) WSB16_CASE(49) WSB16_CASE(50) WSB16_CASE(56) WSB16_CASE(57) WSB16_CASE(58)
 #undef WSB16_CASE
     default: return hipErrorInvalidValue;
   }
   // per instantiation: raise the dynamic-LDS limit once, not per launch
-  static size_t smem_set[32] = {};
-  if (smem > 64 * 1024 && smem > smem_set[mode & 31]) {
+  static size_t smem_set[64] = {};
+  if (smem > 64 * 1024 && smem > smem_set[mode & 63]) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
-    smem_set[mode & 31] = smem;
+    smem_set[mode & 63] = smem;
   }
   hipLaunchKernelGGL(kern, grid, dim3(CONV_THREADS), smem, s, a, static_cast<const char*>(a.wsplit), a.wsplit_npad,
                      nrows_a, ntn, ksplit);
@@ -615,9 +631,13 @@ hipError_t conv_wsplit_build(const ConvArgs& a, void* out, hipStream_t s) {
   const long long nb = std::min<long long>((total + 255) / 256, 1 << 20);
   if (a.wsplit_fmt == WSPLIT_H16) {
     float* tail = reinterpret_cast<float*>(static_cast<char*>(out) + (long long)nch * a.taps * Npad * WROW_H);
-    hipLaunchKernelGGL(k_wmax_scale, dim3(1), dim3(1024), 0, s, a.w, a.ldw, a.w_ts, a.N, a.C_in, a.taps, tail);
+    hipError_t e = hipMemsetAsync(tail, 0, 16, s);
+    if (e != hipSuccess) return e;
+    const long long nm = std::min<long long>(((long long)a.taps * a.N * a.C_in + 2047) / 2048, 1024);
+    hipLaunchKernelGGL(k_wmax_scale, dim3((unsigned)nm), dim3(256), 0, s, a.w, a.ldw, a.w_ts, a.N, a.C_in, a.taps,
+                       tail);
     hipLaunchKernelGGL(k_wsplit_h16, dim3((unsigned)nb), dim3(256), 0, s, a.w, a.ldw, a.w_ts, a.N, a.C_in, a.taps, nch,
-                       Npad, static_cast<unsigned short*>(out), static_cast<const float*>(tail));
+                       Npad, static_cast<unsigned short*>(out), tail);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_wsplit, dim3((unsigned)nb), dim3(256), 0, s, a.w, a.ldw, a.w_ts, a.N, a.C_in, a.taps, nch, Npad,

@@ -56,7 +56,6 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ g
   __shared__ __attribute__((aligned(16))) float h_pw[NT / 64][HALF];  // per-wave copy of its partner columns
   __shared__ float part[2][ROWS];
   __shared__ float bias_h[ROWS];
-  __shared__ float ig_ring[2][ROWS];
   __shared__ int abort_flag;
 
   // 16 blocks per sequence, 4 of them working: block w = 0 / 8 are direction 0's two halves, 1 / 9 direction 1's.
@@ -111,25 +110,19 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ g
     OUT = (a0_.x + a1_.x) + (a0_.y + a1_.y);                                         \
   } while (0)
 
-  // input gates gi (3 x 128 values of a step per workgroup) through a 2-slot LDS ring: threads 128 .. 511 (one value
-  // each; not the gate threads) write step s + 1's values into the ring right after step s's partner poll and issue
-  // the load of step s + 2's, so a load's latency runs under a whole step and never sits in front of a poll (a poll
-  // waits on every earlier load of its wave; loaded at the top of the step, an L2 / MALL miss delayed the poll;
-  // loaded into the gate threads' registers a step ahead, the kernel spilled)
-  const int pf = tid - UNITS;  // prefetch thread index in [0, 384): gate pf / 128, unit pf % 128
-  const bool pfr = pf >= 0 && pf < ROWS;
-  auto gi_at = [&](int s) {
+  // input gates of step s: issued at the top of the step, consumed after the hand-off (a prefetch one step
+  // ahead measured slower: its registers pushed the kernel into scratch)
+  auto load_ig = [&](int s, float& ir, float& iz, float& in) {
     const int t = d ? (T - 1 - s) : s;
-    return gi[t * (6 * H) + d * 3 * H + (pf / UNITS) * H + q * UNITS + pf % UNITS];  // 32-bit offsets (T*1536 < 2^31)
+    const int o = t * (6 * H) + d * 3 * H + gunit;  // 32-bit offset from the uniform base (T * 1536 < 2^31)
+    ir = gi[o];
+    iz = gi[o + H];
+    in = gi[o + 2 * H];
   };
-  float pv = 0.f;
-  if (pfr) {
-    ig_ring[0][pf] = gi_at(0);
-    if (T > 1) pv = gi_at(1);
-  }
-  __syncthreads();
+  float ig_r = 0.f, ig_z = 0.f, ig_n = 0.f;
   for (int s = 0; s < T; ++s) {
     const int t = d ? (T - 1 - s) : s;
+    if (tid < UNITS) load_ig(s, ig_r, ig_z, ig_n);
     // ---- phase A: own columns from h_own(s-1) right away, then each wave fetches the 64 partner values of
     // h(s-1) it needs (one granule per lane) and takes its partner columns. (One polling wave + a barrier
     // measured slower: 2.4 vs 1.9 us/step.)
@@ -158,10 +151,6 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ g
       } else {
         hp[lane] = 0.f;
       }
-      if (pfr && s + 1 < T) {
-        ig_ring[(s + 1) & 1][pf] = pv;  // step s + 1's values (loaded during step s - 1)
-        if (s + 2 < T) pv = gi_at(s + 2);
-      }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -180,10 +169,9 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ g
       const float hr = (part[0][tid] + part[1][tid]) + bias_h[tid];
       const float hz = (part[0][UNITS + tid] + part[1][UNITS + tid]) + bias_h[UNITS + tid];
       const float hn = (part[0][2 * UNITS + tid] + part[1][2 * UNITS + tid]) + bias_h[2 * UNITS + tid];
-      const float* igs = ig_ring[s & 1];
-      const float rr = sigm(hr + igs[tid]);
-      const float zz = sigm(hz + igs[UNITS + tid]);
-      const float nn = tanh_g(igs[2 * UNITS + tid] + hn * rr);
+      const float rr = sigm(hr + ig_r);
+      const float zz = sigm(hz + ig_z);
+      const float nn = tanh_g(ig_n + hn * rr);
       const float hprev = h_own[tid];
       const float hnew = (hprev - nn) * zz + nn;
       h_own[tid] = hnew;

@@ -15,6 +15,8 @@
 // runs) ~6e-8 of the peak, which is the TF form's own rounding (tests/test_gpu_models.py).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "rvcx_kernels.h"
 
 namespace rvcx {
@@ -193,6 +195,201 @@ __global__ void k_sos_fix(const double* __restrict__ y0, long long n, int L, con
     en[2 * c] = z0;
     en[2 * c + 1] = z1;
   }
+}
+
+// ---------------------------------------------------------------- the whole cascade as one linear system
+// The sections of one pass form one 2 nsec-state system (block lower-triangular, as stable as its sections), so a pass
+// is ONE local / carry / fix round instead of one per section, and filtfilt is six launches: the backward local pass
+// applies the forward pass's fix-up while it reads its input, and the last kernel applies the backward one while it
+// reflect-pads. Tables (SosPlan::casc): coef [nsec][5] at 0, w [NS] at 40, pow[s] = A^(L 2^s) [NS][NS] at 48 + 64 s
+// (s < 12), CA[k] = C A^k [NS] at 816 + 8 k (k < L); NS = 2 nsec <= 8.
+namespace {
+constexpr int CASC_W = 40, CASC_POW = 48, CASC_CA = 48 + 64 * 12;
+
+// value t of a pass's final output, from its zero-state output y0 and chunk start states S (NS per chunk)
+template <int NS>
+__device__ __forceinline__ double casc_fixed(const double* y0, const double* S, const double* ca, int L, long long t) {
+  const long long c = t / L;
+  const int k = (int)(t - c * L);
+  double v = y0[t];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) v = fma(ca[CASC_CA + 8 * k + i], S[NS * c + i], v);
+  return v;
+}
+
+// zero-state pass of the cascade over chunk c. Input: x (read reversed when rev), or -- when S_in is set -- the
+// previous pass's final output y0_in + C A^k S_in evaluated on the fly
+template <int NSEC>
+__global__ void k_casc_local(const double* __restrict__ x, const double* __restrict__ S_in, long long n, int rev,
+                             const double* __restrict__ tab, int L, double* __restrict__ y0, double* __restrict__ e) {
+  constexpr int NS = 2 * NSEC;
+  const long long c = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const long long nch = (n + L - 1) / L;
+  if (c >= nch) return;
+  double b0[NSEC], b1[NSEC], b2[NSEC], a1[NSEC], a2[NSEC], z0[NSEC], z1[NSEC];
+#pragma unroll
+  for (int j = 0; j < NSEC; ++j) {
+    b0[j] = tab[5 * j], b1[j] = tab[5 * j + 1], b2[j] = tab[5 * j + 2], a1[j] = tab[5 * j + 3], a2[j] = tab[5 * j + 4];
+    z0[j] = z1[j] = 0.0;
+  }
+  const long long t0 = c * L, t1 = min(n, t0 + L);
+  for (long long t = t0; t < t1; ++t) {
+    const long long ti = rev ? n - 1 - t : t;
+    double u = S_in ? casc_fixed<NS>(x, S_in, tab, L, ti) : x[ti];
+#pragma unroll
+    for (int j = 0; j < NSEC; ++j) {
+      const double y = b0[j] * u + z0[j];
+      z0[j] = b1[j] * u - a1[j] * y + z1[j];
+      z1[j] = b2[j] * u - a2[j] * y;
+      u = y;
+    }
+    y0[t] = u;
+  }
+#pragma unroll
+  for (int j = 0; j < NSEC; ++j) {
+    e[NS * c + 2 * j] = z0[j];
+    e[NS * c + 2 * j + 1] = z1[j];
+  }
+}
+
+// chunk start states S_0 = w x0, S_{c+1} = A^L S_c + e_c (k_sos_carry's segmented Hillis-Steele scan on NS-vectors).
+// x0 = the pass input's first sample: x[0] / x[n - 1] (rev), or the previous pass's output there (S_in set).
+template <int NS>
+__global__ void __launch_bounds__(SCAN_T) k_casc_carry(const double* __restrict__ e, long long nch,
+                                                       const double* __restrict__ tab, const double* __restrict__ x,
+                                                       const double* __restrict__ S_in, long long n, int L, int rev,
+                                                       double* __restrict__ S) {
+  __shared__ double v[NS][SCAN_T];
+  __shared__ double seg[NS];
+  const int t = threadIdx.x;
+  if (t == 0) {
+    const long long i0 = rev ? n - 1 : 0;
+    const double x0 = S_in ? casc_fixed<NS>(x, S_in, tab, L, i0) : x[i0];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      seg[i] = tab[CASC_W + i] * x0;
+      S[i] = seg[i];
+    }
+  }
+  __syncthreads();
+  for (long long c0 = 0; c0 + 1 < nch; c0 += SCAN_T) {
+    const long long c = c0 + t;  // this thread produces S_{c+1} from e_c
+    const bool act = c + 1 < nch;
+    double a[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) a[i] = act ? e[NS * c + i] : 0.0;
+    for (int sidx = 0; (1 << sidx) < SCAN_T; ++sidx) {
+#pragma unroll
+      for (int i = 0; i < NS; ++i) v[i][t] = a[i];
+      __syncthreads();
+      const int d = 1 << sidx;
+      if (t >= d) {
+        const double* M = tab + CASC_POW + 64 * sidx;
+        double u[NS];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) u[i] = v[i][t - d];
+#pragma unroll
+        for (int r = 0; r < NS; ++r) {
+          double acc = a[r];
+#pragma unroll
+          for (int q = 0; q < NS; ++q) acc = fma(M[8 * r + q], u[q], acc);
+          a[r] = acc;
+        }
+      }
+      __syncthreads();
+    }
+    // + A^{L (t+1)} S_seg
+    double sv[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) sv[i] = seg[i];
+    const int pw = t + 1;
+    for (int sidx = 0; (1 << sidx) <= pw; ++sidx) {
+      if (pw & (1 << sidx)) {
+        const double* M = tab + CASC_POW + 64 * sidx;
+        double r[NS];
+#pragma unroll
+        for (int rr = 0; rr < NS; ++rr) {
+          double acc = 0.0;
+#pragma unroll
+          for (int q = 0; q < NS; ++q) acc = fma(M[8 * rr + q], sv[q], acc);
+          r[rr] = acc;
+        }
+#pragma unroll
+        for (int i = 0; i < NS; ++i) sv[i] = r[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NS; ++i) a[i] += sv[i];
+    if (act) {
+#pragma unroll
+      for (int i = 0; i < NS; ++i) S[NS * (c + 1) + i] = a[i];
+    }
+    __syncthreads();
+    const long long last = min(nch - 2, c0 + SCAN_T - 1);  // the segment's last produced state
+    if (c == last) {
+#pragma unroll
+      for (int i = 0; i < NS; ++i) seg[i] = a[i];
+    }
+    __syncthreads();
+  }
+}
+
+// the backward pass's final output (its fix-up applied on the fly), un-reversed, trimmed of the odd extension and
+// reflect-padded by t_pad (k_filt_pad's indexing)
+template <int NS>
+__global__ void k_casc_final_pad(const double* __restrict__ y0b, const double* __restrict__ Sb,
+                                 const double* __restrict__ tab, int L, long long ne, int padlen, long long n,
+                                 long long t_pad, double* __restrict__ pad64, float* __restrict__ pad32) {
+  const long long m = n + 2 * t_pad;
+  for (long long k = blockIdx.x * (long long)blockDim.x + threadIdx.x; k < m; k += (long long)gridDim.x * blockDim.x) {
+    long long j = k - t_pad;
+    if (j < 0) j = -j;
+    if (j >= n) j = 2 * (n - 1) - j;
+    const double v = casc_fixed<NS>(y0b, Sb, tab, L, ne - 1 - (j + padlen));
+    if (pad64) pad64[k] = v;
+    pad32[k] = (float)v;
+  }
+}
+
+template <int NSEC>
+hipError_t casc_filtfilt(const SosPlan& p, const double* ext, long long ne, int padlen, long long n, long long t_pad,
+                         double* ws, double* pad64, float* pad32, hipStream_t s) {
+  constexpr int NS = 2 * NSEC;
+  const int L = p.casc_L;
+  const long long nch = (ne + L - 1) / L;
+  double* y0f = ws;
+  double* y0b = y0f + ne;
+  double* e = y0b + ne;
+  double* Sf = e + NS * nch;
+  double* Sb = Sf + NS * nch;
+  const unsigned g = (unsigned)((nch + 63) / 64);
+  hipLaunchKernelGGL(k_casc_local<NSEC>, dim3(g), dim3(64), 0, s, ext, nullptr, ne, 0, p.casc, L, y0f, e);
+  hipLaunchKernelGGL(k_casc_carry<NS>, dim3(1), dim3(SCAN_T), 0, s, e, nch, p.casc, ext, nullptr, ne, L, 0, Sf);
+  // backward over the reversed forward output (y0f fixed up with Sf on the fly)
+  hipLaunchKernelGGL(k_casc_local<NSEC>, dim3(g), dim3(64), 0, s, y0f, Sf, ne, 1, p.casc, L, y0b, e);
+  hipLaunchKernelGGL(k_casc_carry<NS>, dim3(1), dim3(SCAN_T), 0, s, e, nch, p.casc, y0f, Sf, ne, L, 1, Sb);
+  const long long m = n + 2 * t_pad;
+  const unsigned gb = (unsigned)std::min<long long>((m + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_casc_final_pad<NS>, dim3(gb), dim3(256), 0, s, y0b, Sb, p.casc, L, ne, padlen, n, t_pad, pad64,
+                     pad32);
+  return hipGetLastError();
+}
+}  // namespace
+
+hipError_t casc_filtfilt_pad(const SosPlan& p, const double* ext, long long ne, int padlen, long long n,
+                             long long t_pad, double* ws, double* pad64, float* pad32, hipStream_t s) {
+  switch (p.nsec) {
+    case 1: return casc_filtfilt<1>(p, ext, ne, padlen, n, t_pad, ws, pad64, pad32, s);
+    case 2: return casc_filtfilt<2>(p, ext, ne, padlen, n, t_pad, ws, pad64, pad32, s);
+    case 3: return casc_filtfilt<3>(p, ext, ne, padlen, n, t_pad, ws, pad64, pad32, s);
+    case 4: return casc_filtfilt<4>(p, ext, ne, padlen, n, t_pad, ws, pad64, pad32, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+size_t casc_ws_doubles(long long ne, int L) {
+  const long long nch = (ne + L - 1) / L;
+  return (size_t)(2 * ne + 3 * 8 * nch + 16);
 }
 
 size_t sos_ws_doubles(long long n_ext, int L) {

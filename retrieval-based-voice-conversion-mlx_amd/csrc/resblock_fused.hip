@@ -75,24 +75,18 @@ __global__ void k_rb_wsplit(const float* __restrict__ w, int C, int k, unsigned 
 // planes) holds {sc, 1 / (sc * RB_XS)}. Activations are split at RB_XS = 2^-4.
 constexpr float RB_XS = 1.f / 16.f;
 __global__ void k_rb_wmax(const float* __restrict__ w, long long n, float* __restrict__ tail) {
-  __shared__ float red[16];
   float m = 0.f;
-  for (long long i = threadIdx.x; i < n; i += blockDim.x) m = fmaxf(m, fabsf(w[i]));
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) m = fmaxf(m, red[i]);
-    int e = 0;
-    (void)frexpf(m, &e);
-    const float sc = m > 0.f ? ldexpf(1.f, 8 - e) : 1.f;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    m = fmaxf(m, fabsf(w[i]));
+  absmax_wave_publish(m, reinterpret_cast<unsigned*>(tail) + 2);
+}
+__global__ void k_rb_wsplit_h16(const float* __restrict__ w, int C, int k, int NP, unsigned short* __restrict__ out,
+                                float* __restrict__ tail) {
+  const float sc = h16_weight_scale(reinterpret_cast<const unsigned*>(tail)[2]);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     tail[0] = sc;
     tail[1] = 1.f / (sc * RB_XS);
   }
-}
-__global__ void k_rb_wsplit_h16(const float* __restrict__ w, int C, int k, int NP, unsigned short* __restrict__ out,
-                                const float* __restrict__ tail) {
-  const float sc = tail[0];
   const int NCH = C / 16;
   const long long total = (long long)k * NCH * C * 16;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
@@ -501,9 +495,13 @@ hipError_t rb_wsplit_build(const float* w, int C, int k, void* out, hipStream_t 
   const long long nb = std::min<long long>((total + 255) / 256, 1 << 20);
   if (wfmt == RB_WF16) {
     float* tail = reinterpret_cast<float*>(static_cast<char*>(out) + (long long)k * (C / 16) * 2 * C * 32);
-    hipLaunchKernelGGL(k_rb_wmax, dim3(1), dim3(1024), 0, s, w, (long long)k * C * C, tail);
+    hipError_t e = hipMemsetAsync(tail, 0, 16, s);
+    if (e != hipSuccess) return e;
+    const long long n = (long long)k * C * C;
+    hipLaunchKernelGGL(k_rb_wmax, dim3((unsigned)std::min<long long>((n + 2047) / 2048, 1024)), dim3(256), 0, s, w, n,
+                       tail);
     hipLaunchKernelGGL(k_rb_wsplit_h16, dim3((unsigned)nb), dim3(256), 0, s, w, C, k, 2,
-                       static_cast<unsigned short*>(out), static_cast<const float*>(tail));
+                       static_cast<unsigned short*>(out), tail);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_rb_wsplit, dim3((unsigned)nb), dim3(256), 0, s, w, C, k, static_cast<unsigned short*>(out));

@@ -36,6 +36,7 @@ void set_highpass_sos(Ctx& c, const double* sos, int nsec) {
   SosPlan p;
   p.nsec = nsec;
   p.L = 256;
+  if (nsec > 4) throw Error(RVCX_E_INVALID, "highpass: more than 4 sections");
   std::vector<double> tab((size_t)nsec * p.stride(), 0.0);
   double gain = 1.0;  // DC gain of the sections before j
   for (int j = 0; j < nsec; ++j) {
@@ -69,6 +70,60 @@ void set_highpass_sos(Ctx& c, const double* sos, int nsec) {
       M[0] = n0, M[1] = n1, M[2] = n2, M[3] = n3;
     }
   }
+  // the cascade as ONE system of NS = 2 nsec states (iir_scan.hip casc_filtfilt_pad): its A and C by stepping the
+  // cascade from unit states with zero input, the steady state w = the per-section states above, A^(L 2^s) and
+  // the rows C A^k of the chunk fix-up
+  const int NS = 2 * nsec, L = p.casc_L;
+  const size_t casc_off = tab.size();
+  tab.resize(casc_off + 48 + 64 * 12 + 8 * (size_t)L, 0.0);
+  double* ct = tab.data() + casc_off;
+  std::vector<double> A((size_t)NS * NS), C(NS);
+  auto step = [&](const double* z, double x, double* zo) {
+    double u = x;
+    for (int j = 0; j < nsec; ++j) {
+      const double* t = tab.data() + (size_t)j * p.stride();
+      const double y = t[0] * u + z[2 * j];
+      zo[2 * j] = t[1] * u - t[3] * y + z[2 * j + 1];
+      zo[2 * j + 1] = t[2] * u - t[4] * y;
+      u = y;
+    }
+    return u;
+  };
+  for (int i = 0; i < NS; ++i) {
+    std::vector<double> z(NS, 0.0), zo(NS, 0.0);
+    z[i] = 1.0;
+    C[i] = step(z.data(), 0.0, zo.data());
+    for (int r = 0; r < NS; ++r) A[(size_t)r * NS + i] = zo[r];
+  }
+  for (int j = 0; j < nsec; ++j) {
+    const double* t = tab.data() + (size_t)j * p.stride();
+    for (int q = 0; q < 5; ++q) ct[5 * j + q] = t[q];
+    ct[40 + 2 * j] = t[8];
+    ct[40 + 2 * j + 1] = t[9];
+  }
+  auto mul = [&](const std::vector<double>& X, const std::vector<double>& Y) {
+    std::vector<double> Z((size_t)NS * NS, 0.0);
+    for (int r = 0; r < NS; ++r)
+      for (int q = 0; q < NS; ++q)
+        for (int k = 0; k < NS; ++k) Z[(size_t)r * NS + q] += X[(size_t)r * NS + k] * Y[(size_t)k * NS + q];
+    return Z;
+  };
+  std::vector<double> M((size_t)NS * NS, 0.0);
+  for (int i = 0; i < NS; ++i) M[(size_t)i * NS + i] = 1.0;
+  std::vector<double> row(C);  // C A^k
+  for (int k = 0; k < L; ++k) {
+    for (int i = 0; i < NS; ++i) ct[48 + 64 * 12 + 8 * k + i] = row[i];
+    std::vector<double> nr(NS, 0.0);
+    for (int q = 0; q < NS; ++q)
+      for (int i = 0; i < NS; ++i) nr[q] += row[i] * A[(size_t)i * NS + q];
+    row = nr;
+    M = mul(A, M);  // A^(k + 1)
+  }
+  for (int sidx = 0; sidx < 12; ++sidx) {  // pow[s] = A^(L 2^s), NS x NS in an 8 x 8 block
+    for (int r = 0; r < NS; ++r)
+      for (int q = 0; q < NS; ++q) ct[48 + 64 * sidx + 8 * r + q] = M[(size_t)r * NS + q];
+    M = mul(M, M);
+  }
   RVCX_HIP(hipSetDevice(c.device));
   c.hp_sos_buf.~DevBuf();
   new (&c.hp_sos_buf) DevBuf();
@@ -80,6 +135,7 @@ void set_highpass_sos(Ctx& c, const double* sos, int nsec) {
   c.hp_sos_buf.bytes = bytes;
   RVCX_HIP(hipMemcpy(c.hp_sos_buf.p, tab.data(), bytes, hipMemcpyHostToDevice));
   p.dev = static_cast<const double*>(c.hp_sos_buf.p);
+  p.casc = p.dev + casc_off;
   c.hp_sos = p;
 }
 

@@ -314,6 +314,8 @@ hipError_t change_rms_f32src(const float* src, long long n_src, int sr_src, floa
 struct SosPlan {
   int nsec = 0, L = 256;
   const double* dev = nullptr;  // nsec x stride doubles: coef[0..4] @0, w[2] @8, pow[11][4] @16, CA[L][2] @64
+  const double* casc = nullptr;  // the cascade as one system (iir_scan.hip casc_filtfilt_pad), chunks of casc_L
+  int casc_L = 128;
   int stride() const { return 64 + 2 * L; }
   const double* coef(int j) const { return dev + (size_t)j * stride(); }
   const double* w(int j) const { return coef(j) + 8; }
@@ -321,6 +323,10 @@ struct SosPlan {
   const double* ca(int j) const { return coef(j) + 64; }
 };
 size_t sos_ws_doubles(long long n_ext, int L);
+// filtfilt over the odd-extended input ext [ne] as two passes of the whole cascade (p.casc), trimmed and reflect-padded
+hipError_t casc_filtfilt_pad(const SosPlan& p, const double* ext, long long ne, int padlen, long long n,
+                             long long t_pad, double* ws, double* pad64, float* pad32, hipStream_t s);
+size_t casc_ws_doubles(long long ne, int L);
 hipError_t sos_pass(const SosPlan& p, const double* x, long long n, int rev, double* out, double* ws, hipStream_t s);
 // filtfilt (odd padding 3*(order+1)) through the SOS plan + reflect pad t_pad (pipeline.py:439, :459)
 hipError_t filtfilt_sos_pad(const SosPlan& p, int order, const double* x, long long n, long long t_pad, double* ws,

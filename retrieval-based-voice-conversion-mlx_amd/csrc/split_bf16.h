@@ -72,6 +72,20 @@ __device__ __forceinline__ unsigned pk_f16(float x, float y) {
 __device__ __forceinline__ float f16lo_f(unsigned p) { return (float)__builtin_bit_cast(f16x2, p)[0]; }
 __device__ __forceinline__ float f16hi_f(unsigned p) { return (float)__builtin_bit_cast(f16x2, p)[1]; }
 
+// Per-tensor weight scale of the fp16 images: max |w| is gathered by every workgroup of the build grid into one word
+// (non-negative floats order as their bit patterns: atomicMax on the bits, one per wave), then the split kernel turns
+// it into the power of two sc with max |w| sc in [128, 256) (small weights stay normal fp16).
+__device__ __forceinline__ void absmax_wave_publish(float m, unsigned* dst) {
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(dst, __float_as_uint(m));
+}
+__device__ __forceinline__ float h16_weight_scale(unsigned mbits) {
+  const float m = __uint_as_float(mbits);
+  int e = 0;
+  (void)frexpf(m, &e);  // m = f 2^e, f in [0.5, 1)
+  return m > 0.f ? ldexpf(1.f, 8 - e) : 1.f;
+}
+
 // 4 consecutive channels of one LDS row as the two fp16 planes (NPL = 1: the hi plane alone, the reduced-precision mode)
 template <int NPL>
 __device__ __forceinline__ void put_h16x4(char* row, int c4, f32x4 v) {

@@ -486,7 +486,7 @@ class Engine:
         T = int(x.shape[0])
         T_out = (T + 2 * padding - dilation * (K - 1) - 1) // stride + 1
         y = torch.empty((T_out, N), dtype=torch.float32, device=self.device)
-        m = {"default": 0, "f32": 1, "split": 2, "wsb": 3, "gs": 4, "h16": 5, "f16": 6}[math]
+        m = {"default": 0, "f32": 1, "split": 2, "wsb": 3, "gs": 4, "h16": 5, "f16": 6, "gs_h16": 7}[math]
         self._check(self.lib.rvcx_conv1d(self.ctx, _ptr(x), T, C, _ptr(wk), _ptr(b), N, K, dilation, padding, stride,
                                          m, _ptr(y), T_out, self.stream()), "conv1d")
         return y

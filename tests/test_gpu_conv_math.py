@@ -52,7 +52,7 @@ def test_split_math_is_fp32_accurate(engine, T, C, N, K, dil, stride, spread):
     # "wsb": the same split arithmetic on the weight-streamed kernel (conv_wsb.hip), where the shape allows it
     wsb = stride == 1 and C % 32 == 0 and (K - 1) * dil <= 64
     gs = C % 32 == 0  # "gs": the gather-streamed kernel (conv_gs.hip: per-step A gather, split-K by the size policy)
-    for mode in ("f32", "split") + (("wsb", "h16", "f16") if wsb else ()) + (("gs",) if gs else ()):
+    for mode in ("f32", "split") + (("wsb", "h16", "f16") if wsb else ()) + (("gs", "gs_h16") if gs else ()):
         y = engine.conv1d(x, w, bias, dilation=dil, padding=pad, stride=stride, math=mode).cpu().numpy()
         assert y.shape == ref.shape
         errs[mode] = float(np.max(np.abs(y - ref) / (mag + np.abs(bias) + 1e-30)))
@@ -70,6 +70,7 @@ def test_split_math_is_fp32_accurate(engine, T, C, N, K, dil, stride, spread):
     print(f"\n{T}x{C}->{N} k{K}: " + " ".join(f"{k} {v:.2e}" for k, v in errs.items()))
     if gs:
         assert errs["gs"] < 1e-6, errs
+        assert errs["gs_h16"] < 1e-6 and errs["gs_h16"] <= 4.0 * errs["f32"] + 1e-8, errs
 
 
 def test_context_math_mode_switch(engine):

@@ -9,6 +9,7 @@
 #   prof              rocprofv3 --kernel-trace --stats of the C2 bench + timeline + kernel-family table
 #   pmc               the three HBM / MFMA PMC passes of one C2 step (tools/pmc_traffic.sh)
 #   bc                build/bench_conv table (checks + every tile)
+#   pmcconv=CASE,CFG  the PMC passes of bench_conv case CASE on tile cfg CFG (tools/pmc_conv.sh + pmc_conv.py)
 #   gru               build/bench_gru (BiGRU steps: full, hand-off only, math only)
 #   ab=E1;E2;...      same-box A/B of the C2 bench under env settings (',' for spaces inside one setting)
 #   ablib=LIB         same-box A/B of the C2 bench: LIB vs the in-tree librvcx.so
@@ -58,6 +59,10 @@ for step in "$@"; do
     bc)
       timeout -k 10 400 ./build/bench_conv 20 ${arg//,/ } > $O/bench_conv_$TAG.txt 2>&1 || { tail $O/bench_conv_$TAG.txt; exit 1; }
       cat $O/bench_conv_$TAG.txt ;;
+    pmcconv)
+      bash tools/pmc_conv.sh ${arg%%,*} ${arg##*,} || exit 1
+      python3 tools/pmc_conv.py pmc_c${arg%%,*}_g${arg##*,} > $O/pmcconv_${TAG}_${arg%%,*}_${arg##*,}.txt 2>&1
+      cat $O/pmcconv_${TAG}_${arg%%,*}_${arg##*,}.txt ;;
     gru)
       for m in 0 1 2 0 1 2; do
         r=$(RVCX_GRU_MODE=$m timeout -k 10 60 ./build/bench_gru 1568 1 10) || { echo "bench_gru mode $m failed"; exit 1; }
