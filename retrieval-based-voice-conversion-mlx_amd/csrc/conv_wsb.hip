@@ -108,6 +108,10 @@ __global__ void k_wsplit_h16(const float* __restrict__ w, int ldw, long long w_t
   }
 }
 
+#ifndef WSB_EXP  // measurement aid (build/exp bench_conv only): 1 no A halo loads, 2 no B loads
+#define WSB_EXP 0
+#endif
+
 #ifndef WSB_WAVES_128x64
 #define WSB_WAVES_128x64 3
 #endif
@@ -324,9 +328,7 @@ __global__ __launch_bounds__(CONV_THREADS, (BM == 128 && BN == 64 && !TWO_D) ? W
 // C layout of a 16x16 tile: lane l holds column l % 16, rows 4 (l / 16) + r, r = 0..3.
 // MODE: bits 0-1 the pre-activation (pre_fn), bit 2 a pre-mask row multiplier (conv_gs.hip's MODE), bit 4 the
 // two-plane fp16 arithmetic (split_bf16.h put_h16x4; weights from the k_wsplit_h16 image), bit 3 (with bit 4) the
-// opt-in reduced precision: the fp16 hi planes' product alone, bit 5 (with bit 4) two A halo buffers in LDS: the next
-// chunk's halo is written into the idle buffer, so a chunk switch is one barrier instead of write-between-two (the
-// fp16 rows are 144 B, so two halos of the generator's widest tap span, 178 rows, still fit three workgroups per CU)
+// opt-in reduced precision: the fp16 hi planes' product alone
 template <int BM, int BN, int WM, int WN, int MODE>
 __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 : 3) void conv_wsb16_kernel(const ConvArgs a, const char* __restrict__ wsp,
                                                                      const int Npad, const int nrows_a, const int ntn,
@@ -336,7 +338,6 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
   constexpr bool PMASK = (MODE & 4) != 0;
   constexpr bool H16 = (MODE & 16) != 0;
   constexpr bool LOWP = H16 && (MODE & 8) != 0;
-  constexpr bool DBUF = H16 && (MODE & 32) != 0;
   constexpr int NQ = LOWP ? 1 : (H16 ? 2 : 3);  // planes an MFMA step reads
   constexpr int NQI = H16 ? 2 : 3;               // planes of the weight image
   constexpr int RS = H16 ? ERS_H : ERS;          // LDS row stride
@@ -344,7 +345,7 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
   constexpr int TN16 = BN / (WN * 16);
   static_assert(WM * WN == 4 && TM16 >= 1 && TN16 >= 1, "4 waves, whole 16x16 sub-tiles");
   extern __shared__ __attribute__((aligned(16))) char smem_w16[];
-  char* As = smem_w16;  // the halo being read (DBUF: one of two, alternating per chunk)
+  char* const As = smem_w16;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -393,7 +394,11 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
       const long long g = row0 + r;
       const bool ok = r < nrows_a && g >= 0 && g < a.T_in;
       const long long gc = ok ? g : 0;
+#if WSB_EXP & 1
+      apre[v] = f32x4{1.f, 2.f, 3.f, (float)(c0 + v)};
+#else
       apre[v] = *reinterpret_cast<const f32x4*>(src0 + gc * a.ldx);
+#endif
       if constexpr (PMASK) apm[v] = PM[gc];
       aok |= ok ? (1u << v) : 0u;
     }
@@ -430,7 +435,14 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
 #pragma unroll
     for (int tn = 0; tn < TN16; ++tn)
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) dst[tn][q] = *reinterpret_cast<const bf16x8*>(bp[tn] + o + q * WBLK);
+      for (int q = 0; q < NQ; ++q) {
+#if WSB_EXP & 2
+        const int u = it + tn + q;
+        dst[tn][q] = __builtin_bit_cast(bf16x8, (int4){u, u + 1, u + 2, u + 3});
+#else
+        dst[tn][q] = *reinterpret_cast<const bf16x8*>(bp[tn] + o + q * WBLK);
+#endif
+      }
   };
   auto compute = [&](int tap, const BFrag& bf) __attribute__((always_inline)) {
     const int toff = tap * a.dil * RS;
@@ -471,11 +483,9 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
   const int taps = a.taps, total = (a.C_in / EK) * taps;
   const int per = (total + ksplit - 1) / ksplit;
   const int it0 = zsplit * per, it1 = min(total, it0 + per);
-  const size_t hbytes = (size_t)nrows_a * RS;  // one halo image
   if (it0 < it1) {
     BFrag b0, b1;
     int ch = it0 / taps, tap = it0 - ch * taps;
-    if constexpr (DBUF) As = smem_w16 + (ch & 1) * hbytes;
     load_a_regs(ch * EK);
     write_a_regs();
     if ((ch + 1) * taps < it1) load_a_regs((ch + 1) * EK);
@@ -488,18 +498,10 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
       if (++tap == taps) {
         tap = 0;
         if (++ch * taps < it1) {
-          if constexpr (DBUF) {
-            // the idle buffer was last read in chunk ch - 2, before the barrier that ended chunk ch - 1
-            As = smem_w16 + (ch & 1) * hbytes;
-            write_a_regs();
-            if ((ch + 1) * taps < it1) load_a_regs((ch + 1) * EK);
-            __syncthreads();
-          } else {
-            __syncthreads();
-            write_a_regs();
-            if ((ch + 1) * taps < it1) load_a_regs((ch + 1) * EK);
-            __syncthreads();
-          }
+          __syncthreads();
+          write_a_regs();
+          if ((ch + 1) * taps < it1) load_a_regs((ch + 1) * EK);
+          __syncthreads();
         }
       }
     };
@@ -530,14 +532,7 @@ hipError_t launch_wsb16(const ConvArgs& a, int ntn_enable, int ksplit, hipStream
   const int nrows_a = BM + (a.taps - 1) * a.dil;
   const int mtiles = (a.T_out + BM - 1) / BM;
   const bool h16 = a.wsplit_fmt == WSPLIT_H16;
-  // RVCX_WSB_DBUF=1: two halo buffers in the fp16 modes (one barrier per chunk). Off by default: -0.13 ms in the C2
-  // step without it (r04f, same box), the conv family's kernel time unchanged
-  static const bool dbuf_env = [] {
-    const char* e = std::getenv("RVCX_WSB_DBUF");
-    return e && std::atoi(e) == 1;
-  }();
-  const bool dbuf = h16 && dbuf_env && 3 * 2 * (size_t)nrows_a * ERS_H <= 160 * 1024;
-  const size_t smem = (size_t)nrows_a * (h16 ? ERS_H : ERS) * (dbuf ? 2 : 1);
+  const size_t smem = (size_t)nrows_a * (h16 ? ERS_H : ERS);
   if (a.wsplit_npad % BN != 0 || ksplit < 1 || (ksplit > 1 && !a.ws)) return hipErrorInvalidValue;
   if (a.lowp && !h16) return hipErrorInvalidValue;  // the reduced-precision mode reads the fp16 image's hi plane
   if (h16 && !H16OK) return hipErrorInvalidValue;   // fp16 instantiations only for the tiles the policy picks
@@ -545,8 +540,7 @@ hipError_t launch_wsb16(const ConvArgs& a, int ntn_enable, int ksplit, hipStream
   const int ntn = ntn_enable ? ntiles : 0;
   dim3 grid(ntn ? mtiles * ntiles : mtiles, ntn ? 1 : ntiles, a.batch * ksplit);
   // the reduced-precision opt-in only without a pre-mask (the generator's convs)
-  const int mode = pre_mode(a.pre_act) | (a.pre_mask ? 4 : 0) | (h16 ? 16 : 0) | (h16 && a.lowp && !a.pre_mask ? 8 : 0) |
-                   (dbuf && !a.pre_mask ? 32 : 0);
+  const int mode = pre_mode(a.pre_act) | (a.pre_mask ? 4 : 0) | (h16 ? 16 : 0) | (h16 && a.lowp && !a.pre_mask ? 8 : 0);
   void (*kern)(const ConvArgs, const char*, int, int, int, int);
   switch (mode) {
 #define WSB16_CASE(M) \
@@ -554,17 +548,16 @@ hipError_t launch_wsb16(const ConvArgs& a, int ntn_enable, int ksplit, hipStream
     WSB16_CASE(0) WSB16_CASE(1) WSB16_CASE(2) WSB16_CASE(4) WSB16_CASE(5) WSB16_CASE(6)
     WSB16_CASE(16) WSB16_CASE(17) WSB16_CASE(18) WSB16_CASE(20) WSB16_CASE(21) WSB16_CASE(22)
     WSB16_CASE(24) WSB16_CASE(25) WSB16_CASE(26)
-    WSB16_CASE(48) WSB16_CASE(49) WSB16_CASE(50) WSB16_CASE(56) WSB16_CASE(57) WSB16_CASE(58)
 #undef WSB16_CASE
     default: return hipErrorInvalidValue;
   }
   // per instantiation: raise the dynamic-LDS limit once, not per launch
-  static size_t smem_set[64] = {};
-  if (smem > 64 * 1024 && smem > smem_set[mode & 63]) {
+  static size_t smem_set[32] = {};
+  if (smem > 64 * 1024 && smem > smem_set[mode & 31]) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
-    smem_set[mode & 63] = smem;
+    smem_set[mode & 31] = smem;
   }
   hipLaunchKernelGGL(kern, grid, dim3(CONV_THREADS), smem, s, a, static_cast<const char*>(a.wsplit), a.wsplit_npad,
                      nrows_a, ntn, ksplit);
@@ -666,16 +659,20 @@ hipError_t conv_wsb_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream
   // the fp16 image only on the 16x16x32 kernel (1-D)
   if (a.wsplit_fmt == WSPLIT_H16 && (two_d || cfg < 23)) return hipErrorInvalidValue;
   if (two_d) return cfg == 21 ? launch_wsb<128, 64, 2, 2, true>(a, ntn_enable, ksplit, s) : hipErrorInvalidValue;
+  if (a.wsplit_fmt == WSPLIT_H16 && (cfg == 23 || cfg == 27)) {
+    hipError_t e = conv_wsc_launch(a, cfg, ntn_enable, ksplit, s);
+    if (e != hipErrorInvalidValue) return e;
+  }
   switch (cfg) {
     case 20: return launch_wsb<256, 32, 4, 1, false>(a, ntn_enable, ksplit, s);
     case 21: return launch_wsb<128, 64, 2, 2, false>(a, ntn_enable, ksplit, s);
     case 22: return launch_wsb<128, 128, 2, 2, false>(a, ntn_enable, ksplit, s);
     case 23: return launch_wsb16<128, 64, 2, 2, true>(a, ntn_enable, ksplit, s);
     case 24: return launch_wsb16<256, 32, 4, 1, true>(a, ntn_enable, ksplit, s);
-    case 25: return launch_wsb16<128, 128, 2, 2>(a, ntn_enable, ksplit, s);
+    case 25: return launch_wsb16<128, 128, 2, 2, true>(a, ntn_enable, ksplit, s);
     case 26: return launch_wsb16<256, 64, 4, 1>(a, ntn_enable, ksplit, s);
     case 27: return launch_wsb16<128, 64, 1, 4, true>(a, ntn_enable, ksplit, s);
-    case 28: return launch_wsb16<256, 64, 2, 2>(a, ntn_enable, ksplit, s);
+    case 28: return launch_wsb16<256, 64, 2, 2, true>(a, ntn_enable, ksplit, s);
     default: return hipErrorInvalidValue;
   }
 }
