@@ -57,7 +57,7 @@ int main(int argc, char** argv) {
   const int only_cfg = argc > 3 ? atoi(argv[3]) : -2;
   if (only_case < 0) {
   // correctness on a small shape for every forced config x pipe
-  // shape 0: every config; the others (ragged T, odd chunk counts, k = 5 / 11): the fp16 image on cfg 23 (conv_wsc.hip)
+  // shape 0: every config; the others (ragged T, odd chunk counts, k = 5 / 11): the fp16 image on cfg 23
   struct Shape { int T, C, N, taps, dil; };
   const Shape shapes[] = {{1000, 128, 128, 7, 3}, {777, 96, 64, 11, 5}, {777, 96, 64, 5, 1}, {500, 64, 192, 11, 1},
                           {300, 32, 64, 7, 5}};

@@ -659,10 +659,6 @@ hipError_t conv_wsb_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream
   // the fp16 image only on the 16x16x32 kernel (1-D)
   if (a.wsplit_fmt == WSPLIT_H16 && (two_d || cfg < 23)) return hipErrorInvalidValue;
   if (two_d) return cfg == 21 ? launch_wsb<128, 64, 2, 2, true>(a, ntn_enable, ksplit, s) : hipErrorInvalidValue;
-  if (a.wsplit_fmt == WSPLIT_H16 && (cfg == 23 || cfg == 27)) {
-    hipError_t e = conv_wsc_launch(a, cfg, ntn_enable, ksplit, s);
-    if (e != hipErrorInvalidValue) return e;
-  }
   switch (cfg) {
     case 20: return launch_wsb<256, 32, 4, 1, false>(a, ntn_enable, ksplit, s);
     case 21: return launch_wsb<128, 64, 2, 2, false>(a, ntn_enable, ksplit, s);

@@ -166,9 +166,6 @@ hipError_t conv_gs_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream_
 int conv_wsplit_npad(int N);
 long long conv_wsplit_bytes(const ConvArgs& a);
 hipError_t conv_wsplit_build(const ConvArgs& a, void* out, hipStream_t s);
-// conv_wsc.hip: the weight-streamed fp16-split kernel with a static load schedule (taps 3 / 7 / 11, one split-K slice);
-// hipErrorInvalidValue when the conv is not one it takes
-hipError_t conv_wsc_launch(const ConvArgs& a, int cfg, int ntn_enable, int ksplit, hipStream_t s);
 hipError_t conv_wsb_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream_t s, bool two_d = false,
                            int ksplit = 1);
 // fused ResBlock dilation pair (resblock_fused.hip): y (acc_mode) <- conv2(lrelu(conv1_d(lrelu(x)) + b1)) + b2 + x,
