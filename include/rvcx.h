@@ -345,6 +345,14 @@ int rvcx_set_conv_math(rvcx_ctx* ctx, int mode);
 int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const float* d_w, const float* d_bias, int N,
                 int taps, int dilation, int pad, int stride, int math, float* d_y, int64_t T_out, void* stream);
 
+/* One 3x3 / pad-1 Conv2d forward, NHWC: d_x [H][W][C_in], d_w [9][N][C_in] (torch weight [N][C_in][3][3] permuted to
+ * (kh * 3 + kw, N, C_in)), d_bias [N] (optional), d_y [H][W][N]; act 0 none, 1 ReLU. The RMVPE U-Net's conv
+ * (RMVPE.py:13-57 ConvBlockRes, torch.nn.Conv2d(kernel 3, padding 1)), exposed for the numerics tests of its
+ * few-channel kernels (C_in, N in {16, 32}: csrc/conv2d_small.hip): math 0 = the context's arithmetic (the two-plane
+ * fp16 split by default), 1 = exact fp32 (v_mfma_f32_16x16x4_f32). Other shapes take the general 2-D path. */
+int rvcx_conv2d3x3(rvcx_ctx* ctx, const float* d_x, int H, int W, int C_in, const float* d_w, const float* d_bias,
+                   int N, int act, int math, float* d_y, void* stream);
+
 /* One ResBlock dilation pair as one fused kernel (csrc/resblock_fused.hip), time-major: d_x, d_y [B][T][C] (distinct
  * buffers), d_w1 / d_w2 [k][C][C] (torch weight [C][C][k] permuted), d_b1 / d_b2 [C]:
  *     out = conv2(lrelu(conv1_d(lrelu(x), 0.1) + b1, 0.1)) + b2 + x     (zero padding; conv2 dilation 1)

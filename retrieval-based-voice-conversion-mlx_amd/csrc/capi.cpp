@@ -199,6 +199,11 @@ void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double
           : (a.force_cfg >= 30 ? 2
              : (a.force_cfg >= 20 && !two_d) ? 1 : (a.force_cfg < 0 ? conv_wsb_route(a, two_d) : 0));
   const long long need = conv_plan_splitk(a, two_d);
+  // the few-channel 3x3 convs' fp16-split form reads a pre-split image (conv2d_small.hip)
+  if (two_d && !a.wsb && stat && !a.wsplit && conv_math_of(a) == 3 && conv2d_small_fits(a)) {
+    a.wsplit_fmt = WSPLIT_S2D;
+    a.wsplit = c.wsplit_for(a, s);
+  }
   if (a.wsb) {
     // the weight-streamed kernel's fp16 image: the two-plane fp16 arithmetic (math 3) or the reduced-precision mode
     if (!a.wsplit)
@@ -235,7 +240,8 @@ void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double
   // the launch's arithmetic ceiling (the rest of the family is priced at the bf16 split's, a lower bound for the few
   // launches on the fp32-input MFMA)
   const double peak = (a.wsb && a.wsplit_fmt == WSPLIT_H16) ? ((a.lowp && a.wsb == 1) ? Ctx::PEAK_F16 : Ctx::PEAK_F16X2)
-                                                            : Ctx::PEAK_SPLIT;
+                      : (a.wsplit && a.wsplit_fmt == WSPLIT_S2D) ? Ctx::PEAK_F16X2
+                                                                  : Ctx::PEAK_SPLIT;
   Ctx::ProfRec r{get_ev(), get_ev(), flops, two_d ? 1 : 0, two_d ? a.T_out * a.W_out : a.T_out, a.N, a.C_in,
                  a.taps, a.batch * a.batch_inner, a.ksplit, alg_bytes, peak};
   RVCX_HIP(hipEventRecord(r.a, s));
@@ -636,6 +642,32 @@ int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const floa
       a.wsplit = img;
     }
     launch_conv(*ctx, a, false, static_cast<hipStream_t>(stream), -1.0);
+  });
+}
+
+int rvcx_conv2d3x3(rvcx_ctx* ctx, const float* d_x, int H, int W, int C_in, const float* d_w, const float* d_bias,
+                   int N, int act, int math, float* d_y, void* stream) {
+  return guard(ctx, [&] {
+    set_device(ctx);
+    ctx->check_device_status();
+    if (!d_x || !d_w || !d_y || H <= 0 || W <= 0 || C_in <= 0 || N <= 0 || act < 0 || act > 1 || math < 0 || math > 1)
+      throw Error(RVCX_E_INVALID, "rvcx_conv2d3x3: bad argument");
+    if ((int64_t)H * W * (C_in > N ? C_in : N) > INT32_MAX) throw Error(RVCX_E_SHAPE, "rvcx_conv2d3x3: size out of range");
+    ConvArgs a;
+    a.x = d_x; a.ldx = C_in; a.T_in = H; a.W_in = W; a.C_in = C_in;
+    a.w = d_w; a.ldw = C_in; a.w_ts = (long long)N * C_in; a.taps = 9; a.KH = 3; a.KW = 3; a.padh = 1; a.padw = 1;
+    a.y = d_y; a.ldy = N; a.T_out = H; a.W_out = W; a.N = N; a.bias = d_bias;
+    a.act = act ? ACT_RELU : ACT_NONE;
+    a.math = math == 1 ? 1 : 0;
+    if (a.math == 0 && ctx->conv_math > 0) a.math = ctx->conv_math;
+    if (conv_math_of(a) == 3 && conv2d_small_fits(a)) {
+      // a fresh image every call, never the address-keyed cache (the caller may reuse d_w with new weights)
+      a.wsplit_fmt = WSPLIT_S2D;
+      void* img = ctx->buf<char>("conv.test.s2d", (size_t)small2d_wsplit_bytes(a), static_cast<hipStream_t>(stream));
+      check(small2d_wsplit_build(a, img, static_cast<hipStream_t>(stream)), "small2d_wsplit_build");
+      a.wsplit = img;
+    }
+    launch_conv(*ctx, a, true, static_cast<hipStream_t>(stream), -1.0);
   });
 }
 

@@ -613,11 +613,13 @@ int conv_wsplit_npad(int N) { return (N + 127) / 128 * 128; }
 
 // chunks of 32 input channels, the last one zero-padded; the fp16 image carries a 256-B tail (its scales)
 long long conv_wsplit_bytes(const ConvArgs& a) {
+  if (a.wsplit_fmt == WSPLIT_S2D) return small2d_wsplit_bytes(a);
   const long long steps = (long long)((a.C_in + EK - 1) / EK) * a.taps * conv_wsplit_npad(a.N);
   return a.wsplit_fmt == WSPLIT_H16 ? steps * WROW_H + 256 : steps * WROW;
 }
 
 hipError_t conv_wsplit_build(const ConvArgs& a, void* out, hipStream_t s) {
+  if (a.wsplit_fmt == WSPLIT_S2D) return small2d_wsplit_build(a, out, s);
   const int nch = (a.C_in + EK - 1) / EK, Npad = conv_wsplit_npad(a.N);
   if (nch < 1 || a.taps < 1 || a.N < 1) return hipErrorInvalidValue;
   const long long total = (long long)nch * a.taps * Npad * EK;

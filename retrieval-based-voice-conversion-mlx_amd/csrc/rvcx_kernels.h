@@ -38,7 +38,8 @@ enum OutMap : int {
 };
 
 // Implicit-GEMM convolution:  y[b][m][n] = epi( sum_tap sum_c pre(X[b][row(m,tap)][c]) * W[tap][n][c] )
-enum WsplitFmt : int { WSPLIT_BF16 = 0, WSPLIT_H16 = 1 };
+// WSPLIT_S2D: the few-channel 3x3 convs' fp16 image (conv2d_small.hip k_s2d_wsplit: fragment-major, no column padding)
+enum WsplitFmt : int { WSPLIT_BF16 = 0, WSPLIT_H16 = 1, WSPLIT_S2D = 2 };
 
 struct ConvArgs {
   // A operand (activations)
@@ -125,6 +126,9 @@ hipError_t conv2d(const ConvArgs& a, hipStream_t s);
 // the shapes conv2d_small_fits accepts there (RVCX_NO_SMALL2D=1 disables)
 bool conv2d_small_fits(const ConvArgs& a);
 hipError_t conv2d_small(const ConvArgs& a, hipStream_t s);
+// their WSPLIT_S2D image (the fp16-split form reads it; built by conv_wsplit_build for that format)
+long long small2d_wsplit_bytes(const ConvArgs& a);
+hipError_t small2d_wsplit_build(const ConvArgs& a, void* out, hipStream_t s);
 // choose split-K for small output grids; returns the workspace floats needed (0 = no split)
 long long conv_plan_splitk(ConvArgs& a, bool two_d);
 

@@ -491,6 +491,23 @@ class Engine:
                                          m, _ptr(y), T_out, self.stream()), "conv1d")
         return y
 
+    def conv2d3x3(self, x, w, bias=None, relu: bool = False, math: str = "default"):
+        """torch.nn.functional.conv2d(x.permute(2, 0, 1)[None], w, bias, padding=1)[0].permute(1, 2, 0) on the device
+        kernel: x [H][W][C_in] (NHWC), w [N][C_in][3][3] (torch layout) -> [H][W][N] fp32 (rvcx_conv2d3x3); math
+        "default" = the context's arithmetic, "f32" = exact fp32."""
+        torch = self.torch
+        x = self._dev(x, torch.float32)
+        w = torch.as_tensor(w, dtype=torch.float32)
+        N, C = int(w.shape[0]), int(w.shape[1])
+        wk = self._dev(w.permute(2, 3, 0, 1).reshape(9, N, C).contiguous(), torch.float32)
+        b = self._dev(bias, torch.float32) if bias is not None else None
+        H, W = int(x.shape[0]), int(x.shape[1])
+        y = torch.empty((H, W, N), dtype=torch.float32, device=self.device)
+        m = {"default": 0, "f32": 1}[math]
+        self._check(self.lib.rvcx_conv2d3x3(self.ctx, _ptr(x), H, W, C, _ptr(wk), _ptr(b), N, 1 if relu else 0, m,
+                                            _ptr(y), self.stream()), "conv2d3x3")
+        return y
+
     def resblock_pair(self, x, w1, b1, w2, b2, dilation: int, acc=None, acc_mode: int = 0, acc_div: float = 1.0,
                       cfg: int = 0):
         """One ResBlock dilation pair on the fused kernel (rvcx_resblock_pair): x [B][T][C] time-major, w1/w2

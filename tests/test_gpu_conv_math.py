@@ -86,3 +86,39 @@ def test_context_math_mode_switch(engine):
         engine.set_conv_math("default")
     assert np.array_equal(a, c)  # the context mode reaches the kernel
     assert not np.array_equal(a, b) and np.allclose(a, b, rtol=1e-5, atol=1e-4)
+
+
+SMALL2D = [  # H, W, C_in, N, spread: the RMVPE U-Net's few-channel 3x3 convs (csrc/conv2d_small.hip)
+    (64, 128, 16, 16, 0),   # level 0
+    (48, 128, 16, 32, 0),   # level 0 -> 1 channels
+    (40, 64, 32, 32, 0),    # level 1
+    (40, 64, 32, 16, 0),    # decoder 32 -> 16
+    (33, 128, 16, 3, 0),    # the 16 -> 3 output conv, ragged rows
+    (36, 64, 32, 32, 10),   # operands spread over 2^+-10
+]
+
+
+@pytest.mark.parametrize("H,W,C,N,spread", SMALL2D)
+def test_unet_small_2d_convs_are_fp32_accurate(engine, H, W, C, N, spread):
+    """The default arithmetic (two-plane fp16 split, k_conv2d_h16) and the exact-f32 form against fp64: both within
+    1e-6 of sum |x w|, the split at most 4x the f32 form's error."""
+    rng = np.random.Generator(np.random.PCG64(H * 131 + C + N))
+    x = rng.standard_normal((H, W, C)).astype(np.float32)
+    w = (rng.standard_normal((N, C, 3, 3)) / np.sqrt(9 * C)).astype(np.float32)
+    if spread:
+        x *= np.exp2(rng.integers(-spread, spread + 1, size=x.shape)).astype(np.float32)
+    bias = rng.standard_normal(N).astype(np.float32)
+    xd = torch.from_numpy(x.astype(np.float64)).permute(2, 0, 1)[None]
+    wd = torch.from_numpy(w.astype(np.float64))
+    ref = torch.relu(torch.nn.functional.conv2d(xd, wd, torch.from_numpy(bias.astype(np.float64)), padding=1))
+    mag = torch.nn.functional.conv2d(xd.abs(), wd.abs(), None, padding=1) + np.abs(bias)[None, :, None, None]
+    ref = ref[0].permute(1, 2, 0).numpy()
+    mag = mag[0].permute(1, 2, 0).numpy() + 1e-30
+    errs = {}
+    for mode in ("f32", "default"):
+        y = engine.conv2d3x3(x, w, bias, relu=True, math=mode).cpu().numpy()
+        assert y.shape == ref.shape
+        errs[mode] = float(np.max(np.abs(y - ref) / mag))
+    print(f"\n2-D {H}x{W} {C}->{N}: " + " ".join(f"{k} {v:.2e}" for k, v in errs.items()))
+    assert errs["f32"] < 1e-6, errs
+    assert errs["default"] < 1e-6 and errs["default"] <= 4.0 * errs["f32"] + 1e-8, errs
