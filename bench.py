@@ -36,7 +36,7 @@ BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense BF16 / FP16 MFMA (no spa
 SPLIT_PEAK_TFLOPS = round(BF16_PEAK_TFLOPS / 6.0, 1)
 H16_PEAK_TFLOPS = round(BF16_PEAK_TFLOPS / 3.0, 1)
 CONV_KERNEL = ("conv_wsb16_kernel / conv_gs16_kernel / conv_gsw16_kernel / k_rb_pair / conv_emu_kernel / conv_gemm_kernel / "
-               "conv_tiny_kernel / k_conv2d_small "
+               "conv_tiny_kernel / conv_tiny_rows_kernel / k_conv2d_small / k_conv2d_h16 "
                "(+ splitk_reduce): every conv, linear and matmul launch of the step, Σ algorithmic fp32 FLOPs / Σ "
                "HIP-event kernel time")
 SR_IN = 16000

@@ -6,7 +6,7 @@ WRITE_SIZE is taken as is. The bench runs warm-up + 1 timed step + 1 event pass 
 carries the events), so each kernel of the step appears `steps` times; per-launch numbers are averages.
 usage: python tools/pmc_traffic.py gpurun_out [kernel-substring,...] > profiles/pmc_traffic.json
 Default family: the conv dispatches bench.py's roofline counts (conv_emu / conv_wsb / k_rb_pair / conv_gemm /
-conv_tiny / conv2d_small);
+conv_tiny / conv_tiny_rows / k_conv2d_small / k_conv2d_h16);
 the split-K reduce kernels' bytes are added to the family's total, launches count the conv kernels only.
 The record carries the source-tree hash (rvcx.provenance) so bench.py can tell whether it applies.
 """
@@ -35,7 +35,7 @@ def main():
     d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
     keys = (sys.argv[2] if len(sys.argv) > 2 else
             "conv_emu_kernel,conv_wsb_kernel,conv_wsb16_kernel,conv_gs16_kernel,conv_gsw16_kernel,k_rb_pair,conv_gemm_kernel,"
-            "conv_tiny_kernel,k_conv2d_small").split(",")
+            "conv_tiny,k_conv2d_").split(",")
     key = ",".join(keys)
     fam = lambda k: any(s in k for s in keys)  # noqa: E731
     bytes_fam = lambda k: fam(k) or "splitk_reduce" in k  # noqa: E731
@@ -58,7 +58,8 @@ def main():
     if dump:
         lines = [r for r in open(dump[0]) if r.strip()]
         calls = max(1, round(n / max(1, len(lines))))
-        alg = sum(float(r.split(",")[-1]) for r in lines)
+        # columns: 2d, M, N, C_in, taps, batch, ksplit, ms, flops, algorithmic bytes, the launch's MFMA ceiling (TF)
+        alg = sum(float(r.split(",")[9]) for r in lines)
         rec["step_hbm_bytes"] = (2.0 * tot_f + tot_w) * 1024 / calls
         rec["step_alg_bytes"] = alg
         rec["step_ratio"] = rec["step_hbm_bytes"] / alg if alg > 0 else None
