@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cmath>
+#include <string>
 
 #include "split_bf16.h"
 
@@ -294,6 +295,279 @@ __global__ __launch_bounds__(64) void k_flash_attn(const float* __restrict__ qkv
   (void)nsplit;
 }
 
+// ---- The same attention in the two-plane fp16 split (split_bf16.h put_h16x4; the default since round 4): three
+// v_mfma_f32_32x32x16_f16 products per step into two accumulators (h h' and l h' + h l', combined as acc + 2^-11 acc2)
+// instead of six bf16 products, and K / V from fragment-major images built once per call by k_kv_split16 (every
+// query-block wave of the bf16 kernel re-split the same K and V blocks: ~30 VALU per 8 values per wave). q, k, v and
+// the relative tables are scaled by 2^-4 before the split (inputs up to 2^20 stay finite fp16; the softmax
+// probabilities need none) and the scales are multiplied back exactly: S by 2^8, O by 2^4.
+// Image of one (batch x head, 32-key block): K: [NS][plane][64 lanes][8 fp16] (lane (li, hk): key li, dims
+// 16 s + 8 hk ..), then V: [NT][2][plane][64 lanes][8 fp16] (lane (li, hk): dim 32 t + li, keys crow(8 s2 + e, hk)).
+constexpr float FA_XS = 1.f / 16.f;
+
+__device__ __forceinline__ void split8h(const float (&v)[8], f16x8 (&out)[2]) {
+  unsigned h[4], l[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    h[p] = pk_f16(v[2 * p], v[2 * p + 1]);
+    l[p] = pk_f16((v[2 * p] - f16lo_f(h[p])) * H16_LO, (v[2 * p + 1] - f16hi_f(h[p])) * H16_LO);
+  }
+  out[0] = __builtin_bit_cast(f16x8, make_uint4(h[0], h[1], h[2], h[3]));
+  out[1] = __builtin_bit_cast(f16x8, make_uint4(l[0], l[1], l[2], l[3]));
+}
+
+__device__ __forceinline__ void mfma3(const f16x8 (&a)[2], const f16x8 (&b)[2], f32x16& c, f32x16& c2) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[0], c, 0, 0, 0);
+  c2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[1], b[0], c2, 0, 0, 0);
+  c2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[0], b[1], c2, 0, 0, 0);
+}
+
+// one wave per (key block, batch x head, fragment): blockIdx.z < NS a K step, else a V^T (t, s2) pair
+template <int DK>
+__global__ __launch_bounds__(64) void k_kv_split16(const float* __restrict__ qkv, int ldq, int T, int nh, int H,
+                                                   uint4* __restrict__ img) {
+  constexpr int NS = DK / 16, NT = DK / 32;
+  constexpr int FR = NS * 2 + NT * 2 * 2;  // 1 KB fragment planes per (bh, key block)
+  const int lane = threadIdx.x, li = lane & 31, hk = lane >> 5;
+  const int kb = blockIdx.x, bh = blockIdx.y, f = blockIdx.z, nkb = gridDim.x;
+  const int b = bh / nh, h = bh % nh;
+  const float* base = qkv + (long long)b * T * ldq;
+  uint4* out = img + ((long long)bh * nkb + kb) * FR * 64 + lane;
+  float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int fr;
+  if (f < NS) {  // K: key li, dims 16 f + 8 hk ..
+    const int j = kb * FA_K + li;
+    if (j < T) {
+      const float4* src = reinterpret_cast<const float4*>(base + (long long)j * ldq + H + h * DK + 16 * f + 8 * hk);
+      const float4 x0 = src[0], x1 = src[1];
+      v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+    }
+    fr = 2 * f;
+  } else {  // V^T: dim 32 t + li, keys crow(8 s2 + e, hk)
+    const int t = (f - NS) >> 1, s2 = (f - NS) & 1;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int jj = kb * FA_K + crow(8 * s2 + e, hk);
+      if (jj < T) v[e] = base[(long long)jj * ldq + 2 * H + h * DK + 32 * t + li];
+    }
+    fr = 2 * NS + (t * 2 + s2) * 2;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] *= FA_XS;
+  f16x8 q[2];
+  split8h(v, q);
+  out[fr * 64] = __builtin_bit_cast(uint4, q[0]);
+  out[(fr + 1) * 64] = __builtin_bit_cast(uint4, q[1]);
+}
+
+template <int DK>
+__global__ __launch_bounds__(64, 2) void k_flash_attn_h16(const float* __restrict__ qkv, int ldq, int T, int nh, int H,
+                                                       float qscale, int kb_per_split, const float* __restrict__ rel_k,
+                                                       const float* __restrict__ rel_v, int window,
+                                                       const float* __restrict__ mask, const uint4* __restrict__ img,
+                                                       float* __restrict__ part_o, float* __restrict__ part_ml) {
+  constexpr int NS = DK / 16;
+  constexpr int NT = DK / 32;
+  constexpr int FR = NS * 2 + NT * 2 * 2;
+  __shared__ float relq[FA_Q][FA_NW + 1];
+  __shared__ float pband[FA_Q][FA_NW + 1];
+  const int lane = threadIdx.x, li = lane & 31, hk = lane >> 5;
+  const int q0 = blockIdx.x * FA_Q, split = blockIdx.y, bh = blockIdx.z;
+  const int b = bh / nh, h = bh % nh;
+  const int BH = gridDim.z;
+  const float* base = qkv + (long long)b * T * ldq;
+  const int i = q0 + li;
+  const bool qok = i < T;
+  const int nw = rel_k ? 2 * window + 1 : 0;
+  const float* mk = mask ? mask + (long long)b * T : nullptr;
+  const float mi = (mk && qok) ? mk[i] : 1.f;
+  const int nkb = (T + FA_K - 1) / FA_K;
+  const uint4* kvimg = img + (long long)bh * nkb * FR * 64 + lane;
+
+  // Q^T fragments (scaled by qscale 2^-4), kept for the whole key range
+  f16x8 qf[NS][2];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (qok) {
+      const float4* src = reinterpret_cast<const float4*>(base + (long long)i * ldq + h * DK + 16 * s + 8 * hk);
+      const float4 x0 = src[0], x1 = src[1];
+      const float qs = qscale * FA_XS;
+      v[0] = x0.x * qs; v[1] = x0.y * qs; v[2] = x0.z * qs; v[3] = x0.w * qs;
+      v[4] = x1.x * qs; v[5] = x1.y * qs; v[6] = x1.z * qs; v[7] = x1.w * qs;
+    }
+    split8h(v, qf[s]);
+  }
+  const int kb0 = split * kb_per_split, kb1 = min(nkb, kb0 + kb_per_split);
+  const bool band_split = nw && kb0 < kb1 && (kb1 * FA_K - 1 >= q0 - window) && (kb0 * FA_K <= q0 + FA_Q - 1 + window);
+  if (band_split) {
+    f32x16 rq, rq2;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) rq[r] = rq2[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (li < nw) {
+        const float* src = rel_k + li * DK + 16 * s + 8 * hk;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = src[e] * FA_XS;
+      }
+      f16x8 rf[2];
+      split8h(v, rf);
+      mfma3(rf, qf[s], rq, rq2);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int od = crow(r, hk);
+      relq[li][od] = (rq[r] + rq2[r] * H16_LO_INV) * 256.f;
+      pband[li][od] = 0.f;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+  f32x16 o[NT], o2[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[t][r] = o2[t][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+
+  for (int kb = kb0; kb < kb1; ++kb) {
+    const int j0 = kb * FA_K;
+    const uint4* fr = kvimg + (long long)kb * FR * 64;
+    // S^T = K Q^T for keys j0.. (rows) x this wave's queries (columns)
+    f32x16 sc, sc2;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sc[r] = sc2[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      f16x8 kf[2];
+      kf[0] = __builtin_bit_cast(f16x8, fr[(2 * s) * 64]);
+      kf[1] = __builtin_bit_cast(f16x8, fr[(2 * s + 1) * 64]);
+      mfma3(kf, qf[s], sc, sc2);
+    }
+    float mloc = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int j = j0 + crow(r, hk);
+      float v = (sc[r] + sc2[r] * H16_LO_INV) * 256.f;
+      if (nw) {
+        const int od = j - i + window;
+        if (od >= 0 && od < nw) v = v + relq[li][od];
+      }
+      if (mk && j < T && mi * mk[j] == 0.f) v = -1e4f;
+      if (j >= T) v = -INFINITY;
+      sc[r] = v;
+      mloc = fmaxf(mloc, v);
+    }
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32));
+    const float m_new = fmaxf(m_run, mloc);
+    const float alpha = expf(m_run - m_new);
+    float lsum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sc[r] = expf(sc[r] - m_new);
+      lsum += sc[r];
+    }
+    lsum += __shfl_xor(lsum, 32);
+    l_run = l_run * alpha + lsum;
+    m_run = m_new;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        o[t][r] *= alpha;
+        o2[t][r] *= alpha;
+      }
+    if (band_split) {
+      const bool band = (j0 + FA_K - 1 >= q0 - window) && (j0 <= q0 + FA_Q - 1 + window);
+      if (hk == 0)
+        for (int od = 0; od < nw; ++od) pband[li][od] *= alpha;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (band) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int od = j0 + crow(r, hk) - i + window;
+          if (od >= 0 && od < nw) pband[li][od] += sc[r];
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    // O^T += V^T P^T
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      float pv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) pv[e] = sc[8 * s2 + e];
+      f16x8 pf[2];
+      split8h(pv, pf);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int f = 2 * NS + (t * 2 + s2) * 2;
+        f16x8 vf[2];
+        vf[0] = __builtin_bit_cast(f16x8, fr[f * 64]);
+        vf[1] = __builtin_bit_cast(f16x8, fr[(f + 1) * 64]);
+        mfma3(vf, pf, o[t], o2[t]);
+      }
+    }
+  }
+  if (band_split) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      float pv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) pv[e] = pband[li][16 * s2 + 8 * hk + e];
+      f16x8 pf[2];
+      split8h(pv, pf);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int od = 16 * s2 + 8 * hk + e;
+          v[e] = od < nw ? rel_v[od * DK + 32 * t + li] * FA_XS : 0.f;
+        }
+        f16x8 vf[2];
+        split8h(v, vf);
+        mfma3(vf, pf, o[t], o2[t]);
+      }
+    }
+  }
+  float* ot = &relq[0][0];
+  const long long slab = ((long long)split * BH + bh) * T;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int r = 0; r < 16; ++r) ot[li * (FA_NW + 1) + crow(r, hk)] = (o[t][r] + o2[t][r] * H16_LO_INV) * 16.f;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int idx = k * 64 + lane, rr = idx >> 3, c4 = (idx & 7) * 4;
+      if (q0 + rr < T) {
+        const float* src = ot + rr * (FA_NW + 1) + c4;
+        const f32x4 v = {src[0], src[1], src[2], src[3]};
+        *reinterpret_cast<f32x4*>(part_o + (slab + q0 + rr) * DK + 32 * t + c4) = v;
+      }
+    }
+  }
+  if (qok && hk == 0) {
+    const long long row = slab + i;
+    part_ml[2 * row] = m_run;
+    part_ml[2 * row + 1] = l_run;
+  }
+}
+
 // out[b][i][h*DK + d] = sum_s O_s[d] e^(m_s - M) / sum_s l_s e^(m_s - M)
 // Merges the key splits: one row (bh, query i) per DK/4 lanes, each lane a float4 of the head dimension. The split
 // weights exp(m_s - M) are computed per lane group (was: per output element, with 64-bit index divisions per element),
@@ -348,6 +622,23 @@ int flash_attn_splits(int B, int nh, int T) {
   return ns;
 }
 
+// RVCX_FA_MATH=split: the three-plane bf16 kernel (A/B aid); default the two-plane fp16 split with K / V images
+static bool fa_h16() {
+  static const bool v = [] {
+    const char* e = std::getenv("RVCX_FA_MATH");
+    return !(e && std::string(e) == "split");
+  }();
+  return v;
+}
+
+// part_o's floats: the split partials, then (fp16 form) the K / V fragment images
+long long flash_attn_ws_floats(int B, int nh, int T, int dk, int nsplit) {
+  const long long parts = (long long)nsplit * B * nh * T * dk;
+  const long long nkb = (T + FA_K - 1) / FA_K;
+  const long long img = (long long)B * nh * nkb * (dk / 16 * 2 + dk / 32 * 4) * 64 * 4;  // uint4 = 4 floats
+  return parts + img;
+}
+
 hipError_t flash_attn(const float* qkv, int ldq, int B, int T, int nh, int dk, float qscale, const float* rel_k,
                       const float* rel_v, int window, const float* mask, float* part_o, float* part_ml, int nsplit,
                       float* out, int ldo, hipStream_t s) {
@@ -359,14 +650,28 @@ hipError_t flash_attn(const float* qkv, int ldq, int B, int T, int nh, int dk, f
   const int qb = (T + FA_Q - 1) / FA_Q, kb = (T + FA_K - 1) / FA_K;
   const int per = (kb + nsplit - 1) / nsplit;
   dim3 grid(qb, nsplit, B * nh);
-  if (dk == 64)
+  if (dk != 64 && dk != 96) return hipErrorInvalidValue;
+  if (fa_h16()) {
+    // the K / V images after the partials (the caller sized part_o with flash_attn_ws_floats)
+    uint4* img = reinterpret_cast<uint4*>(part_o + (long long)nsplit * B * nh * T * dk);
+    if ((reinterpret_cast<uintptr_t>(img) & 15) != 0) return hipErrorInvalidValue;
+    dim3 g2(kb, B * nh, dk / 16 + dk / 16);  // NS K steps + 2 NT V^T pairs (NS = 2 NT)
+    if (dk == 64) {
+      hipLaunchKernelGGL(k_kv_split16<64>, g2, dim3(64), 0, s, qkv, ldq, T, nh, H, img);
+      hipLaunchKernelGGL(k_flash_attn_h16<64>, grid, dim3(64), 0, s, qkv, ldq, T, nh, H, qscale, per, rel_k, rel_v,
+                         window, mask, img, part_o, part_ml);
+    } else {
+      hipLaunchKernelGGL(k_kv_split16<96>, g2, dim3(64), 0, s, qkv, ldq, T, nh, H, img);
+      hipLaunchKernelGGL(k_flash_attn_h16<96>, grid, dim3(64), 0, s, qkv, ldq, T, nh, H, qscale, per, rel_k, rel_v,
+                         window, mask, img, part_o, part_ml);
+    }
+  } else if (dk == 64) {
     hipLaunchKernelGGL(k_flash_attn<64>, grid, dim3(64), 0, s, qkv, ldq, T, nh, H, qscale, per, rel_k, rel_v, window,
                        mask, part_o, part_ml);
-  else if (dk == 96)
+  } else {
     hipLaunchKernelGGL(k_flash_attn<96>, grid, dim3(64), 0, s, qkv, ldq, T, nh, H, qscale, per, rel_k, rel_v, window,
                        mask, part_o, part_ml);
-  else
-    return hipErrorInvalidValue;
+  }
   const long long rows = (long long)B * nh * T;
   if (rows * nsplit * dk >= (1LL << 31) || (ldo & 3) != 0 || (reinterpret_cast<uintptr_t>(out) & 15) != 0)
     return hipErrorInvalidValue;  // 32-bit slab offsets, float4 output rows

@@ -226,7 +226,8 @@ void hubert_layers(Ctx& c, const HubertRun& run, int l0, int l1, hipStream_t s) 
   const bool fused = flash_enabled();
   const int nsplit = flash_attn_splits(B, HHEADS, L);
   float* sc = fused ? nullptr : c.buf<float>("hb.scores", (size_t)B * HHEADS * L * L, s);
-  float* part_o = fused ? c.buf<float>("hb.fa_o", (size_t)nsplit * B * HHEADS * L * (HD / HHEADS), s) : nullptr;
+  float* part_o =
+      fused ? c.buf<float>("hb.fa_o", (size_t)flash_attn_ws_floats(B, HHEADS, L, HD / HHEADS, nsplit), s) : nullptr;
   float* part_ml = fused ? c.buf<float>("hb.fa_ml", (size_t)nsplit * B * HHEADS * L * 2, s) : nullptr;
   float* att = c.buf<float>("hb.att", (size_t)BL * HD, s);
   float* ff = c.buf<float>("hb.ff", (size_t)BL * HFF, s);

@@ -551,7 +551,7 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
   float* sc = fused ? nullptr : c.buf<float>("te.scores", (size_t)B * nh * T * T, s);
   float* rel = fused ? nullptr : c.buf<float>("te.rel", (size_t)B * nh * T * nw, s);
   float* pband = fused ? nullptr : c.buf<float>("te.pband", (size_t)B * nh * T * nw, s);
-  float* part_o = fused ? c.buf<float>("te.fa_o", (size_t)nsplit * B * nh * T * dk, s) : nullptr;
+  float* part_o = fused ? c.buf<float>("te.fa_o", (size_t)flash_attn_ws_floats(B, nh, T, dk, nsplit), s) : nullptr;
   float* part_ml = fused ? c.buf<float>("te.fa_ml", (size_t)nsplit * B * nh * T * 2, s) : nullptr;
   float* att = c.buf<float>("te.att", BT * H, s);
   float* o = c.buf<float>("te.o", BT * H, s);

@@ -200,6 +200,8 @@ hipError_t rb_pair(const RbPairArgs& a, int cfg, hipStream_t s);
 // window (rel_k / rel_v [2w+1][dk]) and key/query mask [B][T]; partials part_o [nsplit][B*nh][T][dk], part_ml
 // [nsplit][B*nh][T][2]; out [B][T][ldo] at column h*dk
 int flash_attn_splits(int B, int nh, int T);
+// floats the caller allocates for part_o: the split partials and the fp16 form's K / V fragment images
+long long flash_attn_ws_floats(int B, int nh, int T, int dk, int nsplit);
 hipError_t flash_attn(const float* qkv, int ldq, int B, int T, int nh, int dk, float qscale, const float* rel_k,
                       const float* rel_v, int window, const float* mask, float* part_o, float* part_ml, int nsplit,
                       float* out, int ldo, hipStream_t s);
