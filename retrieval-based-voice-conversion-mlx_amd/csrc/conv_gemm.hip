@@ -459,6 +459,81 @@ __global__ void splitk_reduce_kernel(const ConvArgs a, const int ksplit, const i
   }
 }
 
+// split-K combine + the post-norm LayerNorm (ConvArgs::ln_g): one 256-thread block per output row, thread t holding
+// columns t + 256 j (N <= 1024); every slab load of a column issued before its ordered sum, as in splitk_reduce_kernel
+// (a wave per row with the loads in a column loop measured 16 us against 5.6 + 7 for the two passes). The arithmetic
+// is splitk_reduce_kernel's epilogue followed by k_layernorm's on (res + v); the mean and variance sum the columns in
+// another order (block-wide), so the result equals the two passes to fp32 rounding of those sums.
+__device__ __forceinline__ float wave_sum64(float v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__global__ __launch_bounds__(256) void splitk_reduce_ln_kernel(const ConvArgs a, const int ksplit) {
+  __shared__ float red[2][4];
+  const long long row = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = (int)(row / a.ws_rows);
+  const long long m = row - (long long)b * a.ws_rows;
+  const long long per_b = a.ws_rows * a.N;
+  const float* bias = a.bias ? a.bias + (long long)b * a.bias_bs : nullptr;
+  const float* R = a.res + (long long)b * a.res_bs + m * a.ldr;
+  const float mk = a.mask ? a.mask[(long long)b * a.mask_bs + m] : 1.f;
+  float* Y = a.y + (long long)b * a.y_bs + m * a.ldy;
+  const float* base = a.ws + (long long)b * ksplit * per_b + m * a.N;
+  float v[4];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = tid + j * 256;
+    float t = 0.f;
+    if (n < a.N) {
+      const float* p = base + n;
+      float acc = 0.f;
+      int k = 0;
+      for (; k + 4 <= ksplit; k += 4) {  // splitk_reduce_kernel's order
+        const float p0 = p[(long long)k * per_b], p1 = p[(long long)(k + 1) * per_b];
+        const float p2 = p[(long long)(k + 2) * per_b], p3 = p[(long long)(k + 3) * per_b];
+        acc += p0;
+        acc += p1;
+        acc += p2;
+        acc += p3;
+      }
+      for (; k < ksplit; ++k) acc += p[(long long)k * per_b];
+      if (bias) acc += bias[n];  // epilogue_store's order: bias, alpha, act, (mask)
+      if (a.alpha != 1.f) acc *= a.alpha;
+      acc = act_fn(acc, a.act, a.slope);
+      if (a.mask) acc *= mk;
+      t = R[n];
+      t = t + acc;
+    }
+    v[j] = t;
+    s += t;
+  }
+  s = wave_sum64(s);
+  if (lane == 0) red[0][wave] = s;
+  __syncthreads();
+  const float mean = ((red[0][0] + red[0][1]) + (red[0][2] + red[0][3])) / (float)a.N;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = tid + j * 256;
+    if (n < a.N) {
+      const float d = v[j] - mean;
+      q += d * d;
+    }
+  }
+  q = wave_sum64(q);
+  if (lane == 0) red[1][wave] = q;
+  __syncthreads();
+  const float var = ((red[1][0] + red[1][1]) + (red[1][2] + red[1][3])) / (float)a.N;
+  const float rstd = 1.f / sqrtf(var + a.ln_eps);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = tid + j * 256;
+    if (n < a.N) Y[n] = (v[j] - mean) * rstd * a.ln_g[n] + a.ln_b[n];
+  }
+}
+
 // Contractions far shorter than one 32-channel MFMA chunk (C_in <= 4 and at most 16 MACs per output: RMVPE's 3x3
 // and 1x1 convs on the 1-channel mel image, the generator's last 1-tap noise conv) would run the MFMA tile on
 // >= 87 % zero padding: one thread per output element instead, an fp32 fma chain over (tap, channel), then the
@@ -654,6 +729,15 @@ __global__ void splitk_reduce_gate_kernel(const ConvArgs a, const int ksplit) {
 }
 
 hipError_t launch_splitk_reduce(const ConvArgs& a, int ksplit, bool two_d, hipStream_t s) {
+  if (a.ln_g) {
+    if (two_d || a.batch_inner != 1 || a.N > 1024 || !a.ln_b || !a.res || a.res_mode != RES_NONE ||
+        a.acc_mode != ACC_STORE || a.out_map != OUT_ROWS || a.gate_h > 0)
+      return hipErrorInvalidValue;
+    const long long rows = (long long)a.batch * a.ws_rows;
+    if (rows >= (1LL << 31)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(splitk_reduce_ln_kernel, dim3((unsigned)rows), dim3(256), 0, s, a, ksplit);
+    return hipGetLastError();
+  }
   if (a.gate_h > 0) {
     if (two_d || a.batch_inner != 1 || a.N != 2 * a.gate_h || !a.gate_g) return hipErrorInvalidValue;
     const long long per_o = a.ws_rows * a.gate_h;
@@ -855,7 +939,8 @@ template <bool TWO_D>
 hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
   if (a.N <= 0 || a.T_out <= 0 || a.batch <= 0) return hipSuccess;
   if (a.C_in <= 0 || a.taps <= 0) return hipErrorInvalidValue;
-  if (a.gate_h > 0 && !(a.ws && a.ksplit > 1)) return hipErrorInvalidValue;  // the gate is applied by the combine
+  // the gate and the LayerNorm are applied by the combine
+  if ((a.gate_h > 0 || a.ln_g) && !(a.ws && a.ksplit > 1)) return hipErrorInvalidValue;
   if (tiny_fits(a)) return launch_tiny(a, TWO_D, s);
   if (a.wsb == 2 && a.wsplit && conv_math(a) >= 2 && conv_gs_eligible(a, TWO_D)) {
     const int ks = (a.ws && a.ksplit > 1) ? a.ksplit : 1;
@@ -954,7 +1039,8 @@ long long conv_plan_splitk(ConvArgs& a, bool two_d) {
   static const int min_tiles = env_cfg("RVCX_SPLITK_TILES", 192);  // grids with at least this many tiles stay unsplit
   static const int min_iters = env_cfg("RVCX_SPLITK_MINITERS", 4);  // shortest contraction worth a split
   // a gated WaveNet in_layer always splits: its gate lives in the combine (ConvArgs::gate_h)
-  if (a.gate_h == 0 && (tiles >= min_tiles || iters < min_iters || (flops < 1.0e8 && iters < 16))) return 0;
+  const bool combine_epi = a.gate_h > 0 || a.ln_g;  // an epilogue only the combine applies: always split
+  if (!combine_epi && (tiles >= min_tiles || iters < min_iters || (flops < 1.0e8 && iters < 16))) return 0;
   int ks = (int)((target + tiles - 1) / tiles);
   // the gather-streamed kernels keep >= 8 (chunk, tap) steps per slice: below that a slice is all prologue and
   // epilogue and the extra slab + combine launch cost more than the parallelism gains (bench_gs r03s, cold: HuBERT
@@ -967,7 +1053,7 @@ long long conv_plan_splitk(ConvArgs& a, bool two_d) {
   // ks 4 beat the 10 and 6 the step count would give)
   if (a.wsb == 2 && two_d && (a.force_cfg < 0 || a.force_cfg == 30) && conv_gsw_eligible(a))
     ks = std::min(ks, (a.C_in + CK - 1) / CK);
-  if (a.gate_h > 0 && iters >= 2) ks = std::max(ks, 2);
+  if (combine_epi && iters >= 2) ks = std::max(ks, 2);
   if (ks < 2) return 0;
   a.ksplit = ks;
   a.ws_rows = two_d ? (long long)a.T_out * a.W_out : a.T_out;

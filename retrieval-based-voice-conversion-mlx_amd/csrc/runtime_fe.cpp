@@ -281,15 +281,16 @@ void hubert_layers(Ctx& c, const HubertRun& run, int l0, int l1, hipStream_t s) 
       ConvArgs f1 = lin(hs, HD, BL, HD, c.W(q + ".ff1.w"), HFF, c.W(q + ".ff1.b"), ff, HFF);
       f1.act = ACT_GELU;
       run1(c, f1, s);
-      ConvArgs f2 = lin(ff, HFF, BL, HFF, c.W(q + ".ff2.w"), HD, c.W(q + ".ff2.b"), hs2, HD);
+      // v2's output is the last layer's LN itself: written straight into the caller's buffer (no tail copy)
+      float* dst = (run.version != 1 && i == HUBERT_LAYERS - 1) ? run.feats : hs;
+      // dst = LN(hs + ff2(ff)) in the split-K combine (final_layer_norm): no hs2 round trip, no separate pass
+      ConvArgs f2 = lin(ff, HFF, BL, HFF, c.W(q + ".ff2.w"), HD, c.W(q + ".ff2.b"), dst, HD);
       f2.res = hs;
       f2.ldr = HD;
-      f2.res_mode = RES_ADD_POST;
+      f2.ln_g = c.W(q + ".ln2.g");
+      f2.ln_b = c.W(q + ".ln2.b");
       run1(c, f2, s);
     }
-    // v2's output is the last layer's LN itself: written straight into the caller's buffer (no tail copy)
-    float* dst = (run.version != 1 && i == HUBERT_LAYERS - 1) ? run.feats : hs;
-    check(layernorm_rows(hs2, nullptr, dst, c.W(q + ".ln2.g"), c.W(q + ".ln2.b"), BL, HD, 1e-5f, nullptr, s), "ln2");
   }
 }
 

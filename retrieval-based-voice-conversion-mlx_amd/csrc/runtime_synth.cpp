@@ -628,15 +628,20 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
       a.pre_mask_bs = T;
       a.act = ACT_RELU;
       run(c, a, s);
-      ConvArgs b = conv(h1, F, T, F, c.W(q + ".ffn2.w"), H, cf.ksize, 1, (cf.ksize - 1) / 2, c.W(q + ".ffn2.b"), o,
+      // x = LN(x + conv_2(.) * mask) in the split-K combine (norm_layers_2, attentions.py:63-66): no separate pass
+      ConvArgs b = conv(h1, F, T, F, c.W(q + ".ffn2.w"), H, cf.ksize, 1, (cf.ksize - 1) / 2, c.W(q + ".ffn2.b"), x,
                         H, T, B);
       b.pre_mask = mask;
       b.pre_mask_bs = T;
       b.mask = mask;
       b.mask_bs = T;
+      b.res = x;
+      b.ldr = H;
+      b.res_bs = (long long)T * H;
+      b.ln_g = c.W(q + ".ln2.g");
+      b.ln_b = c.W(q + ".ln2.b");
       run(c, b, s);
     }
-    check(layernorm_rows(x, o, x, c.W(q + ".ln2.g"), c.W(q + ".ln2.b"), (int)BT, H, 1e-5f, nullptr, s), "ln2");
   }
   float* stats = c.buf<float>("te.stats", BT * 2 * I, s);
   {

@@ -92,6 +92,13 @@ struct ConvArgs {
   int gate_h = 0;
   const float* gate_g = nullptr;
   long long gate_g_bs = 0;
+  // post-norm LayerNorm in the split-K combine (a Transformer block's residual + norm, attentions.py:221-231 with
+  // norm_layers_2, modeling_hubert.py final_layer_norm): y[m] = LN(res[m] + v[m]) * ln_g + ln_b over the N columns, v the
+  // epilogue value (bias, alpha, act, mask) with res_mode RES_NONE (res / ldr / res_bs name the LN's residual input).
+  // Forces a split (ksplit >= 2); 1-D, batch_inner 1, N <= 1024. Equals the two passes to fp32 rounding of the row sums.
+  const float* ln_g = nullptr;
+  const float* ln_b = nullptr;
+  float ln_eps = 1e-5f;
   // grid z = batch * batch_inner; pointer offset = zo * *_bs + zi * *_bs2 (mask: zo only)
   int batch = 1;
   int batch_inner = 1;
