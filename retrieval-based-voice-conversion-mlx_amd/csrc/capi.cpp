@@ -255,6 +255,12 @@ void set_i32(int32_t* p, int32_t v, hipStream_t s) {
   hipLaunchKernelGGL(k_set_i32, dim3(1), dim3(1), 0, s, p, v);
   check(hipGetLastError(), "set_i32");
 }
+void set_i32_once(Ctx& c, const std::string& name, int32_t* p, int32_t v, hipStream_t s) {
+  auto it = c.i32_marks.find(name);
+  if (it != c.i32_marks.end() && it->second.first == p && it->second.second == v) return;
+  set_i32(p, v, s);
+  c.i32_marks[name] = {p, v};
+}
 }  // namespace rvcx
 
 extern "C" {

@@ -145,6 +145,9 @@ struct Ctx {
   // buffers whose zero parts survive from call to call (the BiGRU hand-off tags, the NSF source's pad columns): zeroed
   // only when the buffer or its layout changes, not by a fill launch every call
   std::map<std::string, std::pair<const void*, long long>> zero_marks;
+  // small device scalars written from the host (the synthesizer's length / speaker id): the launch is skipped when the
+  // named buffer already holds the value (C2 writes the same two every call)
+  std::map<std::string, std::pair<const void*, int32_t>> i32_marks;
   // returns true when it zeroed
   bool zero_once(const std::string& name, void* p, size_t bytes, long long layout, hipStream_t s) {
     auto& m = zero_marks[name];
@@ -275,6 +278,7 @@ rvcx_pipeline_opts default_pipeline_opts();
 int proposed_key(const std::vector<double>& f0, double threshold);
 int64_t hubert_frames(int64_t n);  // HuBERT output rows for n samples (0 when too short)
 void set_i32(int32_t* p, int32_t v, hipStream_t s);
+void set_i32_once(Ctx& c, const std::string& name, int32_t* p, int32_t v, hipStream_t s);
 // Overlap of independent stages: fork_aux returns the aux stream, ordered after everything queued on s so
 // far (or s itself when overlap is off: kernel timing on, or RVCX_NO_OVERLAP=1); join_aux makes s wait for
 // everything queued on the aux stream so far.

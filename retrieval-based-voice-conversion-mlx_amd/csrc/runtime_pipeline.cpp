@@ -187,8 +187,8 @@ int64_t vc_forward(Ctx& c, const float* audio, int64_t n, const int32_t* pitch, 
   check(upsample2_protect(fx, feats, (int)L, E, phone, T, protect < 0.5f ? pitchf : nullptr, protect, s),
         "upsample");
   int32_t* lens = c.buf<int32_t>("vc.len", 4, s);
-  set_i32(lens, T, s);
-  set_i32(lens + 1, sid, s);
+  set_i32_once(c, "vc.len.T", lens, T, s);
+  set_i32_once(c, "vc.len.sid", lens + 1, sid, s);
   synth_forward(c, 1, T, phone, lens, pitch, pitchf, lens + 1, eps_z, eps_src, seed, out, nullptr, nullptr, s);
   return (int64_t)T * upp;
 }

@@ -2,6 +2,7 @@
 // the forward pass as a sequence of MFMA conv-GEMM launches plus small fused kernels.
 // Reference semantics: rvc/lib/algorithm/{synthesizers,encoders,attentions,modules,residuals}.py,
 // generators/{hifigan_nsf,hifigan}.py (see each block's comment for file:line).
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 
@@ -187,11 +188,18 @@ void finalize_synth(Ctx& c) {
   // flow (residuals.py:103-258, modules.py:5-117). A coupling's WaveNet state lives in one [T][2H] buffer: the
   // residual stream h in columns [0, H), the skip sum in [H, 2H). `pre` is packed with H zero rows appended, so its
   // launch also clears the skip sum; the cond layers of all couplings are one [flow_n * cl][gin] GEMM.
+  // The Flip before each coupling of the reverse pass (residuals.py:233-258) is folded into the weights when there is an
+  // even number of them: the reverse loop's k-th coupling (k = flow_n - 1 - f) with k even sees the channels reversed,
+  // so its `pre` reads the upper half with its input columns reversed and its `post` writes the lower half with its
+  // output rows (and bias) reversed; after the last (odd k) coupling the layout is the reference's again.
   std::vector<float> condw, condb;
   for (int f = 0; f < g.flow_n; ++f) {
     const std::string p = "flow.flows." + std::to_string(2 * f);
     const std::string q = "flow." + std::to_string(f);
+    const bool rev = g.flow_n % 2 == 0 && (g.flow_n - 1 - f) % 2 == 0;
     std::vector<float> prew = get(c, M, p + ".pre.weight", {H, I / 2, 1}).v, preb = get(c, M, p + ".pre.bias", {H}).v;
+    if (rev)
+      for (int o = 0; o < H; ++o) std::reverse(prew.begin() + (size_t)o * (I / 2), prew.begin() + (size_t)(o + 1) * (I / 2));
     prew.resize((size_t)2 * H * (I / 2), 0.f);
     preb.resize((size_t)2 * H, 0.f);
     c.alloc_weight(q + ".pre.w", prew);
@@ -210,8 +218,15 @@ void finalize_synth(Ctx& c) {
       c.alloc_weight(q + ".rs" + l + ".w", get(c, M, p + ".enc.res_skip_layers." + l + ".weight", {rs, H, 1}).v);
       c.alloc_weight(q + ".rs" + l + ".b", get(c, M, p + ".enc.res_skip_layers." + l + ".bias", {rs}).v);
     }
-    c.alloc_weight(q + ".post.w", get(c, M, p + ".post.weight", {I / 2, H, 1}).v);
-    c.alloc_weight(q + ".post.b", get(c, M, p + ".post.bias", {I / 2}).v);
+    std::vector<float> postw = get(c, M, p + ".post.weight", {I / 2, H, 1}).v, postb = get(c, M, p + ".post.bias", {I / 2}).v;
+    if (rev) {
+      for (int o = 0; o < I / 4; ++o)
+        std::swap_ranges(postw.begin() + (size_t)o * H, postw.begin() + (size_t)(o + 1) * H,
+                         postw.begin() + (size_t)(I / 2 - 1 - o) * H);
+      std::reverse(postb.begin(), postb.end());
+    }
+    c.alloc_weight(q + ".post.w", postw);
+    c.alloc_weight(q + ".post.b", postb);
   }
   c.alloc_weight("flow.cond.w", condw);
   c.alloc_weight("flow.cond.b", condb);
@@ -663,11 +678,21 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
   float* gc = c.buf<float>("flow.gc", (size_t)B * cf.flow_n * cl, s);
   // g -> every coupling's cond_layer(g) in one GEMM (modules.py:32-35, :92-93)
   run(c, lin(g, cf.gin, B, cf.gin, c.W("flow.cond.w"), cf.flow_n * cl, c.W("flow.cond.b"), gc, cf.flow_n * cl), s);
+  const bool fold = cf.flow_n % 2 == 0;  // the flips folded into the couplings' weights (finalize)
   for (int f = cf.flow_n - 1; f >= 0; --f) {
     const std::string q = "flow." + std::to_string(f);
-    check(channel_flip(z, xf, (int)BT, I, s), "flip");
+    // this coupling's x0 (pre's input) and x1 (post's residual and output) columns of the state
+    float* x0 = xf;
+    float* x1 = xf + I / 2;
+    if (fold) {
+      const bool rev = (cf.flow_n - 1 - f) % 2 == 0;
+      x0 = rev ? z + I / 2 : z;
+      x1 = rev ? z : z + I / 2;
+    } else {
+      check(channel_flip(z, xf, (int)BT, I, s), "flip");
+    }
     {  // h = pre(x0) * mask, and the skip sum cleared (the zero rows of the packed pre weight)
-      ConvArgs a = lin(xf, I, (int)BT, I / 2, c.W(q + ".pre.w"), 2 * H, c.W(q + ".pre.b"), hs, 2 * H);
+      ConvArgs a = lin(x0, I, (int)BT, I / 2, c.W(q + ".pre.w"), 2 * H, c.W(q + ".pre.b"), hs, 2 * H);
       a.mask = mask;
       run(c, a, s);
     }
@@ -693,14 +718,14 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
       run(c, a, s);
     }
     {  // x1 = (x1 - m) * mask, m = post(h) * mask
-      ConvArgs a = lin(hs + H, 2 * H, (int)BT, H, c.W(q + ".post.w"), I / 2, c.W(q + ".post.b"), xf + I / 2, I);
-      a.res = xf + I / 2;
+      ConvArgs a = lin(hs + H, 2 * H, (int)BT, H, c.W(q + ".post.w"), I / 2, c.W(q + ".post.b"), x1, I);
+      a.res = x1;
       a.ldr = I;
       a.res_mode = RES_RSUB_POST;
       a.mask = mask;
       run(c, a, s);
     }
-    std::swap(z, xf);
+    if (!fold) std::swap(z, xf);
   }
   if (z_out) RVCX_HIP(hipMemcpyAsync(z_out, z, BT * I * sizeof(float), hipMemcpyDeviceToDevice, s));
   // ---- dec(z * mask, nsff0, g)
