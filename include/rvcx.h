@@ -226,6 +226,24 @@ int rvcx_pipeline(rvcx_ctx* ctx, const double* d_audio, int64_t n, int sid, doub
                   int64_t t_pad, int64_t t_pad_tgt, const float* d_eps_z, const float* d_eps_src, uint64_t seed,
                   float* d_out, int64_t cap, int64_t* n_out, double* d_f0, void* stream);
 
+/* Device workspace (SURVEY.md 8(b) "Ownership"; replaces nothing in the reference, whose MLX / torch allocators own
+ * all scratch). Every intermediate of a call (activations, split-K slabs, filter state, attention partials ...) lives
+ * in the context's named pool, allocated on first use and kept across calls; the weights and their pre-split images
+ * are not part of it.
+ * rvcx_workspace_bytes: the pool a pipeline call of B utterances of n samples under opts takes (B = 1 as
+ *   rvcx_pipeline_ex, B > 1 as rvcx_pipeline_batch). It runs that call once on zero audio on `stream` from an empty
+ *   pool (loaded models required; outputs discarded) and reports every region the pool took, regrown ones included,
+ *   so an arena of that size holds the call; the pool is released again before it returns.
+ * rvcx_set_workspace: hand the context a caller-owned device arena (e.g. a torch uint8 tensor's data_ptr(), 256-B
+ *   aligned), valid until replaced or the context is destroyed: the pool is then carved from it and never allocated,
+ *   and a call that would need more fails with RVCX_E_OOM. NULL, 0 returns to internal allocation. The current pool
+ *   is released first (the device is synchronised).
+ * rvcx_workspace_info: bytes the pool holds now, the arena size and the arena bytes carved so far (any may be NULL). */
+int rvcx_workspace_bytes(rvcx_ctx* ctx, int B, int64_t n, const rvcx_pipeline_opts* opts, int64_t* bytes,
+                         void* stream);
+int rvcx_set_workspace(rvcx_ctx* ctx, void* d_base, int64_t bytes);
+int rvcx_workspace_info(const rvcx_ctx* ctx, int64_t* held, int64_t* arena_bytes, int64_t* arena_used);
+
 /* Kernel timing for roofline reporting: when enabled, every implicit-GEMM conv launch (the MFMA
  * kernel family that carries ~all FLOPs) is bracketed by hipEvents recorded on its own stream.
  * rvcx_profile_read synchronises those events and returns the summed kernel time (ms), the

@@ -569,6 +569,70 @@ int rvcx_pipeline_ex(rvcx_ctx* ctx, const double* d_audio, int64_t n, const rvcx
   });
 }
 
+int rvcx_set_workspace(rvcx_ctx* ctx, void* d_base, int64_t bytes) {
+  return guard(ctx, [&] {
+    if ((d_base && bytes <= 0) || (!d_base && bytes != 0) || (reinterpret_cast<uintptr_t>(d_base) & 255))
+      throw Error(RVCX_E_INVALID, "rvcx_set_workspace: a 256-B aligned base with bytes > 0, or NULL and 0");
+    set_device(ctx);
+    ctx->release_pool();
+    ctx->arena = static_cast<char*>(d_base);
+    ctx->arena_bytes = d_base ? (size_t)bytes : 0;
+  });
+}
+
+int rvcx_workspace_info(const rvcx_ctx* ctx, int64_t* held, int64_t* arena_bytes, int64_t* arena_used) {
+  if (!ctx) return RVCX_E_INVALID;
+  if (held) *held = (int64_t)ctx->pool_bytes();
+  if (arena_bytes) *arena_bytes = (int64_t)ctx->arena_bytes;
+  if (arena_used) *arena_used = (int64_t)ctx->arena_used;
+  return RVCX_OK;
+}
+
+int rvcx_workspace_bytes(rvcx_ctx* ctx, int B, int64_t n, const rvcx_pipeline_opts* opts, int64_t* bytes,
+                         void* stream) {
+  return guard(ctx, [&] {
+    if (!ctx->ready[0] || !ctx->ready[1] || !ctx->ready[2]) throw Error(RVCX_E_STATE, "models not finalized");
+    if (!opts || !bytes || n <= 0 || B < 1) throw Error(RVCX_E_INVALID, "rvcx_workspace_bytes: bad arguments");
+    set_device(ctx);
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    // the call itself on zero audio, from an empty internally allocated pool; the pool is released again after, and
+    // a caller arena stays attached (its regions are carved anew by the next call)
+    char* const arena = ctx->arena;
+    const size_t arena_bytes = ctx->arena_bytes;
+    ctx->release_pool();
+    ctx->arena = nullptr;
+    ctx->arena_bytes = 0;
+    DevBuf audio, out;
+    const int64_t m = n + 2 * opts->t_pad;
+    const int64_t cap = (m / 160 + (opts->t_center > 0 ? n / opts->t_center : 0) + 2) * ctx->scfg.upp();
+    int64_t need = 0;
+    try {
+      RVCX_HIP(hipMalloc(&audio.p, sizeof(double) * (size_t)(B * n)));
+      RVCX_HIP(hipMalloc(&out.p, sizeof(float) * (size_t)(B * cap)));
+      RVCX_HIP(hipMemsetAsync(audio.p, 0, sizeof(double) * (size_t)(B * n), s));
+      if (B == 1) {
+        pipeline_forward_ex(*ctx, static_cast<const double*>(audio.p), n, *opts, nullptr, nullptr, 0,
+                            static_cast<float*>(out.p), cap, nullptr, s);
+      } else {
+        std::vector<int32_t> sids((size_t)B, opts->sid);
+        pipeline_forward_batch(*ctx, static_cast<const double*>(audio.p), n, n, B, *opts, sids.data(), nullptr, nullptr, 0,
+                               static_cast<float*>(out.p), cap, nullptr, nullptr, s);
+      }
+      RVCX_HIP(hipStreamSynchronize(s));
+      need = (int64_t)ctx->carved;
+    } catch (...) {
+      ctx->release_pool();
+      ctx->arena = arena;
+      ctx->arena_bytes = arena_bytes;
+      throw;
+    }
+    ctx->release_pool();
+    ctx->arena = arena;
+    ctx->arena_bytes = arena_bytes;
+    *bytes = need;
+  });
+}
+
 int rvcx_device_status(rvcx_ctx* ctx, void* stream) {
   return guard(ctx, [&] {
     RVCX_HIP(hipSetDevice(ctx->device));

@@ -40,11 +40,12 @@ struct HostTensor {
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
+  bool borrowed = false;  // carved from the caller's workspace arena (rvcx_set_workspace): not freed here
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
   ~DevBuf() {
-    if (p) (void)hipFree(p);
+    if (p && !borrowed) (void)hipFree(p);
   }
 };
 
@@ -173,6 +174,27 @@ struct Ctx {
   float* alloc_weight(const std::string& name, const std::vector<float>& data);
   template <class T>
   T* buf(const std::string& name, size_t count, hipStream_t s);
+  // caller-owned workspace arena (rvcx_set_workspace): the named pool is carved from it (256-B aligned, bump order)
+  // instead of hipMalloc; a buffer that has to grow takes a new region; past the end a call fails with RVCX_E_OOM
+  char* arena = nullptr;
+  size_t arena_bytes = 0, arena_used = 0;
+  size_t carved = 0;  // bytes the pool has taken since the last release (every region, regrown ones included)
+  // synchronise the device and drop the named pool, with the marks that describe its contents (zeroed buffers,
+  // memoised scalars, BiGRU tag counters)
+  void release_pool() {
+    RVCX_HIP(hipDeviceSynchronize());
+    ws.clear();
+    zero_marks.clear();
+    i32_marks.clear();
+    gru_tags.clear();
+    arena_used = 0;
+    carved = 0;
+  }
+  size_t pool_bytes() const {
+    size_t t = 0;
+    for (const auto& kv : ws) t += kv.second ? kv.second->bytes : 0;
+    return t;
+  }
 };
 
 template <class T>
@@ -184,11 +206,23 @@ T* Ctx::buf(const std::string& name, size_t count, hipStream_t s) {
   if (!slot || slot->bytes < bytes) {
     if (slot && slot->p) RVCX_HIP(hipStreamSynchronize(s));
     slot.reset(new DevBuf());
-    if (hipMalloc(&slot->p, bytes) != hipSuccess) {
+    if (arena) {
+      const size_t off = (arena_used + 255) & ~size_t(255);
+      if (off + bytes > arena_bytes) {
+        ws.erase(name);
+        throw Error(RVCX_E_OOM, "workspace arena exhausted: " + name + " needs " + std::to_string(bytes) + " B at offset " +
+                                    std::to_string(off) + " of " + std::to_string(arena_bytes));
+      }
+      slot->p = arena + off;
+      slot->borrowed = true;
+      arena_used = off + bytes;
+    } else if (hipMalloc(&slot->p, bytes) != hipSuccess) {
       (void)hipGetLastError();
+      ws.erase(name);
       throw Error(RVCX_E_OOM, "workspace allocation failed: " + name + " (" + std::to_string(bytes) + " B)");
     }
     slot->bytes = bytes;
+    carved += bytes;
   }
   return static_cast<T*>(slot->p);
 }

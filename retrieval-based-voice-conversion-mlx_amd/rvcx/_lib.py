@@ -29,6 +29,7 @@ EXPORTS = [
     "rvcx_rt_geometry", "rvcx_rt_reset", "rvcx_rt_process", "rvcx_hubert_batch", "rvcx_rmvpe_batch",
     "rvcx_pipeline_batch", "rvcx_set_highpass_sos", "rvcx_highpass_pad", "rvcx_device_status", "rvcx_index_parse",
     "rvcx_set_conv_math", "rvcx_conv1d", "rvcx_conv2d3x3", "rvcx_resblock_pair", "rvcx_crepe", "rvcx_split_audio",
+    "rvcx_workspace_bytes", "rvcx_set_workspace", "rvcx_workspace_info",
 ]
 
 
@@ -139,6 +140,9 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "rvcx_pipeline_batch": (i32, [vp, vp, i64, i64, i32, P(PipelineOpts), P(ctypes.c_int32), vp, vp, u64, vp, i64,
                                       P(i64), vp, vp, vp]),
         "rvcx_set_highpass_sos": (i32, [vp, vp, i32]),
+        "rvcx_workspace_bytes": (i32, [vp, i32, i64, P(PipelineOpts), P(i64), vp]),
+        "rvcx_set_workspace": (i32, [vp, vp, i64]),
+        "rvcx_workspace_info": (i32, [vp, P(i64), P(i64), P(i64)]),
         "rvcx_highpass_pad": (i32, [vp, vp, i64, i64, vp, vp, vp]),
         "rvcx_hubert_batch": (i32, [vp, vp, i64, i64, i32, i32, vp, i64, P(i64), vp]),
         "rvcx_rmvpe_batch": (i32, [vp, vp, i64, i64, i32, f32, vp, i64, P(i64), vp, vp]),

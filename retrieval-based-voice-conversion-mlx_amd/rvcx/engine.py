@@ -343,6 +343,30 @@ class Engine:
         res = out[: no.value]
         return (res, f0) if want_f0 else res
 
+    def workspace_bytes(self, n: int, B: int = 1, opts=None) -> int:
+        """Device scratch a pipeline call of B utterances of n samples takes (rvcx_workspace_bytes: one call on zero
+        audio from an empty pool; the pool is released after)."""
+        o = opts if opts is not None else self.pipeline_opts()
+        v = ctypes.c_int64(0)
+        self._check(self.lib.rvcx_workspace_bytes(self.ctx, int(B), int(n), ctypes.byref(o), ctypes.byref(v),
+                                                  self.stream()), "workspace_bytes")
+        return int(v.value)
+
+    def set_workspace(self, arena=None):
+        """Carve the context's scratch from a caller-owned device tensor (rvcx_set_workspace; None: back to internal
+        allocation). The tensor is kept referenced here for as long as it is attached."""
+        base = 0 if arena is None else arena.data_ptr()
+        nbytes = 0 if arena is None else arena.numel() * arena.element_size()
+        self._check(self.lib.rvcx_set_workspace(self.ctx, ctypes.c_void_p(base or None), int(nbytes)),
+                    "set_workspace")
+        self._arena = arena
+
+    def workspace_info(self):
+        """(bytes the pool holds, arena bytes, arena bytes carved)."""
+        v = [ctypes.c_int64(0) for _ in range(3)]
+        self._check(self.lib.rvcx_workspace_info(self.ctx, *(ctypes.byref(x) for x in v)), "workspace_info")
+        return tuple(int(x.value) for x in v)
+
     def pipeline_opts(self, **kw) -> "_lib.PipelineOpts":
         """rvcx_pipeline_opts with the C defaults, overridden by keyword (field names of the struct)."""
         o = _lib.PipelineOpts()
