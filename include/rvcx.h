@@ -101,6 +101,23 @@ int rvcx_crepe(rvcx_ctx* ctx, const float* d_audio, int64_t n, float f0_min, flo
                float* d_f0, float* d_periodicity, float* d_probs, int64_t cap_frames, int64_t* frames_out,
                void* stream);
 
+/* rvcx_crepe with a choice of semantics: 0 = as rvcx_crepe (the MLX port's CREPE.get_f0); 1 = rvc/'s CREPE.get_f0
+ * (rvc/lib/predictors/f0.py:31-55): torchcrepe.predict's framing (zero padding of 512, unbiased std), its default
+ * viterbi decoder (torchcrepe.decode.viterbi: the sigmoid outputs outside [f0_min, f0_max] masked, softmax over the
+ * bins, librosa.sequence.viterbi with the +-11-bin triangular transition matrix), periodicity = the output at the
+ * decoded bin, then torchcrepe.filter.median(periodicity, 3), filter.mean(f0, 3) and f0 = 0 where the periodicity <
+ * threshold. torchcrepe dithers the decoded cents with scipy.stats.triang noise on [-20, 20] cents: d_dither [F]
+ * (optional, semantics 1 only) supplies it, NULL decodes without. torchcrepe / librosa are not importable here: the
+ * restatement follows their published source (parity unpinned; tests/test_gpu_crepe.py checks it against
+ * oracle/crepe.py's numpy restatement). Any n > 0. In rvcx_pipeline_opts: f0_method 2 (no dither). */
+int rvcx_crepe_ex(rvcx_ctx* ctx, const float* d_audio, int64_t n, float f0_min, float f0_max, float threshold,
+                  int semantics, const float* d_dither, float* d_f0, float* d_periodicity, float* d_probs,
+                  int64_t cap_frames, int64_t* frames_out, void* stream);
+/* The decode alone (the tail of rvcx_crepe_ex after the network: CREPE._decode + filters for semantics 0,
+ * torchcrepe's viterbi + rvc/'s filters for 1) on caller-given probabilities d_probs [F][360]. */
+int rvcx_crepe_decode(rvcx_ctx* ctx, const float* d_probs, int64_t F, float f0_min, float f0_max, float threshold,
+                      int semantics, const float* d_dither, float* d_f0, float* d_periodicity, void* stream);
+
 /* split_audio.process_audio (rvc/lib/tools/split_audio.py:5-27; rvc/infer/infer.py:282-284): the non-silent
  * intervals librosa.effects.split(audio, top_db=-silence_thresh_db, frame_length=int(min_silence_len_ms/1000*sr),
  * hop_length=frame_length//2) returns. d_audio [n] fp64 on device; intervals (HOST [cap][2] int64, start/end
@@ -190,7 +207,8 @@ typedef struct {
                                        > 0 needs rvcx_index_load */
   int f0_method;                    /* 0 = RMVPE (default), 1 = CREPE with the loaded RVCX_MODEL_CREPE weights
                                        (PitchExtractor.extract, pitch_extractors.py:155-156; f0_min 50, f0_max
-                                       1100, threshold 0.1) */
+                                       1100, threshold 0.1), 2 = CREPE as rvc/ runs it (pipeline.py:223-234;
+                                       rvcx_crepe_ex semantics 1, without the dither) */
 } rvcx_pipeline_opts;
 
 /* Defaults of the rvc/ Config (x_pad 1, x_query 6, x_center 38, x_max 41; rvc/configs/config.py) at

@@ -7,6 +7,12 @@ torchcrepe's (rvc/lib/predictors/f0.py:25-57 calls torchcrepe.predict); torchcre
 absent here, so parity against the reference's own run is UNPINNED: this file follows the MLX source
 line by line and the device path is checked against it.
 
+get_f0_rvc restates the rvc/ side (rvc/lib/predictors/f0.py:31-55): torchcrepe.predict's framing (preprocess:
+zero padding of 512, unbiased std), postprocess + decode.viterbi (softmax of the masked sigmoid outputs,
+librosa.sequence.viterbi with the +-11-bin triangular transition matrix), convert.bins_to_frequency (with the
+caller's dither values in place of scipy.stats.triang draws) and filter.median / filter.mean (window 3). These are
+restated from torchcrepe's and librosa's published source (neither is importable here): UNPINNED as well.
+
 Weights use torchcrepe's state-dict names and torch layouts (conv{i}.weight [O][I][K][1],
 conv{i}_BN.{weight,bias,running_mean,running_var}, classifier.weight [360][in_features]);
 rvcx.weights.load_crepe_weights maps the MLX npz (tools/convert_crepe_weights.py) onto them.
@@ -113,3 +119,80 @@ def get_f0(w, audio: np.ndarray, f0_min: float = 50.0, f0_max: float = 1100.0, t
     if return_periodicity:
         return f0, per, probs
     return f0
+
+
+# ---------------------------------------------------------------- rvc/ semantics (torchcrepe.predict + viterbi)
+def frame_audio_torch(audio: np.ndarray) -> np.ndarray:
+    """torchcrepe.preprocess (pad=True): zero pad 512 per side, 1024-sample frames every 160 (1 + n//160 of them),
+    minus the mean, divided by max(1e-10, unbiased std). float32 as torch computes it."""
+    a = torch.as_tensor(np.asarray(audio, dtype=np.float32))
+    n_frames = 1 + len(audio) // HOP_SIZE
+    ap = F.pad(a[None], (WINDOW_SIZE // 2, WINDOW_SIZE // 2))[0]
+    frames = ap.unfold(0, WINDOW_SIZE, HOP_SIZE)[:n_frames].clone()
+    frames -= frames.mean(dim=1, keepdim=True)
+    frames /= torch.clamp(frames.std(dim=1, keepdim=True), min=1e-10)
+    return frames.numpy()
+
+
+def torchcrepe_bin_range(f0_min: float, f0_max: float):
+    """postprocess: bins [frequency_to_bins(fmin) (floor), frequency_to_bins(fmax, ceil)) stay, the rest -inf."""
+    lo = int(np.floor((1200.0 * np.log2(f0_min / 10.0) - 1997.3794084376191) / 20.0))
+    hi = int(np.ceil((1200.0 * np.log2(f0_max / 10.0) - 1997.3794084376191) / 20.0))
+    return max(0, min(PITCH_BINS, lo)), max(0, min(PITCH_BINS, hi))
+
+
+def viterbi_bins(probs: np.ndarray, f0_min: float, f0_max: float) -> np.ndarray:
+    """decode.viterbi on the masked sigmoid outputs: softmax over the bins (float32), then
+    librosa.sequence.viterbi(prob, transition): log(prob + tiny) float32, log(transition + tiny) float64, uniform
+    p_init, values in float64, first argmax; returns the bin path [F]."""
+    lo, hi = torchcrepe_bin_range(f0_min, f0_max)
+    p = np.asarray(probs, dtype=np.float32).copy()
+    p[:, :lo] = -np.inf
+    p[:, hi:] = -np.inf
+    seq = torch.softmax(torch.as_tensor(p), dim=1).numpy()
+    eps = np.finfo(np.float32).tiny
+    xx, yy = np.meshgrid(range(PITCH_BINS), range(PITCH_BINS))
+    trans = np.maximum(12 - abs(xx - yy), 0)
+    trans = trans / trans.sum(axis=1, keepdims=True)
+    log_trans = np.log(trans + eps)
+    log_prob = np.log(seq + eps)
+    log_p_init = np.log(np.full(PITCH_BINS, 1.0 / PITCH_BINS) + eps)
+    n = log_prob.shape[0]
+    value = log_prob[0] + log_p_init
+    ptr = np.zeros((n, PITCH_BINS), dtype=np.int64)
+    rows = np.arange(PITCH_BINS)
+    for t in range(1, n):
+        trans_out = value[None, :] + log_trans.T  # [j][k] = value[k] + log_trans[k][j]
+        ptr[t] = np.argmax(trans_out, axis=1)
+        value = log_prob[t] + trans_out[rows, ptr[t]]
+    state = np.zeros(n, dtype=np.int64)
+    state[-1] = np.argmax(value)
+    for t in range(n - 2, -1, -1):
+        state[t] = ptr[t + 1, state[t + 1]]
+    return state
+
+
+def get_f0_rvc(w, audio: np.ndarray, f0_min: float = 50.0, f0_max: float = 1100.0, threshold: float = 0.1,
+               dither=None, probs=None):
+    """rvc/'s CREPE.get_f0: -> (f0 float32 [F], filtered periodicity float32 [F], probabilities [F][360]).
+    probs: decode these instead of running the network (the device's own, to check the decode alone)."""
+    if probs is None:
+        probs = forward(w, frame_audio_torch(audio))
+    probs = np.asarray(probs, dtype=np.float32)
+    bins = viterbi_bins(probs, f0_min, f0_max)
+    cents = (20 * bins).astype(np.float32) + np.float32(1997.3794084376191)
+    if dither is not None:
+        cents = cents + np.asarray(dither, dtype=np.float32)
+    f0 = np.float32(10.0) * np.exp2(cents / np.float32(1200.0))
+    per = probs[np.arange(len(bins)), bins]
+    n = len(bins)
+    pm = np.empty(n, dtype=np.float32)
+    fm = np.empty(n, dtype=np.float32)
+    for i in range(n):  # torchcrepe.filter.median / mean, window 3, edges over the 2 samples inside
+        s, e = max(0, i - 1), min(n, i + 2)
+        w3 = np.sort(per[s:e])
+        pm[i] = w3[(len(w3) - 1) // 2]
+        v = f0[s:e]
+        fm[i] = ((v[0] + v[1]) + v[2]) / np.float32(3.0) if len(v) == 3 else (v.sum(dtype=np.float32) / np.float32(len(v)))
+    fm[pm < threshold] = 0
+    return fm, pm, probs

@@ -1,5 +1,7 @@
 // extern "C" boundary (include/rvcx.h). Every entry point converts C++ exceptions into an
 // rvcx_status and stores the message for rvcx_last_error.
+#include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -396,6 +398,48 @@ int rvcx_crepe(rvcx_ctx* ctx, const float* d_audio, int64_t n, float f0_min, flo
     const int64_t F = crepe_forward(*ctx, d_audio, n, f0_min, f0_max, threshold, d_f0, nullptr, d_periodicity,
                                     d_probs, static_cast<hipStream_t>(stream));
     if (frames_out) *frames_out = F;
+  });
+}
+
+int rvcx_crepe_ex(rvcx_ctx* ctx, const float* d_audio, int64_t n, float f0_min, float f0_max, float threshold,
+                  int semantics, const float* d_dither, float* d_f0, float* d_periodicity, float* d_probs,
+                  int64_t cap_frames, int64_t* frames_out, void* stream) {
+  return guard(ctx, [&] {
+    if (!ctx->ready[RVCX_MODEL_CREPE]) throw Error(RVCX_E_STATE, "crepe weights not finalized");
+    if (!d_audio || !d_f0 || n <= 0 || semantics < 0 || semantics > 1 || (d_dither && semantics != 1))
+      throw Error(RVCX_E_INVALID, "rvcx_crepe_ex: bad arguments");
+    if (cap_frames < 1 + n / 160) throw Error(RVCX_E_SHAPE, "rvcx_crepe_ex: output capacity below 1 + n/160 frames");
+    set_device(ctx);
+    const int64_t F = crepe_forward(*ctx, d_audio, n, f0_min, f0_max, threshold, d_f0, nullptr, d_periodicity, d_probs,
+                                    static_cast<hipStream_t>(stream), semantics, d_dither);
+    if (frames_out) *frames_out = F;
+  });
+}
+
+int rvcx_crepe_decode(rvcx_ctx* ctx, const float* d_probs, int64_t F, float f0_min, float f0_max, float threshold,
+                      int semantics, const float* d_dither, float* d_f0, float* d_periodicity, void* stream) {
+  return guard(ctx, [&] {
+    if (!d_probs || !d_f0 || F <= 0 || F > INT32_MAX / 360 || semantics < 0 || semantics > 1 ||
+        (d_dither && semantics != 1) || !(f0_min > 0.f) || !(f0_max >= f0_min))
+      throw Error(RVCX_E_INVALID, "rvcx_crepe_decode: bad arguments");
+    set_device(ctx);
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    float* f0r = ctx->buf<float>("cr.f0raw", (size_t)F, s);
+    float* pr = ctx->buf<float>("cr.perraw", (size_t)F, s);
+    const double off = 1997.3794084376191;
+    if (semantics == 1) {
+      const int minidx = (int)std::min(360.0, std::max(0.0, std::floor((1200.0 * std::log2(f0_min / 10.0) - off) / 20.0)));
+      const int maxidx = (int)std::min(360.0, std::max(0.0, std::ceil((1200.0 * std::log2(f0_max / 10.0) - off) / 20.0)));
+      if (minidx >= maxidx) throw Error(RVCX_E_INVALID, "rvcx_crepe_decode: [f0_min, f0_max] covers no pitch bin");
+      float* lp = ctx->buf<float>("cr.lp", (size_t)F * 360, s);
+      int* ptr = ctx->buf<int>("cr.ptr", (size_t)F * 360, s);
+      int* bins = ctx->buf<int>("cr.bins", (size_t)F, s);
+      check(crepe_decode_viterbi(d_probs, (int)F, minidx, maxidx, d_dither, threshold, lp, ptr, bins, f0r, pr, d_f0,
+                                 nullptr, d_periodicity, s), "crepe_decode_viterbi");
+    } else {
+      check(crepe_decode(d_probs, (int)F, 1200.0 * std::log2(f0_min / 10.0), 1200.0 * std::log2(f0_max / 10.0),
+                         threshold, f0r, pr, d_f0, nullptr, d_periodicity, s), "crepe_decode");
+    }
   });
 }
 

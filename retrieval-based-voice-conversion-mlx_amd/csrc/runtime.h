@@ -241,7 +241,8 @@ int64_t split_intervals(Ctx& c, const double* audio, int64_t n, int sr, double s
                         int64_t* iv, int64_t cap, hipStream_t s);
 // CREPE.get_f0 (rvc_mlx/lib/mlx/crepe.py:282-325) on audio [n] fp32: returns F = 1 + n/160
 int64_t crepe_forward(Ctx& c, const float* audio, int64_t n, double f0_min, double f0_max, float thr, float* f0,
-                      double* f0d, float* per, float* probs, hipStream_t s);
+                      double* f0d, float* per, float* probs_out, hipStream_t s, int sem = 0,
+                      const float* dither = nullptr);
 int64_t hubert_forward(Ctx& c, const float* audio, int64_t n, int version, float* feats, int64_t cap,
                        hipStream_t s);
 // HuBERT in three parts, so a caller can issue the encoder's last layers later on another stream:

@@ -114,10 +114,13 @@ void finalize_crepe(Ctx& c) {
 
 // CREPE.get_f0 (crepe.py:282-325) over audio [n] fp32 @16 kHz: F = 1 + n/160 frames. Writes the filtered f0
 // (fp32 [F]; fp64 copy when f0d), the filtered periodicity and the raw probabilities [F][360] when asked.
+// sem 1: rvc/'s CREPE.get_f0 instead (rvc/lib/predictors/f0.py:31-55): torchcrepe.predict's framing (zero padding,
+// unbiased std) and viterbi decode (dither [F] cents from the caller, or none), median / mean of 3, f0 = 0 where the
+// periodicity < thr.
 int64_t crepe_forward(Ctx& c, const float* audio, int64_t n, double f0_min, double f0_max, float thr, float* f0,
-                      double* f0d, float* per, float* probs_out, hipStream_t s) {
+                      double* f0d, float* per, float* probs_out, hipStream_t s, int sem, const float* dither) {
   if (!c.ready[M]) throw Error(RVCX_E_STATE, "crepe weights not finalized");
-  if (n <= WIN / 2) throw Error(RVCX_E_INVALID, "crepe: input shorter than 513 samples (reflect pad of 512)");
+  if (sem == 0 && n <= WIN / 2) throw Error(RVCX_E_INVALID, "crepe: input shorter than 513 samples (reflect pad of 512)");
   if (!(f0_min > 0.0) || !(f0_max >= f0_min)) throw Error(RVCX_E_INVALID, "crepe: need 0 < f0_min <= f0_max");
   const int64_t F = 1 + n / HOP;
   int cap[6];
@@ -133,7 +136,7 @@ int64_t crepe_forward(Ctx& c, const float* audio, int64_t n, double f0_min, doub
   float* hp = c.buf<float>("cr.pool", (size_t)nb * 128 * cap[0], s);
   for (int64_t f0i = 0; f0i < F; f0i += nb) {
     const int B = (int)std::min<int64_t>(nb, F - f0i);
-    check(crepe_frames(audio, n, f0i, B, fr, FRAME_LD, s), "crepe_frames");
+    check(crepe_frames(audio, n, f0i, B, fr, FRAME_LD, s, sem), "crepe_frames");
     {  // conv1: rows of 32 samples every 4 (376 rows cover the 1532-sample padded frame), 16 taps at dilation 8
       ConvArgs a = conv1d_args(fr, 4, (FRAME_LD - 32) / 4 + 1, 32, c.W("cr.conv1.w"), cap[0], K1 / 32, 8, 0,
                                c.W("cr.conv1.b"), hc, 256, B);
@@ -168,6 +171,20 @@ int64_t crepe_forward(Ctx& c, const float* audio, int64_t n, double f0_min, doub
   }
   float* f0r = c.buf<float>("cr.f0raw", (size_t)F, s);
   float* pr = c.buf<float>("cr.perraw", (size_t)F, s);
+  if (sem == 1) {
+    // torchcrepe.postprocess: bins below frequency_to_bins(fmin) (floor) and from frequency_to_bins(fmax, ceil) on
+    // are masked (clamped to the 360 bins here)
+    const double off = 1997.3794084376191;
+    const int minidx = (int)std::min(360.0, std::max(0.0, std::floor((1200.0 * std::log2(f0_min / 10.0) - off) / 20.0)));
+    const int maxidx = (int)std::min(360.0, std::max(0.0, std::ceil((1200.0 * std::log2(f0_max / 10.0) - off) / 20.0)));
+    if (minidx >= maxidx) throw Error(RVCX_E_INVALID, "crepe: [f0_min, f0_max] covers no pitch bin");
+    float* lp = c.buf<float>("cr.lp", (size_t)F * BINS, s);
+    int* ptr = c.buf<int>("cr.ptr", (size_t)F * BINS, s);
+    int* bins = c.buf<int>("cr.bins", (size_t)F, s);
+    check(crepe_decode_viterbi(probs, (int)F, minidx, maxidx, dither, thr, lp, ptr, bins, f0r, pr, f0, f0d, per, s),
+          "crepe_decode_viterbi");
+    return F;
+  }
   const double lo = 1200.0 * std::log2(f0_min / 10.0), hi = 1200.0 * std::log2(f0_max / 10.0);
   check(crepe_decode(probs, (int)F, lo, hi, thr, f0r, pr, f0, f0d, per, s), "crepe_decode");
   return F;

@@ -228,8 +228,9 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
                             double* f0_out, hipStream_t s) {
   if (c.hp_order == 0) throw Error(RVCX_E_STATE, "pipeline: high-pass filter not configured");
   if (o.t_pad < 0 || o.t_pad_tgt < 0 || o.t_pad >= n) throw Error(RVCX_E_INVALID, "pipeline: bad t_pad");
-  if (o.f0_method != 0 && o.f0_method != 1) throw Error(RVCX_E_INVALID, "pipeline: f0_method must be 0 (rmvpe) or 1 (crepe)");
-  if (o.f0_method == 1 && c.scfg.f0 && !c.ready[RVCX_MODEL_CREPE])
+  if (o.f0_method < 0 || o.f0_method > 2)
+    throw Error(RVCX_E_INVALID, "pipeline: f0_method must be 0 (rmvpe), 1 (crepe, MLX) or 2 (crepe, rvc/)");
+  if (o.f0_method >= 1 && c.scfg.f0 && !c.ready[RVCX_MODEL_CREPE])
     throw Error(RVCX_E_STATE, "pipeline: f0_method crepe but no CREPE weights finalized");
   if (o.index_rate > 0 && !c.ivf) throw Error(RVCX_E_STATE, "pipeline: index_rate > 0 but no feature index loaded");
   if (o.index_rate > 0 && c.ivf->view.d != c.scfg.emb_dim)
@@ -330,10 +331,11 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
   float* pitchf = nullptr;
   if (guided) {
   double* f0 = c.buf<double>("pl.f0", (size_t)F, s);
-  if (o.f0_method == 1) {
+  if (o.f0_method >= 1) {
     // CREPE (PitchExtractor.extract, rvc_mlx/lib/mlx/pitch_extractors.py:155-156, with PipelineMLX's f0_min 50 /
-    // f0_max 1100 and CREPE.get_f0's threshold 0.1): no BiGRU, so HuBERT's remaining layers go out first and
-    // overlap the CREPE convs on the aux stream
+    // f0_max 1100 and CREPE.get_f0's threshold 0.1; f0_method 2: rvc/'s CREPE.get_f0, pipeline.py:223-234, viterbi
+    // decode without its dither): no BiGRU, so HuBERT's remaining layers go out first and overlap the CREPE convs on
+    // the aux stream
     if (c.before_gru) {
       auto rest = std::move(c.before_gru);
       c.before_gru = nullptr;
@@ -341,7 +343,7 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
       rest(s);
     }
     float* f0f = c.buf<float>("pl.f0f", (size_t)F, s);
-    crepe_forward(c, pad32, m, 50.0, 1100.0, 0.1f, f0f, f0, nullptr, nullptr, s);
+    crepe_forward(c, pad32, m, 50.0, 1100.0, 0.1f, f0f, f0, nullptr, nullptr, s, o.f0_method == 2 ? 1 : 0);
   } else {
     rmvpe_forward(c, pad32, m, o.rmvpe_threshold > 0 ? o.rmvpe_threshold : 0.03f, f0, F, nullptr, s);
   }
@@ -426,8 +428,9 @@ int64_t pipeline_forward_batch(Ctx& c, const double* audio, int64_t n, int64_t l
   if (B < 1) throw Error(RVCX_E_INVALID, "pipeline_batch: B < 1");
   if (c.hp_order == 0) throw Error(RVCX_E_STATE, "pipeline: high-pass filter not configured");
   if (o.t_pad < 0 || o.t_pad_tgt < 0 || o.t_pad >= n) throw Error(RVCX_E_INVALID, "pipeline: bad t_pad");
-  if (o.f0_method != 0 && o.f0_method != 1) throw Error(RVCX_E_INVALID, "pipeline: f0_method must be 0 (rmvpe) or 1 (crepe)");
-  if (o.f0_method == 1 && c.scfg.f0 && !c.ready[RVCX_MODEL_CREPE])
+  if (o.f0_method < 0 || o.f0_method > 2)
+    throw Error(RVCX_E_INVALID, "pipeline: f0_method must be 0 (rmvpe), 1 (crepe, MLX) or 2 (crepe, rvc/)");
+  if (o.f0_method >= 1 && c.scfg.f0 && !c.ready[RVCX_MODEL_CREPE])
     throw Error(RVCX_E_STATE, "pipeline: f0_method crepe but no CREPE weights finalized");
   if (o.t_max > 0 && n + 160 > o.t_max)
     throw Error(RVCX_E_INVALID, "pipeline_batch: utterances longer than t_max take the single-utterance path");
@@ -456,10 +459,11 @@ int64_t pipeline_forward_batch(Ctx& c, const double* audio, int64_t n, int64_t l
   int32_t* pitch = nullptr;
   float* pitchf = nullptr;
   if (guided) {
-  if (o.f0_method == 1) {  // CREPE per utterance (frames of all rows would not batch any better: B x F frames)
+  if (o.f0_method >= 1) {  // CREPE per utterance (frames of all rows would not batch any better: B x F frames)
     float* f0f = c.buf<float>("pb.f0f", (size_t)F, s);
     for (int b = 0; b < B; ++b)
-      crepe_forward(c, pad32 + (size_t)b * ldm, m, 50.0, 1100.0, 0.1f, f0f, f0 + (size_t)b * F, nullptr, nullptr, s);
+      crepe_forward(c, pad32 + (size_t)b * ldm, m, 50.0, 1100.0, 0.1f, f0f, f0 + (size_t)b * F, nullptr, nullptr, s,
+                    o.f0_method == 2 ? 1 : 0);
   } else {
     rmvpe_forward_b(c, pad32, m, ldm, B, o.rmvpe_threshold > 0 ? o.rmvpe_threshold : 0.03f, f0, F, hidden_out, s);
   }

@@ -215,10 +215,16 @@ hipError_t flash_attn(const float* qkv, int ldq, int B, int T, int nh, int dk, f
 // CREPE (crepe.hip): frames [nf][ld] (254 zeros | 1024 normalised samples | 254 zeros) of frames f_first..;
 // relu -> BatchNorm (bn = mean | 1/sqrt(var+eps) | gamma | beta, C each) -> max over row pairs [rows_in][C] ->
 // [rows_in/2][C]; decode + 3-tap filters: probs [F][360] -> f0 (fp32), f0d (fp64, optional), per (optional)
-hipError_t crepe_frames(const float* audio, long long n, long long f_first, int nf, float* out, int ld, hipStream_t s);
+hipError_t crepe_frames(const float* audio, long long n, long long f_first, int nf, float* out, int ld, hipStream_t s,
+                        int torch_sem = 0);
 hipError_t crepe_relu_bn_pool(const float* x, long long rows_in, int C, const float* bn, float* y, hipStream_t s);
 hipError_t crepe_decode(const float* probs, int F, double lo_cents, double hi_cents, float thr, float* f0_raw,
                         float* per_raw, float* f0, double* f0d, float* per, hipStream_t s);
+// torchcrepe's viterbi decode + rvc/'s filters (bins [minidx, maxidx) allowed; dither [F] cents or NULL): workspace
+// lp [F][360] fp32, ptr [F][360] int32, bins [F] int32
+hipError_t crepe_decode_viterbi(const float* probs, int F, int minidx, int maxidx, const float* dither, float thr,
+                                float* lp, int* ptr, int* bins, float* f0_raw, float* per_raw, float* f0, double* f0d,
+                                float* per, hipStream_t s);
 hipError_t noise_conv_add(const float* har, long long har_bs, int stride, int taps, const float* wf, const float* nb,
                           float* y, int B, int T, int C, hipStream_t s);
 hipError_t upsample2_protect(const float* feats, const float* feats0, int L, int D, float* out, int T, const float* pitchf,

@@ -29,7 +29,8 @@ EXPORTS = [
     "rvcx_rt_geometry", "rvcx_rt_reset", "rvcx_rt_process", "rvcx_hubert_batch", "rvcx_rmvpe_batch",
     "rvcx_pipeline_batch", "rvcx_set_highpass_sos", "rvcx_highpass_pad", "rvcx_device_status", "rvcx_index_parse",
     "rvcx_set_conv_math", "rvcx_conv1d", "rvcx_conv2d3x3", "rvcx_resblock_pair", "rvcx_crepe", "rvcx_split_audio",
-    "rvcx_workspace_bytes", "rvcx_set_workspace", "rvcx_workspace_info",
+    "rvcx_workspace_bytes", "rvcx_set_workspace", "rvcx_workspace_info", "rvcx_crepe_ex",
+    "rvcx_crepe_decode",
 ]
 
 
@@ -129,6 +130,8 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "rvcx_f0_autotune": (i32, [vp, vp, i64, f64, i32, vp]),
         "rvcx_rmvpe_decode": (i32, [vp, vp, i64, f32, vp, vp]),
         "rvcx_crepe": (i32, [vp, vp, i64, f32, f32, f32, vp, vp, vp, i64, P(i64), vp]),
+        "rvcx_crepe_ex": (i32, [vp, vp, i64, f32, f32, f32, i32, vp, vp, vp, vp, i64, P(i64), vp]),
+        "rvcx_crepe_decode": (i32, [vp, vp, i64, f32, f32, f32, i32, vp, vp, vp, vp]),
         "rvcx_split_audio": (i32, [vp, vp, i64, i32, f64, i32, P(i64), i64, P(i64), vp]),
         "rvcx_index_load": (i32, [vp, vp, i64]),
         "rvcx_index_unload": (i32, [vp]),

@@ -135,9 +135,11 @@ class Engine:
                                                            else "tiny")
 
     def crepe(self, audio, f0_min: float = 50.0, f0_max: float = 1100.0, threshold: float = 0.1,
-              want_periodicity: bool = False, want_probs: bool = False):
+              want_periodicity: bool = False, want_probs: bool = False, semantics: str = "mlx", dither=None):
         """CREPE.get_f0 (rvc_mlx/lib/mlx/crepe.py:282-325): audio [N] (16 kHz) -> f0 fp32 [1 + N//160] on device
-        (and the filtered periodicity [F], the probabilities [F, 360])."""
+        (and the filtered periodicity [F], the probabilities [F, 360]). semantics="rvc": rvc/'s CREPE.get_f0
+        (torchcrepe.predict + viterbi, rvc/lib/predictors/f0.py:31-55; rvcx_crepe_ex); dither: its [F] cents noise
+        (torchcrepe draws scipy.stats.triang(c=0.5, loc=-20, scale=40)), None = none."""
         t = self.torch
         a = self._dev(audio, t.float32).reshape(-1)
         n = a.numel()
@@ -146,15 +148,33 @@ class Engine:
         per = t.empty((F,), dtype=t.float32, device=self.device) if want_periodicity else None
         probs = t.empty((F, 360), dtype=t.float32, device=self.device) if want_probs else None
         fo = ctypes.c_int64(0)
-        self._check(self.lib.rvcx_crepe(self.ctx, a.data_ptr(), n, float(f0_min), float(f0_max), float(threshold),
-                                        f0.data_ptr(), _ptr(per), _ptr(probs), F, ctypes.byref(fo), self.stream()),
-                    "crepe")
+        sem = {"mlx": 0, "rvc": 1}[semantics]
+        d = None if dither is None else self._dev(dither, t.float32).reshape(-1)
+        if d is not None and d.numel() != F:
+            raise ValueError(f"dither needs {F} values")
+        self._check(self.lib.rvcx_crepe_ex(self.ctx, a.data_ptr(), n, float(f0_min), float(f0_max), float(threshold),
+                                           sem, _ptr(d), f0.data_ptr(), _ptr(per), _ptr(probs), F, ctypes.byref(fo),
+                                           self.stream()), "crepe")
         out = [f0]
         if want_periodicity:
             out.append(per)
         if want_probs:
             out.append(probs)
         return out[0] if len(out) == 1 else tuple(out)
+
+    def crepe_decode(self, probs, f0_min: float = 50.0, f0_max: float = 1100.0, threshold: float = 0.1,
+                     semantics: str = "rvc", dither=None):
+        """rvcx_crepe_decode: the decode + filters alone on probabilities [F][360] -> (f0 [F], periodicity [F])."""
+        t = self.torch
+        p = self._dev(probs, t.float32).contiguous()
+        F = int(p.shape[0])
+        f0 = t.empty((F,), dtype=t.float32, device=self.device)
+        per = t.empty((F,), dtype=t.float32, device=self.device)
+        d = None if dither is None else self._dev(dither, t.float32).reshape(-1)
+        self._check(self.lib.rvcx_crepe_decode(self.ctx, p.data_ptr(), F, float(f0_min), float(f0_max),
+                                               float(threshold), {"mlx": 0, "rvc": 1}[semantics], _ptr(d),
+                                               f0.data_ptr(), per.data_ptr(), self.stream()), "crepe_decode")
+        return f0, per
 
     @property
     def upp(self) -> int:

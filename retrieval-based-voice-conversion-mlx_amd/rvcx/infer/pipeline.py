@@ -39,16 +39,16 @@ class Config:
 
 class PipelineRVCX:
     # pipeline_mlx.py:82 / pitch_extractors.py:44 minus the pyworld CPU methods (dio, pm, harvest). "crepe" and
-    # "crepe-tiny" run CREPE as rvc_mlx/lib/mlx/crepe.py defines it (reflect padding, biased std, weighted-argmax
-    # decode) and therefore need semantics="mlx": the rvc/ path calls torchcrepe.predict (zero padding, unbiased
-    # std, viterbi decode; rvc/lib/predictors/f0.py:40-53), which is not reproduced. "fcpe" is the MLX stub's RMVPE
-    # with threshold 0.006 x 5 (rvc_mlx/lib/mlx/fcpe.py:129-132) and needs semantics="mlx" too (rvc/'s torchfcpe
-    # model is not available).
+    # "crepe-tiny" run CREPE as each side defines it: semantics="mlx" as rvc_mlx/lib/mlx/crepe.py (reflect padding,
+    # biased std, weighted-argmax decode), semantics="rvc" as rvc/lib/predictors/f0.py:31-55 (torchcrepe.predict:
+    # zero padding, unbiased std, viterbi decode; its triangular dither of the decoded cents only with
+    # crepe_dither=True in get_f0, as it is random; pipeline() decodes without it). "fcpe" is the MLX stub's RMVPE with threshold 0.006 x 5
+    # (rvc_mlx/lib/mlx/fcpe.py:129-132) and needs semantics="mlx" (rvc/'s torchfcpe model is not available).
     SUPPORTED_F0_METHODS = ("rmvpe", "crepe", "crepe-tiny", "fcpe")
 
     def __init__(self, tgt_sr, config, hubert_model: Optional[HubertModel] = None,
                  rmvpe_model: Optional[RMVPE0Predictor] = None, f0_method: str = "rmvpe", semantics: str = "rvc",
-                 crepe_weights=None):
+                 crepe_weights=None, crepe_dither: bool = False):
         if semantics not in ("rvc", "mlx"):
             raise ValueError("semantics must be 'rvc' or 'mlx'")
         self.x_pad, self.x_query, self.x_center, self.x_max = config.x_pad, config.x_query, config.x_center, \
@@ -69,6 +69,7 @@ class PipelineRVCX:
         self.hubert_model = hubert_model
         self.rmvpe_model = rmvpe_model
         self.semantics = semantics
+        self.crepe_dither = bool(crepe_dither)
         # {"full": path-or-state, "tiny": ...} (or one path for "full"); None = $RVCX_CREPE_DIR/crepe_{model}.npz
         self.crepe_weights = crepe_weights if isinstance(crepe_weights, dict) or crepe_weights is None \
             else {"full": crepe_weights}
@@ -84,10 +85,6 @@ class PipelineRVCX:
         if m == "fcpe" and self.semantics != "mlx":
             raise ValueError("f0_method 'fcpe' needs torchfcpe's model on the rvc/ path (rvc/lib/predictors/f0.py:60-89); "
                              "semantics='mlx' runs the MLX port's FCPE (its RMVPE fallback)")
-        if m in ("crepe", "crepe-tiny") and self.semantics != "mlx":
-            raise ValueError(f"f0_method {m!r} on the rvc/ path is torchcrepe.predict with its viterbi decoder "
-                             "(rvc/lib/predictors/f0.py:40-53), which this path does not reproduce; semantics='mlx' "
-                             "runs the MLX port's CREPE (rvc_mlx/lib/mlx/crepe.py: weighted-argmax decode)")
 
     def _crepe(self, eng, f0_method):
         """Load the CREPE weights f0_method names into the engine (once per model kind)."""
@@ -101,7 +98,7 @@ class PipelineRVCX:
         """(f0_method, rmvpe_threshold) of rvcx_pipeline_opts for an f0 method name."""
         if f0_method in ("crepe", "crepe-tiny"):
             self._crepe(eng, f0_method)
-            return 1, 0.03
+            return (1 if self.semantics == "mlx" else 2), 0.03
         if f0_method == "fcpe":
             return 0, 0.006 * 5
         return 0, 0.03
@@ -148,6 +145,11 @@ class PipelineRVCX:
         xa = np.asarray(x, dtype=np.float32).reshape(-1)
         if method == 1:  # PitchExtractor.extract -> CREPE.get_f0(x, f0_min=50, f0_max=1100) (pipeline_mlx.py:140)
             f0 = eng.crepe(xa, self.f0_min, self.f0_max, 0.1).double()
+        elif method == 2:  # CREPE(...).get_f0(x, self.f0_min, self.f0_max, p_len, model) (pipeline.py:223-234)
+            dither = None
+            if self.crepe_dither:  # torchcrepe.convert.dither: scipy.stats.triang(c=0.5, loc=-20, scale=40)
+                dither = np.random.default_rng().triangular(-20.0, 0.0, 20.0, size=1 + len(xa) // 160)
+            f0 = eng.crepe(xa, self.f0_min, self.f0_max, 0.1, semantics="rvc", dither=dither).double()
         else:
             f0 = eng.rmvpe(xa, thr)
         shift = float(pitch)

@@ -50,3 +50,31 @@ def test_decode_known_answers():
     c1 = np.float32((oc.CENTS[200] + oc.CENTS[201]) / 2)
     np.testing.assert_allclose(f0[1], 10 * 2 ** (c1 / 1200), rtol=1e-6)
     assert f0[3] == np.float32(10.0) and per[3] == 0  # nothing in range: cents 0 -> 10 Hz, periodicity 0
+
+
+def test_rvc_semantics_oracle_framing_and_viterbi():
+    """oracle.crepe's restatement of rvc/'s CREPE (torchcrepe.predict): zero-padded frames with unit unbiased std
+    (the edge frames see the zeros), and a viterbi path that follows a clean track moving <= 1 bin per frame, masks
+    the bins outside [f0_min, f0_max) and keeps the track through a short low-probability gap."""
+    from oracle import crepe as oc
+
+    n = 16000
+    a = np.sin(2 * np.pi * 200.0 * np.arange(n) / 16000.0).astype(np.float32)
+    fr = oc.frame_audio_torch(a)
+    assert fr.shape == (1 + n // 160, 1024)
+    np.testing.assert_allclose(fr[50].std(ddof=1), 1.0, rtol=1e-5)
+    assert np.all(fr[0][:512] == fr[0][0])  # zero padding: the first half of frame 0 is one constant
+    F = 120
+    track = (120 + np.round(10 * np.sin(np.arange(F) / 8.0))).astype(int)
+    probs = np.full((F, 360), 0.05, dtype=np.float32)
+    probs[np.arange(F), track] = 0.99
+    probs[60:64] = 0.05  # a gap: the path stays near the track
+    bins = oc.viterbi_bins(probs, 50.0, 1100.0)
+    keep = np.r_[0:60, 64:F]
+    np.testing.assert_array_equal(bins[keep], track[keep])
+    assert np.all(np.abs(bins[60:64] - track[59]) <= 11)
+    lo, hi = oc.torchcrepe_bin_range(50.0, 1100.0)
+    assert (lo, hi) == (39, 308)
+    probs2 = probs.copy()
+    probs2[:, 20] = 1.0  # below f0_min: masked, never chosen
+    assert np.all(oc.viterbi_bins(probs2, 50.0, 1100.0) >= lo)

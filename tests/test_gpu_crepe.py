@@ -91,3 +91,76 @@ def test_pipeline_crepe_and_fcpe(engine, crepe_case):
     np.testing.assert_array_equal(pl.last_f0.cpu().numpy(), want.cpu().numpy())
     with pytest.raises(ValueError):
         PipelineMLX(48000, Config(), HubertModel(engine), RMVPE0Predictor(engine)).get_f0(x, 0, f0_method="fcpe")
+
+
+# ---------------------------------------------------------------- rvc/ semantics (torchcrepe.predict + viterbi)
+def test_crepe_rvc_semantics_vs_oracle(engine, crepe_case):
+    """rvc/'s CREPE.get_f0 (rvcx_crepe_ex semantics 1): the torchcrepe framing gives the oracle's probabilities
+    (oracle.crepe.frame_audio_torch + forward) to 1e-4, and the viterbi decode + filters with the same dither values
+    give the oracle's f0 / periodicity on the device's own probabilities."""
+    from oracle import crepe as oc
+
+    audio, cases = crepe_case
+    w = cases["tiny"][0]
+    engine.load_crepe(w)
+    F = 1 + len(audio) // 160
+    dither = np.random.default_rng(5).triangular(-20.0, 0.0, 20.0, size=F).astype(np.float32)
+    f0, per, probs = engine.crepe(audio, 50.0, 1100.0, 0.1, want_periodicity=True, want_probs=True, semantics="rvc",
+                                  dither=dither)
+    probs = probs.cpu().numpy()
+    probs_o = oc.forward(w, oc.frame_audio_torch(audio))
+    assert np.abs(probs - probs_o).max() / np.abs(probs_o).max() < 1e-4
+    f0_o, per_o, _ = oc.get_f0_rvc(w, audio, dither=dither, probs=probs)
+    np.testing.assert_allclose(f0.cpu().numpy(), f0_o, rtol=2e-6, atol=0)
+    np.testing.assert_array_equal(per.cpu().numpy(), per_o)
+
+
+def _structured_probs(F, seed):
+    """sigmoid-like outputs with a moving pitch track (a vibrato, an octave jump, a gap of unvoiced frames)."""
+    rng = np.random.default_rng(seed)
+    t = np.arange(F)
+    track = 150 + 40 * np.sin(2 * np.pi * t / 90.0)
+    track[F // 2:] += 60
+    probs = rng.uniform(0.0, 0.35, size=(F, 360))
+    bump = 0.95 * np.exp(-0.5 * ((np.arange(360)[None, :] - track[:, None]) / 1.5) ** 2)
+    probs = np.maximum(probs, bump)
+    probs[F // 3:F // 3 + 12] = rng.uniform(0.0, 0.06, size=(12, 360))
+    return probs.astype(np.float32)
+
+
+@pytest.mark.parametrize("lo,hi,thr", [(50.0, 1100.0, 0.1), (100.0, 400.0, 0.5)])
+def test_crepe_viterbi_decode_vs_oracle(engine, lo, hi, thr):
+    """The viterbi decode alone (rvcx_crepe_decode) on structured probabilities: the oracle's restatement of
+    torchcrepe.decode.viterbi / librosa.sequence.viterbi and rvc/'s filters, f0 to fp32 rounding, the periodicity
+    exactly; the path follows the track (a bin-exact decode, not a constant)."""
+    from oracle import crepe as oc
+
+    probs = _structured_probs(400, 9)
+    f0, per = engine.crepe_decode(probs, lo, hi, thr, semantics="rvc")
+    f0_o, per_o, _ = oc.get_f0_rvc(None, None, lo, hi, thr, probs=probs)
+    np.testing.assert_allclose(f0.cpu().numpy(), f0_o, rtol=2e-6, atol=0)
+    np.testing.assert_array_equal(per.cpu().numpy(), per_o)
+    voiced = f0_o > 0
+    assert 0.5 < voiced.mean() < 1.0 and len(np.unique(np.round(f0_o[voiced]))) > 20
+
+
+def test_pipeline_crepe_rvc_semantics(engine, crepe_case):
+    """PipelineRVCX(semantics="rvc") with f0_method crepe-tiny: get_f0 is rvcx_crepe_ex semantics 1 + f0_post, and the
+    device pipeline (rvcx_pipeline_opts.f0_method 2) decodes CREPE on the high-passed, t_pad-padded input."""
+    from rvcx.infer import Config, HubertModel, PipelineMLX, RMVPE0Predictor, Synthesizer
+
+    audio, cases = crepe_case
+    w = cases["tiny"][0]
+    pl = PipelineMLX(48000, Config(), HubertModel(engine), RMVPE0Predictor(engine), semantics="rvc",
+                     crepe_weights={"tiny": w})
+    x = audio.astype(np.float64)
+    coarse, f0 = pl.get_f0(x, len(x) // 160, f0_method="crepe-tiny")
+    ref = engine.crepe(audio, 50.0, 1100.0, 0.1, semantics="rvc").double()
+    c_ref, _, f_ref = engine.f0_post(ref, 0.0)
+    np.testing.assert_array_equal(coarse, c_ref.cpu().numpy())
+    np.testing.assert_array_equal(f0, f_ref.cpu().numpy())
+    y = pl.pipeline(None, Synthesizer(engine), 0, x, f0_method="crepe-tiny", seed=3)
+    assert y.ndim == 1 and np.isfinite(y).all() and np.abs(y).max() > 0
+    _, p32 = engine.highpass_pad(x, pl.t_pad)
+    want = engine.f0_post(engine.crepe(p32, 50.0, 1100.0, 0.1, semantics="rvc").double(), 0.0)[2]
+    np.testing.assert_array_equal(pl.last_f0.cpu().numpy(), want.cpu().numpy())
