@@ -360,19 +360,23 @@ __global__ __launch_bounds__(64) void k_kv_split16(const float* __restrict__ qkv
   out[(fr + 1) * 64] = __builtin_bit_cast(uint4, q[1]);
 }
 
-template <int DK>
-__global__ __launch_bounds__(64, 2) void k_flash_attn_h16(const float* __restrict__ qkv, int ldq, int T, int nh, int H,
-                                                       float qscale, int kb_per_split, const float* __restrict__ rel_k,
-                                                       const float* __restrict__ rel_v, int window,
-                                                       const float* __restrict__ mask, const uint4* __restrict__ img,
-                                                       float* __restrict__ part_o, float* __restrict__ part_ml) {
+// NW waves per block: the same query block, key splits blockIdx.y * NW + wave, merged in LDS at the end into one
+// partial per block (the split partials written to HBM and re-read by k_flash_combine drop NW-fold; NW = 1: one
+// wave, one partial each)
+template <int DK, int NW>
+__global__ __launch_bounds__(64 * NW, 2) void k_flash_attn_h16(
+    const float* __restrict__ qkv, int ldq, int T, int nh, int H, float qscale, int kb_per_split,
+    const float* __restrict__ rel_k, const float* __restrict__ rel_v, int window, const float* __restrict__ mask,
+    const uint4* __restrict__ img, float* __restrict__ part_o, float* __restrict__ part_ml) {
   constexpr int NS = DK / 16;
   constexpr int NT = DK / 32;
   constexpr int FR = NS * 2 + NT * 2 * 2;
-  __shared__ float relq[FA_Q][FA_NW + 1];
-  __shared__ float pband[FA_Q][FA_NW + 1];
-  const int lane = threadIdx.x, li = lane & 31, hk = lane >> 5;
-  const int q0 = blockIdx.x * FA_Q, split = blockIdx.y, bh = blockIdx.z;
+  __shared__ float relq_s[NW][FA_Q][FA_NW + 1];
+  __shared__ float pband_s[NW][FA_Q][FA_NW + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, li = lane & 31, hk = lane >> 5;
+  float (*relq)[FA_NW + 1] = relq_s[wave];
+  float (*pband)[FA_NW + 1] = pband_s[wave];
+  const int q0 = blockIdx.x * FA_Q, split = blockIdx.y * NW + wave, bh = blockIdx.z;
   const int b = bh / nh, h = bh % nh;
   const int BH = gridDim.z;
   const float* base = qkv + (long long)b * T * ldq;
@@ -539,32 +543,73 @@ __global__ __launch_bounds__(64, 2) void k_flash_attn_h16(const float* __restric
       }
     }
   }
-  float* ot = &relq[0][0];
-  const long long slab = ((long long)split * BH + bh) * T;
+  if constexpr (NW == 1) {
+    float* ot = &relq[0][0];
+    const long long slab = ((long long)split * BH + bh) * T;
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int t = 0; t < NT; ++t) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-    for (int r = 0; r < 16; ++r) ot[li * (FA_NW + 1) + crow(r, hk)] = (o[t][r] + o2[t][r] * H16_LO_INV) * 16.f;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      for (int r = 0; r < 16; ++r) ot[li * (FA_NW + 1) + crow(r, hk)] = (o[t][r] + o2[t][r] * H16_LO_INV) * 16.f;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int idx = k * 64 + lane, rr = idx >> 3, c4 = (idx & 7) * 4;
-      if (q0 + rr < T) {
-        const float* src = ot + rr * (FA_NW + 1) + c4;
-        const f32x4 v = {src[0], src[1], src[2], src[3]};
-        *reinterpret_cast<f32x4*>(part_o + (slab + q0 + rr) * DK + 32 * t + c4) = v;
+      for (int k = 0; k < 4; ++k) {
+        const int idx = k * 64 + lane, rr = idx >> 3, c4 = (idx & 7) * 4;
+        if (q0 + rr < T) {
+          const float* src = ot + rr * (FA_NW + 1) + c4;
+          const f32x4 v = {src[0], src[1], src[2], src[3]};
+          *reinterpret_cast<f32x4*>(part_o + (slab + q0 + rr) * DK + 32 * t + c4) = v;
+        }
       }
     }
-  }
-  if (qok && hk == 0) {
-    const long long row = slab + i;
-    part_ml[2 * row] = m_run;
-    part_ml[2 * row + 1] = l_run;
+    if (qok && hk == 0) {
+      const long long row = slab + i;
+      part_ml[2 * row] = m_run;
+      part_ml[2 * row + 1] = l_run;
+    }
+  } else {
+    // block merge: M = max of the waves' running maxima per query, each wave's tile scaled by e^(m_w - M) and
+    // summed into LDS in wave order (deterministic), L likewise; one partial (M, L, sum) per block
+    __shared__ float mrow[NW][FA_Q];
+    __shared__ float lsum[FA_Q];
+    __shared__ float acc[FA_Q][DK + 4];
+    if (hk == 0) mrow[wave][li] = m_run;
+    __syncthreads();
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) M = fmaxf(M, mrow[w][li]);
+    const float e = m_run == -INFINITY ? 0.f : expf(m_run - M);
+    for (int w = 0; w < NW; ++w) {
+      if (wave == w) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float v = (o[t][r] + o2[t][r] * H16_LO_INV) * 16.f * e;
+            float& a = acc[li][32 * t + crow(r, hk)];
+            a = w == 0 ? v : a + v;
+          }
+        if (hk == 0) lsum[li] = w == 0 ? l_run * e : lsum[li] + l_run * e;
+      }
+      __syncthreads();
+    }
+    const long long slab = ((long long)blockIdx.y * BH + bh) * T;
+    for (int idx = threadIdx.x; idx < FA_Q * DK / 4; idx += 64 * NW) {
+      const int rr = idx / (DK / 4), c4 = (idx - rr * (DK / 4)) * 4;
+      if (q0 + rr < T) {
+        const f32x4 v = {acc[rr][c4], acc[rr][c4 + 1], acc[rr][c4 + 2], acc[rr][c4 + 3]};
+        *reinterpret_cast<f32x4*>(part_o + (slab + q0 + rr) * DK + c4) = v;
+      }
+    }
+    if (wave == 0 && qok && hk == 0) {
+      const long long row = slab + i;
+      part_ml[2 * row] = M;
+      part_ml[2 * row + 1] = lsum[li];
+    }
   }
 }
 
@@ -651,19 +696,37 @@ hipError_t flash_attn(const float* qkv, int ldq, int B, int T, int nh, int dk, f
   const int per = (kb + nsplit - 1) / nsplit;
   dim3 grid(qb, nsplit, B * nh);
   if (dk != 64 && dk != 96) return hipErrorInvalidValue;
+  int nparts = nsplit;  // partials the combine merges
   if (fa_h16()) {
     // the K / V images after the partials (the caller sized part_o with flash_attn_ws_floats)
     uint4* img = reinterpret_cast<uint4*>(part_o + (long long)nsplit * B * nh * T * dk);
     if ((reinterpret_cast<uintptr_t>(img) & 15) != 0) return hipErrorInvalidValue;
     dim3 g2(kb, B * nh, dk / 16 + dk / 16);  // NS K steps + 2 NT V^T pairs (NS = 2 NT)
+    // NW key splits per block merged in LDS (RVCX_FA_NW 1: one wave per split, every split a partial)
+    static const int nw_env = [] {
+      const char* e = std::getenv("RVCX_FA_NW");
+      return e ? std::atoi(e) : 4;
+    }();
+    const int NWB = (nw_env == 4 && nsplit >= 4) ? 4 : 1;
+    nparts = (nsplit + NWB - 1) / NWB;
+    const int per_w = (kb + nparts * NWB - 1) / (nparts * NWB);
+    dim3 gw(qb, nparts, B * nh);
     if (dk == 64) {
       hipLaunchKernelGGL(k_kv_split16<64>, g2, dim3(64), 0, s, qkv, ldq, T, nh, H, img);
-      hipLaunchKernelGGL(k_flash_attn_h16<64>, grid, dim3(64), 0, s, qkv, ldq, T, nh, H, qscale, per, rel_k, rel_v,
-                         window, mask, img, part_o, part_ml);
+      if (NWB == 4)
+        hipLaunchKernelGGL((k_flash_attn_h16<64, 4>), gw, dim3(256), 0, s, qkv, ldq, T, nh, H, qscale, per_w, rel_k,
+                           rel_v, window, mask, img, part_o, part_ml);
+      else
+        hipLaunchKernelGGL((k_flash_attn_h16<64, 1>), gw, dim3(64), 0, s, qkv, ldq, T, nh, H, qscale, per_w, rel_k,
+                           rel_v, window, mask, img, part_o, part_ml);
     } else {
       hipLaunchKernelGGL(k_kv_split16<96>, g2, dim3(64), 0, s, qkv, ldq, T, nh, H, img);
-      hipLaunchKernelGGL(k_flash_attn_h16<96>, grid, dim3(64), 0, s, qkv, ldq, T, nh, H, qscale, per, rel_k, rel_v,
-                         window, mask, img, part_o, part_ml);
+      if (NWB == 4)
+        hipLaunchKernelGGL((k_flash_attn_h16<96, 4>), gw, dim3(256), 0, s, qkv, ldq, T, nh, H, qscale, per_w, rel_k,
+                           rel_v, window, mask, img, part_o, part_ml);
+      else
+        hipLaunchKernelGGL((k_flash_attn_h16<96, 1>), gw, dim3(64), 0, s, qkv, ldq, T, nh, H, qscale, per_w, rel_k,
+                           rel_v, window, mask, img, part_o, part_ml);
     }
   } else if (dk == 64) {
     hipLaunchKernelGGL(k_flash_attn<64>, grid, dim3(64), 0, s, qkv, ldq, T, nh, H, qscale, per, rel_k, rel_v, window,
@@ -678,9 +741,9 @@ hipError_t flash_attn(const float* qkv, int ldq, int B, int T, int nh, int dk, f
   const int rpb = 4 * (64 / (dk / 4));  // rows per 256-thread block
   const unsigned nb = (unsigned)((rows + rpb - 1) / rpb);
   if (dk == 64)
-    hipLaunchKernelGGL(k_flash_combine<64>, dim3(nb), dim3(256), 0, s, part_o, part_ml, nsplit, B * nh, T, nh, out, ldo);
+    hipLaunchKernelGGL(k_flash_combine<64>, dim3(nb), dim3(256), 0, s, part_o, part_ml, nparts, B * nh, T, nh, out, ldo);
   else
-    hipLaunchKernelGGL(k_flash_combine<96>, dim3(nb), dim3(256), 0, s, part_o, part_ml, nsplit, B * nh, T, nh, out, ldo);
+    hipLaunchKernelGGL(k_flash_combine<96>, dim3(nb), dim3(256), 0, s, part_o, part_ml, nparts, B * nh, T, nh, out, ldo);
   return hipGetLastError();
 }
 
