@@ -164,3 +164,19 @@ def test_pipeline_crepe_rvc_semantics(engine, crepe_case):
     _, p32 = engine.highpass_pad(x, pl.t_pad)
     want = engine.f0_post(engine.crepe(p32, 50.0, 1100.0, 0.1, semantics="rvc").double(), 0.0)[2]
     np.testing.assert_array_equal(pl.last_f0.cpu().numpy(), want.cpu().numpy())
+
+
+@pytest.mark.parametrize("method", [1, 2])
+def test_pipeline_batch_crepe_rows_match_single(engine, crepe_case, method):
+    """rvcx_pipeline_batch with f0_method 1 (MLX CREPE) / 2 (rvc/'s CREPE, viterbi): each row's adjusted f0 equals
+    rvcx_pipeline_ex's on that utterance alone (CREPE runs per row in both), and the outputs are finite."""
+    audio, cases = crepe_case
+    engine.load_crepe(cases["tiny"][0])
+    engine.set_pipeline_highpass()
+    x = np.stack([audio.astype(np.float64), 0.7 * np.roll(audio, 4000).astype(np.float64)])
+    opts = engine.pipeline_opts(f0_method=method, protect=0.33)
+    y, f0 = engine.pipeline_batch(x, opts, sids=0, seed=3, want_f0=True)
+    assert torch.isfinite(y).all()
+    for b in range(2):
+        _, f0b = engine.pipeline_ex(x[b], opts, seed=3, want_f0=True)
+        np.testing.assert_array_equal(f0[b].cpu().numpy(), f0b.cpu().numpy())
