@@ -11,7 +11,9 @@ Model files (all loaded without executing anything from the file):
   * MLX ``.npz`` / ``.safetensors`` written by tools/convert_rvc_model.py (remapped names, MLX
     layouts, already fused) plus an optional sibling ``.json`` config list (infer_mlx.py:146-205).
 HuBERT/ContentVec and RMVPE weights come from local files only (no download: the reference's
-``load_embedding``/``from_pretrained`` fetch over the network, rvc/lib/utils.py:125-153).
+``load_embedding``/``from_pretrained`` fetch over the network, rvc/lib/utils.py:125-153): the MLX tree's
+``hubert_mlx.npz`` / ``rmvpe_mlx.npz`` (tools/convert_hubert.py, tools/convert_rmvpe.py layouts) or the
+torch ``pytorch_model.bin`` / ``model.safetensors`` / ``rmvpe.pt`` (``HUBERT_CANDIDATES``, ``RMVPE_CANDIDATES``).
 """
 from __future__ import annotations
 
@@ -30,9 +32,15 @@ from .pipeline import Config, PipelineRVCX
 # infer_mlx.py:130-176 defaults when an MLX file has no config (40 kHz v2)
 _MLX_DEFAULT_40K = SynthConfig(upsample_rates=(10, 10, 2, 2), upsample_kernel_sizes=(16, 16, 4, 4), sr=40000)
 
-HUBERT_CANDIDATES = ("rvc/models/embedders/contentvec/pytorch_model.bin",
+# Searched relative to the working directory, the MLX tree's own files first, as RVC_MLX does
+# (infer_mlx.py:258-264 for HuBERT; RMVPE0Predictor's default, rvc_mlx/lib/mlx/rmvpe.py:256-258), then the
+# rvc/ torch files (rvc/lib/utils.py:125-153, RMVPE.py:429-434).
+HUBERT_CANDIDATES = ("rvc_mlx/models/embedders/contentvec/hubert_mlx.npz",
+                     "rvc/models/embedders/contentvec/hubert_mlx.npz",
+                     "rvc/models/embedders/contentvec/pytorch_model.bin",
                      "rvc/models/embedders/contentvec/model.safetensors")
-RMVPE_CANDIDATES = ("rvc/models/predictors/rmvpe.pt",)
+RMVPE_CANDIDATES = ("rvc_mlx/models/predictors/rmvpe_mlx.npz",
+                    "rvc/models/predictors/rmvpe.pt")
 
 
 def mlx_to_reference_state(weights: Mapping[str, np.ndarray]) -> Dict[str, np.ndarray]:

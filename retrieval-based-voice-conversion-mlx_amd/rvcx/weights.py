@@ -6,10 +6,12 @@ Handles the on-disk formats of the path:
     (rvc/train/process/extract_model.py:57-109), loaded with
     ``torch.load(weights_only=True)`` only.
   - live torch parametrization names ``*.parametrizations.weight.original0/1``.
-  - MLX ``.npz`` / ``.safetensors`` exported by tools/convert_rvc_model.py are
-    NOT accepted here (their fusion adds +1e-8 to the norm,
-    tools/convert_rvc_model.py:357); they carry already-fused weights under
-    remapped keys, see ``unmap_mlx_keys``.
+  - the MLX tree's own HuBERT and RMVPE files (``hubert_mlx.npz``, tools/convert_hubert.py:36-70;
+    ``rmvpe_mlx.npz``, tools/convert_rmvpe.py:26-83): ``load_state_file`` recognises their names and
+    layouts and inverts them (``mlx_hubert_to_reference``, ``mlx_rmvpe_to_reference``).
+  - MLX voice ``.npz`` / ``.safetensors`` exported by tools/convert_rvc_model.py: already-fused weights
+    under remapped keys; ``unmap_mlx_keys`` here, the layouts in rvcx/infer/infer.py
+    ``mlx_to_reference_state``.
 
 Weight-norm fusion matches torch exactly (``torch._weight_norm``: w = g * v / ||v||,
 norm over every dim except ``dim``, no epsilon). ``dim`` is 0 for every RVC conv
@@ -91,20 +93,108 @@ def load_rvc_checkpoint(path: str):
 
 
 def load_state_file(path: str) -> Dict[str, np.ndarray]:
-    """Load a bare state dict (``rmvpe.pt``, ``pytorch_model.bin``, ``.safetensors``, ``.npz``)."""
+    """Load a bare state dict (``rmvpe.pt``, ``pytorch_model.bin``, ``.safetensors``, ``.npz``). MLX-tree
+    HuBERT / RMVPE files (``hubert_mlx.npz``, ``rmvpe_mlx.npz``) come back under the reference's torch names
+    and layouts."""
     if path.endswith(".safetensors"):
         from safetensors.numpy import load_file
 
-        return normalize_state(load_file(path))
+        return normalize_state(to_reference_layout(load_file(path)))
     if path.endswith(".npz"):
         with np.load(path, allow_pickle=False) as z:
-            return normalize_state({k: z[k] for k in z.files})
+            return normalize_state(to_reference_layout({k: z[k] for k in z.files}))
     import torch
 
     sd = torch.load(path, map_location="cpu", weights_only=True)
     if isinstance(sd, dict) and "weight" in sd and isinstance(sd["weight"], dict):
         sd = sd["weight"]
     return normalize_state(sd)
+
+
+def _np32(v) -> np.ndarray:
+    return np.asarray(v.detach().cpu().numpy() if hasattr(v, "detach") else v)
+
+
+def is_mlx_hubert(keys) -> bool:
+    """tools/convert_hubert.py:26-31 stores the fused positional-conv weight as ``encoder.pos_conv_embed.weight``
+    (no ``.conv.``); a torch/HF ContentVec state never has that key."""
+    return "encoder.pos_conv_embed.weight" in set(keys)
+
+
+def is_mlx_rmvpe(keys) -> bool:
+    """tools/convert_rmvpe.py:56-74 renames the BiGRU to ``fc.bigru.*`` and the classifier to ``fc.linear.*``."""
+    return any(k.startswith("fc.bigru.") or k.startswith("fc.linear.") or (k.startswith("unet.") and ".blocks." in k)
+               for k in keys)
+
+
+def mlx_hubert_to_reference(sd: Mapping[str, object]) -> Dict[str, np.ndarray]:
+    """Invert tools/convert_hubert.py:26-67: ``encoder.pos_conv_embed.weight`` (O, K, I/G), already fused by
+    the weight-norm parametrization) -> ``encoder.pos_conv_embed.conv.weight`` (O, I/G, K);
+    ``encoder.pos_conv_embed.bias`` -> ``...conv.bias``; the feature-encoder Conv1d weights (O, K, I) ->
+    (O, I, K); linears and norms unchanged (MLX nn.Linear is (O, I) like torch). A stray ``hubert.`` prefix
+    (convert_hubert.py:40-41 strips it) is dropped too."""
+    out: Dict[str, np.ndarray] = {}
+    for k, v in sd.items():
+        a = _np32(v)
+        n = k[len("hubert."):] if k.startswith("hubert.") else k
+        if n == "encoder.pos_conv_embed.weight":
+            n, a = "encoder.pos_conv_embed.conv.weight", a.transpose(0, 2, 1)
+        elif n == "encoder.pos_conv_embed.bias":
+            n = "encoder.pos_conv_embed.conv.bias"
+        elif n.startswith("feature_extractor.conv_layers.") and n.endswith(".conv.weight") and a.ndim == 3:
+            a = a.transpose(0, 2, 1)
+        out[n] = np.ascontiguousarray(a)
+    return out
+
+
+_RMVPE_BLOCK_INNER = {"conv1": "conv.0", "bn1": "conv.1", "conv2": "conv.3", "bn2": "conv.4"}
+_RMVPE_BLOCK = re.compile(r"^(unet\.(encoder|intermediate|decoder)\.layers\.\d+)\.blocks\.(\d+)\.([a-z0-9_]+)\.(.*)$")
+_RMVPE_DEC_HEAD = re.compile(r"^(unet\.decoder\.layers\.\d+)\.(conv1_trans|bn1)\.(.*)$")
+_RMVPE_GRU = re.compile(r"^fc\.bigru\.(forward|backward)_grus\.0\.(weight_ih|weight_hh|bias_ih|bias_hh)$")
+
+
+def mlx_rmvpe_to_reference(sd: Mapping[str, object]) -> Dict[str, np.ndarray]:
+    """Invert tools/convert_rmvpe.py:26-83 (E2E of rvc/lib/predictors/RMVPE.py:289-340):
+      * ``unet.{encoder,intermediate}.layers.L.blocks.B.X`` -> ``...layers.L.conv.B.Y`` and
+        ``unet.decoder.layers.L.blocks.B.X`` -> ``...layers.L.conv2.B.Y``, with the ConvBlockRes members
+        X = conv1 / bn1 / conv2 / bn2 -> Y = conv.0 / conv.1 / conv.3 / conv.4 (``shortcut`` unchanged);
+      * ``unet.decoder.layers.L.conv1_trans`` / ``.bn1`` -> ``.conv1.0`` / ``.conv1.1``;
+      * ``fc.bigru.{forward,backward}_grus.0.W`` -> ``fc.0.gru.W_l0`` / ``W_l0_reverse``; ``fc.linear`` -> ``fc.1``;
+      * Conv2d weights (O, H, W, I) -> (O, I, H, W); the ConvTranspose2d weight (O, H, W, I) -> (I, O, H, W)."""
+    out: Dict[str, np.ndarray] = {}
+    for k, v in sd.items():
+        a = _np32(v)
+        n, trans = k, False
+        m = _RMVPE_BLOCK.match(k)
+        if m:
+            head, part, blk, member, rest = m.groups()
+            holder = "conv2" if part == "decoder" else "conv"
+            n = f"{head}.{holder}.{blk}.{_RMVPE_BLOCK_INNER.get(member, member)}.{rest}"
+        else:
+            m = _RMVPE_DEC_HEAD.match(k)
+            if m:
+                head, member, rest = m.groups()
+                trans = member == "conv1_trans"
+                n = f"{head}.conv1.{0 if trans else 1}.{rest}"
+            else:
+                m = _RMVPE_GRU.match(k)
+                if m:
+                    n = f"fc.0.gru.{m.group(2)}_l0{'_reverse' if m.group(1) == 'backward' else ''}"
+                elif k.startswith("fc.linear."):
+                    n = "fc.1." + k[len("fc.linear."):]
+        if a.ndim == 4 and k.endswith("weight"):
+            a = a.transpose(3, 0, 1, 2) if trans else a.transpose(0, 3, 1, 2)
+        out[n] = np.ascontiguousarray(a)
+    return out
+
+
+def to_reference_layout(sd: Mapping[str, object]) -> Mapping[str, object]:
+    """MLX-tree HuBERT / RMVPE states -> reference names and layouts; any other state passes through."""
+    if is_mlx_hubert(sd.keys()):
+        return mlx_hubert_to_reference(sd)
+    if is_mlx_rmvpe(sd.keys()):
+        return mlx_rmvpe_to_reference(sd)
+    return sd
 
 
 _MLX_RULES = [

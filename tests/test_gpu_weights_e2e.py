@@ -155,3 +155,36 @@ def test_mlx_npz_model_matches_pth(model_files, hubert_w, rmvpe_w):
         finally:
             rvc.close()
     assert np.array_equal(outs[0], outs[1])
+
+
+def test_mlx_tree_hubert_rmvpe_files(model_files, monkeypatch):
+    """RVC_MLX(voice_mlx.npz) with the MLX tree's own hubert_mlx.npz / rmvpe_mlx.npz found where
+    the reference looks for them (infer_mlx.py:258-264, rvc_mlx/lib/mlx/rmvpe.py:256-258), written by the numpy
+    restatement of tools/convert_hubert.py / tools/convert_rmvpe.py (tests/mlx_convert.py). The pipeline output
+    must be bit-identical to the same voice with the torch ContentVec .bin and rmvpe.pt."""
+    from mlx_convert import hubert_to_mlx, rmvpe_to_mlx
+    from rvcx import synthetic
+    from rvcx.infer import RVC_MLX
+
+    d = model_files["dir"]
+    root = os.path.join(d, "mlx_tree")
+    os.makedirs(os.path.join(root, "rvc_mlx/models/embedders/contentvec"), exist_ok=True)
+    os.makedirs(os.path.join(root, "rvc_mlx/models/predictors"), exist_ok=True)
+    np.savez(os.path.join(root, "rvc_mlx/models/embedders/contentvec/hubert_mlx.npz"),
+             **hubert_to_mlx(synthetic.hubert_state(4)))
+    np.savez(os.path.join(root, "rvc_mlx/models/predictors/rmvpe_mlx.npz"), **rmvpe_to_mlx(synthetic.rmvpe_state(5)))
+    g = golden("pipeline_2p5s.npz")
+    voice = os.path.join(d, "voice_mlx.npz")
+    ref = RVC_MLX(voice, hubert_path=os.path.join(d, "pytorch_model.bin"), rmvpe_path=os.path.join(d, "rmvpe.pt"))
+    try:
+        out_torch = _run(ref.engine, g)
+    finally:
+        ref.close()
+    monkeypatch.chdir(root)
+    rvc = RVC_MLX(voice)
+    try:
+        out_mlx = _run(rvc.engine, g)
+        rvc.engine.check_device_status()
+    finally:
+        rvc.close()
+    assert np.array_equal(out_mlx, out_torch), "MLX-tree HuBERT/RMVPE files differ from the torch files"
