@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256) void k_conv2d_small(const ConvArgs a, const in
 // tap of 32 channels, three products per K step (h h' into acc, l h' + h l' into acc2). The f32 kernel above spends
 // 32 cycles per 16x16x4 MFMA: 9216 MFMA cycles per wave at level 0; here 1920. The weights come pre-split (k_s2d_wsplit,
 // once per tensor, cached by the runtime as WSPLIT_S2D): [K step][16-column group][plane][64 lanes][16 B], lane l holding
-// K rows 8 (l / 16) .. + 7 of column l % 16 (one ds_read_b128 per fragment), then the {scale, 1 / (scale 2^-4)} tail; a
+// K rows 8 (l / 16) .. + 7 of column l % 16 (one ds_read_b128 per fragment), then the per-column 1 / (scale 2^-4) tail; a
 // block copies it into LDS beside its tile (a block building it from the fp32 weights itself ran 10-45 % slower than
 // the exact-f32 kernel, r04l). A pixel's LDS row is [hi plane | lo plane | 16 B pad] (80 or 144 B: a quarter-wave's
 // 16-B reads of 16 consecutive pixels hit distinct bank groups).
@@ -326,8 +326,9 @@ __global__ __launch_bounds__(256) void k_conv2d_h16(const ConvArgs a, const int 
       }
     }
   }
-  // ---- epilogue (k_conv2d_small's): acc + 2^-11 acc2, times 1 / (weight scale x activation scale) from the image tail
-  const float inv = static_cast<const float*>(a.wsplit)[KS * NT * 2 * 64 * 4 + 1];
+  // ---- epilogue (k_conv2d_small's): acc + 2^-11 acc2, times 1 / (column weight scale x activation scale) from the
+  // image tail
+  const float* invt = static_cast<const float*>(a.wsplit) + KS * NT * 2 * 64 * 4;
   float* Y = a.y + (long long)b * a.y_bs;
   const int act = a.act;
 #pragma unroll
@@ -335,6 +336,7 @@ __global__ __launch_bounds__(256) void k_conv2d_h16(const ConvArgs a, const int 
     const int n = t * 16 + li;
     const bool n_ok = n < a.N;
     const float bn = (a.bias && n_ok) ? a.bias[n] : 0.f;
+    const float inv = invt[n];
 #pragma unroll
     for (int p = 0; p < TPW; ++p) {
       long long m[4];
@@ -391,20 +393,19 @@ hipError_t launch_small(const ConvArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(kern, grid, dim3(256), lds, s, a, RH);
   return hipGetLastError();
 }
-// the image: one block; max |w| (block-wide), the power-of-two scale, then the lane-major fragments and the tail
+// the image: one block; max |w| per output column (LDS atomics on the bits), each column's power-of-two scale (conv_wsb.hip
+// k_wsplit_h16's rule), then the lane-major fragments and the tail inv[32] = 1 / (scale_n 2^-4)
 __global__ __launch_bounds__(256) void k_s2d_wsplit(const float* __restrict__ w, long long w_ts, int ldw, int N, int CIN,
                                                     int NT, unsigned short* __restrict__ out) {
-  __shared__ float red[4];
+  __shared__ unsigned cmax[32];
   const int tid = threadIdx.x;
-  float m = 0.f;
+  if (tid < 32) cmax[tid] = 0u;
+  __syncthreads();
   for (int i = tid; i < 9 * N * CIN; i += 256) {
     const int c = i % CIN, tn = i / CIN;
-    m = fmaxf(m, fabsf(w[(long long)(tn / N) * w_ts + (long long)(tn % N) * ldw + c]));
+    atomicMax(&cmax[tn % N], __float_as_uint(fabsf(w[(long long)(tn / N) * w_ts + (long long)(tn % N) * ldw + c])));
   }
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  if ((tid & 63) == 0) red[tid >> 6] = m;
   __syncthreads();
-  const float sc = h16_weight_scale(__float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
   const int KS = CIN == 16 ? 5 : 9;
   for (int e = tid; e < KS * NT * 64; e += 256) {
     const int l = e & 63, knt = e >> 6;
@@ -413,6 +414,7 @@ __global__ __launch_bounds__(256) void k_s2d_wsplit(const float* __restrict__ w,
     const int tap = CIN == 16 ? 2 * ks + (g >> 1) : ks;
     const int c0 = CIN == 16 ? 8 * (g & 1) : 8 * g;
     const bool ok = tap < 9 && n < N;
+    const float sc = h16_weight_scale(cmax[n]);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float v = ok ? w[(long long)tap * w_ts + (long long)n * ldw + c0 + j] * sc : 0.f;
@@ -421,10 +423,9 @@ __global__ __launch_bounds__(256) void k_s2d_wsplit(const float* __restrict__ w,
       out[((size_t)(knt * 2 + 1) * 64 + l) * 8 + j] = (unsigned short)pk_f16((v - f16lo_f(h)) * H16_LO, 0.f);
     }
   }
-  if (tid == 0) {
+  if (tid < 32) {
     float* tail = reinterpret_cast<float*>(out + (size_t)KS * NT * 2 * 64 * 8);
-    tail[0] = sc;
-    tail[1] = 1.f / (sc * H16_XS);
+    tail[tid] = 1.f / (h16_weight_scale(cmax[tid]) * H16_XS);
   }
 }
 

@@ -46,17 +46,21 @@ __device__ __forceinline__ void mma_h16(const bf16x8 (&af)[2], const bf16x8 (&bf
     acc2[tn] = c;
   }
 }
-// acc + 2^-11 acc2, times 1 / (weight scale x activation scale) from the fp16 image's tail (at tail_off bytes)
-template <int TM16, int TN16>
-__device__ __forceinline__ void h16_finish(const char* wsp, size_t tail_off, f32x4 (&acc)[TM16][TN16],
+// acc + 2^-11 acc2, times 1 / (column weight scale x activation scale) from the fp16 image's tail (at tail_off bytes:
+// one inverse scale per output column, conv_wsb.hip k_wsplit_h16); lane column n0 + wn * TN16 * 16 + tn * 16 + lane % 16
+template <int TM16, int TN16, int WN>
+__device__ __forceinline__ void h16_finish(const char* wsp, size_t tail_off, int n0, f32x4 (&acc)[TM16][TN16],
                                            const f32x4 (&acc2)[TM16][TN16]) {
-  const float inv = *reinterpret_cast<const float*>(wsp + tail_off + sizeof(float));
+  const int wn = (threadIdx.x >> 6) % WN;
+  const float* inv = reinterpret_cast<const float*>(wsp + tail_off) + n0 + wn * TN16 * 16 + (threadIdx.x & 15);
 #pragma unroll
-  for (int tm = 0; tm < TM16; ++tm)
+  for (int tn = 0; tn < TN16; ++tn) {
+    const float iv = inv[tn * 16];
 #pragma unroll
-    for (int tn = 0; tn < TN16; ++tn)
+    for (int tm = 0; tm < TM16; ++tm)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[tm][tn][r] = (acc[tm][tn][r] + acc2[tm][tn][r] * H16_LO_INV) * inv;
+      for (int r = 0; r < 4; ++r) acc[tm][tn][r] = (acc[tm][tn][r] + acc2[tm][tn][r] * H16_LO_INV) * iv;
+  }
 }
 
 // MODE bits 0-1: the pre-activation (pre_fn: none, leaky ReLU, other), bit 2: a 1-D pre-mask row multiplier --
@@ -286,7 +290,7 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gs16_kernel(const ConvAr
     for (int p = 0; p < GS_D - 1; ++p)
       if (base + p < it1) step(base + p, p);
   }
-  if constexpr (H16) h16_finish(wsp, (size_t)total * bstep, acc, acc2);
+  if constexpr (H16) h16_finish<TM16, TN16, WN>(wsp, (size_t)total * bstep, n0, acc, acc2);
   store_tile16<TM16, TN16, WM, WN>(a, m0, n0, b, zsplit, ksplit, Mtot, acc);
 }
 
@@ -503,7 +507,7 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gsw16_kernel(const ConvA
       }
     }
   }
-  if constexpr (H16) h16_finish(wsp, (size_t)nch * 9 * bstep, acc, acc2);
+  if constexpr (H16) h16_finish<TM16, TN16, WN>(wsp, (size_t)nch * 9 * bstep, n0, acc, acc2);
   store_tile16<TM16, TN16, WM, WN>(a, h0 * W, n0, b, zsplit, ksplit, (long long)H * W, acc);
 }
 

@@ -1,15 +1,16 @@
 // fp32 implicit-GEMM convolution with the weights pre-split in HBM ("weight-streamed B"), for the long 1-D convs of
-// the generator (ResBlocks, ConvTranspose phases, conv_pre): the same exact 3-plane bf16 arithmetic as
-// conv_emu.hip (x = x0 + x1 + x2, six plane products smallest first, one fp32 accumulator), restructured so the
-// (chunk, tap) loop has no barrier and no conversion work:
-//   * the weights are split ONCE (k_wsplit, cached per weight tensor by the runtime) into rows of
-//     [hi | mid | lo] x 32 channels per (chunk, tap, output channel), so every lane loads its MFMA B fragments
-//     straight from L2/L1 as 16-byte vectors, one iteration ahead, into registers (two register sets);
+// the generator (ResBlocks, ConvTranspose phases, conv_pre). Two arithmetics: the default, conv_wsb16_kernel with the
+// two-plane fp16 split (split_bf16.h put_h16x4: x = h + 2^-11 l, three v_mfma_f32_16x16x32_f16 products per step, the
+// weights from the per-column-scaled k_wsplit_h16 image), and the exact 3-plane bf16 split of conv_emu.hip
+// (x = x0 + x1 + x2, six plane products smallest first; conv_wsb_kernel and the bf16 instantiations of
+// conv_wsb16_kernel, rvcx_set_conv_math mode 2). Both are restructured so the (chunk, tap) loop has no barrier and no
+// conversion work:
+//   * the weights are split ONCE (k_wsplit / k_wsplit_h16, cached per weight tensor by the runtime) into lane-major
+//     1 KB plane blocks per (chunk, tap, 16-column group), so every lane loads its MFMA B fragments straight from
+//     L2/L1 as 16-byte vectors, one iteration ahead, into registers (two register sets);
 //   * only the activation halo goes through LDS (split once per 32-channel chunk and reused by every tap); the
 //     next chunk's halo is prefetched into registers during the current chunk's taps;
-//   * per-wave tiles of 64 x 32 (two accumulators) double the MFMA work per LDS A fragment read.
-// A (chunk, tap) step is then 6*TN global B loads, 6*TM LDS reads and 12*TM*TN MFMAs; barriers only at chunk
-// changes (two per 32 input channels).
+//   * barriers only at chunk changes (two per 32 input channels).
 #include <algorithm>
 #include <cstdlib>
 
@@ -64,31 +65,27 @@ __global__ void k_wsplit(const float* __restrict__ w, int ldw, long long w_ts, i
 }
 
 // The two-plane fp16 image (split_bf16.h put_h16x4 arithmetic) of the same weights: per (chunk, tap) step and 16-column
-// group two 1 KB blocks [h | l], lane-major as k_wsplit's. The weights are scaled by a power of two s (max |w| s in
-// [128, 256): small weights stay normal fp16) and the activations by 2^-4 (inputs up to 2^20 stay finite); the image's
-// tail holds {s, 1 / (s 2^-4)}, which the kernel's epilogue multiplies back in exactly.
+// group two 1 KB blocks [h | l], lane-major as k_wsplit's. Each output column n is scaled by its own power of two s_n
+// (max over the column's taps and channels of |w| s_n in [128, 256): a column far below the tensor's largest -- a dead
+// or near-dead weight-norm channel -- keeps its full 22 significand bits instead of sinking into fp16's subnormals), the
+// activations by 2^-4 (inputs up to 2^20 stay finite). The image's tail holds inv[Npad] = 1 / (s_n 2^-4), which the
+// kernels' epilogues multiply back in per column (exact powers of two), then the columns' max |w| bits (build scratch).
 constexpr int WROW_H = 2 * PLANE;  // bytes of one (chunk, tap, column) row of the fp16 image
-// max |w| over the grid into tail word 2 (zeroed before; a single 1024-thread workgroup took 0.2-0.5 ms per tensor)
-__global__ void k_wmax_scale(const float* __restrict__ w, int ldw, long long w_ts, int N, int C_in, int taps,
-                             float* __restrict__ tail) {
+// max |w| of each column (one wave per column; columns >= N get 0) into colmax[Npad]
+__global__ void k_wmax_col(const float* __restrict__ w, int ldw, long long w_ts, int N, int C_in, int taps, int Npad,
+                           unsigned* __restrict__ colmax) {
+  const int n = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (n >= Npad) return;
   float m = 0.f;
-  const long long total = (long long)taps * N * C_in;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C_in);
-    const long long r = i / C_in;
-    const int n = (int)(r % N), tap = (int)(r / N);
-    m = fmaxf(m, fabsf(w[tap * w_ts + (long long)n * ldw + c]));
-  }
-  absmax_wave_publish(m, reinterpret_cast<unsigned*>(tail) + 2);
+  if (n < N)
+    for (int tap = 0; tap < taps; ++tap)
+      for (int c = lane; c < C_in; c += 64) m = fmaxf(m, fabsf(w[tap * w_ts + (long long)n * ldw + c]));
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if (lane == 0) colmax[n] = __float_as_uint(m);
 }
 __global__ void k_wsplit_h16(const float* __restrict__ w, int ldw, long long w_ts, int N, int C_in, int taps,
                              int nchunks, int Npad, unsigned short* __restrict__ out, float* __restrict__ tail) {
-  const float sc = h16_weight_scale(reinterpret_cast<const unsigned*>(tail)[2]);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    tail[0] = sc;
-    tail[1] = 1.f / (sc * H16_XS);
-  }
+  const unsigned* colmax = reinterpret_cast<const unsigned*>(tail) + Npad;
   const long long total = (long long)nchunks * taps * Npad * EK;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
@@ -98,6 +95,8 @@ __global__ void k_wsplit_h16(const float* __restrict__ w, int ldw, long long w_t
     const long long ct = r / Npad;
     const int tap = (int)(ct % taps), ch = (int)(ct / taps);
     const int cc = ch * EK + c;
+    const float sc = h16_weight_scale(colmax[n]);
+    if (ct == 0 && c == 0) tail[n] = 1.f / (sc * H16_XS);
     const float v = (n < N && cc < C_in) ? w[tap * w_ts + (long long)n * ldw + cc] * sc : 0.f;
     const unsigned h = pk_f16(v, 0.f);
     const unsigned l = pk_f16((v - f16lo_f(h)) * H16_LO, 0.f);
@@ -511,18 +510,20 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
     }
   }
   if constexpr (H16) {
-    // acc + 2^-11 acc2, times 1 / (weight scale x activation scale) from the image tail: exact powers of two
-    const float inv = *reinterpret_cast<const float*>(wsp + (size_t)total * bstep + sizeof(float));
+    // acc + 2^-11 acc2, times 1 / (column weight scale x activation scale) from the image tail: exact powers of two
+    const float* inv = reinterpret_cast<const float*>(wsp + (size_t)total * bstep) + n0 + wn * TN16 * 16 + lc;
 #pragma unroll
-    for (int tm = 0; tm < TM16; ++tm)
+    for (int tn = 0; tn < TN16; ++tn) {
+      const float iv = inv[tn * 16];
 #pragma unroll
-      for (int tn = 0; tn < TN16; ++tn)
+      for (int tm = 0; tm < TM16; ++tm)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float v = acc[tm][tn][r];
           if constexpr (!LOWP) v += acc2[tm][tn][r] * H16_LO_INV;
-          acc[tm][tn][r] = v * inv;
+          acc[tm][tn][r] = v * iv;
         }
+    }
   }
   store_tile16<TM16, TN16, WM, WN>(a, m0, n0, b, zsplit, ksplit, (long long)a.T_out, acc);
 }
@@ -611,11 +612,12 @@ bool conv_wsb_eligible(const ConvArgs& a, bool two_d) {
 
 int conv_wsplit_npad(int N) { return (N + 127) / 128 * 128; }
 
-// chunks of 32 input channels, the last one zero-padded; the fp16 image carries a 256-B tail (its scales)
+// chunks of 32 input channels, the last one zero-padded; the fp16 image carries a tail of 2 x Npad words (the columns'
+// inverse scales, then their max |w| bits)
 long long conv_wsplit_bytes(const ConvArgs& a) {
   if (a.wsplit_fmt == WSPLIT_S2D) return small2d_wsplit_bytes(a);
   const long long steps = (long long)((a.C_in + EK - 1) / EK) * a.taps * conv_wsplit_npad(a.N);
-  return a.wsplit_fmt == WSPLIT_H16 ? steps * WROW_H + 256 : steps * WROW;
+  return a.wsplit_fmt == WSPLIT_H16 ? steps * WROW_H + 8LL * conv_wsplit_npad(a.N) : steps * WROW;
 }
 
 hipError_t conv_wsplit_build(const ConvArgs& a, void* out, hipStream_t s) {
@@ -626,11 +628,8 @@ hipError_t conv_wsplit_build(const ConvArgs& a, void* out, hipStream_t s) {
   const long long nb = std::min<long long>((total + 255) / 256, 1 << 20);
   if (a.wsplit_fmt == WSPLIT_H16) {
     float* tail = reinterpret_cast<float*>(static_cast<char*>(out) + (long long)nch * a.taps * Npad * WROW_H);
-    hipError_t e = hipMemsetAsync(tail, 0, 16, s);
-    if (e != hipSuccess) return e;
-    const long long nm = std::min<long long>(((long long)a.taps * a.N * a.C_in + 2047) / 2048, 1024);
-    hipLaunchKernelGGL(k_wmax_scale, dim3((unsigned)nm), dim3(256), 0, s, a.w, a.ldw, a.w_ts, a.N, a.C_in, a.taps,
-                       tail);
+    hipLaunchKernelGGL(k_wmax_col, dim3((unsigned)(Npad / 4)), dim3(256), 0, s, a.w, a.ldw, a.w_ts, a.N, a.C_in, a.taps,
+                       Npad, reinterpret_cast<unsigned*>(tail) + Npad);
     hipLaunchKernelGGL(k_wsplit_h16, dim3((unsigned)nb), dim3(256), 0, s, a.w, a.ldw, a.w_ts, a.N, a.C_in, a.taps, nch,
                        Npad, static_cast<unsigned short*>(out), tail);
     return hipGetLastError();

@@ -71,22 +71,23 @@ __global__ void k_rb_wsplit(const float* __restrict__ w, int C, int k, unsigned 
 }
 
 // the fp16 images: ((tap * NCH + s) * NP + q) planes of [C_out][16 slots] fp16 (q = 0 hi, 1 the 2^11-scaled residual:
-// put_h16x4's arithmetic) of w * sc, sc a power of two with max |w| sc in [128, 256); the image's tail (after the
-// planes) holds {sc, 1 / (sc * RB_XS)}. Activations are split at RB_XS = 2^-4.
+// put_h16x4's arithmetic) of w * sc_o, sc_o a power of two per OUTPUT CHANNEL with max |w[., o, .]| sc_o in [128, 256)
+// (conv_wsb.hip k_wsplit_h16's rule); the image's tail (after the planes) holds inv[C] = 1 / (sc_o * RB_XS), then the
+// channels' max |w| bits (build scratch). Activations are split at RB_XS = 2^-4.
 constexpr float RB_XS = 1.f / 16.f;
-__global__ void k_rb_wmax(const float* __restrict__ w, long long n, float* __restrict__ tail) {
+// one wave per output channel o: max over taps and input channels of |w[tap][o][c]|
+__global__ void k_rb_wmax(const float* __restrict__ w, int C, int k, unsigned* __restrict__ chmax) {
+  const int o = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (o >= C) return;
   float m = 0.f;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
-    m = fmaxf(m, fabsf(w[i]));
-  absmax_wave_publish(m, reinterpret_cast<unsigned*>(tail) + 2);
+  for (int tap = 0; tap < k; ++tap)
+    for (int c = lane; c < C; c += 64) m = fmaxf(m, fabsf(w[((long long)tap * C + o) * C + c]));
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+  if (lane == 0) chmax[o] = __float_as_uint(m);
 }
 __global__ void k_rb_wsplit_h16(const float* __restrict__ w, int C, int k, int NP, unsigned short* __restrict__ out,
                                 float* __restrict__ tail) {
-  const float sc = h16_weight_scale(reinterpret_cast<const unsigned*>(tail)[2]);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    tail[0] = sc;
-    tail[1] = 1.f / (sc * RB_XS);
-  }
+  const unsigned* chmax = reinterpret_cast<const unsigned*>(tail) + C;
   const int NCH = C / 16;
   const long long total = (long long)k * NCH * C * 16;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
@@ -96,6 +97,8 @@ __global__ void k_rb_wsplit_h16(const float* __restrict__ w, int C, int k, int N
     const int och = (int)(r % C);
     r /= C;
     const int s = (int)(r % NCH), tap = (int)(r / NCH);
+    const float sc = h16_weight_scale(chmax[och]);
+    if (r == 0 && j == 0) tail[och] = 1.f / (sc * RB_XS);
     const float v = w[((long long)tap * C + och) * C + 16 * s + rb_pi(j)] * sc;
     const unsigned h = pk_f16(v, 0.f);
     const long long base = (((long long)(tap * NCH + s) * NP) * C + och) * 16 + j;
@@ -363,13 +366,18 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
     f32x16 acc[TN], acc2[TN];
     run_conv(wl_of(job), (second ? TS : XS) + (size_t)(tg * TN * 32 + li) * ROW + hk * 16, second ? 1 : a.d, acc, acc2);
     if constexpr (H16) {
-      // acc + 2^-11 acc2, times 1 / (weight scale x activation scale) from the weight image's tail
-      const float inv = *reinterpret_cast<const float*>(static_cast<const char*>(second ? a.w2s : a.w1s) +
-                                                        (size_t)nsteps * NQI * QS + sizeof(float));
+      // acc + 2^-11 acc2, times 1 / (output-channel weight scale x activation scale) from the weight image's tail:
+      // accumulator element r is output channel ob * 32 + 8 (r / 4) + 4 hk + r % 4 (the bias layout above)
+      const float* invp = reinterpret_cast<const float*>(static_cast<const char*>(second ? a.w2s : a.w1s) +
+                                                         (size_t)nsteps * NQI * QS) + ob * 32 + 4 * hk;
+      f32x4 inv[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) inv[m] = *reinterpret_cast<const f32x4*>(invp + 8 * m);
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[tn][r] = (NQ > 1 ? acc[tn][r] + acc2[tn][r] * H16_LO_INV : acc[tn][r]) * inv;
+        for (int r = 0; r < 16; ++r)
+          acc[tn][r] = (NQ > 1 ? acc[tn][r] + acc2[tn][r] * H16_LO_INV : acc[tn][r]) * inv[r >> 2][r & 3];
     }
     if (!second) {
       // conv1 -> TS = split(lrelu(conv1 + b1)); TS row p <-> time t0 - h2 + p, zero outside [0, T)
@@ -484,9 +492,9 @@ bool rb_pair_fits(int C, int k, int d) {
   return h2 * d <= RB_MAXH1 && 2 * h2 < 32;
 }
 
-// the fp16 image: two planes + a 256-B tail (its scales)
+// the fp16 image: two planes + a tail of 2 x C words (the output channels' inverse scales, their max |w| bits)
 long long rb_wsplit_bytes(int C, int k, int wfmt) {
-  return wfmt == RB_WF16 ? (long long)k * (C / 16) * 2 * C * 32 + 256 : (long long)k * (C / 16) * 3 * C * 32;
+  return wfmt == RB_WF16 ? (long long)k * (C / 16) * 2 * C * 32 + 8LL * C : (long long)k * (C / 16) * 3 * C * 32;
 }
 
 hipError_t rb_wsplit_build(const float* w, int C, int k, void* out, hipStream_t s, int wfmt) {
@@ -495,11 +503,8 @@ hipError_t rb_wsplit_build(const float* w, int C, int k, void* out, hipStream_t 
   const long long nb = std::min<long long>((total + 255) / 256, 1 << 20);
   if (wfmt == RB_WF16) {
     float* tail = reinterpret_cast<float*>(static_cast<char*>(out) + (long long)k * (C / 16) * 2 * C * 32);
-    hipError_t e = hipMemsetAsync(tail, 0, 16, s);
-    if (e != hipSuccess) return e;
-    const long long n = (long long)k * C * C;
-    hipLaunchKernelGGL(k_rb_wmax, dim3((unsigned)std::min<long long>((n + 2047) / 2048, 1024)), dim3(256), 0, s, w, n,
-                       tail);
+    hipLaunchKernelGGL(k_rb_wmax, dim3((unsigned)((C + 3) / 4)), dim3(256), 0, s, w, C, k,
+                       reinterpret_cast<unsigned*>(tail) + C);
     hipLaunchKernelGGL(k_rb_wsplit_h16, dim3((unsigned)nb), dim3(256), 0, s, w, C, k, 2,
                        static_cast<unsigned short*>(out), tail);
     return hipGetLastError();

@@ -12,20 +12,30 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-CASES = [  # T, C_in, N, taps, dil, stride, scale_spread
-    (3000, 128, 128, 11, 5, 1, 0),
-    (2000, 64, 64, 3, 1, 1, 0),
-    (4000, 32, 32, 7, 3, 1, 0),
-    (1550, 192, 768, 3, 1, 1, 0),
-    (775, 768, 2304, 1, 1, 1, 0),       # HuBERT qkv (GEMM pipeline)
-    (150, 3072, 768, 1, 1, 1, 0),       # long contraction: split-K
-    (5000, 512, 512, 3, 1, 2, 0),       # HuBERT strided feature conv
-    (1000, 37, 45, 5, 2, 1, 0),         # ragged channels (scalar paths)
-    (3000, 256, 200, 7, 3, 1, 0),       # N not a multiple of the tile (weight-streamed: padded columns)
-    (2500, 64, 32, 11, 5, 1, 4),        # narrow N (weight-streamed 256 x 32 tile), spread operands
-    (2000, 128, 64, 7, 1, 1, 12),       # operands spread over 2^+-12
-    (196, 512, 512, 9, 1, 1, 0),        # the U-Net's deepest 1-D analogue: 9 taps, few rows, long K (split-K)
-    (1599, 768, 3072, 1, 1, 1, 0),      # HuBERT FFN at the 30 s (C4) length
+CASES = [  # T, C_in, N, taps, dil, stride, scale_spread (activations), weight spread (see _wspread)
+    (3000, 128, 128, 11, 5, 1, 0, 0),
+    (2000, 64, 64, 3, 1, 1, 0, 0),
+    (4000, 32, 32, 7, 3, 1, 0, 0),
+    (1550, 192, 768, 3, 1, 1, 0, 0),
+    (775, 768, 2304, 1, 1, 1, 0, 0),       # HuBERT qkv (GEMM pipeline)
+    (150, 3072, 768, 1, 1, 1, 0, 0),       # long contraction: split-K
+    (5000, 512, 512, 3, 1, 2, 0, 0),       # HuBERT strided feature conv
+    (1000, 37, 45, 5, 2, 1, 0, 0),         # ragged channels (scalar paths)
+    (3000, 256, 200, 7, 3, 1, 0, 0),       # N not a multiple of the tile (weight-streamed: padded columns)
+    (2500, 64, 32, 11, 5, 1, 4, 0),        # narrow N (weight-streamed 256 x 32 tile), spread operands
+    (2000, 128, 64, 7, 1, 1, 12, 0),       # operands spread over 2^+-12
+    (196, 512, 512, 9, 1, 1, 0, 0),        # the U-Net's deepest 1-D analogue: 9 taps, few rows, long K (split-K)
+    (1599, 768, 3072, 1, 1, 1, 0, 0),      # HuBERT FFN at the 30 s (C4) length
+    # weight spread (trained weight-norm checkpoints fuse a per-output-channel g, so a dead or
+    # near-dead channel sits orders of magnitude below the tensor's largest): per-column scales over 2^+-12 and one
+    # column at 2^-20 of the tensor max, on the weight-streamed, gather-streamed and split-K shapes
+    (3000, 128, 128, 11, 5, 1, 0, "ch12"),
+    (3000, 128, 128, 7, 1, 1, 4, "dead20"),
+    (2000, 64, 64, 3, 1, 1, 0, "ch12"),
+    (3000, 256, 200, 7, 3, 1, 0, "ch12"),
+    (775, 768, 2304, 1, 1, 1, 0, "ch12"),
+    (196, 512, 512, 9, 1, 1, 0, "dead20"),
+    (1550, 192, 768, 3, 1, 1, 0, "ch12"),
 ]
 
 
@@ -38,14 +48,34 @@ def _ref(x, w, bias, dil, pad, stride):
     return y.numpy(), ya.numpy()
 
 
-@pytest.mark.parametrize("T,C,N,K,dil,stride,spread", CASES)
-def test_split_math_is_fp32_accurate(engine, T, C, N, K, dil, stride, spread):
+def _wspread(rng, N, kind):
+    """Per-output-column weight scales (powers of two, so the fp64 reference sees exactly the scaled weights): "ch12"
+    spreads the columns over 2^+-12 and puts one at 2^-20 of the largest; "dead20" leaves every column at 1 but
+    one at 2^-20."""
+    if kind == "ch12":
+        s = np.exp2(rng.integers(-12, 13, size=N)).astype(np.float64)
+        s[0] = 2.0 ** 12
+        s[min(5, N - 1)] = 2.0 ** -8  # 2^-20 of the max
+    else:
+        s = np.ones(N)
+        s[min(3, N - 1)] = 2.0 ** -20
+    return s
+
+
+@pytest.mark.parametrize("T,C,N,K,dil,stride,spread,wsp", CASES)
+def test_split_math_is_fp32_accurate(engine, T, C, N, K, dil, stride, spread, wsp):
+    """Every arithmetic against fp64, per output element relative to its own sum |x w| (+ |bias|): a column whose
+    weights are 2^-20 of the tensor's largest is held to the same bar as the largest one."""
     rng = np.random.Generator(np.random.PCG64(T * 7 + C))
     x = rng.standard_normal((T, C)).astype(np.float32)
     w = (rng.standard_normal((N, C, K)) / np.sqrt(C * K)).astype(np.float32)
     if spread:
         x *= np.exp2(rng.integers(-spread, spread + 1, size=x.shape)).astype(np.float32)
     bias = rng.standard_normal(N).astype(np.float32)
+    if wsp:
+        cs = _wspread(rng, N, wsp)
+        w = (w * cs[:, None, None]).astype(np.float32)
+        bias = (bias * cs).astype(np.float32)
     pad = dil * (K - 1) // 2
     ref, mag = _ref(x, w, bias, dil, pad, stride)
     errs = {}
@@ -55,7 +85,7 @@ def test_split_math_is_fp32_accurate(engine, T, C, N, K, dil, stride, spread):
     for mode in ("f32", "split") + (("wsb", "h16", "f16") if wsb else ()) + (("gs", "gs_h16") if gs else ()):
         y = engine.conv1d(x, w, bias, dilation=dil, padding=pad, stride=stride, math=mode).cpu().numpy()
         assert y.shape == ref.shape
-        errs[mode] = float(np.max(np.abs(y - ref) / (mag + np.abs(bias) + 1e-30)))
+        errs[mode] = float(np.max(np.abs(y - ref) / (mag + np.abs(bias) + 1e-300)))
     # both within fp32 rounding of the contraction; the split mode no worse than native fp32 (+ slack for the
     # different summation order of equally accurate evaluations)
     assert errs["f32"] < 1e-6, errs
@@ -88,32 +118,38 @@ def test_context_math_mode_switch(engine):
     assert not np.array_equal(a, b) and np.allclose(a, b, rtol=1e-5, atol=1e-4)
 
 
-SMALL2D = [  # H, W, C_in, N, spread: the RMVPE U-Net's few-channel 3x3 convs (csrc/conv2d_small.hip)
-    (64, 128, 16, 16, 0),   # level 0
-    (48, 128, 16, 32, 0),   # level 0 -> 1 channels
-    (40, 64, 32, 32, 0),    # level 1
-    (40, 64, 32, 16, 0),    # decoder 32 -> 16
-    (33, 128, 16, 3, 0),    # the 16 -> 3 output conv, ragged rows
-    (36, 64, 32, 32, 10),   # operands spread over 2^+-10
+SMALL2D = [  # H, W, C_in, N, spread, weight spread: the RMVPE U-Net's few-channel 3x3 convs (csrc/conv2d_small.hip)
+    (64, 128, 16, 16, 0, 0),   # level 0
+    (48, 128, 16, 32, 0, 0),   # level 0 -> 1 channels
+    (40, 64, 32, 32, 0, 0),    # level 1
+    (40, 64, 32, 16, 0, 0),    # decoder 32 -> 16
+    (33, 128, 16, 3, 0, 0),    # the 16 -> 3 output conv, ragged rows
+    (36, 64, 32, 32, 10, 0),   # operands spread over 2^+-10
+    (40, 64, 32, 32, 0, "ch12"),   # per-column weight scales over 2^+-12, one column at 2^-20 of the max
+    (64, 128, 16, 16, 0, "dead20"),
 ]
 
 
-@pytest.mark.parametrize("H,W,C,N,spread", SMALL2D)
-def test_unet_small_2d_convs_are_fp32_accurate(engine, H, W, C, N, spread):
+@pytest.mark.parametrize("H,W,C,N,spread,wsp", SMALL2D)
+def test_unet_small_2d_convs_are_fp32_accurate(engine, H, W, C, N, spread, wsp):
     """The default arithmetic (two-plane fp16 split, k_conv2d_h16) and the exact-f32 form against fp64: both within
-    1e-6 of sum |x w|, the split at most 4x the f32 form's error."""
+    1e-6 of each output's sum |x w|, the split at most 4x the f32 form's error."""
     rng = np.random.Generator(np.random.PCG64(H * 131 + C + N))
     x = rng.standard_normal((H, W, C)).astype(np.float32)
     w = (rng.standard_normal((N, C, 3, 3)) / np.sqrt(9 * C)).astype(np.float32)
     if spread:
         x *= np.exp2(rng.integers(-spread, spread + 1, size=x.shape)).astype(np.float32)
     bias = rng.standard_normal(N).astype(np.float32)
+    if wsp:
+        cs = _wspread(rng, N, wsp)
+        w = (w * cs[:, None, None, None]).astype(np.float32)
+        bias = (bias * cs).astype(np.float32)
     xd = torch.from_numpy(x.astype(np.float64)).permute(2, 0, 1)[None]
     wd = torch.from_numpy(w.astype(np.float64))
     ref = torch.relu(torch.nn.functional.conv2d(xd, wd, torch.from_numpy(bias.astype(np.float64)), padding=1))
     mag = torch.nn.functional.conv2d(xd.abs(), wd.abs(), None, padding=1) + np.abs(bias)[None, :, None, None]
     ref = ref[0].permute(1, 2, 0).numpy()
-    mag = mag[0].permute(1, 2, 0).numpy() + 1e-30
+    mag = mag[0].permute(1, 2, 0).numpy() + 1e-300
     errs = {}
     for mode in ("f32", "default"):
         y = engine.conv2d3x3(x, w, bias, relu=True, math=mode).cpu().numpy()

@@ -119,3 +119,31 @@ def test_fused_pair_rejects_unsupported(engine):
     w1, b1, w2, b2 = _weights(rng, 128, 3)
     with pytest.raises(RvcxError):
         engine.resblock_pair(x, w1, b1, w2, b2, 1)
+
+
+@pytest.mark.parametrize("C,k,d", [(32, 11, 5), (64, 7, 3), (32, 3, 1)])
+def test_fused_pair_fp16_per_channel_weight_spread(engine, C, k, d):
+    """per-output-channel weight scales over 2^+-12 (and one channel at 2^-20 of the tensor's
+    largest) in both convs, the residual x and b2 scaled with conv2's channel so every output channel lives at its
+    own magnitude. Each channel is held to the fp32-class bar relative to ITS OWN peak (the fp16 images carry one
+    power-of-two scale per output channel, resblock_fused.hip k_rb_wsplit_h16)."""
+    rng = np.random.Generator(np.random.PCG64(4242 + C + k))
+    T = 3000
+    x = rng.standard_normal((1, T, C)).astype(np.float32)
+    w1, b1, w2, b2 = _weights(rng, C, k)
+    s1 = np.exp2(rng.integers(-12, 13, size=C)).astype(np.float64)
+    s2 = np.exp2(rng.integers(-12, 13, size=C)).astype(np.float64)
+    s2[0], s2[7] = 2.0 ** 12, 2.0 ** -8   # channel 7 at 2^-20 of the largest
+    w1 = (w1 * s1[:, None, None]).astype(np.float32)
+    b1 = (b1 * s1).astype(np.float32)
+    w2 = (w2 * s2[:, None, None]).astype(np.float32)
+    b2 = (b2 * s2).astype(np.float32)
+    x = (x * s2[None, None, :]).astype(np.float32)
+    ref = _ref(x, w1, b1, w2, b2, d)[0]
+    peak = np.abs(ref).max(axis=0)
+    for cfg, bar in ((0, 2e-6), (1 << 4, 6e-6)):
+        y = engine.resblock_pair(x, w1, b1, w2, b2, d, cfg=cfg).cpu().numpy()[0]
+        err = np.abs(y - ref).max(axis=0) / peak
+        print(f"\nfused pair C{C} k{k} spread, cfg {cfg}: worst channel {err.max():.2e} (ch {int(err.argmax())}), "
+              f"2^-20 channel {err[7]:.2e}")
+        assert err.max() < bar, (cfg, float(err.max()), int(err.argmax()))
