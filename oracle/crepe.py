@@ -141,7 +141,18 @@ def torchcrepe_bin_range(f0_min: float, f0_max: float):
     return max(0, min(PITCH_BINS, lo)), max(0, min(PITCH_BINS, hi))
 
 
-def viterbi_bins(probs: np.ndarray, f0_min: float, f0_max: float) -> np.ndarray:
+RVC_CREPE_BATCH = 512  # rvc/lib/predictors/f0.py:38 (torchcrepe.predict batch_size)
+
+
+def viterbi_bins(probs: np.ndarray, f0_min: float, f0_max: float, batch: int = RVC_CREPE_BATCH) -> np.ndarray:
+    """torchcrepe.predict runs postprocess -- and so decode.viterbi -- once per batch of `batch` frames (f0.py:38-49),
+    each batch a sequence of its own from the uniform initial state; the bin paths are concatenated."""
+    probs = np.asarray(probs)
+    return np.concatenate([_viterbi_seq(probs[i:i + batch], f0_min, f0_max)
+                           for i in range(0, len(probs), batch)]) if len(probs) else np.zeros(0, np.int64)
+
+
+def _viterbi_seq(probs: np.ndarray, f0_min: float, f0_max: float) -> np.ndarray:
     """decode.viterbi on the masked sigmoid outputs: softmax over the bins (float32), then
     librosa.sequence.viterbi(prob, transition): log(prob + tiny) float32, log(transition + tiny) float64, uniform
     p_init, values in float64, first argmax; returns the bin path [F]."""

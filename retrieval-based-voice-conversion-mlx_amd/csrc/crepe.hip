@@ -251,8 +251,17 @@ __global__ __launch_bounds__(VT) void k_crepe_logprob(const float* __restrict__ 
 // (S_k the row sum) and log(tiny) outside it: the out-of-band candidates reduce to the global maximum of value[t-1]
 // (its first index) plus log(tiny), which wins only when that index lies outside j's band. ptr [F][360]; the last
 // state is the first argmax of value[F-1], then the back-pointers are followed (one lane).
-__global__ __launch_bounds__(VT) void k_crepe_viterbi(const float* __restrict__ lp, int F, int* __restrict__ ptr,
-                                                      int* __restrict__ bins) {
+// torchcrepe.predict decodes each batch of `seg` frames (rvc/lib/predictors/f0.py:38-49: batch_size 512) on its own --
+// postprocess, and so decode.viterbi, runs once per batch from the uniform initial state -- so block b decodes frames
+// [b seg, min(F, (b + 1) seg)) as an independent sequence (the segments also run in parallel).
+__global__ __launch_bounds__(VT) void k_crepe_viterbi(const float* __restrict__ lp_all, int F_all, int seg,
+                                                      int* __restrict__ ptr_all, int* __restrict__ bins_all) {
+  const int t0 = blockIdx.x * seg;
+  if (t0 >= F_all) return;
+  const int F = min(seg, F_all - t0);
+  const float* lp = lp_all + (long long)t0 * CR_BINS;
+  int* ptr = ptr_all + (long long)t0 * CR_BINS;
+  int* bins = bins_all + t0;
   __shared__ double val[2][CR_BINS];
   __shared__ double rv[VT / 64];
   __shared__ int ri[VT / 64];
@@ -384,11 +393,11 @@ __global__ void k_crepe_rvc_filter(const float* __restrict__ f0r, const float* _
 
 hipError_t crepe_decode_viterbi(const float* probs, int F, int minidx, int maxidx, const float* dither, float thr,
                                 float* lp, int* ptr, int* bins, float* f0_raw, float* per_raw, float* f0, double* f0d,
-                                float* per, hipStream_t s) {
+                                float* per, hipStream_t s, int seg) {
   if (F <= 0) return hipSuccess;
-  if (minidx < 0 || maxidx > CR_BINS || minidx >= maxidx) return hipErrorInvalidValue;
+  if (minidx < 0 || maxidx > CR_BINS || minidx >= maxidx || seg < 1) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_crepe_logprob, dim3(F), dim3(VT), 0, s, probs, minidx, maxidx, lp);
-  hipLaunchKernelGGL(k_crepe_viterbi, dim3(1), dim3(VT), 0, s, lp, F, ptr, bins);
+  hipLaunchKernelGGL(k_crepe_viterbi, dim3((F + seg - 1) / seg), dim3(VT), 0, s, lp, F, seg, ptr, bins);
   hipLaunchKernelGGL(k_crepe_rvc_pitch, dim3((F + 255) / 256), dim3(256), 0, s, probs, bins, dither, F, f0_raw, per_raw);
   hipLaunchKernelGGL(k_crepe_rvc_filter, dim3((F + 255) / 256), dim3(256), 0, s, f0_raw, per_raw, F, thr, f0, f0d, per);
   return hipGetLastError();

@@ -221,10 +221,12 @@ hipError_t crepe_relu_bn_pool(const float* x, long long rows_in, int C, const fl
 hipError_t crepe_decode(const float* probs, int F, double lo_cents, double hi_cents, float thr, float* f0_raw,
                         float* per_raw, float* f0, double* f0d, float* per, hipStream_t s);
 // torchcrepe's viterbi decode + rvc/'s filters (bins [minidx, maxidx) allowed; dither [F] cents or NULL): workspace
-// lp [F][360] fp32, ptr [F][360] int32, bins [F] int32
+// lp [F][360] fp32, ptr [F][360] int32, bins [F] int32. Every run of `seg` frames is decoded as its own sequence
+// (torchcrepe.predict's batches, CREPE_RVC_BATCH at rvc/'s batch_size); the filters run over all F frames.
+constexpr int CREPE_RVC_BATCH = 512;  // rvc/lib/predictors/f0.py:38
 hipError_t crepe_decode_viterbi(const float* probs, int F, int minidx, int maxidx, const float* dither, float thr,
                                 float* lp, int* ptr, int* bins, float* f0_raw, float* per_raw, float* f0, double* f0d,
-                                float* per, hipStream_t s);
+                                float* per, hipStream_t s, int seg = CREPE_RVC_BATCH);
 hipError_t noise_conv_add(const float* har, long long har_bs, int stride, int taps, const float* wf, const float* nb,
                           float* y, int B, int T, int C, hipStream_t s);
 hipError_t upsample2_protect(const float* feats, const float* feats0, int L, int D, float* out, int T, const float* pitchf,

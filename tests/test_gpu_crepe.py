@@ -144,6 +144,34 @@ def test_crepe_viterbi_decode_vs_oracle(engine, lo, hi, thr):
     assert 0.5 < voiced.mean() < 1.0 and len(np.unique(np.round(f0_o[voiced]))) > 20
 
 
+def test_crepe_viterbi_decode_per_512_frame_batch(engine):
+    """torchcrepe.predict (batch_size 512, rvc/lib/predictors/f0.py:38-49) decodes every 512-frame batch as
+    its own viterbi sequence. F = 1300 (three batches, the last ragged) with the pitch track crossing both boundaries:
+    the device decode equals the oracle's per-batch decode, and a whole-sequence decode differs from it (so the
+    segmentation is observable on this input)."""
+    from oracle import crepe as oc
+
+    F = 1300
+    rng = np.random.default_rng(21)
+    t = np.arange(F)
+    track = 180 + 35 * np.sin(2 * np.pi * t / 700.0)
+    probs = rng.uniform(0.0, 0.3, size=(F, 360))
+    probs = np.maximum(probs, 0.9 * np.exp(-0.5 * ((np.arange(360)[None, :] - track[:, None]) / 1.5) ** 2))
+    # an ambiguous stretch at each boundary: a second, equally strong track 30 bins up, which the viterbi of a fresh
+    # batch (uniform prior) and of a continued sequence (the previous state's band) resolve differently
+    for b in (512, 1024):
+        probs[b - 6:b + 6] = np.maximum(probs[b - 6:b + 6],
+                                        0.95 * np.exp(-0.5 * ((np.arange(360)[None, :] - track[b - 6:b + 6, None] - 30)
+                                                              / 1.5) ** 2))
+    probs = probs.astype(np.float32)
+    f0, per = engine.crepe_decode(probs, 50.0, 1100.0, 0.1, semantics="rvc")
+    f0_o, per_o, _ = oc.get_f0_rvc(None, None, 50.0, 1100.0, 0.1, probs=probs)
+    np.testing.assert_allclose(f0.cpu().numpy(), f0_o, rtol=2e-6, atol=0)
+    np.testing.assert_array_equal(per.cpu().numpy(), per_o)
+    whole = oc.viterbi_bins(probs, 50.0, 1100.0, batch=F)
+    assert not np.array_equal(whole, oc.viterbi_bins(probs, 50.0, 1100.0))
+
+
 def test_pipeline_crepe_rvc_semantics(engine, crepe_case):
     """PipelineRVCX(semantics="rvc") with f0_method crepe-tiny: get_f0 is rvcx_crepe_ex semantics 1 + f0_post, and the
     device pipeline (rvcx_pipeline_opts.f0_method 2) decodes CREPE on the high-passed, t_pad-padded input."""
