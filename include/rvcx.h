@@ -251,11 +251,16 @@ int rvcx_pipeline(rvcx_ctx* ctx, const double* d_audio, int64_t n, int sid, doub
  * rvcx_workspace_bytes: the pool a pipeline call of B utterances of n samples under opts takes (B = 1 as
  *   rvcx_pipeline_ex, B > 1 as rvcx_pipeline_batch). It runs that call once on zero audio on `stream` from an empty
  *   pool (loaded models required; outputs discarded) and reports every region the pool took, regrown ones included,
- *   so an arena of that size holds the call; the pool is released again before it returns.
+ *   so an arena of that size holds the call; the pool is released again before it returns. Inputs above t_max are
+ *   sized on the worst-case split plan (the longest chunk any audio can give: the pipeline processes its chunks
+ *   longest first, so the work buffers grow only inside the first chunk), so the size holds for any audio of n samples.
  * rvcx_set_workspace: hand the context a caller-owned device arena (e.g. a torch uint8 tensor's data_ptr(), 256-B
  *   aligned), valid until replaced or the context is destroyed: the pool is then carved from it and never allocated,
  *   and a call that would need more fails with RVCX_E_OOM. NULL, 0 returns to internal allocation. The current pool
- *   is released first (the device is synchronised).
+ *   is released first (the device is synchronised). While attached the arena belongs to the library: every compute
+ *   call carves its regions from offset 0 again (a sized arena then holds any sequence of calls each of which it
+ *   holds alone), and nothing is assumed to survive between calls, so a caller's writes into the arena between calls
+ *   cannot change results -- but they must be stream-ordered after the previous call's work.
  * rvcx_workspace_info: bytes the pool holds now, the arena size and the arena bytes carved so far (any may be NULL). */
 int rvcx_workspace_bytes(rvcx_ctx* ctx, int B, int64_t n, const rvcx_pipeline_opts* opts, int64_t* bytes,
                          void* stream);
@@ -367,6 +372,10 @@ int rvcx_rt_process(rvcx_ctx* ctx, rvcx_rt* rt, const float* d_in, const int32_t
  * fp32 accumulators (csrc/split_bf16.h; error against fp64 measured at or below the fp32-input MFMA's, 5.3x the
  * fp32 MFMA rate). Env RVCX_CONV_MATH=f32 | split | h16 sets the process default. */
 int rvcx_set_conv_math(rvcx_ctx* ctx, int mode);
+
+/* Removed in round 4 (deprecated shim, kept so existing callers link): the reduced-precision generator is now a
+ * per-hop setting, rvcx_rt_opts.gen_precision. Always returns RVCX_E_INVALID with a message saying so. */
+int rvcx_set_generator_precision(rvcx_ctx* ctx, int precision);
 
 /* One Conv1d forward, time-major: d_x [T][C_in], d_w [taps][N][C_in] (torch weight [N][C_in][taps] permuted),
  * d_bias [N] (optional), d_y [T_out][N]; y[t] = bias + sum_k W[k] x[t*stride - pad + k*dilation] (zero outside).

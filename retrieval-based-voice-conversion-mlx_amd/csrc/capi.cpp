@@ -37,6 +37,7 @@ int guard(rvcx_ctx* c, F&& f) {
 void set_device(rvcx_ctx* c) {
   RVCX_HIP(hipSetDevice(c->device));
   c->check_device_status();
+  c->arena_rewind();
 }
 
 }  // namespace
@@ -646,6 +647,11 @@ int rvcx_workspace_bytes(rvcx_ctx* ctx, int B, int64_t n, const rvcx_pipeline_op
     ctx->release_pool();
     ctx->arena = nullptr;
     ctx->arena_bytes = 0;
+    struct PlanScope {
+      Ctx& c;
+      ~PlanScope() { c.sizing_plan = false; }
+    } plan_scope{*ctx};
+    ctx->sizing_plan = true;
     DevBuf audio, out;
     const int64_t m = n + 2 * opts->t_pad;
     const int64_t cap = (m / 160 + (opts->t_center > 0 ? n / opts->t_center : 0) + 2) * ctx->scfg.upp();
@@ -664,6 +670,12 @@ int rvcx_workspace_bytes(rvcx_ctx* ctx, int B, int64_t n, const rvcx_pipeline_op
       }
       RVCX_HIP(hipStreamSynchronize(s));
       need = (int64_t)ctx->carved;
+      // the per-chunk HuBERT feature buffers (pl.hb<i>) sum to the same total over any split plan up to one row and
+      // the 256-B rounding per chunk
+      if (B == 1 && opts->t_max > 0 && n + 160 > opts->t_max && opts->t_center > 0) {
+        const int64_t nts = n > opts->t_center ? (n - 1 - opts->t_center) / opts->t_center + 1 : 0;
+        need += (nts + 1) * ((int64_t)ctx->scfg.emb_dim * 4 + 512);
+      }
     } catch (...) {
       ctx->release_pool();
       ctx->arena = arena;
@@ -710,6 +722,13 @@ int rvcx_set_conv_math(rvcx_ctx* ctx, int mode) {
   return guard(ctx, [&] {
     if (mode < 0 || mode > 3) throw Error(RVCX_E_INVALID, "conv math mode must be 0, 1, 2 or 3");
     ctx->conv_math = mode;
+  });
+}
+
+int rvcx_set_generator_precision(rvcx_ctx* ctx, int) {
+  return guard(ctx, [&] {
+    throw Error(RVCX_E_INVALID,
+                "rvcx_set_generator_precision was removed: set rvcx_rt_opts.gen_precision per streaming hop instead");
   });
 }
 

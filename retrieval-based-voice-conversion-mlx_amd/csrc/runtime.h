@@ -179,6 +179,21 @@ struct Ctx {
   char* arena = nullptr;
   size_t arena_bytes = 0, arena_used = 0;
   size_t carved = 0;  // bytes the pool has taken since the last release (every region, regrown ones included)
+  bool sizing_plan = false;  // rvcx_workspace_bytes: long inputs take the worst-case chunk plan (runtime_pipeline.cpp)
+  // Arena mode: every API call carves its regions from offset 0 again (called by the entry points before any work),
+  // so a call never inherits the regions earlier calls regrew. No device synchronisation: a call's work is enqueued
+  // after the previous call's on the caller's stream (the aux stream forks from it), so reuse is stream-ordered -- as
+  // for the named pool without an arena. The marks describing buffer contents go with the regions (a caller that
+  // wrote into its arena between calls cannot leave a stale zeroed buffer or memoised scalar behind).
+  void arena_rewind() {
+    if (!arena) return;
+    ws.clear();
+    zero_marks.clear();
+    i32_marks.clear();
+    gru_tags.clear();
+    arena_used = 0;
+    carved = 0;
+  }
   // synchronise the device and drop the named pool, with the marks that describe its contents (zeroed buffers,
   // memoised scalars, BiGRU tag counters)
   void release_pool() {

@@ -254,7 +254,15 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
     long long* dts = c.buf<long long>("pl.ts", (size_t)std::max(1, nts), s);
     check(split_points(filtered, n, (int)W, o.t_center, o.t_query, sum, dts, nts, s), "split_points");
     opt_ts.resize(nts);
-    if (nts > 0) {
+    if (nts > 0 && c.sizing_plan) {
+      // rvcx_workspace_bytes: the plan whose longest chunk is the longest any audio can give (each split point lies
+      // in [k t_center - t_query, k t_center + t_query]): a middle chunk from the lowest split to the highest next one
+      // (or, with one split, the first chunk up to its highest split); the rest centred
+      for (int k = 0; k < nts; ++k) opt_ts[k] = (int64_t)(k + 1) * o.t_center;
+      if (nts == 1) opt_ts[0] += o.t_query;
+      else opt_ts[0] -= o.t_query, opt_ts[1] += o.t_query;
+      for (auto& t : opt_ts) t = std::max<int64_t>(0, std::min<int64_t>(t, n - 1));
+    } else if (nts > 0) {
       RVCX_HIP(hipMemcpyAsync(opt_ts.data(), dts, sizeof(long long) * nts, hipMemcpyDeviceToHost, s));
       RVCX_HIP(hipStreamSynchronize(s));
       c.check_device_status();
@@ -298,7 +306,15 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
   const bool guided = c.scfg.f0;
   const int split = (ax != s && guided) ? gate_layer : HUBERT_LAYERS;
   std::vector<HubertRun> hruns(chunks.size());
-  for (size_t i = 0; i < chunks.size(); ++i) {
+  // chunks are processed longest first: every later chunk fits the shared work buffers the first one grew, so a
+  // call regrows nothing past its first chunk (a caller-sized arena, rvcx_workspace_bytes, holds any split plan);
+  // the per-chunk noise offsets, seeds and output positions keep the reference's order (computed up front below)
+  std::vector<size_t> order(chunks.size());
+  for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) {
+    return chunks[x].a1 - chunks[x].a0 > chunks[y].a1 - chunks[y].a0;
+  });
+  for (size_t i : order) {
     const int64_t len = chunks[i].a1 - chunks[i].a0;
     const int64_t cap_rows = len / 320 + 8;
     cfeats[i] = c.buf<float>("pl.hb" + std::to_string(i), (size_t)cap_rows * E, ax);
@@ -378,11 +394,36 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
   // 6. voice conversion per chunk (pipeline.py:486-512), outputs trimmed t_pad_tgt per side
   const int upp = c.scfg.upp();
   const int I = c.scfg.I;
-  int64_t written = 0, ez_off = 0, es_off = 0;
-  uint64_t cseed = seed;
-  const bool fuse_trim = chunks.size() == 1 && o.volume_envelope == 1.0;
+  // per chunk, in the reference's order: frames T = min(len / 160, 2 L) (vc_forward), noise offsets, seed, output
+  // position
+  const size_t nch = chunks.size();
+  std::vector<int64_t> ez_off(nch), es_off(nch), pos(nch);
+  std::vector<uint64_t> cseed(nch);
+  int64_t written = 0;
+  {
+    int64_t ez = 0, es = 0;
+    uint64_t sd = seed;
+    for (size_t i = 0; i < nch; ++i) {
+      ez_off[i] = ez;
+      es_off[i] = es;
+      cseed[i] = sd;
+      pos[i] = written;
+      if (nch > 1) {
+        const int64_t T = std::min<int64_t>((chunks[i].a1 - chunks[i].a0) / W, 2 * cL[i]);
+        ez += (int64_t)I * T;
+        es += c.scfg.src_noise_total(1, T);  // this chunk's decoder draws (include/rvcx.h layouts)
+        const int64_t keep = T * upp - 2 * o.t_pad_tgt;
+        if (keep <= 0) throw Error(RVCX_E_SHAPE, "pipeline: chunk too short for the padding");
+        written += keep;
+      }
+      sd += 0x9E3779B97F4A7C15ull;
+    }
+    if (written > cap)
+      throw Error(RVCX_E_CAPACITY, "pipeline: output needs more than " + std::to_string(cap) + " samples");
+  }
+  const bool fuse_trim = nch == 1 && o.volume_envelope == 1.0;
   const float* trimmed = out;
-  for (size_t i = 0; i < chunks.size(); ++i) {
+  for (size_t i : order) {
     const Chunk& ch = chunks[i];
     const int64_t len = ch.a1 - ch.a0;
     const int64_t cap_vc = (len / W) * upp;
@@ -390,22 +431,20 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
     // pitch[:, f_lo:f_hi], then [:p_len] inside voice_conversion with p_len = min(len/160, 2L)
     const int64_t nvc = vc_forward(c, pad32 + ch.a0, len, pitch ? pitch + ch.f_lo : nullptr,
                                    pitchf ? pitchf + ch.f_lo : nullptr, ch.f_hi - ch.f_lo, o.sid,
-                                   o.protect, o.index_rate, eps_z ? eps_z + ez_off : nullptr,
-                                   eps_src ? eps_src + es_off : nullptr, cseed, vc, cap_vc, s, cfeats[i], cL[i]);
-    const int64_t T = nvc / upp;
-    ez_off += (int64_t)I * T;
-    es_off += c.scfg.src_noise_total(1, T);  // this chunk's decoder draws (include/rvcx.h layouts)
+                                   o.protect, o.index_rate, eps_z ? eps_z + ez_off[i] : nullptr,
+                                   eps_src ? eps_src + es_off[i] : nullptr, cseed[i], vc, cap_vc, s, cfeats[i], cL[i]);
     const int64_t keep = nvc - 2 * o.t_pad_tgt;
     if (keep <= 0) throw Error(RVCX_E_SHAPE, "pipeline: chunk too short for the padding");
-    if (written + keep > cap)
-      throw Error(RVCX_E_CAPACITY, "pipeline: output needs more than " + std::to_string(cap) + " samples");
+    if (nch == 1) {
+      if (keep > cap)
+        throw Error(RVCX_E_CAPACITY, "pipeline: output needs more than " + std::to_string(cap) + " samples");
+      written = keep;
+    }
     if (fuse_trim)
       trimmed = vc + o.t_pad_tgt;  // one chunk, no envelope: the peak normalisation reads it in place
     else
-      RVCX_HIP(hipMemcpyAsync(out + written, vc + o.t_pad_tgt, (size_t)keep * sizeof(float), hipMemcpyDeviceToDevice,
+      RVCX_HIP(hipMemcpyAsync(out + pos[i], vc + o.t_pad_tgt, (size_t)keep * sizeof(float), hipMemcpyDeviceToDevice,
                               s));
-    written += keep;
-    cseed += 0x9E3779B97F4A7C15ull;
   }
   // 7. volume envelope (pipeline.py:545-549) and peak normalisation (:550-552)
   if (o.volume_envelope != 1.0) {

@@ -363,6 +363,11 @@ class Engine:
         res = out[: no.value]
         return (res, f0) if want_f0 else res
 
+    def set_generator_precision(self, precision):
+        """Removed in round 4: the fp16 streaming generator is a per-hop option (StreamGroup.process(...,
+        gen_precision=...), rvcx_rt_opts.gen_precision). Raises RvcxError(RVCX_E_INVALID) with that message."""
+        self._check(self.lib.rvcx_set_generator_precision(self.ctx, int(precision)), "set_generator_precision")
+
     def workspace_bytes(self, n: int, B: int = 1, opts=None) -> int:
         """Device scratch a pipeline call of B utterances of n samples takes (rvcx_workspace_bytes: one call on zero
         audio from an empty pool; the pool is released after)."""

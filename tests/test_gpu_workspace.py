@@ -56,3 +56,62 @@ def test_workspace_bytes_grows_with_the_call(engine):
     long = engine.workspace_bytes(6 * 16000)
     batch = engine.workspace_bytes(2 * 16000, B=4)
     assert 0 < short < long and short < batch
+
+
+def _split_opts(engine):
+    # a multi-chunk plan at test sizes: t_max 3 s, t_center 2 s, t_query 0.5 s (pipeline.py:440-452 with x_max 3,
+    # x_center 2, x_query 0.5)
+    return engine.pipeline_opts(t_pad=16000, t_pad_tgt=48000, t_max=48000, t_center=32000, t_query=8000)
+
+
+def _speech_with_gaps(n, gaps, seed=5):
+    a = _audio(n, seed)
+    for g in gaps:
+        a[g:g + 800] *= 1e-4
+    return a
+
+
+def test_workspace_query_holds_long_inputs_with_off_centre_splits(engine):
+    """for inputs above t_max the chunk plan depends on the audio. Quiet stretches at the low end of the
+    first split window and the high end of the second give the longest middle chunk real audio can give; an arena
+    of the queried size (sized on the worst-case plan) holds the call, bit-identical to internal allocation."""
+    engine.set_pipeline_highpass()
+    o = _split_opts(engine)
+    n = 8 * 16000
+    audio = _speech_with_gaps(n, [32000 - 8000 + 10, 64000 + 8000 - 900])
+    ref = engine.pipeline_ex(audio, o, seed=3).cpu()
+    need = engine.workspace_bytes(n, opts=o)
+    arena = torch.empty(need, dtype=torch.uint8, device=engine.device)
+    try:
+        engine.set_workspace(arena)
+        out = engine.pipeline_ex(audio, o, seed=3).cpu()
+        used = engine.workspace_info()[2]
+        assert 0 < used <= need
+        assert torch.equal(out, ref)
+    finally:
+        engine.set_workspace(None)
+
+
+def test_workspace_arena_short_then_long_call(engine):
+    """an arena sized for the long call carries a short call and then the long one (each call carves its
+    regions from offset 0: the short call's regions are not kept beside the long call's), and writes by the caller
+    into the arena between calls do not leak into results (the memoised zeros / scalars go with the regions)."""
+    engine.set_pipeline_highpass()
+    o = _split_opts(engine)
+    long_n, short_n = 8 * 16000, int(2.5 * 16000)
+    a_long, a_short = _speech_with_gaps(long_n, [30000, 70000]), _audio(short_n, 9)
+    ref_long = engine.pipeline_ex(a_long, o, seed=1).cpu()
+    ref_short = engine.pipeline_ex(a_short, o, seed=2).cpu()
+    need = engine.workspace_bytes(long_n, opts=o)
+    assert need >= engine.workspace_bytes(short_n, opts=o)
+    arena = torch.empty(need, dtype=torch.uint8, device=engine.device)
+    try:
+        engine.set_workspace(arena)
+        assert torch.equal(engine.pipeline_ex(a_short, o, seed=2).cpu(), ref_short)
+        assert torch.equal(engine.pipeline_ex(a_long, o, seed=1).cpu(), ref_long)
+        arena.fill_(0x5A)
+        assert torch.equal(engine.pipeline_ex(a_short, o, seed=2).cpu(), ref_short)
+        arena.fill_(0xA5)
+        assert torch.equal(engine.pipeline_ex(a_long, o, seed=1).cpu(), ref_long)
+    finally:
+        engine.set_workspace(None)
