@@ -370,8 +370,16 @@ int rvcx_rt_process(rvcx_ctx* ctx, rvcx_rt* rt, const float* d_in, const int32_t
  * MFMA rate), 3 = as 2, except that the generator's weight-streamed convs and fused ResBlock pairs split both
  * operands into two fp16 planes (x = h + 2^-11 l, 11 significand bits each) with three plane products into two
  * fp32 accumulators (csrc/split_bf16.h; error against fp64 measured at or below the fp32-input MFMA's, 5.3x the
- * fp32 MFMA rate). Env RVCX_CONV_MATH=f32 | split | h16 sets the process default. */
+ * fp32 MFMA rate). Env RVCX_CONV_MATH=f32 | split | h16 sets the process default when RVCX_EXPERIMENTAL=1. */
 int rvcx_set_conv_math(rvcx_ctx* ctx, int mode);
+
+/* The effective configuration as a NUL-terminated JSON object (cap bytes; *len, optional, gets its length): the
+ * context's contraction arithmetic, whether developer knobs are enabled, and every RVCX_* environment variable of the
+ * process with whether it is honoured. The RVCX_* tuning / A-B switches (tile and split-K policy, kernel-path and
+ * arithmetic overrides such as RVCX_CONV_MATH) are read only when RVCX_EXPERIMENTAL=1: without it they are ignored and
+ * listed here as not honoured. RVCX_E_CAPACITY when cap is too small (the string is truncated). ctx may be NULL (the
+ * process-wide fields only; no device is touched). */
+int rvcx_config_info(const rvcx_ctx* ctx, char* buf, int64_t cap, int64_t* len);
 
 /* Removed in round 4 (deprecated shim, kept so existing callers link): the reduced-precision generator is now a
  * per-hop setting, rvcx_rt_opts.gen_precision. Always returns RVCX_E_INVALID with a message saying so. */

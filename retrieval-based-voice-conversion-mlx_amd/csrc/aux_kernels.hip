@@ -963,7 +963,7 @@ hipError_t filtfilt_sos_pad(const SosPlan& p, int order, const double* x, long l
   double* sw = yb + ne;
   hipLaunchKernelGGL(k_odd_ext, dim3(nblocks(ne)), dim3(TB), 0, s, x, n, padlen, ext);
   static const bool per_section = [] {  // RVCX_SOS_PER_SECTION=1: one local / carry / fix round per section (A/B aid)
-    const char* e = std::getenv("RVCX_SOS_PER_SECTION");
+    const char* e = rvcx_knob("RVCX_SOS_PER_SECTION");
     return e && std::atoi(e) != 0;
   }();
   if (p.casc && !per_section) return casc_filtfilt_pad(p, ext, ne, padlen, n, t_pad, yf, pad64, pad32, s);

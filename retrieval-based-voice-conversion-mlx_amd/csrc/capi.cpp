@@ -5,10 +5,25 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
+#include <unistd.h>
 
 #include "runtime.h"
 
+extern char** environ;
+
 using namespace rvcx;
+
+namespace rvcx {
+static bool experimental_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("RVCX_EXPERIMENTAL");
+    return e && std::atoi(e) == 1;
+  }();
+  return on;
+}
+const char* rvcx_knob(const char* name) { return experimental_on() ? std::getenv(name) : nullptr; }
+}  // namespace rvcx
 
 struct rvcx_ctx : public Ctx {};
 struct rvcx_rt {
@@ -49,7 +64,7 @@ hipStream_t Ctx::aux_stream() {
     // RVCX_AUX_PRIO=1: the aux stream (HuBERT beside RMVPE) at the device's least priority, so the critical RMVPE
     // chain's workgroups are dispatched first when both queues have work
     static const int low = [] {
-      const char* e = std::getenv("RVCX_AUX_PRIO");
+      const char* e = rvcx_knob("RVCX_AUX_PRIO");
       return e ? std::atoi(e) : 0;
     }();
     int least = 0, greatest = 0;
@@ -103,7 +118,7 @@ Ctx::~Ctx() {
 
 hipStream_t fork_aux(Ctx& c, hipStream_t s) {
   static const bool no_overlap = [] {
-    const char* e = std::getenv("RVCX_NO_OVERLAP");
+    const char* e = rvcx_knob("RVCX_NO_OVERLAP");
     return e && std::atoi(e) != 0;
   }();
   if (c.prof || no_overlap) return s;
@@ -158,11 +173,11 @@ const void* Ctx::rb_wsplit_for(const float* w, int C, int k, int wfmt, hipStream
 
 void launch_rb_pair(Ctx& c, const RbPairArgs& a_in, hipStream_t s) {
   static const int cfg = [] {
-    const char* e = std::getenv("RVCX_RB_CFG");
+    const char* e = rvcx_knob("RVCX_RB_CFG");
     return e ? std::atoi(e) : 0;
   }();
   static const int flags = [] {
-    const char* e = std::getenv("RVCX_RB_FLAGS");
+    const char* e = rvcx_knob("RVCX_RB_FLAGS");
     return e ? std::atoi(e) : 0;
   }();
   RbPairArgs a = a_in;
@@ -723,6 +738,41 @@ int rvcx_set_conv_math(rvcx_ctx* ctx, int mode) {
     if (mode < 0 || mode > 3) throw Error(RVCX_E_INVALID, "conv math mode must be 0, 1, 2 or 3");
     ctx->conv_math = mode;
   });
+}
+
+int rvcx_config_info(const rvcx_ctx* ctx, char* buf, int64_t cap, int64_t* len) {
+  // JSON: the effective contraction arithmetic, the developer-knob opt-in and every RVCX_* variable of the process
+  // environment with whether it is honoured (ctx may be NULL: the process-wide part only, no device needed)
+  std::string j = "{\"arch\": \"gfx950\"";
+  if (ctx) j += ", \"conv_math_ctx\": " + std::to_string(ctx->conv_math);
+  const char* cm = rvcx_knob("RVCX_CONV_MATH");
+  j += ", \"conv_math_default\": \"" + std::string(cm ? cm : "h16") + "\"";
+  j += ", \"experimental\": " + std::string(experimental_on() ? "true" : "false");
+  if (ctx) j += ", \"arena_bytes\": " + std::to_string(ctx->arena_bytes);
+  j += ", \"env\": {";
+  bool first = true;
+  for (char** e = environ; e && *e; ++e) {
+    if (std::strncmp(*e, "RVCX_", 5) != 0) continue;
+    const char* eq = std::strchr(*e, '=');
+    if (!eq) continue;
+    std::string k(*e, eq - *e), v(eq + 1);
+    std::string ve;
+    for (char ch : v)
+      if (ch != '"' && ch != '\\' && (unsigned char)ch >= 32) ve += ch;
+    const bool honoured = k == "RVCX_EXPERIMENTAL" || k == "RVCX_PROF_DUMP" || k == "RVCX_GRU_SPIN_LIMIT" ||
+                          k == "RVCX_LIB" || experimental_on();
+    j += std::string(first ? "" : ", ") + "\"" + k + "\": {\"value\": \"" + ve + "\", \"honoured\": " +
+         (honoured ? "true" : "false") + "}";
+    first = false;
+  }
+  j += "}}";
+  if (len) *len = (int64_t)j.size();
+  if (buf && cap > 0) {
+    const size_t n = std::min<size_t>(j.size(), (size_t)cap - 1);
+    std::memcpy(buf, j.data(), n);
+    buf[n] = 0;
+  }
+  return (int64_t)j.size() < cap || !buf ? RVCX_OK : RVCX_E_CAPACITY;
 }
 
 int rvcx_set_generator_precision(rvcx_ctx* ctx, int) {

@@ -484,7 +484,7 @@ hipError_t small2d_wsplit_build(const ConvArgs& a, void* out, hipStream_t s) {
 
 hipError_t conv2d_small(const ConvArgs& a, hipStream_t s) {
   static const bool h16_ok = [] {  // RVCX_SMALL2D_F32=1: the exact-f32 form whatever the conv arithmetic (A/B aid)
-    const char* e = std::getenv("RVCX_SMALL2D_F32");
+    const char* e = rvcx_knob("RVCX_SMALL2D_F32");
     return !(e && std::atoi(e) != 0);
   }();
   if (h16_ok && conv_math_of(a) == 3 && a.wsplit && a.wsplit_fmt == WSPLIT_S2D) {

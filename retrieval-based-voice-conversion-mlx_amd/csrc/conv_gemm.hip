@@ -696,7 +696,7 @@ hipError_t launch_tiny(const ConvArgs& a, bool two_d, hipStream_t s) {
 
 bool xcd_enabled() {
   static const bool v = [] {
-    const char* e = std::getenv("RVCX_NO_XCD");
+    const char* e = rvcx_knob("RVCX_NO_XCD");
     return !(e && std::atoi(e) != 0);
   }();
   return v;
@@ -817,7 +817,7 @@ hipError_t launch_forced_asb(const ConvArgs& a, hipStream_t s) {
 // A-tile staging: serial (1) or 4 loads in flight per thread (4); RVCX_CONV_ASB overrides the default
 inline int default_asb() {
   static const int v = [] {
-    const char* e = std::getenv("RVCX_CONV_ASB");
+    const char* e = rvcx_knob("RVCX_CONV_ASB");
     return e ? std::atoi(e) : 1;
   }();
   return v;
@@ -836,7 +836,7 @@ hipError_t launch_forced(const ConvArgs& a, hipStream_t s) {
 // otherwise; split-K when the output grid cannot fill 256 CUs.
 // RVCX_CFG_LONG / RVCX_CFG_SHORT / RVCX_CFG_NARROW override a class (measurement aid).
 inline int env_cfg(const char* name, int dflt) {
-  const char* e = std::getenv(name);
+  const char* e = rvcx_knob(name);
   return e ? std::atoi(e) : dflt;
 }
 // contraction arithmetic: 1 = native fp32 MFMA (conv_gemm_kernel), 2 = fp32 through the 3-way bf16 split everywhere
@@ -846,7 +846,7 @@ inline int env_cfg(const char* name, int dflt) {
 // RVCX_CONV_MATH (f32 | split | h16)
 inline int conv_math(const ConvArgs& a) {
   static const int env = [] {
-    const char* e = std::getenv("RVCX_CONV_MATH");
+    const char* e = rvcx_knob("RVCX_CONV_MATH");
     if (e && (std::string(e) == "f32" || std::string(e) == "1")) return 1;
     if (e && (std::string(e) == "split" || std::string(e) == "2")) return 2;
     return 3;
@@ -896,7 +896,7 @@ inline void cfg_tile(int cfg, int& BM, int& BN) {
 
 inline bool small2d_enabled() {
   static const bool v = [] {
-    const char* e = std::getenv("RVCX_NO_SMALL2D");
+    const char* e = rvcx_knob("RVCX_NO_SMALL2D");
     return !(e && std::atoi(e) != 0);
   }();
   return v;
@@ -964,7 +964,7 @@ hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
   // plain GEMMs (1-D, one tap, stride 1) take the double-buffered pipeline unless a.pipe < 0 or
   // RVCX_NO_PIPE=1; a.pipe > 0 forces it (benchmarks)
   static const bool pipe_env = [] {
-    const char* e = std::getenv("RVCX_NO_PIPE");
+    const char* e = rvcx_knob("RVCX_NO_PIPE");
     return !(e && std::atoi(e) != 0);
   }();
   const bool gemm = !TWO_D && a.taps == 1 && a.stride == 1;
@@ -1062,7 +1062,7 @@ long long conv_plan_splitk(ConvArgs& a, bool two_d) {
 
 bool conv_wsb_wants(const ConvArgs& a) {
   static const bool off = [] {
-    const char* e = std::getenv("RVCX_NO_WSB");
+    const char* e = rvcx_knob("RVCX_NO_WSB");
     return e && std::atoi(e) != 0;
   }();
   if (off || conv_math(a) < 2 || !conv_wsb_eligible(a)) return false;

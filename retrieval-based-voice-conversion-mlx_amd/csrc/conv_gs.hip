@@ -312,7 +312,7 @@ hipError_t launch_gs(const ConvArgs& a, int ntn_enable, int ksplit, hipStream_t 
   const size_t smem = (size_t)2 * BM * (h16 ? ERS_H : ERS);
   // M-fastest tile runs when the pre-split weight (6 B per element) outweighs the activation operand (4 B)
   static const int mf_env = [] {
-    const char* e = std::getenv("RVCX_GS_MFAST");
+    const char* e = rvcx_knob("RVCX_GS_MFAST");
     return e ? std::atoi(e) : -1;
   }();
   const double wbytes = 6.0 * a.N * a.C_in * a.taps, abytes = 4.0 * (double)Mtot * a.C_in * a.batch;
@@ -565,7 +565,7 @@ bool conv_gs_tile(int cfg, int& BM, int& BN) {
 // the windowed 2-D kernel: 3x3 / pad 1 / stride 1, same-size images at most 32 pixels wide with 32 % W == 0
 bool conv_gsw_eligible(const ConvArgs& a) {
   static const bool on = [] {
-    const char* e = std::getenv("RVCX_NO_GSW");
+    const char* e = rvcx_knob("RVCX_NO_GSW");
     return !(e && std::atoi(e) != 0);
   }();
   return on && conv_gs_eligible(a, true) && a.KH == 3 && a.KW == 3 && a.padh == 1 && a.padw == 1 &&

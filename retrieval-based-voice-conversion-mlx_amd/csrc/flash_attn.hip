@@ -658,7 +658,7 @@ __global__ __launch_bounds__(256) void k_flash_combine(const float* __restrict__
 // per split
 int flash_attn_splits(int B, int nh, int T) {
   static const int waves = [] {  // RVCX_FA_WAVES: target query-block x split waves (A/B aid)
-    const char* e = std::getenv("RVCX_FA_WAVES");
+    const char* e = rvcx_knob("RVCX_FA_WAVES");
     return e ? std::max(1, std::atoi(e)) : 4096;  // same-box C2: 512 18.12, 1024 17.91, 2048 17.98, 4096 17.84 ms
   }();
   const int qb = (T + FA_Q - 1) / FA_Q, kb = (T + FA_K - 1) / FA_K;
@@ -670,7 +670,7 @@ int flash_attn_splits(int B, int nh, int T) {
 // RVCX_FA_MATH=split: the three-plane bf16 kernel (A/B aid); default the two-plane fp16 split with K / V images
 static bool fa_h16() {
   static const bool v = [] {
-    const char* e = std::getenv("RVCX_FA_MATH");
+    const char* e = rvcx_knob("RVCX_FA_MATH");
     return !(e && std::string(e) == "split");
   }();
   return v;
@@ -704,7 +704,7 @@ hipError_t flash_attn(const float* qkv, int ldq, int B, int T, int nh, int dk, f
     dim3 g2(kb, B * nh, dk / 16 + dk / 16);  // NS K steps + 2 NT V^T pairs (NS = 2 NT)
     // NW key splits per block merged in LDS (RVCX_FA_NW 1: one wave per split, every split a partial)
     static const int nw_env = [] {
-      const char* e = std::getenv("RVCX_FA_NW");
+      const char* e = rvcx_knob("RVCX_FA_NW");
       return e ? std::atoi(e) : 4;
     }();
     const int NWB = (nw_env == 4 && nsplit >= 4) ? 4 : 1;

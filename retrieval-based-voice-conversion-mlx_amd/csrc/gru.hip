@@ -203,13 +203,15 @@ hipError_t gru_bidir(const float* gi, const float* whh_f, const float* bhh_f, co
   }
   *next_tag = tag0 + (unsigned)T + 1;
   static const int adj = [] {  // RVCX_GRU_ADJACENT=1: partners in adjacent blocks (different XCDs; A/B aid)
-    const char* e = std::getenv("RVCX_GRU_ADJACENT");
+    const char* e = rvcx_knob("RVCX_GRU_ADJACENT");
     return e ? std::atoi(e) : 0;
   }();
-  unsigned spin = SPIN_LIMIT;  // test hook: a tiny RVCX_GRU_SPIN_LIMIT forces the timeout path
+  // fault-injection test hook, read without the RVCX_EXPERIMENTAL opt-in (it cannot change a result, only force the
+  // loud timeout path): a tiny RVCX_GRU_SPIN_LIMIT makes the hand-off time out
+  unsigned spin = SPIN_LIMIT;
   if (const char* e = std::getenv("RVCX_GRU_SPIN_LIMIT")) spin = (unsigned)std::strtoul(e, nullptr, 10);
   static const int mode = [] {
-    const char* e = std::getenv("RVCX_GRU_MODE");
+    const char* e = rvcx_knob("RVCX_GRU_MODE");
     return e ? std::atoi(e) : 0;
   }();
   auto kern = mode == 1 ? k_gru_bidir<1> : (mode == 2 ? k_gru_bidir<2> : k_gru_bidir<0>);

@@ -342,7 +342,7 @@ void launch_rb_pair(Ctx& c, const RbPairArgs& a, hipStream_t s);
 // (A/B measurement aid), RVCX_RB_CFG picks a tile configuration
 inline bool rb_fuse_enabled() {
   static const bool v = [] {
-    const char* e = std::getenv("RVCX_NO_RBFUSE");
+    const char* e = rvcx_knob("RVCX_NO_RBFUSE");
     return !(e && std::atoi(e) != 0);
   }();
   return v;
@@ -352,7 +352,7 @@ inline bool rb_fuse_enabled() {
 // score path (A/B measurement aid)
 inline bool flash_enabled() {
   static const bool v = [] {
-    const char* e = std::getenv("RVCX_NO_FLASH");
+    const char* e = rvcx_knob("RVCX_NO_FLASH");
     return !(e && std::atoi(e) != 0);
   }();
   return v;

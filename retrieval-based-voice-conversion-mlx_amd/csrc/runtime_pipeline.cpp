@@ -295,7 +295,7 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
   //    the U-Net then shares the GPU with less of HuBERT and the rest of HuBERT fills the BiGRU's idle CUs.
   hipStream_t ax = fork_aux(c, s);
   static const int gate_layer = [] {
-    const char* e = std::getenv("RVCX_HUBERT_GATE");  // first layer issued beside the BiGRU (12: none)
+    const char* e = rvcx_knob("RVCX_HUBERT_GATE");  // first layer issued beside the BiGRU (12: none)
     // A/B on MI355X (BiGRU launched first), round 2: 2 21.84 ms, 3 21.87, 4 21.96, 1 22.03, 0 22.12, 6 22.30; round 4 (same
     // box, 4 runs each, profiles/r04q_ab_hubert_gate.txt): 0 13.39 ms, 1 13.45, 2 13.53 -- with the fp16-split U-Net
     // and HuBERT the whole encoder fits beside the BiGRU, and the U-Net then shares the GPU with the front alone

@@ -454,7 +454,7 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
       static const int rb_maxc = [] {
         // widest stage taking the fused pair: 32 channels (same-box A/B of C2: fused 32 + weight-streamed 64
         // 21.97 ms, fused 32 + 64 22.46, weight-streamed both 23.07; RVCX_RB_MAXC overrides)
-        const char* e = std::getenv("RVCX_RB_MAXC");
+        const char* e = rvcx_knob("RVCX_RB_MAXC");
         return e ? std::atoi(e) : 32;
       }();
       bool fuse = rb_fuse_enabled() && C <= rb_maxc;

@@ -9,6 +9,12 @@
 
 namespace rvcx {
 
+// Process-wide developer knobs (RVCX_* environment variables: A/B switches, tile / split-K policy overrides, the
+// contraction arithmetic): honoured ONLY when RVCX_EXPERIMENTAL=1 is set, so a stray variable in a user's shell cannot
+// change a result or a kernel path. Returns getenv(name), or nullptr without the opt-in. rvcx_config_info reports
+// the opt-in and every RVCX_* variable present (honoured or ignored). Defined in capi.cpp.
+const char* rvcx_knob(const char* name);
+
 enum Act : int {
   ACT_NONE = 0,
   ACT_LRELU = 1,    // leaky relu with slope

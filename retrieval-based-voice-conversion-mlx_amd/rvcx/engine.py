@@ -363,6 +363,18 @@ class Engine:
         res = out[: no.value]
         return (res, f0) if want_f0 else res
 
+    def config_info(self) -> dict:
+        """The effective configuration (rvcx_config_info): contraction arithmetic, whether RVCX_* developer knobs are
+        honoured (RVCX_EXPERIMENTAL=1), and each RVCX_* variable of the environment."""
+        import json
+
+        n = ctypes.c_int64(0)
+        self.lib.rvcx_config_info(self.ctx, None, 0, ctypes.byref(n))
+        buf = ctypes.create_string_buffer(int(n.value) + 1)
+        self._check(self.lib.rvcx_config_info(self.ctx, ctypes.cast(buf, ctypes.c_void_p), len(buf), ctypes.byref(n)),
+                    "config_info")
+        return json.loads(buf.value.decode())
+
     def set_generator_precision(self, precision):
         """Removed in round 4: the fp16 streaming generator is a per-hop option (StreamGroup.process(...,
         gen_precision=...), rvcx_rt_opts.gen_precision). Raises RvcxError(RVCX_E_INVALID) with that message."""

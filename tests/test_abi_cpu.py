@@ -101,3 +101,39 @@ def test_index_parse_rejects_huge_counts():
     struct.pack_into("<Q", buf, at, (1 << 61) + 4)
     with pytest.raises(_lib.RvcxError):
         _lib.index_parse(bytes(buf))
+
+
+_KNOB_PROBE = r"""
+import ctypes, json, sys
+lib = ctypes.CDLL(sys.argv[1])
+lib.rvcx_config_info.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
+buf = ctypes.create_string_buffer(4096)
+n = ctypes.c_int64(0)
+assert lib.rvcx_config_info(None, ctypes.cast(buf, ctypes.c_void_p), 4096, ctypes.byref(n)) == 0
+print(buf.value.decode())
+"""
+
+
+@pytest.mark.parametrize("experimental", [False, True])
+def test_env_knobs_need_the_experimental_opt_in(experimental):
+    """RVCX_* tuning / arithmetic switches are honoured only with RVCX_EXPERIMENTAL=1; without it
+    RVCX_CONV_MATH=f32 is ignored (the default arithmetic stays) and rvcx_config_info lists it as not honoured."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from rvcx import _lib
+
+    env = {k: v for k, v in os.environ.items() if not k.startswith("RVCX_")}
+    env["RVCX_CONV_MATH"] = "f32"
+    env["RVCX_NO_WSB"] = "1"
+    if experimental:
+        env["RVCX_EXPERIMENTAL"] = "1"
+    out = subprocess.run([sys.executable, "-c", _KNOB_PROBE, _lib.LIB_PATH], env=env, capture_output=True, text=True,
+                         timeout=120, check=True).stdout
+    info = json.loads(out.strip().splitlines()[-1])
+    assert info["experimental"] is experimental
+    assert info["conv_math_default"] == ("f32" if experimental else "h16")
+    assert info["env"]["RVCX_CONV_MATH"] == {"value": "f32", "honoured": experimental}
+    assert info["env"]["RVCX_NO_WSB"]["honoured"] is experimental

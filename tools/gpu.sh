@@ -14,6 +14,7 @@
 #   ab=E1;E2;...      same-box A/B of the C2 bench under env settings (',' for spaces inside one setting)
 #   ablib=LIB         same-box A/B of the C2 bench: LIB vs the in-tree librvcx.so
 set -o pipefail
+export RVCX_EXPERIMENTAL=1  # the A/B and measurement steps below use RVCX_* developer knobs
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 TAG=${1:?tag}; shift
