@@ -143,6 +143,36 @@ def cpu_baseline(n_samples: int, reps: int = 3):
                              "median of 5"}}
 
 
+def _pmc_family_traffic(name):
+    """HBM bytes per launch of one kernel family from profiles/pmc_traffic.json (its "families" table, the same PMC
+    passes as _pmc_traffic), only when measured on this exact source tree; else None."""
+    from rvcx.provenance import source_tree_hash
+
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if rec.get("tree") != source_tree_hash():
+        return None
+    fam = (rec.get("families") or {}).get(name)
+    return round(fam["hbm_bytes_per_launch"]) if fam else None
+
+
+def _dominant(fams, steps):
+    """The kernel family with the most event time per step, priced at its own arithmetic's ceiling."""
+    name, f = max(fams.items(), key=lambda kv: kv[1]["ms"])
+    ms = f["ms"] / steps
+    tf = f["flops"] / (f["ms"] / 1e3) / 1e12 if f["ms"] > 0 else 0.0
+    ceil = f["flops"] / (f["ceiling_ms"] / 1e3) / 1e12 if f["ceiling_ms"] > 0 else SPLIT_PEAK_TFLOPS
+    per_launch_ms = f["ms"] / max(1, f["launches"])
+    return {"kernel": name, "gflop_per_step": round(f["flops"] / steps / 1e9, 2), "ms_per_step": round(ms, 3),
+            "tflops": round(tf, 3), "ceiling_tflops": round(ceil, 1), "frac": round(tf / ceil, 4) if ceil else None,
+            "launches_per_step": f["launches"] // max(1, steps), "avg_launch_us": round(per_launch_ms * 1e3, 2),
+            "alg_bytes_per_launch": round(f["bytes"] / max(1, f["launches"])),
+            "traffic_bytes_per_launch": _pmc_family_traffic(name)}
+
+
 def _pmc_traffic():
     """HBM bytes per conv-GEMM launch from the committed PMC passes (tools/pmc_traffic.sh + pmc_traffic.py:
     FETCH_SIZE and WRITE_SIZE in separate rocprofv3 runs of this bench, FETCH_SIZE doubled per
@@ -489,7 +519,7 @@ def main():
         for i in range(args.steps):
             step(args.warmup + i)
         eng.profile(False)
-    k_ms, k_flops, k_launches, c_ms = eng.profile_read(with_ceiling=True)
+    (k_ms, k_flops, k_launches, c_ms), fams = eng.profile_read_kinds()
     eng.check_device_status()  # a device-side fault flag (BiGRU hand-off) voids the run
     from rvcx.sharding import reduce_throughput
 
@@ -506,21 +536,29 @@ def main():
     # FLOP-weighted ceiling of the launches' own arithmetic: the launches' time at their ceilings / their time
     peak = k_flops / (c_ms / 1000.0) / 1e12 if c_ms > 0 else SPLIT_PEAK_TFLOPS
     traffic, traffic_src = _pmc_traffic()
-    traffic, traffic_step = traffic if traffic else (None, None)
-    roofline = {"bound": "mfma", "achieved": round(achieved_tflops, 3), "peak": round(peak, 1), "unit": "TFLOP/s",
-                "frac": round(achieved_tflops / peak, 4), "traffic": traffic,
-                "peak_basis": "FLOP-weighted MFMA ceiling of each launch's fp32-accurate arithmetic: dense fp16/bf16 "
-                              f"2500 TF / 3 plane products ({H16_PEAK_TFLOPS}: the two-plane fp16 split of the "
-                              f"generator's weight-streamed convs and fused pairs) or / 6 ({SPLIT_PEAK_TFLOPS}: the "
-                              f"three-plane bf16 split of the rest); native f32 MFMA peak {FP32_PEAK_TFLOPS}",
-                "traffic_unit": "HBM bytes per conv launch", "traffic_source": traffic_src,
-                # the conv family's measured HBM bytes per C2 step against its algorithmic bytes (operands read once,
-                # result written once), the same PMC record
-                "traffic_step": traffic_step,
-                "kernel": CONV_KERNEL,
-                "launches_per_step": k_launches // max(1, args.steps),
-                "kernel_ms_per_step": round(k_ms / args.steps, 3),
-                "alg_gflop_per_step": round(k_flops / args.steps / 1e9, 2)}
+    _, traffic_step = traffic if traffic else (None, None)
+    dom = _dominant(fams, args.steps)
+    # the line's roofline is the DOMINANT kernel's (the family with the most time per step, priced at its own
+    # arithmetic's ceiling; traffic = its PMC-measured HBM bytes per launch); the whole conv family's aggregate rides
+    # along under "family"
+    roofline = {"bound": "mfma", "achieved": dom["tflops"], "peak": dom["ceiling_tflops"], "unit": "TFLOP/s",
+                "frac": dom["frac"], "traffic": dom["traffic_bytes_per_launch"],
+                "traffic_unit": f"HBM bytes per {dom['kernel']} launch (PMC FETCH_SIZE x2 + WRITE_SIZE, "
+                                f"profiles/pmc_traffic.json families; algorithmic {dom['alg_bytes_per_launch']} B)",
+                "kernel": dom["kernel"], "dominant": dom,
+                "peak_basis": "MFMA ceiling of the launch's fp32-accurate arithmetic: dense fp16/bf16 2500 TF / 3 plane "
+                              f"products ({H16_PEAK_TFLOPS}: the two-plane fp16 split) or / 6 ({SPLIT_PEAK_TFLOPS}: the "
+                              f"three-plane bf16 split); native f32 MFMA peak {FP32_PEAK_TFLOPS}",
+                "family": {"kernel": CONV_KERNEL, "achieved": round(achieved_tflops, 3), "peak": round(peak, 1),
+                           "frac": round(achieved_tflops / peak, 4),
+                           "launches_per_step": k_launches // max(1, args.steps),
+                           "kernel_ms_per_step": round(k_ms / args.steps, 3),
+                           "alg_gflop_per_step": round(k_flops / args.steps / 1e9, 2),
+                           # the family's measured HBM bytes per C2 step against its algorithmic bytes (operands read
+                           # once, result written once), the same PMC record
+                           "traffic_step": traffic_step, "traffic_source": traffic_src,
+                           "by_kernel_ms_per_step": {k: round(v["ms"] / args.steps, 3) for k, v in
+                                                     sorted(fams.items(), key=lambda kv: -kv[1]["ms"])}}}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
@@ -537,7 +575,7 @@ def main():
             "config": {"workload": "C2: full RVCv2 48kHz pipeline, one 13.5 s utterance per step per GPU",
                        "samples_16k": n, "audio_sec_per_step_per_gpu": round(audio_sec, 5), "x_pad": 1,
                        "f0_method": "rmvpe", "index_rate": 0, "protect": 0.33, "parallelism": f"dp{world}"},
-            "roofline": roofline, "cpu_baseline": cpu,
+            "roofline": roofline, "cpu_baseline": cpu, "effective_config": eng.config_info(),
             # SURVEY §8(d)'s definition: pinned host audio in -> pinned host audio out, the H2D (1.7 MB fp64) and
             # D2H (2.6 MB fp32) copies on the compute stream inside the timed loop; value above is HBM-resident
             "host_io": {"value": round(tot_io["value"], 3), "unit": "audio-sec/sec",

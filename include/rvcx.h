@@ -284,6 +284,15 @@ int rvcx_profile_read(rvcx_ctx* ctx, double* total_ms, double* total_flops, int6
  * with the ceiling 2500 / 6 TF for the exact bf16 split, 2500 / 3 for the two-plane fp16 split and 2500 for the fp16
  * reduced-precision mode (the dense bf16 / fp16 MFMA peak over the MFMA products per fp32 product). */
 int rvcx_profile_read_ex(rvcx_ctx* ctx, double* total_ms, double* total_flops, int64_t* launches, double* ceiling_ms);
+/* As rvcx_profile_read_ex, plus the same sums per kernel family (the kernel each launch actually ran, after routing):
+ * arrays of nk entries indexed by family id (0 .. RVCX_PROF_KINDS - 1; names from rvcx_profile_kind_name), each
+ * with the summed event time (ms), algorithmic FLOPs, time at the arithmetic's ceiling (ms), algorithmic HBM bytes
+ * (operands read once, result written once) and launch count. A family's time includes its split-K combine. */
+#define RVCX_PROF_KINDS 10
+int rvcx_profile_read_kinds(rvcx_ctx* ctx, double* total_ms, double* total_flops, int64_t* launches, double* ceiling_ms,
+                            int nk, double* k_ms, double* k_flops, double* k_ceiling_ms, double* k_bytes,
+                            int64_t* k_launches);
+const char* rvcx_profile_kind_name(int kind);
 
 /* ---------------------------------------------------------------- feature index (FAISS IndexIVFFlat)
  * The bytes of a faiss .index file (IndexIVFFlat over IndexFlatL2, METRIC_L2, ArrayInvertedLists;

@@ -201,6 +201,7 @@ void launch_rb_pair(Ctx& c, const RbPairArgs& a_in, hipStream_t s) {
   const double bytes = 4.0 * ((double)a.B * a.T * a.C * (2 + (a.acc_mode != ACC_STORE ? 1 : 0)) + 2.0 * a.k * a.C * a.C);
   Ctx::ProfRec r{ev[0], ev[1], flops, 0, a.T, a.C, a.C, -a.k, a.B, 1, bytes,
                  a.wfmt == RB_WF16 ? (a.lowp ? Ctx::PEAK_F16 : Ctx::PEAK_F16X2) : Ctx::PEAK_SPLIT};
+  r.kind = CK_RBPAIR;
   RVCX_HIP(hipEventRecord(r.a, s));
   check(rb_pair(a, cfg, s), "rb_pair");
   RVCX_HIP(hipEventRecord(r.b, s));
@@ -264,6 +265,7 @@ void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double
                  a.taps, a.batch * a.batch_inner, a.ksplit, alg_bytes, peak};
   RVCX_HIP(hipEventRecord(r.a, s));
   check(two_d ? conv2d(a, s) : conv1d(a, s), two_d ? "conv2d" : "conv1d");
+  r.kind = conv_last_kind();
   RVCX_HIP(hipEventRecord(r.b, s));
   c.prof_recs.push_back(r);
 }
@@ -906,8 +908,20 @@ int rvcx_profile_read(rvcx_ctx* ctx, double* total_ms, double* total_flops, int6
 }
 
 int rvcx_profile_read_ex(rvcx_ctx* ctx, double* total_ms, double* total_flops, int64_t* launches, double* ceiling_ms) {
+  return rvcx_profile_read_kinds(ctx, total_ms, total_flops, launches, ceiling_ms, 0, nullptr, nullptr, nullptr,
+                                 nullptr, nullptr);
+}
+
+const char* rvcx_profile_kind_name(int kind) { return (kind >= 0 && kind < CK_COUNT) ? conv_kind_name(kind) : nullptr; }
+
+int rvcx_profile_read_kinds(rvcx_ctx* ctx, double* total_ms, double* total_flops, int64_t* launches, double* ceiling_ms,
+                            int nk, double* k_ms, double* k_flops, double* k_ceiling_ms, double* k_bytes,
+                            int64_t* k_launches) {
   return guard(ctx, [&] {
+    if (nk < 0 || (nk > 0 && (!k_ms || !k_flops || !k_ceiling_ms || !k_bytes || !k_launches)))
+      throw Error(RVCX_E_INVALID, "profile_read_kinds: nk > 0 needs all five per-kind arrays");
     set_device(ctx);
+    for (int k = 0; k < nk; ++k) k_ms[k] = k_flops[k] = k_ceiling_ms[k] = k_bytes[k] = 0.0, k_launches[k] = 0;
     double ms = 0.0, fl = 0.0, cms = 0.0;
     const char* dump = std::getenv("RVCX_PROF_DUMP");  // append one CSV line per conv launch
     FILE* fd = dump ? std::fopen(dump, "a") : nullptr;
@@ -921,6 +935,13 @@ int rvcx_profile_read_ex(rvcx_ctx* ctx, double* total_ms, double* total_flops, i
       ms += t;
       fl += r.flops;
       cms += r.flops / (r.peak_tf * 1e9);
+      if (r.kind >= 0 && r.kind < nk) {
+        k_ms[r.kind] += t;
+        k_flops[r.kind] += r.flops;
+        k_ceiling_ms[r.kind] += r.flops / (r.peak_tf * 1e9);
+        k_bytes[r.kind] += r.bytes;
+        k_launches[r.kind] += 1;
+      }
       ctx->prof_pool.push_back(r.a);
       ctx->prof_pool.push_back(r.b);
     }

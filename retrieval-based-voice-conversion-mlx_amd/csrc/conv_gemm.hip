@@ -933,6 +933,15 @@ int conv_wsb_pick(const ConvArgs& a) {
   b.wsb = 1;
   return pick_wsb(b);
 }
+thread_local int g_conv_kind = CK_OTHER;
+int conv_last_kind() { return g_conv_kind; }
+const char* conv_kind_name(int k) {
+  static const char* const names[CK_COUNT] = {"conv_wsb16_kernel", "conv_wsb_kernel", "conv_gs16_kernel",
+                                              "conv_gsw16_kernel", "k_rb_pair", "k_conv2d_h16/k_conv2d_small",
+                                              "conv_emu_kernel", "conv_gemm_kernel", "conv_tiny_kernel", "other"};
+  return (k >= 0 && k < CK_COUNT) ? names[k] : "other";
+}
+
 namespace {
 
 template <bool TWO_D>
@@ -941,10 +950,14 @@ hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
   if (a.C_in <= 0 || a.taps <= 0) return hipErrorInvalidValue;
   // the gate and the LayerNorm are applied by the combine
   if ((a.gate_h > 0 || a.ln_g) && !(a.ws && a.ksplit > 1)) return hipErrorInvalidValue;
-  if (tiny_fits(a)) return launch_tiny(a, TWO_D, s);
+  if (tiny_fits(a)) {
+    g_conv_kind = CK_TINY;
+    return launch_tiny(a, TWO_D, s);
+  }
   if (a.wsb == 2 && a.wsplit && conv_math(a) >= 2 && conv_gs_eligible(a, TWO_D)) {
     const int ks = (a.ws && a.ksplit > 1) ? a.ksplit : 1;
     const int cfg = a.force_cfg >= 30 ? a.force_cfg : pick_wsb(a);
+    g_conv_kind = (TWO_D && cfg == 30 && conv_gsw_eligible(a)) ? CK_GSW : CK_GS;
     hipError_t e = conv_gs_launch(a, cfg, xcd_enabled() ? 1 : 0, s, TWO_D, ks);
     if (e == hipSuccess && ks > 1) e = launch_splitk_reduce(a, ks, TWO_D, s);
     if (e != hipErrorInvalidValue) return e;
@@ -952,13 +965,18 @@ hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
   if (a.wsb == 1 && a.wsplit && conv_math(a) >= 2 && conv_wsb_eligible(a, TWO_D)) {
     const int ks = (a.ws && a.ksplit > 1) ? a.ksplit : 1;
     const int cfg = TWO_D ? 21 : (a.force_cfg >= 20 ? a.force_cfg : pick_wsb(a));
+    g_conv_kind = cfg >= 23 ? CK_WSB16 : CK_WSB;
     hipError_t e = conv_wsb_launch(a, cfg, xcd_enabled() ? 1 : 0, s, TWO_D, ks);
     if (e == hipSuccess && ks > 1) e = launch_splitk_reduce(a, ks, TWO_D, s);
     if (e != hipErrorInvalidValue) return e;
   }
   // 3x3 convs with 16/32 channels: 16x16x4 MFMA fragments (conv2d_small.hip)
-  if (TWO_D && a.force_cfg < 0 && small2d_enabled() && conv2d_small_fits(a)) return conv2d_small(a, s);
+  if (TWO_D && a.force_cfg < 0 && small2d_enabled() && conv2d_small_fits(a)) {
+    g_conv_kind = CK_SMALL2D;
+    return conv2d_small(a, s);
+  }
   const int cfg = pick_cfg<TWO_D>(a);
+  g_conv_kind = cfg >= 10 ? CK_EMU : CK_GEMM;
   ConvArgs b = a;
   b.force_cfg = cfg;
   // plain GEMMs (1-D, one tap, stride 1) take the double-buffered pipeline unless a.pipe < 0 or

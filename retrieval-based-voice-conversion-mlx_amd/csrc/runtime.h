@@ -122,6 +122,7 @@ struct Ctx {
     int two_d, M, N, C_in, taps, batch, ksplit;  // shape, for RVCX_PROF_DUMP
     double bytes;  // algorithmic HBM bytes: operands read once, result written once (RVCX_PROF_DUMP)
     double peak_tf;  // the MFMA ceiling of the launch's arithmetic, algorithmic fp32 TFLOP/s
+    int kind = CK_OTHER;  // the kernel family that ran (ConvKind)
   };
   std::vector<ProfRec> prof_recs;
   std::vector<hipEvent_t> prof_pool;

@@ -132,6 +132,11 @@ struct ConvArgs {
 };
 
 hipError_t conv1d(const ConvArgs& a, hipStream_t s);
+// the kernel family the last conv1d / conv2d on this host thread launched (kernel-timing records, rvcx_profile)
+enum ConvKind : int { CK_WSB16 = 0, CK_WSB, CK_GS, CK_GSW, CK_RBPAIR, CK_SMALL2D, CK_EMU, CK_GEMM, CK_TINY, CK_OTHER,
+                      CK_COUNT };
+int conv_last_kind();
+const char* conv_kind_name(int k);
 // the contraction arithmetic a launch gets: ConvArgs::math, else RVCX_CONV_MATH (1 fp32 MFMA, 2 bf16 split, 3 fp16 split)
 int conv_math_of(const ConvArgs& a);
 hipError_t conv2d(const ConvArgs& a, hipStream_t s);

@@ -20,7 +20,8 @@ STATUS = {
 }
 
 EXPORTS = [
-    "rvcx_create", "rvcx_destroy", "rvcx_set_generator_precision", "rvcx_config_info", "rvcx_last_error", "rvcx_set_synth_config", "rvcx_upload", "rvcx_finalize",
+    "rvcx_create", "rvcx_destroy", "rvcx_set_generator_precision", "rvcx_config_info", "rvcx_profile_read_kinds",
+    "rvcx_profile_kind_name", "rvcx_last_error", "rvcx_set_synth_config", "rvcx_upload", "rvcx_finalize",
     "rvcx_hubert", "rvcx_rmvpe", "rvcx_f0_post", "rvcx_synth_infer", "rvcx_dec_only", "rvcx_voice_conversion",
     "rvcx_synth_upp", "rvcx_set_highpass", "rvcx_pipeline", "rvcx_pipeline_default_opts", "rvcx_pipeline_ex",
     "rvcx_f0_autotune", "rvcx_rmvpe_decode", "rvcx_profile", "rvcx_profile_read", "rvcx_profile_read_ex", "rvcx_index_load",
@@ -161,6 +162,9 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "rvcx_set_conv_math": (i32, [vp, i32]),
         "rvcx_set_generator_precision": (i32, [vp, i32]),
         "rvcx_config_info": (i32, [vp, vp, i64, P(i64)]),
+        "rvcx_profile_read_kinds": (i32, [vp, P(f64), P(f64), P(i64), P(f64), i32, P(f64), P(f64), P(f64), P(f64),
+                                          P(i64)]),
+        "rvcx_profile_kind_name": (ctypes.c_char_p, [i32]),
         "rvcx_conv1d": (i32, [vp, vp, i64, i32, vp, vp, i32, i32, i32, i32, i32, i32, vp, i64, vp]),
         "rvcx_conv2d3x3": (i32, [vp, vp, i32, i32, i32, vp, vp, i32, i32, i32, vp, vp]),
         "rvcx_resblock_pair": (i32, [vp, vp, i32, i64, i32, vp, vp, vp, vp, i32, i32, i32, f32, i32, vp, vp]),

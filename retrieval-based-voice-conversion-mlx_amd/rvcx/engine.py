@@ -598,3 +598,20 @@ class Engine:
         self._check(self.lib.rvcx_profile_read_ex(self.ctx, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(n),
                                                   ctypes.byref(cm)), "profile_read")
         return (ms.value, fl.value, n.value, cm.value) if with_ceiling else (ms.value, fl.value, n.value)
+
+    def profile_read_kinds(self):
+        """((ms, flops, launches, ceiling_ms) totals, {kernel family: {ms, flops, ceiling_ms, bytes, launches}}) since
+        the last read (rvcx_profile_read_kinds: grouped by the kernel each launch actually ran)."""
+        K = 10  # RVCX_PROF_KINDS
+        arr = lambda T: (T * K)()  # noqa: E731
+        kms, kfl, kcm, kby, kn = arr(ctypes.c_double), arr(ctypes.c_double), arr(ctypes.c_double), \
+            arr(ctypes.c_double), arr(ctypes.c_int64)
+        ms, fl, n, cm = ctypes.c_double(0), ctypes.c_double(0), ctypes.c_int64(0), ctypes.c_double(0)
+        self._check(self.lib.rvcx_profile_read_kinds(self.ctx, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(n),
+                                                     ctypes.byref(cm), K, kms, kfl, kcm, kby, kn), "profile_read_kinds")
+        fam = {}
+        for k in range(K):
+            if kn[k]:
+                fam[self.lib.rvcx_profile_kind_name(k).decode()] = {"ms": kms[k], "flops": kfl[k], "ceiling_ms": kcm[k],
+                                                                    "bytes": kby[k], "launches": int(kn[k])}
+        return (ms.value, fl.value, n.value, cm.value), fam

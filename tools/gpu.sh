@@ -21,7 +21,7 @@ TAG=${1:?tag}; shift
 O=gpurun_out
 
 c2line() {  # ms_per_step and conv-family kernel ms of the last JSON line of $1
-  tail -1 "$1" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["roofline"].get("kernel_ms_per_step"))'
+  tail -1 "$1" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["roofline"]["family"].get("kernel_ms_per_step"))'
 }
 
 for step in "$@"; do
@@ -46,11 +46,12 @@ for step in "$@"; do
         python3 -c "import json; d=json.loads(open('$O/bench_${TAG}_$c.json').read().strip().splitlines()[-1]); print('$c', d['value'], d['unit'], d['ms_per_step'])"
       done ;;
     prof)
+      # 1 warm-up + 3 timed + 3 host-io + 3 roofline-event steps = 10 pipeline calls traced (the summaries divide by 10)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$TAG -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ${arg//,/ } > $O/prof_$TAG.log 2>&1 || { tail -20 $O/prof_$TAG.log; exit 1; }
       DB=$(find $O/prof_$TAG -name "*.db" | head -1)
       python3 tools/timeline.py "$DB" 2 -v > $O/timeline_$TAG.txt 2>&1
-      python3 tools/prof_summary.py "$DB" 7 > $O/kstats_$TAG.txt 2>&1
-      python3 tools/kfamily.py "$DB" 7 > $O/kfamily_$TAG.txt 2>&1
+      python3 tools/prof_summary.py "$DB" 10 > $O/kstats_$TAG.txt 2>&1
+      python3 tools/kfamily.py "$DB" 10 > $O/kfamily_$TAG.txt 2>&1
       head -30 $O/kstats_$TAG.txt ;;
     pmc)
       bash tools/pmc_traffic.sh || exit 1

@@ -48,6 +48,19 @@ def main():
     rec = {"kernel": key, "launches": n, "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
            "traffic_bytes_per_launch": fetch + write,
            "note": "FETCH_SIZE doubled (gfx950 16-B/lane reads), WRITE_SIZE as is; KB counters x 1024"}
+    # per kernel family (the names bench.py's roofline.dominant uses, rvcx_profile_kind_name): HBM bytes per launch of
+    # the family's own kernels (its split-K combines are separate kernels, not attributed)
+    famnames = {"conv_wsb16_kernel": "conv_wsb16_kernel", "conv_wsb_kernel": "conv_wsb_kernel<",
+                "conv_gs16_kernel": "conv_gs16_kernel", "conv_gsw16_kernel": "conv_gsw16_kernel", "k_rb_pair": "k_rb_pair",
+                "k_conv2d_h16/k_conv2d_small": "k_conv2d_", "conv_emu_kernel": "conv_emu_kernel",
+                "conv_gemm_kernel": "conv_gemm_kernel", "conv_tiny_kernel": "conv_tiny"}
+    rec["families"] = {}
+    for fname, sub in famnames.items():
+        fk = [k for k in fe if sub in k]
+        nl = sum(len(fe[k]) for k in fk)
+        if nl:
+            b = sum(2.0 * sum(fe[k]) + sum(wr.get(k, [])) for k in fk) * 1024
+            rec["families"][fname] = {"launches": nl, "hbm_bytes_per_launch": b / nl}
     all_f = sum(sum(v) for v in fe.values()) * 2 * 1024
     all_w = sum(sum(v) for v in wr.values()) * 1024
     rec["all_kernels_bytes"] = all_f + all_w
