@@ -154,6 +154,15 @@ int rvcx_f0_autotune(rvcx_ctx* ctx, double* d_f0, int64_t F, double strength, in
 int rvcx_synth_infer(rvcx_ctx* ctx, int B, int T, const float* d_phone, const int32_t* d_lengths,
                      const int32_t* d_pitch, const float* d_pitchf, const int32_t* d_sid, const float* d_eps_z,
                      const float* d_eps_src, uint64_t seed, float* d_out, float* d_zp, float* d_z, void* stream);
+/* Synthesizer.infer with its remaining arguments and full return value (synthesizers.py:206-243): rate (the partial
+ * re-synthesis of :230-234; < 0 = None, else in (0, 1]) keeps frames head = int(T (1 - rate)) .. T-1 of z_p, x_mask and
+ * nsff0 before the flow, so d_out holds [B][(T - head) upp] and d_zp / d_z [B][T - head][I]; *t_out = T - head.
+ * d_m_p / d_logs_p (optional) [B][T][I] receive the TextEncoder's m_p / logs_p (the rest of the tuple :243). Noise as
+ * rvcx_synth_infer (d_eps_z over all T frames, d_eps_src over the T - head synthesized ones). */
+int rvcx_synth_infer_ex(rvcx_ctx* ctx, int B, int T, const float* d_phone, const int32_t* d_lengths,
+                        const int32_t* d_pitch, const float* d_pitchf, const int32_t* d_sid, double rate,
+                        const float* d_eps_z, const float* d_eps_src, uint64_t seed, float* d_out, float* d_zp,
+                        float* d_z, float* d_m_p, float* d_logs_p, int* t_out, void* stream);
 
 /* HiFiGAN-NSF generator alone (config C3): dec(z, f0, g=emb_g(sid)) with z in reference layout
  * [B][I][T] (rvc/lib/algorithm/generators/hifigan_nsf.py:173-212). out [B][T*upp]. */

@@ -395,14 +395,20 @@ def decoder(w, cfg, x: Tensor, f0, g: Tensor, eps_src) -> Tensor:
 
 
 def synth_infer(w, cfg, phone: Tensor, lengths: Tensor, pitch: Tensor, nsff0: Tensor, sid: Tensor,
-                eps_z: Tensor, eps_src: Tensor):
+                eps_z: Tensor, eps_src: Tensor, rate=None):
     """Synthesizer.infer (rvc/lib/algorithm/synthesizers.py:206-243) with the two RNG draws
-    injected: eps_z for randn_like at :228, eps_src for hifigan.py:223.
-    Returns (o [B,1,T*upp], x_mask, (z, z_p, m_p, logs_p))."""
+    injected: eps_z for randn_like at :228, eps_src for hifigan.py:223 (over the frames the decoder runs on).
+    rate (:230-234): z_p, x_mask and nsff0 from frame int(T * (1 - rate)) on.
+    Returns (o [B,1,T'*upp], x_mask, (z, z_p, m_p, logs_p))."""
     with torch.no_grad():
         g = F.embedding(sid, _t(w, "emb_g.weight")).unsqueeze(-1)
         m_p, logs_p, x_mask = text_encoder(w, cfg, phone, pitch if getattr(cfg, "use_f0", True) else None, lengths)
         z_p = (m_p + torch.exp(logs_p) * eps_z * 0.66666) * x_mask
+        if rate is not None:
+            head = int(z_p.shape[2] * (1.0 - float(rate)))
+            z_p, x_mask = z_p[:, :, head:], x_mask[:, :, head:]
+            if getattr(cfg, "use_f0", True) and nsff0 is not None:
+                nsff0 = nsff0[:, head:]
         z = flow_reverse(w, cfg, z_p, x_mask, g)
         o = decoder(w, cfg, z * x_mask, nsff0, g, eps_src)  # synthesizers.py:233-239
     return o, x_mask, (z, z_p, m_p, logs_p)

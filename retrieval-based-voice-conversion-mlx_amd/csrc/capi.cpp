@@ -541,6 +541,31 @@ int rvcx_synth_infer(rvcx_ctx* ctx, int B, int T, const float* d_phone, const in
   });
 }
 
+int rvcx_synth_infer_ex(rvcx_ctx* ctx, int B, int T, const float* d_phone, const int32_t* d_lengths,
+                        const int32_t* d_pitch, const float* d_pitchf, const int32_t* d_sid, double rate,
+                        const float* d_eps_z, const float* d_eps_src, uint64_t seed, float* d_out, float* d_zp,
+                        float* d_z, float* d_m_p, float* d_logs_p, int* t_out, void* stream) {
+  return guard(ctx, [&] {
+    if (!ctx->ready[0]) throw Error(RVCX_E_STATE, "synthesizer weights not finalized");
+    if (B <= 0 || T <= 0 || !d_phone || !d_lengths || !d_sid || !d_out)
+      throw Error(RVCX_E_INVALID, "rvcx_synth_infer_ex: bad arguments");
+    if (ctx->scfg.f0 && (!d_pitch || !d_pitchf))
+      throw Error(RVCX_E_INVALID, "rvcx_synth_infer_ex: a pitch-guided model needs pitch and pitchf");
+    if (!ctx->scfg.f0) d_pitch = nullptr, d_pitchf = nullptr;
+    // head = int(z_p.shape[2] * (1.0 - rate)) (synthesizers.py:231); rate < 0: no rate
+    int head = 0;
+    if (rate >= 0.0) {
+      const double h = (double)T * (1.0 - rate);
+      if (!(h < (double)T) || h < 0.0) throw Error(RVCX_E_INVALID, "rvcx_synth_infer_ex: rate must be in (0, 1]");
+      head = (int)h;
+    }
+    set_device(ctx);
+    synth_forward(*ctx, B, T, d_phone, d_lengths, d_pitch, d_pitchf, d_sid, d_eps_z, d_eps_src, seed, d_out, d_zp,
+                  d_z, static_cast<hipStream_t>(stream), 0, head, d_m_p, d_logs_p);
+    if (t_out) *t_out = T - head;
+  });
+}
+
 int rvcx_dec_only(rvcx_ctx* ctx, int B, int T, const float* d_z, const float* d_f0, const int32_t* d_sid,
                   const float* d_eps_src, uint64_t seed, float* d_out, void* stream) {
   return guard(ctx, [&] {

@@ -281,7 +281,10 @@ int64_t rmvpe_forward_b(Ctx& c, const float* audio, int64_t n, int64_t lda, int 
                         int64_t cap, float* hidden, hipStream_t s);
 void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* lengths, const int32_t* pitch,
                    const float* pitchf, const int32_t* sid, const float* eps_z, const float* eps_src, uint64_t seed,
-                   float* out, float* zp_out, float* z_out, hipStream_t s, int gen_lowp = 0);
+                   float* out, float* zp_out, float* z_out, hipStream_t s, int gen_lowp = 0, int head = 0,
+                   float* mp_out = nullptr, float* logsp_out = nullptr);
+// head: Synthesizer.infer's rate (synthesizers.py:230-234) as the first kept frame -- the flow and the decoder run on
+// T - head frames (out [B][(T - head) upp], zp_out / z_out [B][T - head][I]); mp_out / logsp_out [B][T][I]
 // gen_lowp: the generator's weight-streamed convs and fused ResBlock pairs on fp16 operands (one MFMA product per
 // step): the realtime hop's opt-in (rvcx_rt_opts::gen_precision), never set by an offline entry point
 void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, const float* f0, const float* g,

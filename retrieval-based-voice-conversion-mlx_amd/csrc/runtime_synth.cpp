@@ -533,7 +533,8 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
 // ------------------------------------------------------------------ Synthesizer.infer
 void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* lengths, const int32_t* pitch,
                    const float* pitchf, const int32_t* sid, const float* eps_z, const float* eps_src, uint64_t seed,
-                   float* out, float* zp_out, float* z_out, hipStream_t s, int gen_lowp) {
+                   float* out, float* zp_out, float* z_out, hipStream_t s, int gen_lowp, int head, float* mp_out,
+                   float* logsp_out) {
   const SynthCfg& cf = c.scfg;
   const int H = cf.H, I = cf.I, F = cf.F, E = cf.emb_dim, nh = cf.n_heads, dk = H / nh, nw = 2 * cf.window + 1;
   const long long BT = (long long)B * T;
@@ -665,15 +666,44 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
     a.mask = mask;
     run(c, a, s);
   }
+  // m_p / logs_p [B][T][I] for the caller (the return tuple of Synthesizer.infer, synthesizers.py:243)
+  if (mp_out)
+    RVCX_HIP(hipMemcpy2DAsync(mp_out, (size_t)I * 4, stats, (size_t)2 * I * 4, (size_t)I * 4, (size_t)BT,
+                              hipMemcpyDeviceToDevice, s));
+  if (logsp_out)
+    RVCX_HIP(hipMemcpy2DAsync(logsp_out, (size_t)I * 4, stats + I, (size_t)2 * I * 4, (size_t)I * 4, (size_t)BT,
+                              hipMemcpyDeviceToDevice, s));
   // ---- z_p = (m + exp(logs) * eps * 0.66666) * mask   (synthesizers.py:228)
   float* z = c.buf<float>("flow.z", BT * I, s);
   float* xf = c.buf<float>("flow.xf", BT * I, s);
   check(zp_sample(stats, B, T, I, eps_z, splitmix(seed ^ 0x5a505f4e4f495345ull), mask, z, s), "zp_sample");
-  if (zp_out) RVCX_HIP(hipMemcpyAsync(zp_out, z, BT * I * sizeof(float), hipMemcpyDeviceToDevice, s));
+  // rate (synthesizers.py:230-234): z_p, x_mask and nsff0 from frame head on; the noise was drawn over all T frames
+  const int Tf = T - head;
+  const long long BTf = (long long)B * Tf;
+  const float* maskf = mask;
+  const float* pitchff = pitchf;
+  if (head > 0) {
+    if (head >= T) throw Error(RVCX_E_SHAPE, "synthesizer: rate leaves no frames");
+    float* z2 = c.buf<float>("flow.z_rate", (size_t)BTf * I, s);
+    RVCX_HIP(hipMemcpy2DAsync(z2, (size_t)Tf * I * 4, z + (size_t)head * I, (size_t)T * I * 4, (size_t)Tf * I * 4,
+                              (size_t)B, hipMemcpyDeviceToDevice, s));
+    float* m2 = c.buf<float>("te.mask_rate", (size_t)BTf, s);
+    RVCX_HIP(hipMemcpy2DAsync(m2, (size_t)Tf * 4, mask + head, (size_t)T * 4, (size_t)Tf * 4, (size_t)B,
+                              hipMemcpyDeviceToDevice, s));
+    if (pitchf) {
+      float* p2 = c.buf<float>("dec.pitchf_rate", (size_t)BTf, s);
+      RVCX_HIP(hipMemcpy2DAsync(p2, (size_t)Tf * 4, pitchf + head, (size_t)T * 4, (size_t)Tf * 4, (size_t)B,
+                                hipMemcpyDeviceToDevice, s));
+      pitchff = p2;
+    }
+    z = z2;
+    maskf = m2;
+  }
+  if (zp_out) RVCX_HIP(hipMemcpyAsync(zp_out, z, BTf * I * sizeof(float), hipMemcpyDeviceToDevice, s));
   // ---- flow reverse (residuals.py:151-164, 233-258; modules.py:78-109)
-  // hs [BT][2H]: the WaveNet residual stream h (columns [0, H)) and its skip sum (columns [H, 2H))
-  float* hs = c.buf<float>("flow.hs", BT * 2 * H, s);
-  float* acts = c.buf<float>("flow.acts", BT * H, s);
+  // hs [BTf][2H]: the WaveNet residual stream h (columns [0, H)) and its skip sum (columns [H, 2H))
+  float* hs = c.buf<float>("flow.hs", BTf * 2 * H, s);
+  float* acts = c.buf<float>("flow.acts", BTf * H, s);
   const int cl = 2 * H * cf.flow_layers;
   float* gc = c.buf<float>("flow.gc", (size_t)B * cf.flow_n * cl, s);
   // g -> every coupling's cond_layer(g) in one GEMM (modules.py:32-35, :92-93)
@@ -689,19 +719,19 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
       x0 = rev ? z + I / 2 : z;
       x1 = rev ? z : z + I / 2;
     } else {
-      check(channel_flip(z, xf, (int)BT, I, s), "flip");
+      check(channel_flip(z, xf, (int)BTf, I, s), "flip");
     }
     {  // h = pre(x0) * mask, and the skip sum cleared (the zero rows of the packed pre weight)
-      ConvArgs a = lin(x0, I, (int)BT, I / 2, c.W(q + ".pre.w"), 2 * H, c.W(q + ".pre.b"), hs, 2 * H);
-      a.mask = mask;
+      ConvArgs a = lin(x0, I, (int)BTf, I / 2, c.W(q + ".pre.w"), 2 * H, c.W(q + ".pre.b"), hs, 2 * H);
+      a.mask = maskf;
       run(c, a, s);
     }
     for (int L = 0; L < cf.flow_layers; ++L) {
       const std::string l = std::to_string(L);
       {  // acts = tanh(in(h)[:H] + g_l[:H]) * sigmoid(in(h)[H:] + g_l[H:])  (commons.py:88-103), in the split-K combine
-        ConvArgs a = conv(hs, 2 * H, T, H, c.W(q + ".in" + l + ".w"), 2 * H, cf.flow_k, 1, (cf.flow_k - 1) / 2,
-                          c.W(q + ".in" + l + ".b"), acts, H, T, B);
-        a.x_bs = (long long)T * 2 * H;
+        ConvArgs a = conv(hs, 2 * H, Tf, H, c.W(q + ".in" + l + ".w"), 2 * H, cf.flow_k, 1, (cf.flow_k - 1) / 2,
+                          c.W(q + ".in" + l + ".b"), acts, H, Tf, B);
+        a.x_bs = (long long)Tf * 2 * H;
         a.gate_h = H;
         a.gate_g = gc + (size_t)f * cl + (size_t)L * 2 * H;
         a.gate_g_bs = (long long)cf.flow_n * cl;
@@ -712,24 +742,24 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
       // h = (h + res(acts)) * mask and skip += skip(acts) as one GEMM over both halves (modules.py:95-107); the skip
       // sum is masked at every layer instead of once at the end: the same values, the mask being exactly 0 / 1
       const bool last = L == cf.flow_layers - 1;
-      ConvArgs a = lin(acts, H, (int)BT, H, wrs, last ? H : 2 * H, brs, last ? hs + H : hs, 2 * H);
+      ConvArgs a = lin(acts, H, (int)BTf, H, wrs, last ? H : 2 * H, brs, last ? hs + H : hs, 2 * H);
       a.acc_mode = ACC_ADD;
-      a.mask = mask;
+      a.mask = maskf;
       run(c, a, s);
     }
     {  // x1 = (x1 - m) * mask, m = post(h) * mask
-      ConvArgs a = lin(hs + H, 2 * H, (int)BT, H, c.W(q + ".post.w"), I / 2, c.W(q + ".post.b"), x1, I);
+      ConvArgs a = lin(hs + H, 2 * H, (int)BTf, H, c.W(q + ".post.w"), I / 2, c.W(q + ".post.b"), x1, I);
       a.res = x1;
       a.ldr = I;
       a.res_mode = RES_RSUB_POST;
-      a.mask = mask;
+      a.mask = maskf;
       run(c, a, s);
     }
     if (!fold) std::swap(z, xf);
   }
-  if (z_out) RVCX_HIP(hipMemcpyAsync(z_out, z, BT * I * sizeof(float), hipMemcpyDeviceToDevice, s));
+  if (z_out) RVCX_HIP(hipMemcpyAsync(z_out, z, BTf * I * sizeof(float), hipMemcpyDeviceToDevice, s));
   // ---- dec(z * mask, nsff0, g)
-  dec_forward(c, B, T, z, mask, pitchf, g, eps_src, seed, out, s, gen_lowp);
+  dec_forward(c, B, Tf, z, maskf, pitchff, g, eps_src, seed, out, s, gen_lowp);
 }
 
 }  // namespace rvcx

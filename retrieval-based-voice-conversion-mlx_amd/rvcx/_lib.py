@@ -21,7 +21,7 @@ STATUS = {
 
 EXPORTS = [
     "rvcx_create", "rvcx_destroy", "rvcx_set_generator_precision", "rvcx_config_info", "rvcx_profile_read_kinds",
-    "rvcx_profile_kind_name", "rvcx_last_error", "rvcx_set_synth_config", "rvcx_upload", "rvcx_finalize",
+    "rvcx_profile_kind_name", "rvcx_synth_infer_ex", "rvcx_last_error", "rvcx_set_synth_config", "rvcx_upload", "rvcx_finalize",
     "rvcx_hubert", "rvcx_rmvpe", "rvcx_f0_post", "rvcx_synth_infer", "rvcx_dec_only", "rvcx_voice_conversion",
     "rvcx_synth_upp", "rvcx_set_highpass", "rvcx_pipeline", "rvcx_pipeline_default_opts", "rvcx_pipeline_ex",
     "rvcx_f0_autotune", "rvcx_rmvpe_decode", "rvcx_profile", "rvcx_profile_read", "rvcx_profile_read_ex", "rvcx_index_load",
@@ -118,6 +118,8 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "rvcx_rmvpe": (i32, [vp, vp, i64, f32, vp, i64, P(i64), vp, vp]),
         "rvcx_f0_post": (i32, [vp, vp, i64, f64, vp, vp, vp, vp]),
         "rvcx_synth_infer": (i32, [vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, u64, vp, vp, vp, vp]),
+        "rvcx_synth_infer_ex": (i32, [vp, i32, i32, vp, vp, vp, vp, vp, f64, vp, vp, u64, vp, vp, vp, vp, vp, P(i32),
+                                      vp]),
         "rvcx_dec_only": (i32, [vp, i32, i32, vp, vp, vp, vp, u64, vp, vp]),
         "rvcx_voice_conversion": (i32, [vp, vp, i64, vp, vp, i32, f32, f64, vp, vp, u64, vp, i64, P(i64), vp]),
         "rvcx_synth_upp": (i32, [vp]),

@@ -276,6 +276,34 @@ class Engine:
                                               _ptr(z), self.stream()), "synth_infer")
         return (out, zp, z) if want_latents else out
 
+    def synth_infer_ex(self, phone, lengths, pitch, pitchf, sid, rate=None, eps_z=None, eps_src=None, seed: int = 0):
+        """Synthesizer.infer with rate and the full return value (rvcx_synth_infer_ex): -> (out [B][T' upp],
+        z_p [B][T'][I], z [B][T'][I], m_p [B][T][I], logs_p [B][T][I]) with T' = T - int(T (1 - rate))."""
+        t = self.torch
+        ph = self._dev(phone, t.float32)
+        B, T = int(ph.shape[0]), int(ph.shape[1])
+        ln = self._dev(lengths, t.int32).reshape(B)
+        pc = None if pitch is None else self._dev(pitch, t.int32).reshape(B, T)
+        pf = None if pitchf is None else self._dev(pitchf, t.float32).reshape(B, T)
+        sd = self._dev(sid, t.int32).reshape(B)
+        ez = None if eps_z is None else self._dev(eps_z, t.float32)
+        es = None if eps_src is None else self._dev(eps_src, t.float32)
+        I = self.synth_cfg.inter_channels
+        out = t.empty((B, T * self.upp), dtype=t.float32, device=self.device)
+        zp = t.empty((B, T, I), dtype=t.float32, device=self.device)
+        z = t.empty((B, T, I), dtype=t.float32, device=self.device)
+        mp = t.empty((B, T, I), dtype=t.float32, device=self.device)
+        lp = t.empty((B, T, I), dtype=t.float32, device=self.device)
+        tn = ctypes.c_int(0)
+        self._check(self.lib.rvcx_synth_infer_ex(self.ctx, B, T, ph.data_ptr(), ln.data_ptr(), _ptr(pc), _ptr(pf),
+                                                 sd.data_ptr(), -1.0 if rate is None else float(rate), _ptr(ez),
+                                                 _ptr(es), ctypes.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), out.data_ptr(),
+                                                 zp.data_ptr(), z.data_ptr(), mp.data_ptr(), lp.data_ptr(),
+                                                 ctypes.byref(tn), self.stream()), "synth_infer_ex")
+        Tn = int(tn.value)
+        return (out.reshape(-1)[: B * Tn * self.upp].reshape(B, Tn * self.upp), zp.reshape(-1)[: B * Tn * I].reshape(B, Tn, I),
+                z.reshape(-1)[: B * Tn * I].reshape(B, Tn, I), mp, lp)
+
     def dec_only(self, z, f0, sid, eps_src=None, seed: int = 0):
         t = self.torch
         zz = self._dev(z, t.float32)

@@ -77,20 +77,24 @@ class Synthesizer:
         self.upp = engine.upp
 
     def infer(self, phone, phone_lengths, pitch, nsff0, sid, rate=None, eps_z=None, eps_src=None, seed: int = 0):
-        if rate is not None:
-            raise NotImplementedError("Synthesizer.infer(rate=...) (partial re-synthesis) is not supported")
+        """synthesizers.py:206-243: -> (o [B][1][T' upp], x_mask [B][1][T'], (z, z_p, m_p, logs_p)) with z / z_p
+        [B][I][T'] and m_p / logs_p [B][I][T]; rate (a float or a one-element tensor) keeps frames
+        int(T (1 - rate)) .. T - 1 before the flow (T' = T without it)."""
         ph = _np(phone).astype(np.float32)
         B, T = ph.shape[0], ph.shape[1]
         guided = bool(self.engine.synth_cfg.use_f0)  # synthesizers.py:233-239: pitch ignored without f0
-        out, zp, z = self.engine.synth_infer(ph, _np(phone_lengths).reshape(B),
-                                             _np(pitch).reshape(B, T) if guided else None,
-                                             _np(nsff0).reshape(B, T) if guided else None,
-                                             _np(sid).reshape(B), eps_z=eps_z,
-                                             eps_src=eps_src, seed=seed, want_latents=True)
+        r = None if rate is None else float(np.asarray(_np(rate)).reshape(-1)[0])
+        out, zp, z, mp, lp = self.engine.synth_infer_ex(ph, _np(phone_lengths).reshape(B),
+                                                        _np(pitch).reshape(B, T) if guided else None,
+                                                        _np(nsff0).reshape(B, T) if guided else None,
+                                                        _np(sid).reshape(B), rate=r, eps_z=eps_z, eps_src=eps_src,
+                                                        seed=seed)
+        head = T - zp.shape[1]
         lengths = _np(phone_lengths).reshape(B)
-        x_mask = (np.arange(T)[None, :] < lengths[:, None]).astype(np.float32)[:, None, :]
+        x_mask = (np.arange(T)[None, :] < lengths[:, None]).astype(np.float32)[:, None, head:]
         o = self.engine.host(out)[:, None, :]
-        return o, x_mask, (self.engine.host(z.transpose(1, 2)), self.engine.host(zp.transpose(1, 2)), None, None)
+        h = self.engine.host
+        return o, x_mask, (h(z.transpose(1, 2)), h(zp.transpose(1, 2)), h(mp.transpose(1, 2)), h(lp.transpose(1, 2)))
 
 
 class CREPE:

@@ -123,7 +123,7 @@ def test_fused_pair_rejects_unsupported(engine):
 
 @pytest.mark.parametrize("C,k,d", [(32, 11, 5), (64, 7, 3), (32, 3, 1)])
 def test_fused_pair_fp16_per_channel_weight_spread(engine, C, k, d):
-    """per-output-channel weight scales over 2^+-12 (and one channel at 2^-20 of the tensor's
+    """per-output-channel weight scales over 2^-24..1 (and one channel at 2^-20 of the tensor's
     largest) in both convs, the residual x and b2 scaled with conv2's channel so every output channel lives at its
     own magnitude. Each channel is held to the fp32-class bar relative to ITS OWN peak (the fp16 images carry one
     power-of-two scale per output channel, resblock_fused.hip k_rb_wsplit_h16)."""
@@ -131,9 +131,11 @@ def test_fused_pair_fp16_per_channel_weight_spread(engine, C, k, d):
     T = 3000
     x = rng.standard_normal((1, T, C)).astype(np.float32)
     w1, b1, w2, b2 = _weights(rng, C, k)
-    s1 = np.exp2(rng.integers(-12, 13, size=C)).astype(np.float64)
-    s2 = np.exp2(rng.integers(-12, 13, size=C)).astype(np.float64)
-    s2[0], s2[7] = 2.0 ** 12, 2.0 ** -8   # channel 7 at 2^-20 of the largest
+    # scales at or below 1 so the activations stay in the generator's range (the fp16 activation planes hold values
+    # up to 2^20, split_bf16.h H16_XS); only the spread between channels matters to the per-channel weight scales
+    s1 = np.exp2(rng.integers(-24, 1, size=C)).astype(np.float64)
+    s2 = np.exp2(rng.integers(-24, 1, size=C)).astype(np.float64)
+    s1[0], s2[0], s2[7] = 1.0, 1.0, 2.0 ** -20   # channel 7 at 2^-20 of the largest
     w1 = (w1 * s1[:, None, None]).astype(np.float32)
     b1 = (b1 * s1).astype(np.float32)
     w2 = (w2 * s2[:, None, None]).astype(np.float32)
