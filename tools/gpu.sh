@@ -14,7 +14,8 @@
 #   ab=E1;E2;...      same-box A/B of the C2 bench under env settings (',' for spaces inside one setting)
 #   ablib=LIB         same-box A/B of the C2 bench: LIB vs the in-tree librvcx.so
 set -o pipefail
-export RVCX_EXPERIMENTAL=1  # the A/B and measurement steps below use RVCX_* developer knobs
+# RVCX_* developer knobs are honoured only with RVCX_EXPERIMENTAL=1: set per step (ab, gru, ablib), so tests, smoke,
+# bench and profiles run exactly as the driver runs them
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 TAG=${1:?tag}; shift
@@ -67,14 +68,14 @@ for step in "$@"; do
       cat $O/pmcconv_${TAG}_${arg%%,*}_${arg##*,}.txt ;;
     gru)
       for m in 0 1 2 0 1 2; do
-        r=$(RVCX_GRU_MODE=$m timeout -k 10 60 ./build/bench_gru 1568 1 10) || { echo "bench_gru mode $m failed"; exit 1; }
+        r=$(RVCX_EXPERIMENTAL=1 RVCX_GRU_MODE=$m timeout -k 10 60 ./build/bench_gru 1568 1 10) || { echo "bench_gru mode $m failed"; exit 1; }
         echo "RVCX_GRU_MODE=$m $r"
       done ;;
     ab)
       IFS=';' read -ra envs <<< "X=0;$arg"
       for rep in 1 2; do
         for e in "${envs[@]}"; do
-          env ${e//,/ } timeout -k 10 200 python bench.py --steps 10 --warmup 3 --no-cpu-baseline > $O/ab_$TAG.log 2>&1 || { echo "bench failed $e"; tail -5 $O/ab_$TAG.log; exit 1; }
+          env RVCX_EXPERIMENTAL=1 ${e//,/ } timeout -k 10 200 python bench.py --steps 10 --warmup 3 --no-cpu-baseline > $O/ab_$TAG.log 2>&1 || { echo "bench failed $e"; tail -5 $O/ab_$TAG.log; exit 1; }
           echo "$e $(c2line $O/ab_$TAG.log)"
         done
       done ;;
