@@ -77,6 +77,7 @@ hipStream_t Ctx::aux_stream() {
     RVCX_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     RVCX_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
     RVCX_HIP(hipEventCreateWithFlags(&ev_gate, hipEventDisableTiming));
+    RVCX_HIP(hipEventCreateWithFlags(&ev_front, hipEventDisableTiming));
   }
   return aux;
 }
@@ -112,6 +113,7 @@ Ctx::~Ctx() {
     (void)hipEventDestroy(ev_fork);
     (void)hipEventDestroy(ev_join);
     (void)hipEventDestroy(ev_gate);
+    (void)hipEventDestroy(ev_front);
     (void)hipStreamDestroy(aux);
   }
 }

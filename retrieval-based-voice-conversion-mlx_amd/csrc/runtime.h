@@ -136,10 +136,14 @@ struct Ctx {
   const void* rb_wsplit_for(const float* w, int C, int k, int wfmt, hipStream_t s);
   // second stream for work independent of the caller's stream (HuBERT beside RMVPE), created lazily
   hipStream_t aux = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_gate = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_gate = nullptr, ev_front = nullptr;
   hipStream_t aux_stream();
   // issued by RMVPE's E2E right before the BiGRU launch (host callback, cleared when taken)
   std::function<void(hipStream_t)> before_gru;
+  // issued by RMVPE's E2E after U-Net encoder level unet_hook_level (or, if the U-Net has no such level, before the
+  // BiGRU launch); host callback, cleared when taken
+  std::function<void(hipStream_t)> at_unet_level;
+  int unet_hook_level = -1;
   // device-side fault flags in pinned host-mapped memory (bit 0: a BiGRU partner hand-off timed out).
   // Kernels store into it; the host reads it after a synchronisation: every compute entry point checks
   // it on entry (faults of earlier, completed calls), the pipeline at its own sync points, and

@@ -578,6 +578,11 @@ static void e2e_chunk(Ctx& c, float* img, int Fc, float* sal, hipStream_t s, int
     }
     float* pooled = c.buf<float>("rm.pool" + std::to_string(i), (size_t)B * (H / 2) * (W / 2) * cout, s);
     check(avgpool2(catb[i] + cout, B * H, W, cout, 2 * cout, pooled, s), "avgpool");
+    if (c.at_unet_level && i == c.unet_hook_level) {  // work the caller wants issued from this point of the U-Net on
+      auto h = std::move(c.at_unet_level);
+      c.at_unet_level = nullptr;
+      h(s);
+    }
     x = pooled;
     ldx = cout;
     H /= 2;
@@ -670,6 +675,11 @@ static void e2e_chunk(Ctx& c, float* img, int Fc, float* sal, hipStream_t s, int
   // work the caller wants issued beside the BiGRU (which occupies 4 CUs): the gate event marks this point of the
   // stream, the BiGRU goes out first and the hook's (many) launches after it, so the host time spent issuing
   // them overlaps the BiGRU instead of delaying its launch
+  if (c.at_unet_level) {  // a hook level the U-Net does not have: issue it now, before the BiGRU's
+    auto h = std::move(c.at_unet_level);
+    c.at_unet_level = nullptr;
+    h(s);
+  }
   std::function<void(hipStream_t)> hook = std::move(c.before_gru);
   c.before_gru = nullptr;
   if (hook && c.ev_gate) RVCX_HIP(hipEventRecord(c.ev_gate, s));

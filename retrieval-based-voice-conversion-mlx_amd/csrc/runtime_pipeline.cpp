@@ -306,6 +306,14 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
   const bool guided = c.scfg.f0;
   const int split = (ax != s && guided) ? gate_layer : HUBERT_LAYERS;
   std::vector<HubertRun> hruns(chunks.size());
+  // HuBERT's feature encoder is issued beside the U-Net from encoder level front_level on (its convs slowed the
+  // U-Net's wide first levels, which are on the critical path, while the deep levels leave most CUs idle); -1:
+  // from the start. Single-chunk RMVPE calls only.
+  static const int front_level = [] {
+    const char* e = rvcx_knob("RVCX_HUBERT_FRONT_LEVEL");
+    return e ? std::atoi(e) : -1;
+  }();
+  const bool delay_front = ax != s && guided && chunks.size() == 1 && o.f0_method == 0 && front_level >= 0;
   // chunks are processed longest first: every later chunk fits the shared work buffers the first one grew, so a
   // call regrows nothing past its first chunk (a caller-sized arena, rvcx_workspace_bytes, holds any split plan);
   // the per-chunk noise offsets, seeds and output positions keep the reference's order (computed up front below)
@@ -314,17 +322,33 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
   std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) {
     return chunks[x].a1 - chunks[x].a0 > chunks[y].a1 - chunks[y].a0;
   });
-  for (size_t i : order) {
-    const int64_t len = chunks[i].a1 - chunks[i].a0;
-    const int64_t cap_rows = len / 320 + 8;
-    cfeats[i] = c.buf<float>("pl.hb" + std::to_string(i), (size_t)cap_rows * E, ax);
-    hruns[i] = hubert_front(c, pad32 + chunks[i].a0, len, len, 1, hubert_version_for(c), cfeats[i], cap_rows, ax);
-    if (chunks.size() == 1) {
-      hubert_layers(c, hruns[i], 0, split, ax);
-    } else {  // several chunks share the HuBERT workspace: each runs to completion before the next
-      hubert_layers(c, hruns[i], 0, HUBERT_LAYERS, ax);
-      cL[i] = hubert_tail(c, hruns[i], ax);
+  auto issue_front = [&]() {
+    for (size_t i : order) {
+      const int64_t len = chunks[i].a1 - chunks[i].a0;
+      const int64_t cap_rows = len / 320 + 8;
+      cfeats[i] = c.buf<float>("pl.hb" + std::to_string(i), (size_t)cap_rows * E, ax);
+      hruns[i] = hubert_front(c, pad32 + chunks[i].a0, len, len, 1, hubert_version_for(c), cfeats[i], cap_rows, ax);
+      if (chunks.size() == 1) {
+        hubert_layers(c, hruns[i], 0, split, ax);
+      } else {  // several chunks share the HuBERT workspace: each runs to completion before the next
+        hubert_layers(c, hruns[i], 0, HUBERT_LAYERS, ax);
+        cL[i] = hubert_tail(c, hruns[i], ax);
+      }
     }
+  };
+  struct FrontScope {
+    Ctx& c;
+    ~FrontScope() { c.at_unet_level = nullptr; c.unet_hook_level = -1; }
+  } front_scope{c};
+  if (delay_front) {
+    c.unet_hook_level = front_level;
+    c.at_unet_level = [&](hipStream_t main) {
+      RVCX_HIP(hipEventRecord(c.ev_front, main));
+      RVCX_HIP(hipStreamWaitEvent(ax, c.ev_front, 0));
+      issue_front();
+    };
+  } else {
+    issue_front();
   }
   // the caller records c.ev_gate on `main` where the rest may start (gate_here), then calls this
   auto gate_here = [&](hipStream_t main) {
