@@ -2,6 +2,8 @@
 // Build: make bench_gru ; run on the GPU box: build/bench_gru [T] [B] [iters].
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -61,7 +63,29 @@ int main(int argc, char** argv) {
   CK_(hipMemcpy(ho.data(), out, ho.size() * 4, hipMemcpyDeviceToHost));
   double cs = 0;
   for (float v : ho) cs += v;
-  printf("T=%d B=%d: %.3f ms/call = %.3f us/step  status=%u checksum=%.6f\n", T, B, ms / iters, 1000.0 * ms / iters / T,
-         st, cs);
+  // fp64 host reference of sequence 0 (both directions; ATen GRUCell), checked on the first min(T, 400) steps of each
+  double maxerr = 0.0;
+  const int Tc = T < 400 ? T : 400;
+  for (int dd = 0; dd < 2; ++dd) {
+    std::vector<double> h(H, 0.0), hg(3 * H);
+    for (int s = 0; s < Tc; ++s) {
+      const int t = dd ? T - 1 - s : s;
+      for (int r = 0; r < 3 * H; ++r) {
+        double a = hb[r];
+        for (int c = 0; c < H; ++c) a += (double)hw[(size_t)r * H + c] * h[c];
+        hg[r] = a;
+      }
+      const float* ig = &hgi[(size_t)t * 6 * H + dd * 3 * H];
+      for (int u = 0; u < H; ++u) {
+        const double rr = 1.0 / (1.0 + std::exp(-(hg[u] + ig[u])));
+        const double zz = 1.0 / (1.0 + std::exp(-(hg[H + u] + ig[H + u])));
+        const double nn = std::tanh(ig[2 * H + u] + hg[2 * H + u] * rr);
+        h[u] = (h[u] - nn) * zz + nn;
+        maxerr = std::max(maxerr, std::fabs(h[u] - (double)ho[(size_t)t * 2 * H + dd * H + u]));
+      }
+    }
+  }
+  printf("T=%d B=%d: %.3f ms/call = %.3f us/step  status=%u checksum=%.6f  max|h - fp64| (first %d steps) %.2e\n", T, B,
+         ms / iters, 1000.0 * ms / iters / T, st, cs, Tc, maxerr);
   return 0;
 }

@@ -185,6 +185,153 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ g
 #undef RVCX_GRU_DOT
 }
 
+// Gate-major layout (round 5): the same 4 workgroups x 768 threads and the same W_hh-in-VGPRs budget (128 weights per
+// thread), but a wave owns ONE gate of all 128 units of its workgroup and a 32-column group of each half of h: wave w
+// = (gate g = w / 4, column group cg = w % 4), lane l holds rows (g, unit l) and (g, unit 64 + l) over own columns
+// [32 cg, 32 cg + 32) and the same 32 partner columns. Every h value a wave reads now feeds two rows, so the per-step
+// LDS broadcast reads of h halve (16 ds_read_b128 per wave instead of 32; they were ~1500 of the CU's LDS cycles per
+// step, the larger part of the math phase), the partner work after the hand-off stays 32 packed FMAs on every wave,
+// and the gate threads sum four column-group partials instead of two.
+template <int MODE>
+__global__ __launch_bounds__(NT, 1) void k_gru_bidir_g(const float* __restrict__ gi, const float* whh_f,
+                                                       const float* bhh_f, const float* whh_b, const float* bhh_b,
+                                                       int T, float* out, unsigned long long* xchg,
+                                                       unsigned* status, unsigned spin_limit, unsigned tag0,
+                                                       int adjacent) {
+  constexpr int CG = 32;  // columns of each half per wave
+  __shared__ __attribute__((aligned(16))) float h_own[UNITS];
+  __shared__ __attribute__((aligned(16))) float h_pw[NT / 64][CG];  // per-wave copy of its partner columns
+  __shared__ float part[4][ROWS];
+  __shared__ float bias_h[ROWS];
+  __shared__ int abort_flag;
+
+  const int w = blockIdx.x & 15;
+  if (adjacent ? w > 3 : (w & 7) > 1) return;
+  const int d = adjacent ? w >> 1 : w & 1;
+  const int q = adjacent ? w & 1 : w >> 3;
+  const int seq = blockIdx.x >> 4;
+  gi += (long long)seq * T * 6 * H;
+  out += (long long)seq * T * 2 * H;
+  xchg += (long long)seq * 4 * 2 * UNITS;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int g = wave >> 2, cg = wave & 3;  // gate, column group (wave-uniform)
+  const float* whh = d ? whh_b : whh_f;
+  const float* bhh = d ? bhh_b : bhh_f;
+  unsigned long long* mine = xchg + ((long long)(d * 2 + q) * 2) * UNITS;
+  unsigned long long* theirs = xchg + ((long long)(d * 2 + (1 - q)) * 2) * UNITS;
+
+  // rows (g, unit lane) and (g, unit 64 + lane) of W_hh (global row g * H + q * UNITS + unit)
+  const int grow0 = g * H + q * UNITS + lane, grow1 = grow0 + 64;
+  const int own0 = q * UNITS + cg * CG, par0 = (1 - q) * UNITS + cg * CG;
+  f32x2 wo0[CG / 2], wo1[CG / 2], wp0[CG / 2], wp1[CG / 2];
+#pragma unroll
+  for (int k = 0; k < CG; k += 4) {
+    float4 v = *reinterpret_cast<const float4*>(&whh[(long long)grow0 * H + own0 + k]);
+    wo0[k / 2] = f32x2{v.x, v.y};
+    wo0[k / 2 + 1] = f32x2{v.z, v.w};
+    v = *reinterpret_cast<const float4*>(&whh[(long long)grow1 * H + own0 + k]);
+    wo1[k / 2] = f32x2{v.x, v.y};
+    wo1[k / 2 + 1] = f32x2{v.z, v.w};
+    v = *reinterpret_cast<const float4*>(&whh[(long long)grow0 * H + par0 + k]);
+    wp0[k / 2] = f32x2{v.x, v.y};
+    wp0[k / 2 + 1] = f32x2{v.z, v.w};
+    v = *reinterpret_cast<const float4*>(&whh[(long long)grow1 * H + par0 + k]);
+    wp1[k / 2] = f32x2{v.x, v.y};
+    wp1[k / 2 + 1] = f32x2{v.z, v.w};
+  }
+  if (tid < UNITS) h_own[tid] = 0.f;
+  if (tid == 0) abort_flag = 0;
+  const int gunit = q * UNITS + tid;
+  if (tid < ROWS) bias_h[tid] = bhh[(tid / UNITS) * H + q * UNITS + tid % UNITS];
+  __syncthreads();
+
+  // two rows' dots over CG columns of h (broadcast float4 reads: each value feeds both rows)
+#define RVCX_GRU_DOT2(W0, W1, HV, O0, O1)                                            \
+  do {                                                                               \
+    f32x2 a0_ = {0.f, 0.f}, a1_ = {0.f, 0.f}, b0_ = {0.f, 0.f}, b1_ = {0.f, 0.f};    \
+    _Pragma("unroll") for (int k = 0; k < CG; k += 4) {                              \
+      const float4 x_ = *reinterpret_cast<const float4*>(&(HV)[k]);                  \
+      const f32x2 xl_ = f32x2{x_.x, x_.y}, xh_ = f32x2{x_.z, x_.w};                  \
+      a0_ = __builtin_elementwise_fma(W0[k / 2], xl_, a0_);                          \
+      a1_ = __builtin_elementwise_fma(W0[k / 2 + 1], xh_, a1_);                      \
+      b0_ = __builtin_elementwise_fma(W1[k / 2], xl_, b0_);                          \
+      b1_ = __builtin_elementwise_fma(W1[k / 2 + 1], xh_, b1_);                      \
+    }                                                                                \
+    O0 = (a0_.x + a1_.x) + (a0_.y + a1_.y);                                          \
+    O1 = (b0_.x + b1_.x) + (b0_.y + b1_.y);                                          \
+  } while (0)
+
+  auto load_ig = [&](int s, float& ir, float& iz, float& in) {
+    const int t = d ? (T - 1 - s) : s;
+    const int o = t * (6 * H) + d * 3 * H + gunit;
+    ir = gi[o];
+    iz = gi[o + H];
+    in = gi[o + 2 * H];
+  };
+  float ig_r = 0.f, ig_z = 0.f, ig_n = 0.f;
+  for (int s = 0; s < T; ++s) {
+    const int t = d ? (T - 1 - s) : s;
+    if (tid < UNITS) load_ig(s, ig_r, ig_z, ig_n);
+    float own0 = 0.f, own1 = 0.f, par0v = 0.f, par1v = 0.f;
+    if constexpr (MODE != 1) RVCX_GRU_DOT2(wo0, wo1, h_own + cg * CG, own0, own1);
+    asm volatile("" : "+v"(own0), "+v"(own1));  // finish the own-column dots before polling
+    {
+      float* hp = h_pw[wave];
+      if (MODE != 2 && s > 0) {
+        const unsigned epoch = tag0 + (unsigned)s;
+        // lanes l and l + 32 poll the same granule (32 partner values per wave)
+        const unsigned long long* slot = theirs + ((s - 1) & 1) * UNITS + cg * CG + (lane & (CG - 1));
+        unsigned long long gv = 0;
+#pragma nounroll
+        for (unsigned spins = 0;; ++spins) {
+          if (spins >= spin_limit) {
+            abort_flag = 1;
+            break;
+          }
+          gv = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((unsigned)(gv >> 32) == epoch) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (lane < CG) hp[lane] = __uint_as_float((unsigned)gv);
+      } else if (lane < CG) {
+        hp[lane] = 0.f;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if constexpr (MODE != 1) RVCX_GRU_DOT2(wp0, wp1, hp, par0v, par1v);
+    }
+    part[cg][g * UNITS + lane] = own0 + par0v;
+    part[cg][g * UNITS + 64 + lane] = own1 + par1v;
+    __syncthreads();
+    if (abort_flag) {
+      if (tid == 0) __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    if (tid < UNITS) {
+      const float hr = ((part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid])) + bias_h[tid];
+      const float hz = ((part[0][UNITS + tid] + part[1][UNITS + tid]) + (part[2][UNITS + tid] + part[3][UNITS + tid])) +
+                       bias_h[UNITS + tid];
+      const float hn = ((part[0][2 * UNITS + tid] + part[1][2 * UNITS + tid]) +
+                        (part[2][2 * UNITS + tid] + part[3][2 * UNITS + tid])) +
+                       bias_h[2 * UNITS + tid];
+      const float rr = sigm(hr + ig_r);
+      const float zz = sigm(hz + ig_z);
+      const float nn = tanh_g(ig_n + hn * rr);
+      const float hprev = h_own[tid];
+      const float hnew = (hprev - nn) * zz + nn;
+      h_own[tid] = hnew;
+      out[(long long)t * (2 * H) + d * H + gunit] = hnew;
+      const unsigned long long gg =
+          ((unsigned long long)(tag0 + (unsigned)(s + 1)) << 32) | (unsigned long long)__float_as_uint(hnew);
+      __hip_atomic_store(&mine[(s & 1) * UNITS + tid], gg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+  }
+#undef RVCX_GRU_DOT2
+}
+
 hipError_t gru_bidir(const float* gi, const float* whh_f, const float* bhh_f, const float* whh_b,
                      const float* bhh_b, int T, float* out, unsigned long long* xchg, unsigned* status,
                      unsigned* next_tag, hipStream_t s, int B) {
@@ -214,7 +361,12 @@ hipError_t gru_bidir(const float* gi, const float* whh_f, const float* bhh_f, co
     const char* e = rvcx_knob("RVCX_GRU_MODE");
     return e ? std::atoi(e) : 0;
   }();
-  auto kern = mode == 1 ? k_gru_bidir<1> : (mode == 2 ? k_gru_bidir<2> : k_gru_bidir<0>);
+  static const int layout = [] {  // RVCX_GRU_LAYOUT: 0 row-major waves (rounds 2-4), 1 gate-major waves (default)
+    const char* e = rvcx_knob("RVCX_GRU_LAYOUT");
+    return e ? std::atoi(e) : 1;
+  }();
+  auto kern = layout == 0 ? (mode == 1 ? k_gru_bidir<1> : (mode == 2 ? k_gru_bidir<2> : k_gru_bidir<0>))
+                          : (mode == 1 ? k_gru_bidir_g<1> : (mode == 2 ? k_gru_bidir_g<2> : k_gru_bidir_g<0>));
   hipLaunchKernelGGL(kern, dim3(16 * B), dim3(NT), 0, s, gi, whh_f, bhh_f, whh_b, bhh_b, T, out, xchg, status, spin,
                      tag0, adj);
   return hipGetLastError();
