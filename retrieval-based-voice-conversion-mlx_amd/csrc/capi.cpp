@@ -862,7 +862,7 @@ int rvcx_conv2d3x3(rvcx_ctx* ctx, const float* d_x, int H, int W, int C_in, cons
   return guard(ctx, [&] {
     set_device(ctx);
     ctx->check_device_status();
-    if (!d_x || !d_w || !d_y || H <= 0 || W <= 0 || C_in <= 0 || N <= 0 || act < 0 || act > 1 || math < 0 || math > 1)
+    if (!d_x || !d_w || !d_y || H <= 0 || W <= 0 || C_in <= 0 || N <= 0 || act < 0 || act > 1 || math < 0 || math > 3)
       throw Error(RVCX_E_INVALID, "rvcx_conv2d3x3: bad argument");
     if ((int64_t)H * W * (C_in > N ? C_in : N) > INT32_MAX) throw Error(RVCX_E_SHAPE, "rvcx_conv2d3x3: size out of range");
     ConvArgs a;
@@ -870,9 +870,23 @@ int rvcx_conv2d3x3(rvcx_ctx* ctx, const float* d_x, int H, int W, int C_in, cons
     a.w = d_w; a.ldw = C_in; a.w_ts = (long long)N * C_in; a.taps = 9; a.KH = 3; a.KW = 3; a.padh = 1; a.padw = 1;
     a.y = d_y; a.ldy = N; a.T_out = H; a.W_out = W; a.N = N; a.bias = d_bias;
     a.act = act ? ACT_RELU : ACT_NONE;
-    a.math = math == 1 ? 1 : 0;
+    a.math = math == 1 ? 1 : (math >= 2 ? 3 : 0);
     if (a.math == 0 && ctx->conv_math > 0) a.math = ctx->conv_math;
-    if (conv_math_of(a) == 3 && conv2d_small_fits(a)) {
+    if (math >= 2) {
+      // the windowed gather-streamed kernels of the U-Net's deep levels in the two-plane fp16 split, split-K by the
+      // size policy: 2 = cfg 30 (64 x 64 tiles, K split over workgroups), 3 = cfg 33 (64 x 32 tiles, K split over
+      // the waves of a workgroup); a fresh image every call
+      a.wsb = 2;
+      a.wsplit_fmt = WSPLIT_H16;
+      if (!conv_gsw_eligible(a)) throw Error(RVCX_E_SHAPE, "rvcx_conv2d3x3: shape not eligible for the windowed kernel");
+      if (math == 3 && C_in < 128) throw Error(RVCX_E_SHAPE, "rvcx_conv2d3x3: the wave-split kernel needs C_in >= 128");
+      a.w_static = 1;
+      a.force_cfg = math == 3 ? 33 : 30;
+      void* img = ctx->buf<char>("conv.test.wsplit", (size_t)conv_wsplit_bytes(a), static_cast<hipStream_t>(stream));
+      check(conv_wsplit_build(a, img, static_cast<hipStream_t>(stream)), "conv_wsplit_build");
+      a.wsplit = img;
+      a.wsplit_npad = conv_wsplit_npad(a.N);
+    } else if (conv_math_of(a) == 3 && conv2d_small_fits(a)) {
       // a fresh image every call, never the address-keyed cache (the caller may reuse d_w with new weights)
       a.wsplit_fmt = WSPLIT_S2D;
       void* img = ctx->buf<char>("conv.test.s2d", (size_t)small2d_wsplit_bytes(a), static_cast<hipStream_t>(stream));

@@ -921,6 +921,9 @@ inline int pick_wsb(const ConvArgs& a) {
   static const int c_long = env_cfg("RVCX_WCFG_LONG", 23);
   static const int c_wide = env_cfg("RVCX_WCFG_WIDE", 23);
   static const int c_gs = env_cfg("RVCX_GCFG", 30);
+  // the U-Net's deep 3x3 levels (>= 4 chunks of 32 input channels) on the wave-K-split windowed kernel (cfg 33)
+  static const bool gswk = env_cfg("RVCX_GSWK", 0) != 0;
+  if (a.wsb == 2 && gswk && a.KH == 3 && a.C_in >= 4 * CK && conv_math(a) == 3 && conv_gsw_eligible(a)) return 33;
   if (a.wsb == 2) return c_gs;  // gather-streamed (conv_gs.hip): the short contractions
   if (a.N <= 32) return c_narrow;
   if (a.taps <= 3) return c_short;
@@ -957,7 +960,7 @@ hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
   if (a.wsb == 2 && a.wsplit && conv_math(a) >= 2 && conv_gs_eligible(a, TWO_D)) {
     const int ks = (a.ws && a.ksplit > 1) ? a.ksplit : 1;
     const int cfg = a.force_cfg >= 30 ? a.force_cfg : pick_wsb(a);
-    g_conv_kind = (TWO_D && cfg == 30 && conv_gsw_eligible(a)) ? CK_GSW : CK_GS;
+    g_conv_kind = (TWO_D && (cfg == 30 || cfg == 33) && conv_gsw_eligible(a)) ? CK_GSW : CK_GS;
     hipError_t e = conv_gs_launch(a, cfg, xcd_enabled() ? 1 : 0, s, TWO_D, ks);
     if (e == hipSuccess && ks > 1) e = launch_splitk_reduce(a, ks, TWO_D, s);
     if (e != hipErrorInvalidValue) return e;
@@ -1044,6 +1047,17 @@ long long conv_plan_splitk(ConvArgs& a, bool two_d) {
   }
   const long long tiles = mtiles * ((a.N + BN - 1) / BN) * a.batch * a.batch_inner;
   const int iters = ((a.C_in + CK - 1) / CK) * a.taps;
+  if (a.wsb == 2 && two_d && BN == 32 && (a.force_cfg < 0 || a.force_cfg == 33) && a.gate_h == 0 && !a.ln_g) {
+    // cfg 33 (conv_gsw16k_kernel): workgroups split K over their 4 waves; split K over workgroups as well only until the
+    // grid reaches the target, and never below one chunk per wave
+    static const int t33 = env_cfg("RVCX_GSWK_TARGET", 256);
+    const int nch = (a.C_in + CK - 1) / CK;
+    int ks = (int)std::min<long long>((t33 + tiles - 1) / tiles, nch / 4);
+    if (ks < 2) return 0;
+    a.ksplit = ks;
+    a.ws_rows = (long long)a.T_out * a.W_out;
+    return (long long)ks * a.ws_rows * a.N * a.batch * a.batch_inner;
+  }
   const double M = two_d ? (double)a.T_out * a.W_out : (double)a.T_out;
   const double flops = 2.0 * M * a.N * (double)a.C_in * a.taps * a.batch * a.batch_inner;
   // split only where the output grid leaves CUs idle AND the contraction is long enough to pay

@@ -583,7 +583,8 @@ class Engine:
     def conv2d3x3(self, x, w, bias=None, relu: bool = False, math: str = "default"):
         """torch.nn.functional.conv2d(x.permute(2, 0, 1)[None], w, bias, padding=1)[0].permute(1, 2, 0) on the device
         kernel: x [H][W][C_in] (NHWC), w [N][C_in][3][3] (torch layout) -> [H][W][N] fp32 (rvcx_conv2d3x3); math
-        "default" = the context's arithmetic, "f32" = exact fp32."""
+        "default" = the context's arithmetic, "f32" = exact fp32, "gsw" / "gswk" = the U-Net deep levels' windowed
+        kernels in the fp16 split (K split over workgroups / over the waves of a workgroup)."""
         torch = self.torch
         x = self._dev(x, torch.float32)
         w = torch.as_tensor(w, dtype=torch.float32)
@@ -592,7 +593,7 @@ class Engine:
         b = self._dev(bias, torch.float32) if bias is not None else None
         H, W = int(x.shape[0]), int(x.shape[1])
         y = torch.empty((H, W, N), dtype=torch.float32, device=self.device)
-        m = {"default": 0, "f32": 1}[math]
+        m = {"default": 0, "f32": 1, "gsw": 2, "gswk": 3}[math]
         self._check(self.lib.rvcx_conv2d3x3(self.ctx, _ptr(x), H, W, C, _ptr(wk), _ptr(b), N, 1 if relu else 0, m,
                                             _ptr(y), self.stream()), "conv2d3x3")
         return y

@@ -158,3 +158,38 @@ def test_unet_small_2d_convs_are_fp32_accurate(engine, H, W, C, N, spread, wsp):
     print(f"\n2-D {H}x{W} {C}->{N}: " + " ".join(f"{k} {v:.2e}" for k, v in errs.items()))
     assert errs["f32"] < 1e-6, errs
     assert errs["default"] < 1e-6 and errs["default"] <= 4.0 * errs["f32"] + 1e-8, errs
+
+
+DEEP2D = [  # H, W, C_in, N: the RMVPE U-Net's deep levels (windowed gather-streamed kernels, conv_gs.hip)
+    (49, 4, 512, 512),    # intermediate (196 px)
+    (98, 8, 256, 256),    # level 3 (784 px)
+    (196, 16, 128, 128),  # level 2 (3136 px)
+    (33, 8, 256, 80),     # ragged rows and a partial 32-column tile
+    (20, 32, 128, 64),
+]
+
+
+@pytest.mark.parametrize("H,W,C,N", DEEP2D)
+def test_unet_deep_level_windowed_kernels(engine, H, W, C, N):
+    """cfg 30 (64 x 64 tiles, K split over workgroups) and cfg 33 (64 x 32 tiles, K split over the 4 waves of a
+    workgroup, partials summed in LDS) against fp64, per output element relative to its own sum |x w|: both within
+    1e-6 and at most 4x the exact-f32 kernel's error."""
+    rng = np.random.Generator(np.random.PCG64(H * 7 + W + C + N))
+    x = rng.standard_normal((H, W, C)).astype(np.float32)
+    w = (rng.standard_normal((N, C, 3, 3)) / np.sqrt(9 * C)).astype(np.float32)
+    bias = rng.standard_normal(N).astype(np.float32)
+    xd = torch.from_numpy(x.astype(np.float64)).permute(2, 0, 1)[None]
+    wd = torch.from_numpy(w.astype(np.float64))
+    ref = torch.relu(torch.nn.functional.conv2d(xd, wd, torch.from_numpy(bias.astype(np.float64)), padding=1))
+    mag = torch.nn.functional.conv2d(xd.abs(), wd.abs(), None, padding=1) + np.abs(bias)[None, :, None, None]
+    ref = ref[0].permute(1, 2, 0).numpy()
+    mag = mag[0].permute(1, 2, 0).numpy() + 1e-300
+    errs = {}
+    for mode in ("f32", "gsw", "gswk"):
+        y = engine.conv2d3x3(x, w, bias, relu=True, math=mode).cpu().numpy()
+        assert y.shape == ref.shape
+        errs[mode] = float(np.max(np.abs(y - ref) / mag))
+    print(f"\n2-D deep {H}x{W} {C}->{N}: " + " ".join(f"{k} {v:.2e}" for k, v in errs.items()))
+    assert errs["f32"] < 1e-6, errs
+    for k in ("gsw", "gswk"):
+        assert errs[k] < 1e-6 and errs[k] <= 4.0 * errs["f32"] + 1e-8, errs
