@@ -107,7 +107,8 @@ __global__ void k_wsplit_h16(const float* __restrict__ w, int ldw, long long w_t
   }
 }
 
-#ifndef WSB_EXP  // measurement aid (build/exp bench_conv only): 1 no A halo loads, 2 no B loads
+#ifndef WSB_EXP  // measurement aid (build/exp bench_conv only): 1 no A halo loads, 2 no B loads, 4 no A split (the halo
+                 // stored to LDS as loaded: the cost a producer-side pre-split image would remove)
 #define WSB_EXP 0
 #endif
 
@@ -419,9 +420,13 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
           for (int j = 0; j < 4; ++j) val[j] = ok ? val[j] : 0.f;
         }
         if constexpr (H16) {
+#if WSB_EXP & 4
+          *reinterpret_cast<f32x4*>(As + r * RS + ac4 * 4) = apre[v];
+#else
 #pragma unroll
           for (int j = 0; j < 4; ++j) val[j] *= H16_XS;
           put_h16x4<NQ>(As + r * RS, ac4, val);
+#endif
         } else {
           put_split4(As + r * RS, ac4, val);
         }

@@ -9,6 +9,7 @@
 #   prof              rocprofv3 --kernel-trace --stats of the C2 bench + timeline + kernel-family table
 #   pmc               the three HBM / MFMA PMC passes of one C2 step (tools/pmc_traffic.sh)
 #   bc                build/bench_conv table (checks + every tile)
+#   bcx=DIR1,DIR2     bench_conv generator shapes with each DIR's librvcx.so after the in-tree one (timing experiments)
 #   pmcconv=CASE,CFG  the PMC passes of bench_conv case CASE on tile cfg CFG (tools/pmc_conv.sh + pmc_conv.py)
 #   gru               build/bench_gru (BiGRU steps: full, hand-off only, math only)
 #   ab=E1;E2;...      same-box A/B of the C2 bench under env settings (',' for spaces inside one setting)
@@ -62,6 +63,15 @@ for step in "$@"; do
     bc)
       timeout -k 10 400 ./build/bench_conv 20 ${arg//,/ } > $O/bench_conv_$TAG.txt 2>&1 || { tail $O/bench_conv_$TAG.txt; exit 1; }
       cat $O/bench_conv_$TAG.txt ;;
+    bcx)
+      # bench_conv on selected generator shapes against alternative library builds (timing-only experiments):
+      # bcx=DIR1,DIR2 runs each DIR's librvcx.so (LD_LIBRARY_PATH) after the in-tree one
+      for lib in "" ${arg//,/ }; do
+        for cc in "1 27" "17 27" "2 23" "3 23" "4 23" "0 23"; do
+          r=$(LD_LIBRARY_PATH=$lib timeout -k 10 60 ./build/bench_conv 40 $cc) || { echo "bench_conv $lib $cc failed"; exit 1; }
+          echo "lib=${lib:-tree} case/cfg=$cc $r"
+        done
+      done ;;
     pmcconv)
       bash tools/pmc_conv.sh ${arg%%,*} ${arg##*,} || exit 1
       python3 tools/pmc_conv.py pmc_c${arg%%,*}_g${arg##*,} > $O/pmcconv_${TAG}_${arg%%,*}_${arg##*,}.txt 2>&1
