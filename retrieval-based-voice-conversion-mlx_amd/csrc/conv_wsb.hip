@@ -112,6 +112,10 @@ __global__ void k_wsplit_h16(const float* __restrict__ w, int ldw, long long w_t
 #define WSB_EXP 0
 #endif
 
+#ifndef WSB16_AFRAG  // A-fragment LDS reads of the fp16 kernel's step: 0 per row block, 1 all up front, 2 one block ahead
+#define WSB16_AFRAG 0
+#endif
+
 #ifndef WSB_WAVES_128x64
 #define WSB_WAVES_128x64 3
 #endif
@@ -450,6 +454,42 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
   };
   auto compute = [&](int tap, const BFrag& bf) __attribute__((always_inline)) {
     const int toff = tap * a.dil * RS;
+#if WSB16_AFRAG
+    if constexpr (H16) {
+      // the step's A fragments requested ahead of their MFMAs (1: all TM16 at the top; 2: one row block ahead)
+      bf16x8 afa[WSB16_AFRAG == 1 ? TM16 : 2][NQ];
+#pragma unroll
+      for (int tm = 0; tm < (WSB16_AFRAG == 1 ? TM16 : 1); ++tm)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) afa[tm][q] = *reinterpret_cast<const bf16x8*>(As + aoff[tm] + toff + q * PLANE);
+      __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler otherwise sinks them to their MFMAs)
+#pragma unroll
+      for (int tm = 0; tm < TM16; ++tm) {
+        const int sl = WSB16_AFRAG == 1 ? tm : (tm & 1);
+        if constexpr (WSB16_AFRAG == 2) {
+          if (tm + 1 < TM16) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q)
+              afa[(tm + 1) & 1][q] = *reinterpret_cast<const bf16x8*>(As + aoff[tm + 1] + toff + q * PLANE);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+        const f16x8 ah = __builtin_bit_cast(f16x8, afa[sl][0]);
+#pragma unroll
+        for (int tn = 0; tn < TN16; ++tn) {
+          const f16x8 bh = __builtin_bit_cast(f16x8, bf[tn][0]);
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc[tm][tn], 0, 0, 0);
+          if constexpr (!LOWP) {
+            f32x4 c = acc2[tm][tn];
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, afa[sl][NQ - 1]), bh, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, __builtin_bit_cast(f16x8, bf[tn][NQ - 1]), c, 0, 0, 0);
+            acc2[tm][tn] = c;
+          }
+        }
+      }
+      return;
+    }
+#endif
 #pragma unroll
     for (int tm = 0; tm < TM16; ++tm) {
       bf16x8 af[NQ];
