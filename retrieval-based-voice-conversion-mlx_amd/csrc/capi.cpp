@@ -210,6 +210,16 @@ void launch_rb_pair(Ctx& c, const RbPairArgs& a_in, hipStream_t s) {
   c.prof_recs.push_back(r);
 }
 
+bool conv_routes_wsb16(Ctx& c, const ConvArgs& a_in) {
+  ConvArgs b = a_in;
+  if (c.conv_math > 0 && b.math == 0) b.math = c.conv_math;
+  if (!(b.w_static || c.is_weight(b.w)) || b.force_cfg >= 0) return false;
+  if (!(conv_math_of(b) == 3 || b.lowp)) return false;  // the fp16 image (launch_conv below)
+  if (conv_wsb_route(b, false) != 1) return false;
+  b.wsb = 1;
+  return conv_plan_splitk(b, false) == 0 && conv_wsb_pick(b) >= 23;
+}
+
 void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double flops) {
   ConvArgs a = a_in;
   if (c.conv_math > 0 && a.math == 0) a.math = c.conv_math;
@@ -232,6 +242,10 @@ void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double
     if (!a.wsplit) a.wsplit = c.wsplit_for(a, s);  // a caller-built image (rvcx_conv1d) is used as given
     a.wsplit_npad = conv_wsplit_npad(a.N);
   }
+  // the two-plane fp16 activation image (x_h16 / y_h16) exists only between weight-streamed fp16 launches
+  if ((a.x_h16 || a.y_h16) && (two_d || a.wsb != 1 || a.wsplit_fmt != WSPLIT_H16 || need > 0 || a.N % 32 != 0 ||
+                               (a.y_h16 && (a.ldy != a.N || a.acc_mode != ACC_STORE || a.mask || a.res))))
+    throw Error(RVCX_E_SHAPE, "conv: the fp16 activation image needs the weight-streamed fp16 kernel without split-K");
   // split-K slabs are per stream: the aux stream's convs run concurrently with the caller's
   if (need > 0) a.ws = c.buf<float>(c.aux && s == c.aux ? "conv.splitk.aux" : "conv.splitk", (size_t)need, s);
   if (flops < 0) {

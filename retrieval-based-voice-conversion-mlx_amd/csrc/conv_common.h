@@ -159,6 +159,22 @@ __device__ __forceinline__ void store_tile16(const ConvArgs& a, int m0, int n0, 
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] *= mv[r];
       }
+      if (a.y_h16) {
+        // the consumer's A operand as the two-plane fp16 image (split_bf16.h put_h16x4 of v * 2^-4): h = f16(x),
+        // l = f16((x - h) 2^11), at bytes [0, 64) and [64, 128) of the row's 32-channel chunk
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float xs = v[r] * (1.f / 16.f);
+          const _Float16 h = (_Float16)xs;
+          const _Float16 l = (_Float16)((xs - (float)h) * 2048.f);
+          _Float16* row = reinterpret_cast<_Float16*>(Y + (mb + r) * a.ldy + (n & ~31));
+          if (ok[r]) {
+            row[n & 31] = h;
+            row[32 + (n & 31)] = l;
+          }
+        }
+        continue;
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         if (ok[r]) Y[(mb + r) * a.ldy + n] = v[r];

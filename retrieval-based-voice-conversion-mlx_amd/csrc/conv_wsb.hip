@@ -342,6 +342,7 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
   constexpr bool PMASK = (MODE & 4) != 0;
   constexpr bool H16 = (MODE & 16) != 0;
   constexpr bool LOWP = H16 && (MODE & 8) != 0;
+  constexpr bool PRESPLIT = H16 && (MODE & 32) != 0;  // A arrives as the h16 image (ConvArgs::x_h16): copied, not split
   constexpr int NQ = LOWP ? 1 : (H16 ? 2 : 3);  // planes an MFMA step reads
   constexpr int NQI = H16 ? 2 : 3;               // planes of the weight image
   constexpr int RS = H16 ? ERS_H : ERS;          // LDS row stride
@@ -414,6 +415,12 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
       if (r < nrows_a) {
         f32x4 val = apre[v];
         const bool ok = (aok >> v) & 1u;
+        if constexpr (PRESPLIT) {
+          // the 16 bytes at this slot already hold the row's planes in the LDS row layout (slot ac4 / 4 of 8)
+          const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+          *reinterpret_cast<f32x4*>(As + r * RS + ac4 * 4) = ok ? val : zero;
+          continue;
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) val[j] = pre_fn<PA>(val[j], a.pre_act, a.pre_slope);
         if constexpr (PMASK) {
@@ -586,24 +593,27 @@ hipError_t launch_wsb16(const ConvArgs& a, int ntn_enable, int ksplit, hipStream
   const int ntn = ntn_enable ? ntiles : 0;
   dim3 grid(ntn ? mtiles * ntiles : mtiles, ntn ? 1 : ntiles, a.batch * ksplit);
   // the reduced-precision opt-in only without a pre-mask (the generator's convs)
-  const int mode = pre_mode(a.pre_act) | (a.pre_mask ? 4 : 0) | (h16 ? 16 : 0) | (h16 && a.lowp && !a.pre_mask ? 8 : 0);
+  // the pre-split A image: the fp16 arithmetic without a pre-activation or pre-mask, rows of exactly C_in channels
+  if (a.x_h16 && (!h16 || a.pre_act != ACT_NONE || a.pre_mask || a.ldx != a.C_in)) return hipErrorInvalidValue;
+  const int mode = pre_mode(a.pre_act) | (a.pre_mask ? 4 : 0) | (h16 ? 16 : 0) | (h16 && a.lowp && !a.pre_mask ? 8 : 0) |
+                   (a.x_h16 ? 32 : 0);
   void (*kern)(const ConvArgs, const char*, int, int, int, int);
   switch (mode) {
 #define WSB16_CASE(M) \
   case M: kern = conv_wsb16_kernel<BM, BN, WM, WN, (H16OK || M < 16) ? M : 0>; break;
     WSB16_CASE(0) WSB16_CASE(1) WSB16_CASE(2) WSB16_CASE(4) WSB16_CASE(5) WSB16_CASE(6)
     WSB16_CASE(16) WSB16_CASE(17) WSB16_CASE(18) WSB16_CASE(20) WSB16_CASE(21) WSB16_CASE(22)
-    WSB16_CASE(24) WSB16_CASE(25) WSB16_CASE(26)
+    WSB16_CASE(24) WSB16_CASE(25) WSB16_CASE(26) WSB16_CASE(48) WSB16_CASE(56)
 #undef WSB16_CASE
     default: return hipErrorInvalidValue;
   }
   // per instantiation: raise the dynamic-LDS limit once, not per launch
-  static size_t smem_set[32] = {};
-  if (smem > 64 * 1024 && smem > smem_set[mode & 31]) {
+  static size_t smem_set[64] = {};
+  if (smem > 64 * 1024 && smem > smem_set[mode & 63]) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
-    smem_set[mode & 31] = smem;
+    smem_set[mode & 63] = smem;
   }
   hipLaunchKernelGGL(kern, grid, dim3(CONV_THREADS), smem, s, a, static_cast<const char*>(a.wsplit), a.wsplit_npad,
                      nrows_a, ntn, ksplit);

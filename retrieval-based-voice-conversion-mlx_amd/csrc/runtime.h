@@ -341,6 +341,9 @@ void set_i32_once(Ctx& c, const std::string& name, int32_t* p, int32_t v, hipStr
 // far (or s itself when overlap is off: kernel timing on, or RVCX_NO_OVERLAP=1); join_aux makes s wait for
 // everything queued on the aux stream so far.
 hipStream_t fork_aux(Ctx& c, hipStream_t s);
+// whether launch_conv would run this 1-D contraction on the weight-streamed fp16 kernel without split-K (the only
+// producer / consumer of the two-plane fp16 activation image, ConvArgs::y_h16 / x_h16)
+bool conv_routes_wsb16(Ctx& c, const ConvArgs& a);
 void join_aux(Ctx& c, hipStream_t s, hipStream_t ax);
 // launch one implicit-GEMM conv (1-D or 2-D) with optional event timing; flops = algorithmic FLOPs
 void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double flops = -1.0);

@@ -492,6 +492,13 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
         }
         continue;
       }
+      // c1 hands its output to c2 as the two-plane fp16 image when both run on the weight-streamed fp16 kernel: c2's
+      // input has no pre-activation (c1's epilogue applies the leaky ReLU) and no other reader, so the image (the
+      // same 4 B per element) replaces the fp32 tensor and c2's halo staging is a copy instead of a split
+      static const bool presplit_on = [] {
+        const char* e = rvcx_knob("RVCX_PRESPLIT");
+        return !(e && std::atoi(e) == 0);
+      }();
       for (size_t m = 0; m < dil.size(); ++m) {
         const int d = dil[m];
         const std::string n1 = rb + ".convs1." + std::to_string(m);
@@ -503,12 +510,16 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
         a1.pre_slope = 0.1f;
         a1.act = ACT_LRELU;
         a1.slope = 0.1f;
-        run(c, a1, s);
         const bool last = (m + 1 == dil.size());
         float* dst = last ? S : RR;
         ConvArgs a2 = conv(T1, C, Ti, C, c.W(n2 + ".w"), C, k, 1, (k - 1) / 2, c.W(n2 + ".b"), dst, C, Ti, B);
         a2.w_static = 1;
         a2.lowp = gen_lowp;
+        if (presplit_on && C % 32 == 0 && conv_routes_wsb16(c, a1) && conv_routes_wsb16(c, a2)) {
+          a1.y_h16 = 1;
+          a2.x_h16 = 1;
+        }
+        run(c, a1, s);
         a2.res = r_in;
         a2.ldr = C;
         a2.res_bs = (long long)Ti * C;

@@ -57,6 +57,10 @@ struct ConvArgs {
   int C_in = 0;         // contraction channels per tap
   int pre_act = ACT_NONE;
   float pre_slope = 0.f;
+  // x is the two-plane fp16 image an h16 epilogue wrote (y_h16 below): per row and 32-channel chunk 128 B = the h
+  // plane (32 fp16) then the 2^11-scaled residual plane, of the values times 2^-4 -- the weight-streamed kernel's LDS
+  // row layout, so its A staging is a plain copy (conv_wsb16_kernel only; ldx = C_in, no pre_act / pre_mask)
+  int x_h16 = 0;
   const float* pre_mask = nullptr;  // [b][row] multiplier applied to input rows (1-D only)
   long long pre_mask_bs = 0;
   // B operand (weights): NK: w + tap*w_ts + n*ldw + c ; KN: w + tap*w_ts + c*ldw + n
@@ -92,6 +96,9 @@ struct ConvArgs {
   long long mask_bs = 0;
   int acc_mode = ACC_STORE;
   float acc_div = 1.f;
+  // write y as that two-plane fp16 image instead of fp32 (after bias / act; ldy = N, N % 32 == 0, ACC_STORE, no mask,
+  // no residual, no split-K; a consumer takes it with x_h16)
+  int y_h16 = 0;
   // WaveNet gate (commons.py:88-103) in the split-K combine: N = 2 gate_h columns; y[m][c] (c < gate_h) =
   // tanh(v[c] + g[c]) * sigmoid(v[c + gate_h] + g[c + gate_h]), v = acc + bias, g = gate_g + b * gate_g_bs. Forces a
   // split (ksplit >= 2); no other epilogue field may be set.
