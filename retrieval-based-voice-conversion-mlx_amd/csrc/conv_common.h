@@ -161,17 +161,22 @@ __device__ __forceinline__ void store_tile16(const ConvArgs& a, int m0, int n0, 
       }
       if (a.y_h16) {
         // the consumer's A operand as the two-plane fp16 image (split_bf16.h put_h16x4 of v * 2^-4): h = f16(x),
-        // l = f16((x - h) 2^11), at bytes [0, 64) and [64, 128) of the row's 32-channel chunk
+        // l = f16((x - h) 2^11), at bytes [0, 64) and [64, 128) of the row's 32-channel chunk. Lanes 2j and 2j + 1 hold
+        // columns n, n + 1: one DPP swap of the packed {h, l} halves lets the even lane store the h pair and the odd
+        // lane the l pair, one dword each (as many store instructions as the fp32 path, not two 2-byte ones each)
+        const bool odd = (lc & 1) != 0;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float xs = v[r] * (1.f / 16.f);
           const _Float16 h = (_Float16)xs;
           const _Float16 l = (_Float16)((xs - (float)h) * 2048.f);
-          _Float16* row = reinterpret_cast<_Float16*>(Y + (mb + r) * a.ldy + (n & ~31));
-          if (ok[r]) {
-            row[n & 31] = h;
-            row[32 + (n & 31)] = l;
-          }
+          const unsigned hl = (unsigned)__builtin_bit_cast(unsigned short, h) |
+                              ((unsigned)__builtin_bit_cast(unsigned short, l) << 16);
+          const unsigned pv = (unsigned)__builtin_amdgcn_mov_dpp((int)hl, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
+          const unsigned word = odd ? ((pv >> 16) | (hl & 0xffff0000u)) : ((hl & 0xffffu) | (pv << 16));
+          unsigned* dst = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(Y + (mb + r) * a.ldy + (n & ~31)) +
+                                                      (odd ? 64 : 0) + ((n & 31) & ~1) * 2);
+          if (ok[r]) *dst = word;
         }
         continue;
       }
