@@ -7,6 +7,7 @@
 #include <cstring>
 #include <string>
 #include <unistd.h>
+#include <vector>
 
 #include "runtime.h"
 
@@ -82,6 +83,31 @@ hipStream_t Ctx::aux_stream() {
   return aux;
 }
 
+hipStream_t Ctx::cu_stream(int ncu) {
+  if (aux_cu && aux_cu_n == ncu) return aux_cu;
+  if (aux_cu) {
+    RVCX_HIP(hipStreamSynchronize(aux_cu));
+    (void)hipStreamDestroy(aux_cu);
+    aux_cu = nullptr;
+  }
+  RVCX_HIP(hipSetDevice(device));
+  int ncus = 0;
+  RVCX_HIP(hipDeviceGetAttribute(&ncus, hipDeviceAttributeMultiprocessorCount, device));
+  if (ncus <= 0) ncus = 256;
+  std::vector<uint32_t> mask((size_t)(ncus + 31) / 32, 0u);
+  int taken = 0;
+  for (int i = 0; i < ncus; ++i)  // spread evenly over the CU index space (and so over the XCDs)
+    if ((long long)(i + 1) * ncu / ncus > (long long)i * ncu / ncus) {
+      mask[(size_t)i / 32] |= 1u << (i % 32);
+      ++taken;
+    }
+  if (taken == 0) mask[0] = 1u;
+  RVCX_HIP(hipExtStreamCreateWithCUMask(&aux_cu, (uint32_t)mask.size(), mask.data()));
+  if (!ev_cu_done) RVCX_HIP(hipEventCreateWithFlags(&ev_cu_done, hipEventDisableTiming));
+  aux_cu_n = ncu;
+  return aux_cu;
+}
+
 unsigned* Ctx::device_status() {
   if (!status_host) {
     RVCX_HIP(hipSetDevice(device));
@@ -116,6 +142,11 @@ Ctx::~Ctx() {
     (void)hipEventDestroy(ev_front);
     (void)hipStreamDestroy(aux);
   }
+  if (aux_cu) {
+    (void)hipStreamSynchronize(aux_cu);
+    (void)hipStreamDestroy(aux_cu);
+  }
+  if (ev_cu_done) (void)hipEventDestroy(ev_cu_done);
 }
 
 hipStream_t fork_aux(Ctx& c, hipStream_t s) {
@@ -247,7 +278,9 @@ void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double
                                (a.y_h16 && (a.ldy != a.N || a.acc_mode != ACC_STORE || a.mask || a.res))))
     throw Error(RVCX_E_SHAPE, "conv: the fp16 activation image needs the weight-streamed fp16 kernel without split-K");
   // split-K slabs are per stream: the aux stream's convs run concurrently with the caller's
-  if (need > 0) a.ws = c.buf<float>(c.aux && s == c.aux ? "conv.splitk.aux" : "conv.splitk", (size_t)need, s);
+  if (need > 0)
+    a.ws = c.buf<float>(c.aux && s == c.aux ? "conv.splitk.aux" : (c.aux_cu && s == c.aux_cu ? "conv.splitk.cu" : "conv.splitk"),
+                        (size_t)need, s);
   if (flops < 0) {
     const double M = two_d ? (double)a.T_out * a.W_out : (double)a.T_out;
     flops = 2.0 * M * a.N * (double)a.C_in * a.taps * a.batch * a.batch_inner;

@@ -138,6 +138,12 @@ struct Ctx {
   hipStream_t aux = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_gate = nullptr, ev_front = nullptr;
   hipStream_t aux_stream();
+  // a third stream restricted to ncu of the device's CUs (hipExtStreamCreateWithCUMask), for work that should leave
+  // the rest of the chip to the critical path (HuBERT's feature encoder beside the U-Net); created on first use
+  hipStream_t aux_cu = nullptr;
+  int aux_cu_n = 0;
+  hipEvent_t ev_cu_done = nullptr;
+  hipStream_t cu_stream(int ncu);
   // issued by RMVPE's E2E right before the BiGRU launch (host callback, cleared when taken)
   std::function<void(hipStream_t)> before_gru;
   // issued by RMVPE's E2E after U-Net encoder level unet_hook_level (or, if the U-Net has no such level, before the

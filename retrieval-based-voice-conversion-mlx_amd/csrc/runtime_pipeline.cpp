@@ -322,18 +322,34 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
   std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) {
     return chunks[x].a1 - chunks[x].a0 > chunks[y].a1 - chunks[y].a0;
   });
+  // HuBERT's feature encoder (and the layers before the gate) on a stream restricted to front_cus CUs, so the U-Net
+  // keeps the rest of the chip (RVCX_FRONT_CUS; 0: the aux stream, all CUs). The aux stream waits for it before the
+  // gated layers.
+  static const int front_cus = [] {
+    const char* e = rvcx_knob("RVCX_FRONT_CUS");
+    return e ? std::atoi(e) : 0;
+  }();
+  hipStream_t afront = ax;
+  if (ax != s && guided && chunks.size() == 1 && front_cus > 0) {
+    afront = c.cu_stream(front_cus);
+    RVCX_HIP(hipStreamWaitEvent(afront, c.ev_fork, 0));  // ordered after the padded input (fork_aux's event)
+  }
   auto issue_front = [&]() {
     for (size_t i : order) {
       const int64_t len = chunks[i].a1 - chunks[i].a0;
       const int64_t cap_rows = len / 320 + 8;
-      cfeats[i] = c.buf<float>("pl.hb" + std::to_string(i), (size_t)cap_rows * E, ax);
-      hruns[i] = hubert_front(c, pad32 + chunks[i].a0, len, len, 1, hubert_version_for(c), cfeats[i], cap_rows, ax);
+      cfeats[i] = c.buf<float>("pl.hb" + std::to_string(i), (size_t)cap_rows * E, afront);
+      hruns[i] = hubert_front(c, pad32 + chunks[i].a0, len, len, 1, hubert_version_for(c), cfeats[i], cap_rows, afront);
       if (chunks.size() == 1) {
-        hubert_layers(c, hruns[i], 0, split, ax);
+        hubert_layers(c, hruns[i], 0, split, afront);
       } else {  // several chunks share the HuBERT workspace: each runs to completion before the next
-        hubert_layers(c, hruns[i], 0, HUBERT_LAYERS, ax);
-        cL[i] = hubert_tail(c, hruns[i], ax);
+        hubert_layers(c, hruns[i], 0, HUBERT_LAYERS, afront);
+        cL[i] = hubert_tail(c, hruns[i], afront);
       }
+    }
+    if (afront != ax) {
+      RVCX_HIP(hipEventRecord(c.ev_cu_done, afront));
+      RVCX_HIP(hipStreamWaitEvent(ax, c.ev_cu_done, 0));
     }
   };
   struct FrontScope {
@@ -344,7 +360,7 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
     c.unet_hook_level = front_level;
     c.at_unet_level = [&](hipStream_t main) {
       RVCX_HIP(hipEventRecord(c.ev_front, main));
-      RVCX_HIP(hipStreamWaitEvent(ax, c.ev_front, 0));
+      RVCX_HIP(hipStreamWaitEvent(afront, c.ev_front, 0));
       issue_front();
     };
   } else {
