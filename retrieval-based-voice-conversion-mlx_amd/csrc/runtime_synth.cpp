@@ -494,10 +494,12 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
       }
       // c1 hands its output to c2 as the two-plane fp16 image when both run on the weight-streamed fp16 kernel: c2's
       // input has no pre-activation (c1's epilogue applies the leaky ReLU) and no other reader, so the image (the
-      // same 4 B per element) replaces the fp32 tensor and c2's halo staging is a copy instead of a split
+      // same 4 B per element) replaces the fp32 tensor and c2's halo staging is a copy instead of a split.
+      // Off by default (RVCX_PRESPLIT=1 turns it on): same-box C2 A/Bs measured it within noise of the fp32 hand-off
+      // (13.03/13.06 ms on vs 12.996/12.954 off), the epilogue's extra split costing what c2's staging saves
       static const bool presplit_on = [] {
         const char* e = rvcx_knob("RVCX_PRESPLIT");
-        return !(e && std::atoi(e) == 0);
+        return e && std::atoi(e) != 0;
       }();
       for (size_t m = 0; m < dil.size(); ++m) {
         const int d = dil[m];
