@@ -348,6 +348,14 @@ hipError_t launch_gs(const ConvArgs& a, int ntn_enable, int ksplit, hipStream_t 
 // chunk switches fall on 3-step group boundaries and the 9 unrolled taps per chunk carry no branch.
 constexpr int GSW_MAXW = 32;
 constexpr int GSW_WROWS = (64 / GSW_MAXW + 2) * (GSW_MAXW + 2);  // largest window: rh = 2 (4 x 34 = 136 pixels)
+// B ring depth of the windowed kernel (3 or 9: the ring slot of a tap is tap % depth). 9 deep issues a whole chunk's
+// weights in one burst (236 VGPRs, no spill) and was no faster in the C2 step (same-box A/B r05k: 3 deep 13.36 /
+// 13.53 / 13.38 ms against 9 deep 13.66 / 13.60 / 13.39): these launches are not waiting on the B loads
+#ifndef GSW_DEPTH
+#define GSW_DEPTH 3
+#endif
+constexpr int GSW_D = GSW_DEPTH;
+static_assert(9 % GSW_D == 0, "the ring slot of a tap is tap % GSW_D: whole chunks of 9 taps");
 
 // MODE bits 0-1 the pre-activation, bit 4 the two-plane fp16 arithmetic (as conv_gs16_kernel)
 template <int MODE>
@@ -361,6 +369,7 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gsw16_kernel(const ConvA
   constexpr bool H16 = (MODE & 16) != 0;
   constexpr int NQ = H16 ? 2 : 3;
   constexpr int RS = H16 ? ERS_H : ERS;
+  constexpr int D = H16 ? GSW_D : GS_D;  // the three-plane form (NQ = 3) keeps the 3-deep ring: 9 deep spills
   constexpr int WV = (GSW_WROWS * EC4 + NT - 1) / NT;  // float4 groups of the window per thread
   extern __shared__ __attribute__((aligned(16))) char smem_gsw[];
 
@@ -429,7 +438,7 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gsw16_kernel(const ConvA
 
   // ---- B ring (conv_gs16_kernel's)
   typedef bf16x8 BFrag[TN16][NQ];
-  BFrag br[GS_D];
+  BFrag br[D];
   const char* bp = wsp + (size_t)((n0 + wn * TN16 * 16) >> 4) * (NQ * GS_BLK) + lane * 16;
   const size_t bstep = (size_t)Npad * NQ * PLANE;
   auto load_b = [&](int st, BFrag& dst) __attribute__((always_inline)) {
@@ -486,7 +495,7 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gsw16_kernel(const ConvA
     auto clampst = [&](int st) { return st < last ? st : last; };
     load_win(c0);
 #pragma unroll
-    for (int p = 0; p < GS_D - 1; ++p) load_b(clampst(it0 + p), br[p]);
+    for (int p = 0; p < D - 1; ++p) load_b(clampst(it0 + p), br[p]);
     store_win();
     if (c0 + 1 < c1) load_win(c0 + 1);
     __syncthreads();
@@ -494,8 +503,8 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gsw16_kernel(const ConvA
       const int base = ch * 9;
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
-        const int p = tap % GS_D;  // ring slot: (step - it0) % 3 = tap % 3 (whole chunks of 9 steps)
-        load_b(clampst(base + tap + GS_D - 1), br[(p + GS_D - 1) % GS_D]);
+        const int p = tap % D;  // ring slot: (step - it0) % D = tap % D (whole chunks of 9 steps)
+        load_b(clampst(base + tap + D - 1), br[(p + D - 1) % D]);
         __builtin_amdgcn_sched_barrier(0);
         compute(tap, br[p]);
       }

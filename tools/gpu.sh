@@ -93,7 +93,7 @@ for step in "$@"; do
       for rep in 1 2 3; do
         for lib in "$arg" retrieval-based-voice-conversion-mlx_amd/rvcx/librvcx.so; do
           RVCX_LIB=$lib timeout -k 10 200 python bench.py --steps 10 --warmup 3 --no-cpu-baseline > $O/ab_$TAG.log 2>&1 || { echo "bench failed $lib"; tail -5 $O/ab_$TAG.log; exit 1; }
-          echo "$(basename $lib) $(c2line $O/ab_$TAG.log)"
+          echo "$lib $(c2line $O/ab_$TAG.log)"
         done
       done ;;
     *) echo "unknown step $name"; exit 2 ;;
