@@ -108,6 +108,26 @@ hipStream_t Ctx::cu_stream(int ncu) {
   return aux_cu;
 }
 
+// split-K arrival counters, one array per stream (the aux stream's split launches run beside the caller's): zeroed
+// once here, and every launch leaves them zero (the last slice of a tile resets its counter). Outside the workspace
+// arena, which is rewound per call
+unsigned* Ctx::splitk_counters(hipStream_t s) {
+  auto& slot = fix_counters[s];
+  if (!slot) {
+    std::unique_ptr<DevBuf> b(new DevBuf());
+    const size_t bytes = sizeof(unsigned) * (size_t)SPLITK_COUNTERS;
+    if (hipMalloc(&b->p, bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      throw Error(RVCX_E_OOM, "split-K counter allocation failed");
+    }
+    b->bytes = bytes;
+    RVCX_HIP(hipMemsetAsync(b->p, 0, bytes, s));
+    RVCX_HIP(hipStreamSynchronize(s));
+    slot = std::move(b);
+  }
+  return static_cast<unsigned*>(slot->p);
+}
+
 unsigned* Ctx::device_status() {
   if (!status_host) {
     RVCX_HIP(hipSetDevice(device));
@@ -278,9 +298,12 @@ void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double
                                (a.y_h16 && (a.ldy != a.N || a.acc_mode != ACC_STORE || a.mask || a.res))))
     throw Error(RVCX_E_SHAPE, "conv: the fp16 activation image needs the weight-streamed fp16 kernel without split-K");
   // split-K slabs are per stream: the aux stream's convs run concurrently with the caller's
-  if (need > 0)
+  if (need > 0) {
     a.ws = c.buf<float>(c.aux && s == c.aux ? "conv.splitk.aux" : (c.aux_cu && s == c.aux_cu ? "conv.splitk.cu" : "conv.splitk"),
                         (size_t)need, s);
+    a.fix_cnt = c.splitk_counters(s);  // the in-kernel combine's tile counters (the dispatcher decides per launch)
+    a.fix_cap = Ctx::SPLITK_COUNTERS;
+  }
   if (flops < 0) {
     const double M = two_d ? (double)a.T_out * a.W_out : (double)a.T_out;
     flops = 2.0 * M * a.N * (double)a.C_in * a.taps * a.batch * a.batch_inner;

@@ -947,8 +947,34 @@ const char* conv_kind_name(int k) {
 
 namespace {
 
+// RVCX_SPLITK_FIXUP=1 (A/B aid, off by default): split-K launches of the store_tile16 kernels combine in-kernel (the
+// last slice of a tile sums the write-through slabs) instead of in a separate splitk_reduce_kernel launch. Correct
+// (the whole -m gpu suite passes with it on, r05n) but not faster here: the U-Net's deep-level convs went from
+// ~10 + 5 us (conv + combine launch) to 15-19 us per conv, the last slice's write-through drain, ticket and serial
+// slab read costing what the kernel boundary did; same-box C2 13.03 / 13.07 ms on vs 12.99 / 12.98 off
+bool splitk_fixup_on() {
+  static const bool v = [] {
+    const char* e = rvcx_knob("RVCX_SPLITK_FIXUP");
+    return e && std::atoi(e) != 0;
+  }();
+  return v;
+}
+
+// whether a split launch on BM x BN tiles may combine in-kernel (store_tile16's last-arrival fix-up): the plain
+// epilogue, and one arrival counter per tile within the caller's counter array
+bool fixup_fits(const ConvArgs& a, unsigned* cnt, int BM, int BN, bool two_d) {
+  if (!cnt || !splitk_fixup_on() || a.ln_g || a.gate_h > 0 || a.batch_inner != 1) return false;
+  const long long M = two_d ? (long long)a.T_out * a.W_out : (long long)a.T_out;
+  const long long tiles = (long long)a.batch * ((M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  return tiles <= a.fix_cap;
+}
+
 template <bool TWO_D>
-hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
+hipError_t dispatch(const ConvArgs& a_in, hipStream_t s) {
+  // the counters go only to the launches whose epilogue is store_tile16 (decided per path below)
+  ConvArgs a = a_in;
+  unsigned* const fix_cnt = a.fix_cnt;
+  a.fix_cnt = nullptr;
   if (a.N <= 0 || a.T_out <= 0 || a.batch <= 0) return hipSuccess;
   if (a.C_in <= 0 || a.taps <= 0) return hipErrorInvalidValue;
   // the gate and the LayerNorm are applied by the combine
@@ -961,16 +987,24 @@ hipError_t dispatch(const ConvArgs& a, hipStream_t s) {
     const int ks = (a.ws && a.ksplit > 1) ? a.ksplit : 1;
     const int cfg = a.force_cfg >= 30 ? a.force_cfg : pick_wsb(a);
     g_conv_kind = (TWO_D && (cfg == 30 || cfg == 33) && conv_gsw_eligible(a)) ? CK_GSW : CK_GS;
-    hipError_t e = conv_gs_launch(a, cfg, xcd_enabled() ? 1 : 0, s, TWO_D, ks);
-    if (e == hipSuccess && ks > 1) e = launch_splitk_reduce(a, ks, TWO_D, s);
+    int BM = 0, BN = 0;
+    conv_gs_tile(cfg, BM, BN);
+    ConvArgs f = a;
+    if (ks > 1 && fixup_fits(a, fix_cnt, BM, BN, TWO_D)) f.fix_cnt = fix_cnt;
+    hipError_t e = conv_gs_launch(f, cfg, xcd_enabled() ? 1 : 0, s, TWO_D, ks);
+    if (e == hipSuccess && ks > 1 && !f.fix_cnt) e = launch_splitk_reduce(a, ks, TWO_D, s);
     if (e != hipErrorInvalidValue) return e;
   }
   if (a.wsb == 1 && a.wsplit && conv_math(a) >= 2 && conv_wsb_eligible(a, TWO_D)) {
     const int ks = (a.ws && a.ksplit > 1) ? a.ksplit : 1;
     const int cfg = TWO_D ? 21 : (a.force_cfg >= 20 ? a.force_cfg : pick_wsb(a));
     g_conv_kind = cfg >= 23 ? CK_WSB16 : CK_WSB;
-    hipError_t e = conv_wsb_launch(a, cfg, xcd_enabled() ? 1 : 0, s, TWO_D, ks);
-    if (e == hipSuccess && ks > 1) e = launch_splitk_reduce(a, ks, TWO_D, s);
+    int BM = 0, BN = 0;
+    conv_wsb_tile(cfg, BM, BN);
+    ConvArgs f = a;  // the fp16 kernel's epilogue is store_tile16; the three-plane one's is conv_store_tile
+    if (ks > 1 && cfg >= 23 && !TWO_D && fixup_fits(a, fix_cnt, BM, BN, TWO_D)) f.fix_cnt = fix_cnt;
+    hipError_t e = conv_wsb_launch(f, cfg, xcd_enabled() ? 1 : 0, s, TWO_D, ks);
+    if (e == hipSuccess && ks > 1 && !f.fix_cnt) e = launch_splitk_reduce(a, ks, TWO_D, s);
     if (e != hipErrorInvalidValue) return e;
   }
   // 3x3 convs with 16/32 channels: 16x16x4 MFMA fragments (conv2d_small.hip)
@@ -1056,7 +1090,8 @@ long long conv_plan_splitk(ConvArgs& a, bool two_d) {
     if (ks < 2) return 0;
     a.ksplit = ks;
     a.ws_rows = (long long)a.T_out * a.W_out;
-    return (long long)ks * a.ws_rows * a.N * a.batch * a.batch_inner;
+    // the in-kernel combine's tile-private slabs cover whole tiles (store_tile16 splitk_fixup)
+    return std::max((long long)ks * a.ws_rows * a.N * a.batch * a.batch_inner, tiles * ks * BM * BN);
   }
   const double M = two_d ? (double)a.T_out * a.W_out : (double)a.T_out;
   const double flops = 2.0 * M * a.N * (double)a.C_in * a.taps * a.batch * a.batch_inner;
@@ -1089,7 +1124,7 @@ long long conv_plan_splitk(ConvArgs& a, bool two_d) {
   if (ks < 2) return 0;
   a.ksplit = ks;
   a.ws_rows = two_d ? (long long)a.T_out * a.W_out : a.T_out;
-  return (long long)ks * a.ws_rows * a.N * a.batch * a.batch_inner;
+  return std::max((long long)ks * a.ws_rows * a.N * a.batch * a.batch_inner, tiles * ks * BM * BN);
 }
 
 bool conv_wsb_wants(const ConvArgs& a) {

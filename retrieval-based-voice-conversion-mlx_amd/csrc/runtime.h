@@ -134,6 +134,10 @@ struct Ctx {
   // pre-split images of the fused ResBlock pair kernel (resblock_fused.hip), per weight tensor
   std::map<std::pair<const void*, int>, std::unique_ptr<DevBuf>> rb_wsplit_cache;
   const void* rb_wsplit_for(const float* w, int C, int k, int wfmt, hipStream_t s);
+  // split-K tile arrival counters per stream (ConvArgs::fix_cnt), allocated and zeroed on a stream's first split launch
+  static constexpr int SPLITK_COUNTERS = 16384;
+  std::map<hipStream_t, std::unique_ptr<DevBuf>> fix_counters;
+  unsigned* splitk_counters(hipStream_t s);
   // second stream for work independent of the caller's stream (HuBERT beside RMVPE), created lazily
   hipStream_t aux = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_gate = nullptr, ev_front = nullptr;

@@ -136,6 +136,12 @@ struct ConvArgs {
   int lowp = 0;
   long long ws_rows = 0;
   float* ws = nullptr;
+  // split-K without the combine launch (round 5): one arrival counter per output tile (zero between launches). Each
+  // slice writes its partial tile with device-scope stores and counts the tile; the last slice to arrive sums the
+  // slices in slice order (splitk_reduce_kernel's arithmetic) and runs the epilogue. Set by the dispatcher only for
+  // the kernels whose epilogue is store_tile16 and the plain epilogue (no gate, no LayerNorm); fix_cap counters
+  unsigned* fix_cnt = nullptr;
+  int fix_cap = 0;
 };
 
 hipError_t conv1d(const ConvArgs& a, hipStream_t s);
