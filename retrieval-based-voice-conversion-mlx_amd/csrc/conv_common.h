@@ -66,6 +66,37 @@ static __device__ __forceinline__ void epilogue_store(const ConvArgs& a, float v
 // -> HBM or the split-K slab, with the shared epilogue (epilogue_store's order of operations, bit-identical). The
 // epilogue switches are uniform and tested once per 4-element group, each around its group-wide operation: tested
 // per element (as epilogue_store does) they cost ~25 scalar branches per output, as much as a short tile's MMA loop.
+// + the NSF noise conv (ConvArgs::nz_*) of output column n, rows mb .. mb + 3 (those with ok[r]): KK = nz_kk at
+// compile time. k_noise_add's order: an fma chain over q from 0, + bias, + v
+template <int KK>
+__device__ __forceinline__ void noise_rows(const ConvArgs& a, int b, long long mb, int n, const bool (&ok)[4],
+                                           f32x4& v) {
+  const int stride = a.nz_stride, C = a.nz_C;
+  const int p = n / C, c = n - p * C;
+  const float* hb = a.nz_har + (long long)b * a.nz_bs;
+  float wq[KK];
+  {
+    int tap = 0, j = 0;
+#pragma unroll
+    for (int q = 0; q < KK; ++q) {
+      wq[q] = a.nz_w[((long long)tap * C + c) * stride + j];
+      if (++j == stride) {
+        j = 0;
+        ++tap;
+      }
+    }
+  }
+  const float nb = a.nz_b[c];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float* x = hb + ((ok[r] ? mb + r : 0) * a.nz_u + p) * stride;
+    float acc = 0.f;
+#pragma unroll
+    for (int q = 0; q < KK; ++q) acc = fmaf(wq[q], x[q], acc);
+    v[r] = v[r] + (acc + nb);
+  }
+}
+
 // Split-K arrival (ConvArgs::fix_cnt): every thread's write-through slab stores have completed (vmcnt counts stores
 // on gfx9) before the workgroup counts its slice of the tile; true in the last slice to arrive, which resets the
 // counter for the next launch. No workgroup waits for another (nothing spins), so a slice that never runs cannot
@@ -237,6 +268,11 @@ __device__ __forceinline__ void store_tile16(const ConvArgs& a, int m0, int n0, 
       } else if (a.acc_mode == ACC_ADD_DIV) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = (dv[r] + v[r]) / a.acc_div;
+      }
+      if (a.nz_har && n_ok) {
+        // the NSF noise conv of these 4 outputs (ConvArgs::nz_*): k_noise_add's arithmetic, y + (sum + b); one
+        // tap (the last stage's stride-1 noise conv: the dispatcher admits nz_kk = 1 only)
+        noise_rows<1>(a, b, mb, n, ok, v);
       }
       if (MK) {
 #pragma unroll

@@ -977,9 +977,16 @@ hipError_t dispatch(const ConvArgs& a_in, hipStream_t s) {
   a.fix_cnt = nullptr;
   if (a.N <= 0 || a.T_out <= 0 || a.batch <= 0) return hipSuccess;
   if (a.C_in <= 0 || a.taps <= 0) return hipErrorInvalidValue;
+  // the fused noise conv lives in store_tile16's unsplit epilogue only (the caller routes it to such a kernel)
+  const bool nz = a.nz_har != nullptr;
+  if (nz && (TWO_D || (a.ws && a.ksplit > 1) || a.nz_C <= 0 || a.nz_stride <= 0 ||
+             a.nz_kk != 1 ||
+             a.N != a.nz_u * a.nz_C || a.out_map != OUT_ROWS || a.y_h16))
+    return hipErrorInvalidValue;
   // the gate and the LayerNorm are applied by the combine
   if ((a.gate_h > 0 || a.ln_g) && !(a.ws && a.ksplit > 1)) return hipErrorInvalidValue;
   if (tiny_fits(a)) {
+    if (nz) return hipErrorInvalidValue;
     g_conv_kind = CK_TINY;
     return launch_tiny(a, TWO_D, s);
   }
@@ -998,6 +1005,7 @@ hipError_t dispatch(const ConvArgs& a_in, hipStream_t s) {
   if (a.wsb == 1 && a.wsplit && conv_math(a) >= 2 && conv_wsb_eligible(a, TWO_D)) {
     const int ks = (a.ws && a.ksplit > 1) ? a.ksplit : 1;
     const int cfg = TWO_D ? 21 : (a.force_cfg >= 20 ? a.force_cfg : pick_wsb(a));
+    if (nz && cfg < 23) return hipErrorInvalidValue;
     g_conv_kind = cfg >= 23 ? CK_WSB16 : CK_WSB;
     int BM = 0, BN = 0;
     conv_wsb_tile(cfg, BM, BN);
@@ -1007,6 +1015,7 @@ hipError_t dispatch(const ConvArgs& a_in, hipStream_t s) {
     if (e == hipSuccess && ks > 1 && !f.fix_cnt) e = launch_splitk_reduce(a, ks, TWO_D, s);
     if (e != hipErrorInvalidValue) return e;
   }
+  if (nz) return hipErrorInvalidValue;  // no store_tile16 kernel took it
   // 3x3 convs with 16/32 channels: 16x16x4 MFMA fragments (conv2d_small.hip)
   if (TWO_D && a.force_cfg < 0 && small2d_enabled() && conv2d_small_fits(a)) {
     g_conv_kind = CK_SMALL2D;

@@ -416,19 +416,42 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
     a.lowp = gen_lowp;
     a.pre_act = ACT_LRELU;
     a.pre_slope = 0.1f;
-    run(c, a, s, 2.0 * B * curT * (double)Cin * C * L.k);
-    // + noise_convs[i](har) (hifigan_nsf.py:196-199), accumulated into y: short kernels (every stage after the
-    // first, <= 16 taps) by a coalesced row kernel (one pass over y), the long first-stage kernel as a framed
-    // implicit GEMM
+    // + noise_convs[i](har) (hifigan_nsf.py:196-199): the last stage's one-tap noise conv in the ConvTranspose's own
+    // epilogue where that runs on the weight-streamed fp16 kernel (ConvArgs::nz_*, k_noise_add's arithmetic:
+    // bit-identical, and y is not read back and rewritten by a second pass: 70 + 34 -> 97 us at C2); the other short
+    // kernels (<= 16 taps) by a coalesced row kernel after it, one pass over y (in the epilogue, their 4 / 8 taps of
+    // per-element loads cost more than the pass: stage 1 120 + 39 -> 173 us, stage 2 93 + 37 -> 130, r05q); the
+    // long first-stage kernel as a framed implicit GEMM
+    int stride = 1, kern = 1, npad = 0, ntap = 1;
+    std::string nn;
+    bool nz_fused = false;
     if (cf.f0) {
-      int stride = 1;
       for (size_t j = i + 1; j < cf.ups.size(); ++j) stride *= cf.ups[j];
-      const int kern = stride == 1 ? 1 : stride * 2 - stride % 2;
-      const int npad = stride == 1 ? 0 : (kern - stride) / 2;
-      const int ntap = kern == 1 ? 1 : 2;
+      kern = stride == 1 ? 1 : stride * 2 - stride % 2;
+      npad = stride == 1 ? 0 : (kern - stride) / 2;
+      ntap = kern == 1 ? 1 : 2;
       if (npad > HAR_PAD || ntap * stride - npad > HAR_PAD + stride)
         throw Error(RVCX_E_SHAPE, "noise conv stride too large for the source padding");
-      const std::string nn = "dec.noise_convs." + std::to_string(i);
+      nn = "dec.noise_convs." + std::to_string(i);
+      static const bool nz_on = [] {  // RVCX_NOISE_FUSE=0: always the separate noise launch (A/B aid)
+        const char* e = rvcx_knob("RVCX_NOISE_FUSE");
+        return !(e && std::atoi(e) == 0);
+      }();
+      const int kk = ntap * stride;
+      if (nz_on && kk == 1 && conv_routes_wsb16(c, a)) {
+        a.nz_har = har + HAR_PAD - npad;
+        a.nz_bs = har_ld;
+        a.nz_stride = stride;
+        a.nz_kk = ntap * stride;
+        a.nz_u = u;
+        a.nz_C = C;
+        a.nz_w = c.W(nn + ".wf");
+        a.nz_b = c.W(nn + ".b");
+        nz_fused = true;
+      }
+    }
+    run(c, a, s, 2.0 * B * curT * (double)Cin * C * L.k);
+    if (cf.f0 && !nz_fused) {
       if (ntap * stride <= 16 && C % 4 == 0 && (long long)B * Ti * (C / 4) < (1LL << 31) && ntap * stride * C <= 4096) {
         check(noise_conv_add(har + HAR_PAD - npad, har_ld, stride, ntap, c.W(nn + ".wf"), c.W(nn + ".b"), y, B, Ti,
                              C, s),

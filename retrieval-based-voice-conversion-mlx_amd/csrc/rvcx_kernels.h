@@ -142,6 +142,16 @@ struct ConvArgs {
   // the kernels whose epilogue is store_tile16 and the plain epilogue (no gate, no LayerNorm); fix_cap counters
   unsigned* fix_cnt = nullptr;
   int fix_cap = 0;
+  // + the NSF noise conv of this output (hifigan_nsf.py:196-199: x = ups(x) + noise_convs(har)), fused into the
+  // epilogue of the polyphase ConvTranspose (1-D, unsplit, store_tile16 kernels, plain bias epilogue; one tap,
+  // nz_kk = 1, the only length the dispatcher admits): output row m,
+  // column n = p * nz_C + c (phase p of nz_u) gets nz_b[c] + sum_q w(q, c) har[(m nz_u + p) nz_stride + q], q < nz_kk,
+  // with w(q, c) = nz_w[((q / nz_stride) nz_C + c) nz_stride + q % nz_stride] (k_noise_add's layout and fma order)
+  const float* nz_har = nullptr;
+  long long nz_bs = 0;
+  int nz_stride = 0, nz_kk = 0, nz_u = 1, nz_C = 0;
+  const float* nz_w = nullptr;
+  const float* nz_b = nullptr;
 };
 
 hipError_t conv1d(const ConvArgs& a, hipStream_t s);
