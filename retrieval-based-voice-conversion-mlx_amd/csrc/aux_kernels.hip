@@ -755,17 +755,24 @@ hipError_t reflect_pad_rows(const float* x, int rows, int C, int pad_r, float* y
                      s, x, rows, C, pad_r, y);
   return hipGetLastError();
 }
+// |STFT| rows of ldm floats: bins 0 .. nb - 1, then zeros up to ldm (the mel GEMM's contraction runs over whole
+// 32-bin chunks)
 __global__ void k_stftmag(const float* spec, int F, int nb, float* mag, int ldm) {
-  const long long n = (long long)F * nb;
+  const long long n = (long long)F * ldm;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    const int f = (int)(i / nb), k = (int)(i % nb);
-    const float re = spec[(long long)f * 2 * nb + k];
-    const float im = spec[(long long)f * 2 * nb + nb + k];
-    mag[(long long)f * ldm + k] = sqrtf(re * re + im * im);
+    const int f = (int)(i / ldm), k = (int)(i % ldm);
+    float v = 0.f;
+    if (k < nb) {
+      const float re = spec[(long long)f * 2 * nb + k];
+      const float im = spec[(long long)f * 2 * nb + nb + k];
+      v = sqrtf(re * re + im * im);
+    }
+    mag[i] = v;
   }
 }
 hipError_t stft_magnitude(const float* spec, int F, int nbins, float* mag, int ldm, hipStream_t s) {
-  hipLaunchKernelGGL(k_stftmag, dim3(nblocks((long long)F * nbins)), dim3(TB), 0, s, spec, F, nbins, mag, ldm);
+  if (ldm < nbins) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_stftmag, dim3(nblocks((long long)F * ldm)), dim3(TB), 0, s, spec, F, nbins, mag, ldm);
   return hipGetLastError();
 }
 

@@ -218,38 +218,105 @@ __device__ __forceinline__ double casc_fixed(const double* y0, const double* S, 
 }
 
 // zero-state pass of the cascade over chunk c. Input: x (read reversed when rev), or -- when S_in is set -- the
-// previous pass's final output y0_in + C A^k S_in evaluated on the fly
+// previous pass's final output y0_in + C A^k S_in evaluated on the fly (casc_fixed's arithmetic). A block of 64 lanes
+// (one chunk each) stages its 64 L consecutive inputs through LDS: read coalesced (consecutive threads, consecutive
+// samples; every load of the block in flight at once) into rows of L + 1 doubles, then each lane runs its chunk's
+// recurrence from its row and leaves the outputs in place, written back coalesced. (One lane reading its own chunk
+// from global memory waited out a load latency per sample or per batch of samples: 25-61 us per pass at C2, r05i-s.)
+constexpr int CASC_LC = 128, CASC_B = 64;  // chunk length (SosPlan::casc_L, compile-time here), chunks per block
+constexpr int CASC_LD = CASC_LC + 1;        // LDS row stride (doubles): lanes 0-31 / 32-63 each cover all banks
+constexpr int CASC_NT = 256;                // threads per block: 4 waves stage, wave 0 runs the 64 recurrences
 template <int NSEC>
-__global__ void k_casc_local(const double* __restrict__ x, const double* __restrict__ S_in, long long n, int rev,
-                             const double* __restrict__ tab, int L, double* __restrict__ y0, double* __restrict__ e) {
-  constexpr int NS = 2 * NSEC;
-  const long long c = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(CASC_NT) void k_casc_local(const double* __restrict__ x, const double* __restrict__ S_in,
+                                                        long long n, int rev, const double* __restrict__ tab,
+                                                        double* __restrict__ y0, double* __restrict__ e) {
+  constexpr int NS = 2 * NSEC, L = CASC_LC;
+  extern __shared__ double smem_casc[];  // rows [CASC_B][CASC_LD], the C A^k rows [L][NS], the input states [65][NS]
+  double* rows = smem_casc;
+  double* ca_s = rows + CASC_B * CASC_LD;
+  double* s_s = ca_s + L * NS;
+  const int tid = threadIdx.x;
   const long long nch = (n + L - 1) / L;
-  if (c >= nch) return;
-  double b0[NSEC], b1[NSEC], b2[NSEC], a1[NSEC], a2[NSEC], z0[NSEC], z1[NSEC];
-#pragma unroll
-  for (int j = 0; j < NSEC; ++j) {
-    b0[j] = tab[5 * j], b1[j] = tab[5 * j + 1], b2[j] = tab[5 * j + 2], a1[j] = tab[5 * j + 3], a2[j] = tab[5 * j + 4];
-    z0[j] = z1[j] = 0.0;
+  const long long tb0 = (long long)blockIdx.x * CASC_B * L;  // the block's first sample (processing order)
+  const int cnt = (int)min((long long)CASC_B * L, n - tb0);  // samples of the block
+  // the previous pass's chunks the block's samples come from: ti in [ta, tb], chunks ci0 .. ci0 + 64 at most
+  const long long ta = rev ? n - 1 - (tb0 + cnt - 1) : tb0;
+  const long long ci0 = ta / L;
+  if (S_in) {
+    for (int i = tid; i < L * NS; i += CASC_NT) {
+      const int k = i / NS, q = i - k * NS;
+      ca_s[i] = tab[CASC_CA + 8 * k + q];
+    }
+    const long long nci = min((long long)CASC_B + 1, nch - ci0);
+    for (int i = tid; i < nci * NS; i += CASC_NT) s_s[i] = S_in[NS * ci0 + i];
   }
-  const long long t0 = c * L, t1 = min(n, t0 + L);
-  for (long long t = t0; t < t1; ++t) {
+  __syncthreads();
+  auto input = [&](long long t) -> double {
     const long long ti = rev ? n - 1 - t : t;
-    double u = S_in ? casc_fixed<NS>(x, S_in, tab, L, ti) : x[ti];
+    if (!S_in) return x[ti];
+    const long long ci = ti / L;
+    const int k = (int)(ti - ci * L);
+    const double* sv = s_s + (ci - ci0) * NS;
+    double v = x[ti];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) v = fma(ca_s[k * NS + i], sv[i], v);
+    return v;
+  };
+  // staging: element i of the block (row i / L, column i % L); 16 loads per thread in flight per group
+  for (int i0 = 0; i0 < cnt; i0 += 16 * CASC_NT) {
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int i = i0 + u * CASC_NT + tid;
+      v[u] = i < cnt ? input(tb0 + i) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int i = i0 + u * CASC_NT + tid;
+      if (i < cnt) rows[(i / L) * CASC_LD + (i % L)] = v[u];
+    }
+  }
+  __syncthreads();
+  const long long c = (long long)blockIdx.x * CASC_B + tid;
+  if (tid < CASC_B && c < nch) {
+    double b0[NSEC], b1[NSEC], b2[NSEC], a1[NSEC], a2[NSEC], z0[NSEC], z1[NSEC];
 #pragma unroll
     for (int j = 0; j < NSEC; ++j) {
-      const double y = b0[j] * u + z0[j];
-      z0[j] = b1[j] * u - a1[j] * y + z1[j];
-      z1[j] = b2[j] * u - a2[j] * y;
-      u = y;
+      b0[j] = tab[5 * j], b1[j] = tab[5 * j + 1], b2[j] = tab[5 * j + 2], a1[j] = tab[5 * j + 3],
+      a2[j] = tab[5 * j + 4];
+      z0[j] = z1[j] = 0.0;
     }
-    y0[t] = u;
-  }
+    double* row = rows + tid * CASC_LD;
+    const int len = (int)min((long long)L, n - c * L);
+    auto step = [&](double u) -> double {
 #pragma unroll
-  for (int j = 0; j < NSEC; ++j) {
-    e[NS * c + 2 * j] = z0[j];
-    e[NS * c + 2 * j + 1] = z1[j];
+      for (int j = 0; j < NSEC; ++j) {
+        const double y = b0[j] * u + z0[j];
+        z0[j] = b1[j] * u - a1[j] * y + z1[j];
+        z1[j] = b2[j] * u - a2[j] * y;
+        u = y;
+      }
+      return u;
+    };
+    int t = 0;
+    for (; t + 16 <= len; t += 16) {  // 16 inputs read ahead of their dependent chain, outputs written in place
+      double u[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) u[k] = row[t + k];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) u[k] = step(u[k]);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) row[t + k] = u[k];
+    }
+    for (; t < len; ++t) row[t] = step(row[t]);
+#pragma unroll
+    for (int j = 0; j < NSEC; ++j) {
+      e[NS * c + 2 * j] = z0[j];
+      e[NS * c + 2 * j + 1] = z1[j];
+    }
   }
+  __syncthreads();
+  for (int i = tid; i < cnt; i += CASC_NT) y0[tb0 + i] = rows[(i / L) * CASC_LD + (i % L)];
 }
 
 // chunk start states S_0 = w x0, S_{c+1} = A^L S_c + e_c (k_sos_carry's segmented Hillis-Steele scan on NS-vectors).
@@ -261,7 +328,9 @@ __global__ void __launch_bounds__(SCAN_T) k_casc_carry(const double* __restrict_
                                                        double* __restrict__ S) {
   __shared__ double v[NS][SCAN_T];
   __shared__ double seg[NS];
+  __shared__ double pw_s[12 * 64];  // the A^(L 2^s) tables: read by every level (from global: one L2 round trip each)
   const int t = threadIdx.x;
+  for (int i = t; i < 12 * 64; i += SCAN_T) pw_s[i] = tab[CASC_POW + i];
   if (t == 0) {
     const long long i0 = rev ? n - 1 : 0;
     const double x0 = S_in ? casc_fixed<NS>(x, S_in, tab, L, i0) : x[i0];
@@ -278,13 +347,26 @@ __global__ void __launch_bounds__(SCAN_T) k_casc_carry(const double* __restrict_
     double a[NS];
 #pragma unroll
     for (int i = 0; i < NS; ++i) a[i] = act ? e[NS * c + i] : 0.0;
+    if (t == 0) {
+      // S_{c0+1} = A^L S_c0 + e_c0: the segment's start state enters through its first element, so the inclusive
+      // scan below yields every S_{c+1} = A^(L (t+1)) S_c0 + sum_j A^(L (t-j)) e_(c0+j) directly (one 6x6 product
+      // instead of a binary power of up to 11 per thread)
+      const double* M = pw_s;
+#pragma unroll
+      for (int r = 0; r < NS; ++r) {
+        double acc = a[r];
+#pragma unroll
+        for (int q = 0; q < NS; ++q) acc = fma(M[8 * r + q], seg[q], acc);
+        a[r] = acc;
+      }
+    }
     for (int sidx = 0; (1 << sidx) < SCAN_T; ++sidx) {
 #pragma unroll
       for (int i = 0; i < NS; ++i) v[i][t] = a[i];
       __syncthreads();
       const int d = 1 << sidx;
       if (t >= d) {
-        const double* M = tab + CASC_POW + 64 * sidx;
+        const double* M = pw_s + 64 * sidx;
         double u[NS];
 #pragma unroll
         for (int i = 0; i < NS; ++i) u[i] = v[i][t - d];
@@ -298,28 +380,6 @@ __global__ void __launch_bounds__(SCAN_T) k_casc_carry(const double* __restrict_
       }
       __syncthreads();
     }
-    // + A^{L (t+1)} S_seg
-    double sv[NS];
-#pragma unroll
-    for (int i = 0; i < NS; ++i) sv[i] = seg[i];
-    const int pw = t + 1;
-    for (int sidx = 0; (1 << sidx) <= pw; ++sidx) {
-      if (pw & (1 << sidx)) {
-        const double* M = tab + CASC_POW + 64 * sidx;
-        double r[NS];
-#pragma unroll
-        for (int rr = 0; rr < NS; ++rr) {
-          double acc = 0.0;
-#pragma unroll
-          for (int q = 0; q < NS; ++q) acc = fma(M[8 * rr + q], sv[q], acc);
-          r[rr] = acc;
-        }
-#pragma unroll
-        for (int i = 0; i < NS; ++i) sv[i] = r[i];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < NS; ++i) a[i] += sv[i];
     if (act) {
 #pragma unroll
       for (int i = 0; i < NS; ++i) S[NS * (c + 1) + i] = a[i];
@@ -356,17 +416,26 @@ hipError_t casc_filtfilt(const SosPlan& p, const double* ext, long long ne, int 
                          double* ws, double* pad64, float* pad32, hipStream_t s) {
   constexpr int NS = 2 * NSEC;
   const int L = p.casc_L;
+  if (L != CASC_LC) return hipErrorInvalidValue;  // k_casc_local's compile-time chunk length
   const long long nch = (ne + L - 1) / L;
   double* y0f = ws;
   double* y0b = y0f + ne;
   double* e = y0b + ne;
   double* Sf = e + NS * nch;
   double* Sb = Sf + NS * nch;
-  const unsigned g = (unsigned)((nch + 63) / 64);
-  hipLaunchKernelGGL(k_casc_local<NSEC>, dim3(g), dim3(64), 0, s, ext, nullptr, ne, 0, p.casc, L, y0f, e);
+  const unsigned g = (unsigned)((nch + CASC_B - 1) / CASC_B);
+  const size_t lds = sizeof(double) * ((size_t)CASC_B * CASC_LD + (size_t)CASC_LC * NS + (size_t)(CASC_B + 1) * NS);
+  static bool lds_set = false;  // per instantiation: allow the ~72 KB of dynamic LDS once
+  if (!lds_set) {
+    hipError_t er = hipFuncSetAttribute(reinterpret_cast<const void*>(k_casc_local<NSEC>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (er != hipSuccess) return er;
+    lds_set = true;
+  }
+  hipLaunchKernelGGL(k_casc_local<NSEC>, dim3(g), dim3(CASC_NT), lds, s, ext, nullptr, ne, 0, p.casc, y0f, e);
   hipLaunchKernelGGL(k_casc_carry<NS>, dim3(1), dim3(SCAN_T), 0, s, e, nch, p.casc, ext, nullptr, ne, L, 0, Sf);
   // backward over the reversed forward output (y0f fixed up with Sf on the fly)
-  hipLaunchKernelGGL(k_casc_local<NSEC>, dim3(g), dim3(64), 0, s, y0f, Sf, ne, 1, p.casc, L, y0b, e);
+  hipLaunchKernelGGL(k_casc_local<NSEC>, dim3(g), dim3(CASC_NT), lds, s, y0f, Sf, ne, 1, p.casc, y0b, e);
   hipLaunchKernelGGL(k_casc_carry<NS>, dim3(1), dim3(SCAN_T), 0, s, e, nch, p.casc, y0f, Sf, ne, L, 1, Sb);
   const long long m = n + 2 * t_pad;
   const unsigned gb = (unsigned)std::min<long long>((m + 255) / 256, 4096);

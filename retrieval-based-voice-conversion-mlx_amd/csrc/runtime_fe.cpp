@@ -324,6 +324,9 @@ int64_t hubert_forward(Ctx& c, const float* audio, int64_t n, int version, float
 namespace {
 
 constexpr int NMEL = 128, NFFT = 1024, HOP = 160, NBIN = NFFT / 2 + 1, NCLS = 360;
+// the mel projection's contraction padded to whole 32-bin chunks (zero magnitudes x zero weights): K = 513 kept it off
+// the streamed fp16 kernels (the three-plane LDS kernel + a split-K combine: 60 + 16 us at C2, r05i)
+constexpr int NBIN_P = 544;
 constexpr int LEVELS = 5, INTER = 4, NBLK = 4, C_BASE = 16, GRU_H = 256;
 
 // librosa.filters.mel(sr=16000, n_fft=1024, n_mels=128, fmin=30, fmax=8000, htk=True, norm='slaney')
@@ -335,7 +338,7 @@ std::vector<float> mel_basis() {
   const double step = (hi - lo) / (n - 1);
   std::vector<double> mel_f(n);
   for (int i = 0; i < n; ++i) mel_f[i] = mel2hz(i == n - 1 ? hi : lo + i * step);
-  std::vector<float> w((size_t)NMEL * NBIN, 0.f);
+  std::vector<float> w((size_t)NMEL * NBIN_P, 0.f);  // [mel][bin], rows of NBIN_P (bins >= NBIN zero)
   for (int i = 0; i < NMEL; ++i) {
     const double fd0 = mel_f[i + 1] - mel_f[i], fd1 = mel_f[i + 2] - mel_f[i + 1];
     const double enorm = 2.0 / (mel_f[i + 2] - mel_f[i]);
@@ -344,7 +347,7 @@ std::vector<float> mel_basis() {
       const double lower = -(mel_f[i] - f) / fd0;
       const double upper = (mel_f[i + 2] - f) / fd1;
       const float tri = (float)std::max(0.0, std::min(lower, upper));
-      w[(size_t)i * NBIN + k] = (float)((double)tri * enorm);
+      w[(size_t)i * NBIN_P + k] = (float)((double)tri * enorm);
     }
   }
   return w;
@@ -718,12 +721,12 @@ int64_t rmvpe_forward_b(Ctx& c, const float* audio, int64_t n, int64_t lda, int 
     a.y_bs = (long long)F * 2 * NBIN;
     run1(c, a, s, 0.0);
   }
-  const int ldm = 516;
+  const int ldm = NBIN_P;
   float* mag = c.buf<float>("rm.mag", (size_t)B * F * ldm, s);
   check(stft_magnitude(spec, B * F, NBIN, mag, ldm, s), "stft_mag");
   float* mel = c.buf<float>("rm.melout", (size_t)B * F * NMEL, s);
   {
-    ConvArgs a = lin(mag, ldm, B * F, NBIN, c.W("rm.mel"), NMEL, nullptr, mel, NMEL);
+    ConvArgs a = lin(mag, ldm, B * F, NBIN_P, c.W("rm.mel"), NMEL, nullptr, mel, NMEL);
     a.act = ACT_LOGCLAMP;
     a.slope = 1e-5f;
     run1(c, a, s);
