@@ -193,3 +193,51 @@ def test_unet_deep_level_windowed_kernels(engine, H, W, C, N):
     assert errs["f32"] < 1e-6, errs
     for k in ("gsw", "gswk"):
         assert errs[k] < 1e-6 and errs[k] <= 4.0 * errs["f32"] + 1e-8, errs
+
+
+_FIXUP_CHILD = r"""
+import sys
+import numpy as np
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+from rvcx.engine import Engine
+d = np.load(sys.argv[3])
+e = Engine(0)
+out = {}
+for i in range(int(d["n"])):
+    for mode in ("gsw", "gswk"):
+        out[f"{mode}{i}"] = e.conv2d3x3(d[f"x{i}"], d[f"w{i}"], d[f"b{i}"], relu=True, math=mode).cpu().numpy()
+e.close()
+np.savez(sys.argv[4], **out)
+"""
+
+
+def test_splitk_in_kernel_combine_is_bit_identical(engine, tmp_path):
+    """The opt-in in-kernel split-K combine (RVCX_SPLITK_FIXUP=1: the last slice of a tile to arrive sums the
+    write-through slabs, conv_common.h splitk_fixup) against the default combine launch, on the U-Net's split deep
+    levels with both windowed kernels: bit-identical (same slice order, same epilogue). The knob is read once per
+    process, so the in-kernel side runs in a child process."""
+    import os
+    import subprocess
+    import sys
+
+    from conftest import PKG, REPO
+
+    shapes = DEEP2D[:4]
+    inp, ref = {"n": np.array(len(shapes))}, {}
+    for i, (H, W, C, N) in enumerate(shapes):
+        rng = np.random.Generator(np.random.PCG64(1000 + i))
+        inp[f"x{i}"] = rng.standard_normal((H, W, C)).astype(np.float32)
+        inp[f"w{i}"] = (rng.standard_normal((N, C, 3, 3)) / np.sqrt(9 * C)).astype(np.float32)
+        inp[f"b{i}"] = rng.standard_normal(N).astype(np.float32)
+        for mode in ("gsw", "gswk"):
+            ref[f"{mode}{i}"] = engine.conv2d3x3(inp[f"x{i}"], inp[f"w{i}"], inp[f"b{i}"], relu=True,
+                                                 math=mode).cpu().numpy()
+    src, dst = str(tmp_path / "in.npz"), str(tmp_path / "out.npz")
+    np.savez(src, **inp)
+    env = dict(os.environ, RVCX_EXPERIMENTAL="1", RVCX_SPLITK_FIXUP="1")
+    r = subprocess.run([sys.executable, "-c", _FIXUP_CHILD, PKG, REPO, src, dst], env=env, capture_output=True,
+                       text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = np.load(dst)
+    for k, v in ref.items():
+        assert np.array_equal(out[k], v), (k, float(np.max(np.abs(out[k] - v))))
