@@ -298,6 +298,17 @@ void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double
                                (a.y_h16 && (a.ldy != a.N || a.acc_mode != ACC_STORE || a.mask || a.res))))
     throw Error(RVCX_E_SHAPE, "conv: the fp16 activation image needs the weight-streamed fp16 kernel without split-K");
   // split-K slabs are per stream: the aux stream's convs run concurrently with the caller's
+  // HuBERT's feature-encoder contractions (issued on the aux stream beside the U-Net, with ~1.5 ms of slack before the
+  // BiGRU) take 64 KB more LDS per workgroup: one or two of them per CU at most, so the U-Net's latency-bound chain
+  // finds free workgroup slots instead of waiting out ~50 us feature-conv workgroups. Same-box A/B (ms/step): r05ac
+  // none 13.53 / 13.47, 64 KB 13.28 / 13.35, 88 KB 13.25 / 13.27, 40 KB 13.39 / 13.51; r05ae none 13.53 / 13.54 /
+  // 13.48 / 13.51, 64 KB 13.39 / 13.16 / 13.37 / 13.33, 88 KB 13.48 / 13.29. Throttling HuBERT's transformer too
+  // (r05aa) costs +0.3-0.5 ms: it runs beside the BiGRU with little slack. RVCX_AUX_LDS=KB overrides (0: off)
+  static const int aux_lds = [] {
+    const char* e = rvcx_knob("RVCX_AUX_LDS");
+    return e ? std::max(0, std::atoi(e)) : 64;
+  }();
+  if (aux_lds > 0 && c.aux_front) a.lds_pad = aux_lds * 1024;
   if (need > 0) {
     a.ws = c.buf<float>(c.aux && s == c.aux ? "conv.splitk.aux" : (c.aux_cu && s == c.aux_cu ? "conv.splitk.cu" : "conv.splitk"),
                         (size_t)need, s);

@@ -472,6 +472,7 @@ hipError_t launch_emu(const ConvArgs& a, int ksplit, int ntn_enable, hipStream_t
   size_t smem = (size_t)(PIPE ? 2 * (BM + BN) : nrows_a + 2 * BN) * ERS;
   smem = std::max(smem, (size_t)4 * 32 * 33 * sizeof(float));  // epilogue staging slots
   if (smem > 160 * 1024) return hipErrorInvalidValue;
+  smem = std::min(smem + (size_t)std::max(0, a.lds_pad), (size_t)160 * 1024);  // occupancy throttle, clamped
   const int vec_a = ((a.ldx & 3) == 0) && ((reinterpret_cast<uintptr_t>(a.x) & 15) == 0) && ((a.x_bs & 3) == 0) &&
                     ((a.x_bs2 & 3) == 0);
   const int vec_b = ((a.ldw & 3) == 0) && ((reinterpret_cast<uintptr_t>(a.w) & 15) == 0) && ((a.w_bs & 3) == 0) &&

@@ -296,6 +296,12 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gs16_kernel(const ConvAr
 
 template <int BM, int BN, int WM, int WN, bool TWO_D, int MODE>
 void launch_gs_mode(const ConvArgs& a, dim3 grid, size_t smem, int ntn, int ksplit, int mfast, hipStream_t s) {
+  static size_t smem_set = 64 * 1024;  // per instantiation: raise the dynamic-LDS limit once (ConvArgs::lds_pad)
+  if (smem > smem_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv_gs16_kernel<BM, BN, WM, WN, TWO_D, MODE>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    smem_set = smem;
+  }
   hipLaunchKernelGGL((conv_gs16_kernel<BM, BN, WM, WN, TWO_D, MODE>), grid, dim3(CONV_THREADS), smem, s, a,
                      static_cast<const char*>(a.wsplit), a.wsplit_npad, ntn, ksplit, mfast);
 }
@@ -309,7 +315,9 @@ hipError_t launch_gs(const ConvArgs& a, int ntn_enable, int ksplit, hipStream_t 
   const int ntn = ntn_enable ? ntiles : 0;
   dim3 grid((unsigned)(ntn ? mtiles * ntiles : mtiles), ntn ? 1 : ntiles, a.batch * ksplit);
   const bool h16 = a.wsplit_fmt == WSPLIT_H16;
-  const size_t smem = (size_t)2 * BM * (h16 ? ERS_H : ERS);
+  // the throttle pad (ConvArgs::lds_pad) is clamped to the CU's 160 KB: above 80 KB it means one workgroup per CU
+  const size_t smem = std::min((size_t)2 * BM * (h16 ? ERS_H : ERS) + (size_t)std::max(0, a.lds_pad),
+                               std::max((size_t)2 * BM * (h16 ? ERS_H : ERS), (size_t)160 * 1024));
   // M-fastest tile runs when the pre-split weight (6 B per element) outweighs the activation operand (4 B)
   static const int mf_env = [] {
     const char* e = rvcx_knob("RVCX_GS_MFAST");

@@ -134,6 +134,9 @@ struct Ctx {
   // pre-split images of the fused ResBlock pair kernel (resblock_fused.hip), per weight tensor
   std::map<std::pair<const void*, int>, std::unique_ptr<DevBuf>> rb_wsplit_cache;
   const void* rb_wsplit_for(const float* w, int C, int k, int wfmt, hipStream_t s);
+  // set while HuBERT's feature encoder is being issued (runtime_pipeline.cpp issue_front): the launches RVCX_AUX_LDS
+  // throttles
+  bool aux_front = false;
   // split-K tile arrival counters per stream (ConvArgs::fix_cnt), allocated and zeroed on a stream's first split launch
   static constexpr int SPLITK_COUNTERS = 16384;
   std::map<hipStream_t, std::unique_ptr<DevBuf>> fix_counters;

@@ -335,6 +335,7 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
     RVCX_HIP(hipStreamWaitEvent(afront, c.ev_fork, 0));  // ordered after the padded input (fork_aux's event)
   }
   auto issue_front = [&]() {
+    c.aux_front = afront != s;  // reset below and by FrontScope (an exception mid-issue)
     for (size_t i : order) {
       const int64_t len = chunks[i].a1 - chunks[i].a0;
       const int64_t cap_rows = len / 320 + 8;
@@ -347,6 +348,7 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
         cL[i] = hubert_tail(c, hruns[i], afront);
       }
     }
+    c.aux_front = false;
     if (afront != ax) {
       RVCX_HIP(hipEventRecord(c.ev_cu_done, afront));
       RVCX_HIP(hipStreamWaitEvent(ax, c.ev_cu_done, 0));
@@ -354,7 +356,11 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
   };
   struct FrontScope {
     Ctx& c;
-    ~FrontScope() { c.at_unet_level = nullptr; c.unet_hook_level = -1; }
+    ~FrontScope() {
+      c.at_unet_level = nullptr;
+      c.unet_hook_level = -1;
+      c.aux_front = false;
+    }
   } front_scope{c};
   if (delay_front) {
     c.unet_hook_level = front_level;

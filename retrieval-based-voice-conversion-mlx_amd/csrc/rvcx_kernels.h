@@ -152,6 +152,9 @@ struct ConvArgs {
   int nz_stride = 0, nz_kk = 0, nz_u = 1, nz_C = 0;
   const float* nz_w = nullptr;
   const float* nz_b = nullptr;
+  // extra dynamic LDS per workgroup (bytes): fewer of this launch's workgroups fit a CU beside the critical stream's
+  // (an occupancy throttle for off-critical-path work; the gather-streamed and LDS-staged kernels honour it)
+  int lds_pad = 0;
 };
 
 hipError_t conv1d(const ConvArgs& a, hipStream_t s);
