@@ -134,6 +134,9 @@ struct Ctx {
   // pre-split images of the fused ResBlock pair kernel (resblock_fused.hip), per weight tensor
   std::map<std::pair<const void*, int>, std::unique_ptr<DevBuf>> rb_wsplit_cache;
   const void* rb_wsplit_for(const float* w, int C, int k, int wfmt, hipStream_t s);
+  // set by the internal callers of synth_forward whose every row has the full length T (the pipeline, its batched form,
+  // the streaming hop): the TextEncoder's attention then runs without the all-ones key mask (ScopedFullLengths)
+  bool synth_full_lengths = false;
   // set while HuBERT's feature encoder is being issued (runtime_pipeline.cpp issue_front): the launches RVCX_AUX_LDS
   // throttles
   bool aux_front = false;
@@ -357,6 +360,12 @@ hipStream_t fork_aux(Ctx& c, hipStream_t s);
 // whether launch_conv would run this 1-D contraction on the weight-streamed fp16 kernel without split-K (the only
 // producer / consumer of the two-plane fp16 activation image, ConvArgs::y_h16 / x_h16)
 bool conv_routes_wsb16(Ctx& c, const ConvArgs& a);
+// marks a synth_forward call whose rows all have the full length T (Ctx::synth_full_lengths) for its lifetime
+struct ScopedFullLengths {
+  Ctx& c;
+  explicit ScopedFullLengths(Ctx& cc) : c(cc) { c.synth_full_lengths = true; }
+  ~ScopedFullLengths() { c.synth_full_lengths = false; }
+};
 void join_aux(Ctx& c, hipStream_t s, hipStream_t ax);
 // launch one implicit-GEMM conv (1-D or 2-D) with optional event timing; flops = algorithmic FLOPs
 void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double flops = -1.0);

@@ -189,7 +189,10 @@ int64_t vc_forward(Ctx& c, const float* audio, int64_t n, const int32_t* pitch, 
   int32_t* lens = c.buf<int32_t>("vc.len", 4, s);
   set_i32_once(c, "vc.len.T", lens, T, s);
   set_i32_once(c, "vc.len.sid", lens + 1, sid, s);
-  synth_forward(c, 1, T, phone, lens, pitch, pitchf, lens + 1, eps_z, eps_src, seed, out, nullptr, nullptr, s);
+  {
+    ScopedFullLengths full(c);
+    synth_forward(c, 1, T, phone, lens, pitch, pitchf, lens + 1, eps_z, eps_src, seed, out, nullptr, nullptr, s);
+  }
   return (int64_t)T * upp;
 }
 
@@ -611,7 +614,10 @@ int64_t pipeline_forward_batch(Ctx& c, const double* audio, int64_t n, int64_t l
   RVCX_HIP(hipMemcpyAsync(meta, hm.data(), sizeof(int32_t) * hm.size(), hipMemcpyHostToDevice, s));
   const int64_t nvc = Tv * upp;
   float* vc = c.buf<float>("pb.vc", (size_t)B * nvc, s);
-  synth_forward(c, B, (int)Tv, phone, meta, pc, pf, meta + B, eps_z, eps_src, seed, vc, nullptr, nullptr, s);
+  {
+    ScopedFullLengths full(c);  // every row Tv long (hm above)
+    synth_forward(c, B, (int)Tv, phone, meta, pc, pf, meta + B, eps_z, eps_src, seed, vc, nullptr, nullptr, s);
+  }
   // 5. trim, volume envelope, peak normalisation per utterance (pipeline.py:545-552)
   const int64_t keep = nvc - 2 * o.t_pad_tgt;
   if (keep <= 0) throw Error(RVCX_E_SHAPE, "pipeline_batch: utterance too short for the padding");

@@ -284,8 +284,11 @@ void rt_process(Ctx& c, RtState& s, const float* in48, const int32_t* sids, cons
   RVCX_HIP(hipMemcpyAsync(dmeta, meta.data(), sizeof(int32_t) * meta.size(), hipMemcpyHostToDevice, st));
   const int64_t n_model = (int64_t)T * upp;
   float* model = c.buf<float>("rt.model", (size_t)B * n_model, st);
-  synth_forward(c, B, T, phone, dmeta, guided ? pitch : nullptr, guided ? pitchf : nullptr, dmeta + B, eps_z, eps_src,
-                seed, model, nullptr, nullptr, st, o.gen_precision);
+  {
+    ScopedFullLengths full(c);  // every stream's hop is T frames (meta above)
+    synth_forward(c, B, T, phone, dmeta, guided ? pitch : nullptr, guided ? pitchf : nullptr, dmeta + B, eps_z,
+                  eps_src, seed, model, nullptr, nullptr, st, o.gen_precision);
+  }
   (void)I;
   check(rt_clip(model, n_model, (int)n_model, B, st), "rt_clip");
   if (o.volume_envelope != 1.0) {  // pipeline.py:299-307 (source = the 16 kHz convert buffer)

@@ -613,7 +613,10 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
     const std::string q = "te." + std::to_string(i);
     run(c, lin(x, H, (int)BT, H, c.W(q + ".qkv.w"), 3 * H, c.W(q + ".qkv.b"), qkv, 3 * H), s);
     if (fused) {  // attentions.py:79-185 in one pass per query block (flash_attn.hip): no [B][nh][T][T] scores
-      check(flash_attn(qkv, 3 * H, B, T, nh, dk, qscale, c.W(q + ".rel_k"), c.W(q + ".rel_v"), cf.window, mask, part_o,
+      // the key mask only where a row is shorter than T: with every length T it is all ones, and its per-element loads
+      // in the key loop cost the TextEncoder's attention ~1/3 of its time (the fill never fires: identical results)
+      check(flash_attn(qkv, 3 * H, B, T, nh, dk, qscale, c.W(q + ".rel_k"), c.W(q + ".rel_v"), cf.window,
+                       c.synth_full_lengths ? nullptr : mask, part_o,
                        part_ml, nsplit, att, H, s),
             "flash_attn");
     } else {
