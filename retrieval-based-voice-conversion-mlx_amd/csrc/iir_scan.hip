@@ -232,6 +232,8 @@ __global__ __launch_bounds__(CASC_NT) void k_casc_local(const double* __restrict
                                                         double* __restrict__ y0, double* __restrict__ e) {
   constexpr int NS = 2 * NSEC, L = CASC_LC;
   extern __shared__ double smem_casc[];  // rows [CASC_B][CASC_LD], the C A^k rows [L][NS], the input states [65][NS]
+  __shared__ double wsc[NS][CASC_B];     // the block scan of the chunk end states
+  __shared__ double pw6[6 * 64];         // A^(L 2^s), s < 6, for that scan
   double* rows = smem_casc;
   double* ca_s = rows + CASC_B * CASC_LD;
   double* s_s = ca_s + L * NS;
@@ -242,6 +244,7 @@ __global__ __launch_bounds__(CASC_NT) void k_casc_local(const double* __restrict
   // the previous pass's chunks the block's samples come from: ti in [ta, tb], chunks ci0 .. ci0 + 64 at most
   const long long ta = rev ? n - 1 - (tb0 + cnt - 1) : tb0;
   const long long ci0 = ta / L;
+  for (int i = tid; i < 6 * 64; i += CASC_NT) pw6[i] = tab[CASC_POW + i];
   if (S_in) {
     for (int i = tid; i < L * NS; i += CASC_NT) {
       const int k = i / NS, q = i - k * NS;
@@ -311,65 +314,30 @@ __global__ __launch_bounds__(CASC_NT) void k_casc_local(const double* __restrict
     for (; t < len; ++t) row[t] = step(row[t]);
 #pragma unroll
     for (int j = 0; j < NSEC; ++j) {
-      e[NS * c + 2 * j] = z0[j];
-      e[NS * c + 2 * j + 1] = z1[j];
+      wsc[2 * j][tid] = z0[j];
+      wsc[2 * j + 1][tid] = z1[j];
     }
-  }
-  __syncthreads();
-  for (int i = tid; i < cnt; i += CASC_NT) y0[tb0 + i] = rows[(i / L) * CASC_LD + (i % L)];
-}
-
-// chunk start states S_0 = w x0, S_{c+1} = A^L S_c + e_c (k_sos_carry's segmented Hillis-Steele scan on NS-vectors).
-// x0 = the pass input's first sample: x[0] / x[n - 1] (rev), or the previous pass's output there (S_in set).
-template <int NS>
-__global__ void __launch_bounds__(SCAN_T) k_casc_carry(const double* __restrict__ e, long long nch,
-                                                       const double* __restrict__ tab, const double* __restrict__ x,
-                                                       const double* __restrict__ S_in, long long n, int L, int rev,
-                                                       double* __restrict__ S) {
-  __shared__ double v[NS][SCAN_T];
-  __shared__ double seg[NS];
-  __shared__ double pw_s[12 * 64];  // the A^(L 2^s) tables: read by every level (from global: one L2 round trip each)
-  const int t = threadIdx.x;
-  for (int i = t; i < 12 * 64; i += SCAN_T) pw_s[i] = tab[CASC_POW + i];
-  if (t == 0) {
-    const long long i0 = rev ? n - 1 : 0;
-    const double x0 = S_in ? casc_fixed<NS>(x, S_in, tab, L, i0) : x[i0];
+  } else if (tid < CASC_B) {
 #pragma unroll
-    for (int i = 0; i < NS; ++i) {
-      seg[i] = tab[CASC_W + i] * x0;
-      S[i] = seg[i];
-    }
+    for (int i = 0; i < NS; ++i) wsc[i][tid] = 0.0;
   }
-  __syncthreads();
-  for (long long c0 = 0; c0 + 1 < nch; c0 += SCAN_T) {
-    const long long c = c0 + t;  // this thread produces S_{c+1} from e_c
-    const bool act = c + 1 < nch;
+  // the block's chunk end states e_k (zero past the last chunk) -> W_k = sum_{j <= k} A^(L (k - j)) e_j, the end state
+  // of chunk k when the block starts from a zero state: a Hillis-Steele scan over the 64 chunk lanes of wave 0 with
+  // the A^(L 2^s) tables (k_casc_carry then adds the block's start state)
+  if (tid < CASC_B) {
     double a[NS];
 #pragma unroll
-    for (int i = 0; i < NS; ++i) a[i] = act ? e[NS * c + i] : 0.0;
-    if (t == 0) {
-      // S_{c0+1} = A^L S_c0 + e_c0: the segment's start state enters through its first element, so the inclusive
-      // scan below yields every S_{c+1} = A^(L (t+1)) S_c0 + sum_j A^(L (t-j)) e_(c0+j) directly (one 6x6 product
-      // instead of a binary power of up to 11 per thread)
-      const double* M = pw_s;
-#pragma unroll
-      for (int r = 0; r < NS; ++r) {
-        double acc = a[r];
-#pragma unroll
-        for (int q = 0; q < NS; ++q) acc = fma(M[8 * r + q], seg[q], acc);
-        a[r] = acc;
-      }
-    }
-    for (int sidx = 0; (1 << sidx) < SCAN_T; ++sidx) {
-#pragma unroll
-      for (int i = 0; i < NS; ++i) v[i][t] = a[i];
-      __syncthreads();
+    for (int i = 0; i < NS; ++i) a[i] = wsc[i][tid];
+    for (int sidx = 0; (1 << sidx) < CASC_B; ++sidx) {
       const int d = 1 << sidx;
-      if (t >= d) {
-        const double* M = pw_s + 64 * sidx;
-        double u[NS];
+      double u[NS];
 #pragma unroll
-        for (int i = 0; i < NS; ++i) u[i] = v[i][t - d];
+      for (int i = 0; i < NS; ++i) u[i] = tid >= d ? wsc[i][tid - d] : 0.0;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (tid >= d) {
+        const double* M = pw6 + 64 * sidx;
 #pragma unroll
         for (int r = 0; r < NS; ++r) {
           double acc = a[r];
@@ -378,20 +346,101 @@ __global__ void __launch_bounds__(SCAN_T) k_casc_carry(const double* __restrict_
           a[r] = acc;
         }
       }
-      __syncthreads();
-    }
-    if (act) {
 #pragma unroll
-      for (int i = 0; i < NS; ++i) S[NS * (c + 1) + i] = a[i];
+      for (int i = 0; i < NS; ++i) wsc[i][tid] = a[i];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    __syncthreads();
-    const long long last = min(nch - 2, c0 + SCAN_T - 1);  // the segment's last produced state
-    if (c == last) {
+    if (c < nch) {
 #pragma unroll
-      for (int i = 0; i < NS; ++i) seg[i] = a[i];
+      for (int i = 0; i < NS; ++i) e[NS * c + i] = a[i];
     }
-    __syncthreads();
   }
+  __syncthreads();
+  for (int i = tid; i < cnt; i += CASC_NT) y0[tb0 + i] = rows[(i / L) * CASC_LD + (i % L)];
+}
+
+// chunk start states S_0 = w x0, S_{c+1} = A^L S_c + e_c, from k_casc_local's block scans (e holds W_k, the end state of
+// chunk k of its 64-chunk block from a zero block start). Block b of this launch (64 threads, one per chunk of local
+// block b) first walks the earlier blocks serially, S_start(j+1) = A^(64 L) S_start(j) + W_63(j) (NS lanes, one row
+// each), then sets S_(c0+k) = A^(L k) S_start(b) + W_(k-1), the power by binary decomposition over the A^(L 2^s) tables.
+// (Round 4's single-block Hillis-Steele scan over all chunks: 26 us per pass at C2; x0 = the pass input's first sample:
+// x[0] / x[n - 1] (rev), or the previous pass's output there (S_in set).)
+template <int NS>
+__global__ void __launch_bounds__(CASC_B) k_casc_carry(const double* __restrict__ e, long long nch,
+                                                       const double* __restrict__ tab, const double* __restrict__ x,
+                                                       const double* __restrict__ S_in, long long n, int L, int rev,
+                                                       double* __restrict__ S) {
+  __shared__ double st[NS];
+  const int tid = threadIdx.x;
+  const long long b = blockIdx.x, c0 = b * CASC_B;
+  if (tid < NS) {
+    const long long i0 = rev ? n - 1 : 0;
+    const double x0 = S_in ? casc_fixed<NS>(x, S_in, tab, L, i0) : x[i0];
+    st[tid] = tab[CASC_W + tid] * x0;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // the earlier blocks' aggregates W_63 come in groups of 256 (all loads of a group in flight), the A^(64 L) row of
+  // lane r in registers: the serial walk then touches only LDS
+  __shared__ double agg[256][NS];
+  double p64[NS];
+#pragma unroll
+  for (int q = 0; q < NS; ++q) p64[q] = tid < NS ? tab[CASC_POW + 64 * 6 + 8 * tid + q] : 0.0;
+  for (long long j0 = 0; j0 < b; j0 += 256) {
+    const int cnt = (int)min((long long)256, b - j0);
+    for (int i = tid; i < cnt * NS; i += CASC_B) {
+      const int jj = i / NS, q = i - jj * NS;
+      agg[jj][q] = e[NS * ((j0 + jj) * CASC_B + CASC_B - 1) + q];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int jj = 0; jj < cnt; ++jj) {
+      double nv = 0.0;
+      if (tid < NS) {
+        double acc = agg[jj][tid];
+#pragma unroll
+        for (int q = 0; q < NS; ++q) acc = fma(p64[q], st[q], acc);
+        nv = acc;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (tid < NS) st[tid] = nv;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+  const long long c = c0 + tid;
+  if (c >= nch) return;
+  double v[NS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) v[i] = st[i];
+  for (int sidx = 0; (1 << sidx) <= tid; ++sidx) {
+    if (tid & (1 << sidx)) {
+      const double* M = tab + CASC_POW + 64 * sidx;
+      double r[NS];
+#pragma unroll
+      for (int rr = 0; rr < NS; ++rr) {
+        double acc = 0.0;
+#pragma unroll
+        for (int q = 0; q < NS; ++q) acc = fma(M[8 * rr + q], v[q], acc);
+        r[rr] = acc;
+      }
+#pragma unroll
+      for (int i = 0; i < NS; ++i) v[i] = r[i];
+    }
+  }
+  if (tid > 0) {
+#pragma unroll
+    for (int i = 0; i < NS; ++i) v[i] += e[NS * (c - 1) + i];
+  }
+#pragma unroll
+  for (int i = 0; i < NS; ++i) S[NS * c + i] = v[i];
 }
 
 // the backward pass's final output (its fix-up applied on the fly), un-reversed, trimmed of the odd extension and
@@ -433,10 +482,10 @@ hipError_t casc_filtfilt(const SosPlan& p, const double* ext, long long ne, int 
     lds_set = true;
   }
   hipLaunchKernelGGL(k_casc_local<NSEC>, dim3(g), dim3(CASC_NT), lds, s, ext, nullptr, ne, 0, p.casc, y0f, e);
-  hipLaunchKernelGGL(k_casc_carry<NS>, dim3(1), dim3(SCAN_T), 0, s, e, nch, p.casc, ext, nullptr, ne, L, 0, Sf);
+  hipLaunchKernelGGL(k_casc_carry<NS>, dim3(g), dim3(CASC_B), 0, s, e, nch, p.casc, ext, nullptr, ne, L, 0, Sf);
   // backward over the reversed forward output (y0f fixed up with Sf on the fly)
   hipLaunchKernelGGL(k_casc_local<NSEC>, dim3(g), dim3(CASC_NT), lds, s, y0f, Sf, ne, 1, p.casc, y0b, e);
-  hipLaunchKernelGGL(k_casc_carry<NS>, dim3(1), dim3(SCAN_T), 0, s, e, nch, p.casc, y0f, Sf, ne, L, 1, Sb);
+  hipLaunchKernelGGL(k_casc_carry<NS>, dim3(g), dim3(CASC_B), 0, s, e, nch, p.casc, y0f, Sf, ne, L, 1, Sb);
   const long long m = n + 2 * t_pad;
   const unsigned gb = (unsigned)std::min<long long>((m + 255) / 256, 4096);
   hipLaunchKernelGGL(k_casc_final_pad<NS>, dim3(gb), dim3(256), 0, s, y0b, Sb, p.casc, L, ne, padlen, n, t_pad, pad64,
