@@ -178,7 +178,9 @@ __device__ __forceinline__ bool splitk_fixup(const ConvArgs& a, int m0, int n0, 
   return true;
 }
 
-template <int TM16, int TN16, int WM, int WN>
+// UP2D: the instantiation may see the ConvTranspose2d phase layout (OUT_UPSAMPLE2D: the 2-D gather-streamed kernel
+// only; compiled out elsewhere)
+template <int TM16, int TN16, int WM, int WN, bool UP2D = false>
 __device__ __forceinline__ void store_tile16(const ConvArgs& a, int m0, int n0, int b, int zsplit, int ksplit,
                                              long long Mtot, f32x4 (&acc)[TM16][TN16]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -277,6 +279,19 @@ __device__ __forceinline__ void store_tile16(const ConvArgs& a, int m0, int n0, 
       if (MK) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] *= mv[r];
+      }
+      if (UP2D && a.out_map == OUT_UPSAMPLE2D) {
+        // the 2x2-phase ConvTranspose2d (epilogue_store's mapping): virtual column n = (ph, pw, co) of input pixel m
+        const int cv = a.out_cv;
+        const int ph = n / (2 * cv), pw = (n / cv) & 1, co = n - (n / cv) * cv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (!ok[r]) continue;
+          const long long m = mb + r;
+          const long long oh = m / a.W_out, ow = m - oh * a.W_out;
+          Y[((2 * oh + ph) * (2 * a.W_out) + (2 * ow + pw)) * a.ldy + co] = v[r];
+        }
+        continue;
       }
       if (a.y_h16) {
         // the consumer's A operand as the two-plane fp16 image (split_bf16.h put_h16x4 of v * 2^-4): h = f16(x),

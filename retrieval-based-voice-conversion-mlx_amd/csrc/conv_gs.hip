@@ -291,7 +291,7 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gs16_kernel(const ConvAr
       if (base + p < it1) step(base + p, p);
   }
   if constexpr (H16) h16_finish<TM16, TN16, WN>(wsp, (size_t)total * bstep, n0, acc, acc2);
-  store_tile16<TM16, TN16, WM, WN>(a, m0, n0, b, zsplit, ksplit, Mtot, acc);
+  store_tile16<TM16, TN16, WM, WN, TWO_D>(a, m0, n0, b, zsplit, ksplit, Mtot, acc);
 }
 
 template <int BM, int BN, int WM, int WN, bool TWO_D, int MODE>
@@ -759,8 +759,12 @@ hipError_t launch_gsw(const ConvArgs& a, int ntn_enable, int ksplit, hipStream_t
 
 bool conv_gs_eligible(const ConvArgs& a, bool two_d) {
   const bool vec_a = ((a.ldx & 3) == 0) && ((reinterpret_cast<uintptr_t>(a.x) & 15) == 0) && ((a.x_bs & 3) == 0);
+  // the 2x2-phase ConvTranspose2d output (OUT_UPSAMPLE2D, the U-Net decoder's up-convs, round 5) with the plain epilogue
+  // (store_tile16 maps it; a split launch's combine does, as for the LDS-staged kernel)
+  const bool up2d = two_d && a.out_map == OUT_UPSAMPLE2D && a.out_cv > 0 && a.N == 4 * a.out_cv && !a.res &&
+                    a.acc_mode == ACC_STORE && !a.mask && !a.y_h16 && !a.nz_har;
   const bool common = a.batch_inner == 1 && !a.b_kn && a.C_in % EK == 0 && a.C_in > 0 && a.taps >= 1 && vec_a &&
-                      a.out_map == OUT_ROWS && a.stride >= 1 && a.dil >= 1;
+                      (a.out_map == OUT_ROWS || up2d) && a.stride >= 1 && a.dil >= 1;
   if (!common) return false;
   // 32-bit element offsets within one batch entry (the A gather)
   const long long rows_in = two_d ? (long long)a.T_in * a.W_in : a.T_in;
