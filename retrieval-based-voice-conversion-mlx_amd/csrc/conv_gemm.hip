@@ -651,6 +651,59 @@ __global__ __launch_bounds__(256) void conv_tiny_rows_kernel(const ConvArgs a) {
   }
 }
 
+// 1x1 convs with few inputs and outputs (the U-Net's ConvBlockRes shortcuts: 16 -> 32, 64 -> 32, 32 -> 16 channels on
+// 50 k - 200 k pixels; round 5): one thread per pixel, its C_in inputs as float4 loads, the weights [C_in][N] and bias in
+// LDS (broadcast reads), N fp32 fma chains, bias + activation, float4 stores. Exact fp32 (the native-f32 MFMA GEMM it
+// replaces took 13-23 us for these byte-bound shapes).
+template <int N, int ACT>
+__global__ __launch_bounds__(256) void conv_rows1x1_kernel(const ConvArgs a) {
+  // (staging the block's input rows through LDS for coalesced loads measured slower: 16 / 20 us vs 12 / 18, r05aq)
+  __shared__ __attribute__((aligned(16))) float ws[64 * 32];
+  __shared__ float bs[32];
+  const int C = a.C_in;
+  for (int i = threadIdx.x; i < C * N; i += blockDim.x) {
+    const int n = i / C, c = i - n * C;
+    ws[c * N + n] = a.w[(long long)n * a.ldw + c];
+  }
+  if (threadIdx.x < N) bs[threadIdx.x] = a.bias ? a.bias[threadIdx.x] : 0.f;
+  __syncthreads();
+  const int rows = a.W_out > 0 ? a.T_out * a.W_out : a.T_out;
+  const int total = rows * a.batch;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int b = i / rows, m = i - b * rows;
+    const f32x4* X = reinterpret_cast<const f32x4*>(a.x + (long long)b * a.x_bs + (long long)m * a.ldx);
+    float acc[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) acc[n] = 0.f;
+    for (int c4 = 0; c4 < C / 4; ++c4) {
+      const f32x4 v = X[c4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const f32x4* wr = reinterpret_cast<const f32x4*>(ws + (4 * c4 + e) * N);
+#pragma unroll
+        for (int n4 = 0; n4 < N / 4; ++n4) {
+          const f32x4 w = wr[n4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) acc[4 * n4 + k] = fmaf(v[e], w[k], acc[4 * n4 + k]);
+        }
+      }
+    }
+    float* Y = a.y + (long long)b * a.y_bs + (long long)m * a.ldy;
+#pragma unroll
+    for (int n = 0; n < N; n += 4) {
+      f32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v = acc[n + e] + bs[n + e];
+        if (ACT == ACT_RELU) v = v > 0.f ? v : 0.f;
+        else if (ACT == ACT_LRELU) v = v > 0.f ? v : v * a.slope;
+        o[e] = v;
+      }
+      *reinterpret_cast<f32x4*>(Y + n) = o;
+    }
+  }
+}
+
 namespace {
 
 // conv_tiny_rows_kernel's shapes: only bias + activation in the epilogue, N in {16, 32}, 16-B aligned output rows
@@ -666,6 +719,34 @@ inline bool tiny_fits(const ConvArgs& a) {
   const long long rows = a.W_out > 0 ? (long long)a.T_out * a.W_out : a.T_out;
   return a.C_in <= TINY_MAX_CIN && a.C_in * a.taps <= 16 && a.force_cfg < 0 &&
          rows * a.N * a.batch * a.batch_inner < (1LL << 30);
+}
+
+// conv_rows1x1_kernel's shapes: a 1x1 / stride-1 conv (1-D or 2-D) with C_in a multiple of 4 up to 64, 16-B aligned
+// input rows, and conv_tiny_rows_kernel's epilogue conditions (RVCX_NO_ROWS1X1=1: off, A/B aid)
+inline bool rows1x1_fits(const ConvArgs& a, bool two_d) {
+  static const bool off = [] {
+    const char* e = rvcx_knob("RVCX_NO_ROWS1X1");
+    return e && std::atoi(e) != 0;
+  }();
+  if (off || a.taps != 1 || a.stride != 1 || a.dil != 1 || a.pad != 0 || a.force_cfg >= 0) return false;
+  if (two_d && (a.KH != 1 || a.KW != 1 || a.padh != 0 || a.padw != 0 || a.T_in != a.T_out || a.W_in != a.W_out))
+    return false;
+  const long long rows = two_d ? (long long)a.T_out * a.W_out : a.T_out;
+  return tiny_rows_fits(a) && a.C_in % 4 == 0 && a.C_in >= 4 && a.C_in <= 64 && (a.ldx & 3) == 0 &&
+         (a.x_bs & 3) == 0 && (reinterpret_cast<uintptr_t>(a.x) & 15) == 0 && rows * a.batch < (1LL << 31) - 65536LL * 256;
+}
+
+hipError_t launch_rows1x1(const ConvArgs& a, bool two_d, hipStream_t s) {
+  const long long rows = two_d ? (long long)a.T_out * a.W_out : a.T_out;
+  const unsigned nb = (unsigned)std::min<long long>((rows * a.batch + 255) / 256, 65536);
+  ConvArgs b = a;
+  if (!two_d) b.W_out = 0;
+#define ROWS1(NN, AC) hipLaunchKernelGGL((conv_rows1x1_kernel<NN, AC>), dim3(nb), dim3(256), 0, s, b)
+  const int act = a.act;
+  if (a.N == 16) { if (act == ACT_RELU) ROWS1(16, ACT_RELU); else if (act == ACT_LRELU) ROWS1(16, ACT_LRELU); else ROWS1(16, ACT_NONE); }
+  else { if (act == ACT_RELU) ROWS1(32, ACT_RELU); else if (act == ACT_LRELU) ROWS1(32, ACT_LRELU); else ROWS1(32, ACT_NONE); }
+#undef ROWS1
+  return hipGetLastError();
 }
 
 hipError_t launch_tiny(const ConvArgs& a, bool two_d, hipStream_t s) {
@@ -989,6 +1070,10 @@ hipError_t dispatch(const ConvArgs& a_in, hipStream_t s) {
     if (nz) return hipErrorInvalidValue;
     g_conv_kind = CK_TINY;
     return launch_tiny(a, TWO_D, s);
+  }
+  if (!nz && !(a.ws && a.ksplit > 1) && rows1x1_fits(a, TWO_D)) {
+    g_conv_kind = CK_TINY;
+    return launch_rows1x1(a, TWO_D, s);
   }
   if (a.wsb == 2 && a.wsplit && conv_math(a) >= 2 && conv_gs_eligible(a, TWO_D)) {
     const int ks = (a.ws && a.ksplit > 1) ? a.ksplit : 1;
