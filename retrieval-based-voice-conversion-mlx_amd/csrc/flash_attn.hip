@@ -388,19 +388,28 @@ __global__ __launch_bounds__(64 * NW, 2) void k_flash_attn_h16(
   const int nkb = (T + FA_K - 1) / FA_K;
   const uint4* kvimg = img + (long long)bh * nkb * FR * 64 + lane;
 
-  // Q^T fragments (scaled by qscale 2^-4), kept for the whole key range
+  // Q^T fragments (scaled by qscale 2^-4), kept for the whole key range. Queries past T read row T - 1 and are
+  // zeroed: no load sits under a lane condition, so all NS steps' loads are in flight together (one round trip, not NS)
   f16x8 qf[NS][2];
+  {
+    const float4* src = reinterpret_cast<const float4*>(base + (long long)min(i, T - 1) * ldq + h * DK + 8 * hk);
+    float4 xq[NS][2];
 #pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (qok) {
-      const float4* src = reinterpret_cast<const float4*>(base + (long long)i * ldq + h * DK + 16 * s + 8 * hk);
-      const float4 x0 = src[0], x1 = src[1];
-      const float qs = qscale * FA_XS;
-      v[0] = x0.x * qs; v[1] = x0.y * qs; v[2] = x0.z * qs; v[3] = x0.w * qs;
-      v[4] = x1.x * qs; v[5] = x1.y * qs; v[6] = x1.z * qs; v[7] = x1.w * qs;
+    for (int s = 0; s < NS; ++s) {
+      xq[s][0] = src[4 * s];
+      xq[s][1] = src[4 * s + 1];
     }
-    split8h(v, qf[s]);
+    const float qs = qscale * FA_XS;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const float4 x0 = xq[s][0], x1 = xq[s][1];
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (qok) {
+        v[0] = x0.x * qs; v[1] = x0.y * qs; v[2] = x0.z * qs; v[3] = x0.w * qs;
+        v[4] = x1.x * qs; v[5] = x1.y * qs; v[6] = x1.z * qs; v[7] = x1.w * qs;
+      }
+      split8h(v, qf[s]);
+    }
   }
   const int kb0 = split * kb_per_split, kb1 = min(nkb, kb0 + kb_per_split);
   const bool band_split = nw && kb0 < kb1 && (kb1 * FA_K - 1 >= q0 - window) && (kb0 * FA_K <= q0 + FA_Q - 1 + window);
@@ -408,14 +417,20 @@ __global__ __launch_bounds__(64 * NW, 2) void k_flash_attn_h16(
     f32x16 rq, rq2;
 #pragma unroll
     for (int r = 0; r < 16; ++r) rq[r] = rq2[r] = 0.f;
+    // rows past the window read row nw - 1 and are zeroed: no load sits under a lane condition, so the NS steps'
+    // loads issue back to back instead of one round trip per step
+    const float* rk = rel_k + min(li, nw - 1) * DK + 8 * hk;
+    f32x4 rkv[NS][2];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (li < nw) {
-        const float* src = rel_k + li * DK + 16 * s + 8 * hk;
+      rkv[s][0] = *reinterpret_cast<const f32x4*>(rk + 16 * s);
+      rkv[s][1] = *reinterpret_cast<const f32x4*>(rk + 16 * s + 4);
+    }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = src[e] * FA_XS;
-      }
+    for (int s = 0; s < NS; ++s) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = li < nw ? rkv[s][e >> 2][e & 3] * FA_XS : 0.f;
       f16x8 rf[2];
       split8h(v, rf);
       mfma3(rf, qf[s], rq, rq2);
@@ -442,24 +457,63 @@ __global__ __launch_bounds__(64 * NW, 2) void k_flash_attn_h16(
     const int j0 = kb * FA_K;
     const uint4* fr = kvimg + (long long)kb * FR * 64;
     // S^T = K Q^T for keys j0.. (rows) x this wave's queries (columns)
+    // the key block's K fragments issued in batches of KB steps ahead of their products (one round trip per batch
+    // instead of one per K step: the scheduler otherwise interleaves load -> wait -> MFMA per step); DK = 96 takes
+    // two batches, all six in flight would not fit beside the accumulators in 256 VGPRs
+    constexpr int KB = DK == 64 ? NS : NS / 2;
     f32x16 sc, sc2;
 #pragma unroll
     for (int r = 0; r < 16; ++r) sc[r] = sc2[r] = 0.f;
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      f16x8 kf[2];
-      kf[0] = __builtin_bit_cast(f16x8, fr[(2 * s) * 64]);
-      kf[1] = __builtin_bit_cast(f16x8, fr[(2 * s + 1) * 64]);
-      mfma3(kf, qf[s], sc, sc2);
+    for (int s0 = 0; s0 < NS; s0 += KB) {
+      uint4 kraw[KB][2];
+#pragma unroll
+      for (int s = 0; s < KB; ++s) {
+        kraw[s][0] = fr[(2 * (s0 + s)) * 64];
+        kraw[s][1] = fr[(2 * (s0 + s) + 1) * 64];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < KB; ++s) {
+        f16x8 kf[2];
+        kf[0] = __builtin_bit_cast(f16x8, kraw[s][0]);
+        kf[1] = __builtin_bit_cast(f16x8, kraw[s][1]);
+        mfma3(kf, qf[s0 + s], sc, sc2);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // the V^T fragments: for DK = 64 all issued now, in flight under the softmax; for DK = 96 per half of the key
+    // block (s2) just before its products (all of them here would not fit in 256 VGPRs)
+    uint4 vraw[NT][2][2];
+    auto load_v = [&](int s2) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int f = 2 * NS + (t * 2 + s2) * 2;
+        vraw[t][s2][0] = fr[f * 64];
+        vraw[t][s2][1] = fr[(f + 1) * 64];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    if constexpr (DK == 64) {
+      load_v(0);
+      load_v(1);
+    }
+    // band blocks only (wave-uniform): the 16 relative-key terms gathered in one batch of LDS reads (clamped
+    // column, out-of-window values discarded)
+    const bool band = band_split && (j0 + FA_K - 1 >= q0 - window) && (j0 <= q0 + FA_Q - 1 + window);
+    float rqv[16];
+    if (band) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) rqv[r] = relq[li][min(max(j0 + crow(r, hk) - i + window, 0), FA_NW)];
     }
     float mloc = -INFINITY;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int j = j0 + crow(r, hk);
       float v = (sc[r] + sc2[r] * H16_LO_INV) * 256.f;
-      if (nw) {
+      if (band) {
         const int od = j - i + window;
-        if (od >= 0 && od < nw) v = v + relq[li][od];
+        if (od >= 0 && od < nw) v = v + rqv[r];
       }
       if (mk && j < T && mi * mk[j] == 0.f) v = -1e4f;
       if (j >= T) v = -INFINITY;
@@ -486,17 +540,25 @@ __global__ __launch_bounds__(64 * NW, 2) void k_flash_attn_h16(
         o2[t][r] *= alpha;
       }
     if (band_split) {
-      const bool band = (j0 + FA_K - 1 >= q0 - window) && (j0 <= q0 + FA_Q - 1 + window);
-      if (hk == 0)
-        for (int od = 0; od < nw; ++od) pband[li][od] *= alpha;
+      // rescale the band sums when a running max moved (alpha == 1 exactly otherwise): the two lanes of a query
+      // take 16 of its 32 columns each, unrolled so the reads issue back to back
+      if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) pband[li][16 * hk + e] *= alpha;
+      }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       if (band) {
+        // a lane's 16 keys sit on 16 distinct diagonals (the other lane of its query on 16 others): all reads can
+        // precede all writes
+        float pb[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) pb[r] = pband[li][min(max(j0 + crow(r, hk) - i + window, 0), FA_NW)];
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int od = j0 + crow(r, hk) - i + window;
-          if (od >= 0 && od < nw) pband[li][od] += sc[r];
+          if (od >= 0 && od < nw) pband[li][od] = pb[r] + sc[r];
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -506,6 +568,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_flash_attn_h16(
     // O^T += V^T P^T
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
+      if constexpr (DK != 64) load_v(s2);
       float pv[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) pv[e] = sc[8 * s2 + e];
@@ -513,10 +576,9 @@ __global__ __launch_bounds__(64 * NW, 2) void k_flash_attn_h16(
       split8h(pv, pf);
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        const int f = 2 * NS + (t * 2 + s2) * 2;
         f16x8 vf[2];
-        vf[0] = __builtin_bit_cast(f16x8, fr[f * 64]);
-        vf[1] = __builtin_bit_cast(f16x8, fr[(f + 1) * 64]);
+        vf[0] = __builtin_bit_cast(f16x8, vraw[t][s2][0]);
+        vf[1] = __builtin_bit_cast(f16x8, vraw[t][s2][1]);
         mfma3(vf, pf, o[t], o2[t]);
       }
     }
@@ -529,13 +591,19 @@ __global__ __launch_bounds__(64 * NW, 2) void k_flash_attn_h16(
       for (int e = 0; e < 8; ++e) pv[e] = pband[li][16 * s2 + 8 * hk + e];
       f16x8 pf[2];
       split8h(pv, pf);
+      // every rel_v load unconditional (rows past the window read row nw - 1, zeroed below): all 8 x NT in flight
+      float rv[NT][8];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) rv[t][e] = rel_v[min(16 * s2 + 8 * hk + e, nw - 1) * DK + 32 * t + li];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         float v[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const int od = 16 * s2 + 8 * hk + e;
-          v[e] = od < nw ? rel_v[od * DK + 32 * t + li] * FA_XS : 0.f;
+          v[e] = od < nw ? rv[t][e] * FA_XS : 0.f;
         }
         f16x8 vf[2];
         split8h(v, vf);
@@ -691,6 +759,7 @@ hipError_t flash_attn(const float* qkv, int ldq, int B, int T, int nh, int dk, f
   if ((ldq & 3) != 0 || (reinterpret_cast<uintptr_t>(qkv) & 15) != 0) return hipErrorInvalidValue;  // float4 rows
   if ((rel_k != nullptr) != (rel_v != nullptr) || (rel_k && 2 * window + 1 > FA_NW) || nsplit < 1)
     return hipErrorInvalidValue;
+  if ((reinterpret_cast<uintptr_t>(rel_k) & 15) != 0) return hipErrorInvalidValue;  // float4 rel_k rows (h16 kernel)
   const int H = nh * dk;
   const int qb = (T + FA_Q - 1) / FA_Q, kb = (T + FA_K - 1) / FA_K;
   const int per = (kb + nsplit - 1) / nsplit;
