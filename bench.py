@@ -240,7 +240,7 @@ def bench_c3(args, eng, dev, dist, rank, world):
     return {"metric": "audio-sec/sec HiFiGAN-NSF generator (C3)", "value": round(tot["value"], 3),
             "unit": "audio-sec/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(tot["elapsed"] / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "fp32", "data": "synthetic z ~ N(0,1), f0 random walk; random-init weights",
+            "vs_baseline": None, "dtype": "fp32-accurate (two-plane fp16 MFMA split)", "data": "synthetic z ~ N(0,1), f0 random walk; random-init weights",
             "config": {"workload": "C3: generator alone, B=32 x 400 frames (128 s of 48 kHz audio) per step",
                        "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "achieved": round(tf, 3), "peak": round(peak, 1), "unit": "TFLOP/s",
@@ -313,7 +313,7 @@ def bench_c4(args, eng, dev, dist, rank, world):
     return {"metric": "audio-sec/sec batched offline VC (C4)", "value": round(tot["value"], 3),
             "unit": "audio-sec/sec", "n_gpus": world, "steps": nsteps, "warmup": args.warmup,
             "ms_per_step": round(tot["elapsed"] / max(1, nsteps) * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak" if args.steps_given else "strong", "vs_baseline": None, "dtype": "fp32",
+            "scaling": "weak" if args.steps_given else "strong", "vs_baseline": None, "dtype": "fp32-accurate (two-plane fp16 MFMA split)",
             "data": "synthetic speech-like 30 s utterances (speech_like(seed=1000+i) per utterance); random-init "
                     "weights",
             "config": {"workload": f"C4: {len(job)} x 30 s utterances, LPT-sharded over {world} GPU(s), batched "
@@ -355,7 +355,8 @@ def bench_c5(args, eng, dev, dist, rank, world):
             "unit": "audio-sec/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(tot["elapsed"] / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32" if args.gen_precision == "fp32" else "fp16 generator (fp32 front end, TextEncoder, flow)",
+            "dtype": ("fp32-accurate (two-plane fp16 MFMA split)" if args.gen_precision == "fp32"
+                      else "fp16 generator (fp32-accurate front end, TextEncoder, flow)"),
             "data": "synthetic speech-like 48 kHz streams; random-init weights",
             "config": {"workload": f"C5: {S} streams x 256 ms hop (block 12288 @48k, convert buffer 13920 @16k, "
                                    "87 frames) per step", "streams": S, "parallelism": f"dp{world}",
@@ -570,7 +571,7 @@ def main():
             "metric": "audio-sec/sec (realtime factor) RVCv2 48kHz pipeline",
             "value": round(value, 3), "unit": "audio-sec/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic (speech-like, seeded); "
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32-accurate (two-plane fp16 MFMA split)", "data": "synthetic (speech-like, seeded); "
             "random-init weights of the RVCv2-48k / ContentVec / RMVPE architectures",
             "config": {"workload": "C2: full RVCv2 48kHz pipeline, one 13.5 s utterance per step per GPU",
                        "samples_16k": n, "audio_sec_per_step_per_gpu": round(audio_sec, 5), "x_pad": 1,

@@ -155,8 +155,10 @@ int rvcx_synth_infer(rvcx_ctx* ctx, int B, int T, const float* d_phone, const in
                      const int32_t* d_pitch, const float* d_pitchf, const int32_t* d_sid, const float* d_eps_z,
                      const float* d_eps_src, uint64_t seed, float* d_out, float* d_zp, float* d_z, void* stream);
 /* Synthesizer.infer with its remaining arguments and full return value (synthesizers.py:206-243): rate (the partial
- * re-synthesis of :230-234; < 0 = None, else in (0, 1]) keeps frames head = int(T (1 - rate)) .. T-1 of z_p, x_mask and
- * nsff0 before the flow, so d_out holds [B][(T - head) upp] and d_zp / d_z [B][T - head][I]; *t_out = T - head.
+ * re-synthesis of :230-234; < 0 = None) keeps z_p, x_mask and nsff0 [:, head:] before the flow with the reference's
+ * head = int(T (1 - rate)) and Python's slice semantics: a negative head (rate > 1) keeps the last -head frames (all T
+ * when -head >= T); a rate that keeps no frame (rate 0) is RVCX_E_SHAPE. d_out holds [B][T' upp] and d_zp / d_z
+ * [B][T'][I] with T' the kept frames; *t_out = T'.
  * d_m_p / d_logs_p (optional) [B][T][I] receive the TextEncoder's m_p / logs_p (the rest of the tuple :243). Noise as
  * rvcx_synth_infer (d_eps_z over all T frames, d_eps_src over the T - head synthesized ones). */
 int rvcx_synth_infer_ex(rvcx_ctx* ctx, int B, int T, const float* d_phone, const int32_t* d_lengths,
@@ -419,10 +421,21 @@ int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const floa
 /* One 3x3 / pad-1 Conv2d forward, NHWC: d_x [H][W][C_in], d_w [9][N][C_in] (torch weight [N][C_in][3][3] permuted to
  * (kh * 3 + kw, N, C_in)), d_bias [N] (optional), d_y [H][W][N]; act 0 none, 1 ReLU. The RMVPE U-Net's conv
  * (RMVPE.py:13-57 ConvBlockRes, torch.nn.Conv2d(kernel 3, padding 1)), exposed for the numerics tests of its
- * few-channel kernels (C_in, N in {16, 32}: csrc/conv2d_small.hip): math 0 = the context's arithmetic (the two-plane
- * fp16 split by default), 1 = exact fp32 (v_mfma_f32_16x16x4_f32). Other shapes take the general 2-D path. */
+ * few-channel kernels (C_in, N in {16, 32}: csrc/conv2d_small.hip) and deep levels: math 0 = the context's arithmetic
+ * (the two-plane fp16 split by default), 1 = exact fp32 (v_mfma_f32_16x16x4_f32), 2 = the deep levels' windowed
+ * gather-streamed kernel in the fp16 split (images at most 32 wide, C_in % 32 == 0, else RVCX_E_SHAPE). Other shapes
+ * take the general 2-D path. */
 int rvcx_conv2d3x3(rvcx_ctx* ctx, const float* d_x, int H, int W, int C_in, const float* d_w, const float* d_bias,
                    int N, int act, int math, float* d_y, void* stream);
+
+/* One ConvTranspose2d(C_in, N, kernel 3, stride 2, padding 1, output_padding 1) forward, NHWC: d_x [H][W][C_in],
+ * d_w [C_in][N][3][3] (the torch layout as stored), d_bias [N] (optional), d_y [2H][2W][N]; act 0 none, 1 ReLU. The
+ * RMVPE U-Net decoder's up-conv (RMVPE.py ResDecoderBlock conv1, torch.nn.ConvTranspose2d), run as the pipeline runs
+ * it: a 2x2-tap phase conv with 4 N virtual output columns whose epilogue scatters the phases. math 0 = the context's
+ * arithmetic (the two-plane fp16 split on the gather-streamed kernel where it applies), 1 = exact fp32. Exposed for the
+ * numerics tests. */
+int rvcx_convtranspose2d_s2(rvcx_ctx* ctx, const float* d_x, int H, int W, int C_in, const float* d_w,
+                            const float* d_bias, int N, int act, int math, float* d_y, void* stream);
 
 /* One ResBlock dilation pair as one fused kernel (csrc/resblock_fused.hip), time-major: d_x, d_y [B][T][C] (distinct
  * buffers), d_w1 / d_w2 [k][C][C] (torch weight [C][C][k] permuted), d_b1 / d_b2 [C]:
@@ -431,7 +444,7 @@ int rvcx_conv2d3x3(rvcx_ctx* ctx, const float* d_x, int H, int W, int C_in, cons
  * Replaces one iteration of ResBlock.forward (rvc/lib/algorithm/residuals.py:71-80) and MRFLayer.forward
  * (generators/hifigan_mrf.py:45-50), plus the ResBlock mean of HiFiGANNSFGenerator.forward (hifigan_nsf.py:190-207)
  * on the last pair. C in {32, 64}, odd k, (k - 1) / 2 * dilation <= 30, else RVCX_E_SHAPE. cfg bits 0-3: the tile
- * (0 = default, RVCX_RB_CFG in the pipeline); bits 4-5 the arithmetic: 0 the exact 3-plane bf16 split, 1 the two-plane
+ * (must be 0: the default tile); bits 4-5 the arithmetic: 0 the exact 3-plane bf16 split, 1 the two-plane
  * fp16 split, 2 fp16 hi planes alone (the realtime reduced-precision mode). Exposed for numerics tests and A/B timing. */
 int rvcx_resblock_pair(rvcx_ctx* ctx, const float* d_x, int B, int64_t T, int C, const float* d_w1, const float* d_b1,
                        const float* d_w2, const float* d_b2, int k, int dilation, int acc_mode, float acc_div, int cfg,

@@ -250,64 +250,28 @@ hipError_t gate_tanh_sigmoid(const float* xin, int ldx, const float* g, long lon
   return hipGetLastError();
 }
 
-// ------------------------------------------------------------------ softmax with relative-position band
-// scores: [B*heads][T][T] (already (q/sqrt(d)).k); rel: [B*heads][T][2w+1] ((q/sqrt(d)).emb_rel_k);
-// mask: [B][T] (attention mask = mask[i]*mask[j], fill -1e4); pband out: [B*heads][T][2w+1].
-__global__ void k_softmax_rel(float* scores, int T, int n_heads, const float* rel, int window, const float* mask,
-                              float* pband) {
-  const int row = blockIdx.x;  // over B*heads*T
-  const int bh = row / T, i = row % T;
-  const int b = bh / n_heads;
-  float* sr = scores + (long long)row * T;
-  const int nw = 2 * window + 1;
-  const float* rr = rel ? rel + (long long)row * nw : nullptr;
-  const float* mk = mask ? mask + (long long)b * T : nullptr;
-  const float mi = mk ? mk[i] : 1.f;
-  __shared__ float red[8];
-  float mx = -INFINITY;
-  for (int j = threadIdx.x; j < T; j += blockDim.x) {
-    float v = sr[j];
-    const int o = j - i + window;
-    if (rr && o >= 0 && o < nw) v = v + rr[o];
-    if (mk && mi * mk[j] == 0.f) v = -1e4f;
-    sr[j] = v;
-    mx = fmaxf(mx, v);
-  }
-  mx = warp_max(mx);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
-  __syncthreads();
-  mx = red[0];
-  for (int w = 1; w < (int)(blockDim.x >> 6); ++w) mx = fmaxf(mx, red[w]);
-  __syncthreads();
-  float sum = 0.f;
-  for (int j = threadIdx.x; j < T; j += blockDim.x) {
-    const float e = expf(sr[j] - mx);
-    sr[j] = e;
-    sum += e;
-  }
-  sum = warp_sum(sum);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sum;
-  __syncthreads();
-  sum = 0.f;
-  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) sum += red[w];
-  const float inv = 1.f / sum;
-  for (int j = threadIdx.x; j < T; j += blockDim.x) sr[j] = sr[j] * inv;
-  if (pband) {
-    __syncthreads();
-    for (int o = threadIdx.x; o < nw; o += blockDim.x) {
-      const int j = i + o - window;
-      pband[(long long)row * nw + o] = (j >= 0 && j < T) ? sr[j] : 0.f;
-    }
+
+// ------------------------------------------------------------------ ConvTranspose2d 3x3 s2 p1 op1 as a 2x2-tap phase conv
+// w [C][co][3][3] (torch layout) -> [tap = 2 dh + dw][4 co][C]: virtual column (ph 2 + pw) co + o of input offset (dh,
+// dw) takes kernel tap (kmap[ph][dh], kmap[pw][dw]) with kmap = {{1, -1}, {2, 0}} (-1: no tap, zero); the runtime's
+// packing of the U-Net decoder's up-conv (runtime_fe.cpp, BN scale 1)
+__global__ void k_upconv_pack(const float* __restrict__ w, int C, int co, float* __restrict__ out) {
+  const long long total = 4LL * 4 * co * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int ii = (int)(i % C);
+    const long long r = i / C;
+    const int n = (int)(r % (4 * co)), tap = (int)(r / (4 * co));
+    const int dh = tap >> 1, dw = tap & 1, ph = n / (2 * co), pw = (n / co) & 1, o = n % co;
+    const int kmap[2][2] = {{1, -1}, {2, 0}};
+    const int kh = kmap[ph][dh], kw = kmap[pw][dw];
+    out[i] = (kh < 0 || kw < 0) ? 0.f : w[(((long long)ii * co + o) * 3 + kh) * 3 + kw];
   }
 }
-hipError_t softmax_rel(float* scores, int T, int n_heads, int B, const float* rel, int window, const float* mask,
-                       float* pband, int, hipStream_t s) {
-  hipLaunchKernelGGL(k_softmax_rel, dim3(B * n_heads * T), dim3(256), 0, s, scores, T, n_heads, rel, window, mask,
-                     pband);
-  return hipGetLastError();
-}
-hipError_t softmax_rows(float* scores, int rows, int cols, hipStream_t s) {
-  hipLaunchKernelGGL(k_softmax_rel, dim3(rows), dim3(256), 0, s, scores, cols, 1, nullptr, 0, nullptr, nullptr);
+
+hipError_t upconv_phase_pack(const float* w, int C, int co, float* out, hipStream_t s) {
+  const long long total = 16LL * co * C;
+  hipLaunchKernelGGL(k_upconv_pack, dim3((unsigned)std::min<long long>((total + 255) / 256, 8192)), dim3(256), 0, s,
+                     w, C, co, out);
   return hipGetLastError();
 }
 
@@ -1027,28 +991,16 @@ hipError_t filtfilt_sos_pad(const SosPlan& p, int order, const double* x, long l
   const int padlen = 3 * (order + 1);
   if (n <= padlen || t_pad >= n || p.nsec < 1) return hipErrorInvalidValue;
   const long long ne = n + 2 * padlen;
+  if (!p.casc) return hipErrorInvalidValue;
   double* ext = ws;
-  double* yf = ext + ne;
-  double* yb = yf + ne;
-  double* sw = yb + ne;
   hipLaunchKernelGGL(k_odd_ext, dim3(nblocks(ne)), dim3(TB), 0, s, x, n, padlen, ext);
-  static const bool per_section = [] {  // RVCX_SOS_PER_SECTION=1: one local / carry / fix round per section (A/B aid)
-    const char* e = rvcx_knob("RVCX_SOS_PER_SECTION");
-    return e && std::atoi(e) != 0;
-  }();
-  if (p.casc && !per_section) return casc_filtfilt_pad(p, ext, ne, padlen, n, t_pad, yf, pad64, pad32, s);
-  hipError_t e = sos_pass(p, ext, ne, 0, yf, sw, s);  // forward, x0 = ext[0]
-  if (e != hipSuccess) return e;
-  e = sos_pass(p, yf, ne, 1, yb, sw, s);  // backward over reversed yf, x0 = yf[ne - 1]
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_filt_pad, dim3(nblocks(n + 2 * t_pad)), dim3(TB), 0, s, yb, ne, padlen, n, t_pad, pad64,
-                     pad32);
-  return hipGetLastError();
+  return casc_filtfilt_pad(p, ext, ne, padlen, n, t_pad, ext + ne, pad64, pad32, s);
 }
 
 size_t filtfilt_sos_ws_doubles(long long n, int order, int L) {
   const long long ne = n + 2 * 3 * (order + 1);
-  return (size_t)(3 * ne) + std::max(sos_ws_doubles(ne, L), casc_ws_doubles(ne, 64));
+  (void)L;
+  return (size_t)(3 * ne) + casc_ws_doubles(ne, 64);
 }
 
 size_t filtfilt_ws_doubles(long long n, int order) {

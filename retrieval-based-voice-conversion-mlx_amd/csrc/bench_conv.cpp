@@ -82,9 +82,9 @@ int main(int argc, char** argv) {
     std::vector<float> ref((size_t)T * N), out((size_t)T * N);
     CK_(hipMemcpy(ref.data(), yr, ref.size() * 4, hipMemcpyDeviceToHost));
     // fmt 1: the two-plane fp16 image (math 3), fmt 2: its reduced-precision hi-plane mode
-    for (int cfg : {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 20, 21, 22, 23, 24, 25, 26, 27, 28})
+    for (int cfg : {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 23, 24, 25, 27})
       for (int fmt : {0, 1, 2}) {
-        if (fmt && cfg != 23 && cfg != 24 && cfg != 25 && cfg != 27 && cfg != 28) continue;
+        if (fmt && cfg != 23 && cfg != 24 && cfg != 25 && cfg != 27) continue;
         if (si > 0 && (cfg != 23 || fmt == 0)) continue;
         const int pipe = -1;
         ConvArgs a;
@@ -203,8 +203,8 @@ int main(int argc, char** argv) {
     const double flops = 2.0 * cs.T * cs.N * (double)cs.Cin * cs.taps;
     // variants: (cfg, math, pipe); cfg -1 = the library's policy for that math
     struct V { int cfg, math, pipe; };
-    std::vector<V> vars = {{-1, 2, 0}, {23, 2, -1}, {24, 2, -1}, {27, 2, -1}, {28, 2, -1}, {23, 3, -1}, {24, 3, -1},
-                           {27, 3, -1}, {28, 3, -1}, {25, 3, -1}, {23, 4, -1}, {27, 4, -1}, {13, 2, -1}, {1, 1, -1}};
+    std::vector<V> vars = {{-1, 2, 0}, {23, 2, -1}, {24, 2, -1}, {27, 2, -1}, {23, 3, -1}, {24, 3, -1},
+                           {27, 3, -1}, {25, 3, -1}, {23, 4, -1}, {27, 4, -1}, {13, 2, -1}, {1, 1, -1}};
     if (cs.taps == 1)
       for (int c : {10, 12, 13, 14, 15}) vars.push_back({c, 2, 1});
     printf("%-28s", cs.name);

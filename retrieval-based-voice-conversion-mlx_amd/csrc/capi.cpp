@@ -16,12 +16,11 @@ extern char** environ;
 using namespace rvcx;
 
 namespace rvcx {
+// read at every knob read (not cached): most knobs are read once into a static at their first use, the BiGRU's
+// fault-injection hook (RVCX_GRU_SPIN_LIMIT) per call, so a test can set and clear it with the opt-in
 static bool experimental_on() {
-  static const bool on = [] {
-    const char* e = std::getenv("RVCX_EXPERIMENTAL");
-    return e && std::atoi(e) == 1;
-  }();
-  return on;
+  const char* e = std::getenv("RVCX_EXPERIMENTAL");
+  return e && std::atoi(e) == 1;
 }
 const char* rvcx_knob(const char* name) { return experimental_on() ? std::getenv(name) : nullptr; }
 }  // namespace rvcx
@@ -53,7 +52,7 @@ int guard(rvcx_ctx* c, F&& f) {
 void set_device(rvcx_ctx* c) {
   RVCX_HIP(hipSetDevice(c->device));
   c->check_device_status();
-  c->arena_rewind();
+  c->begin_call();
 }
 
 }  // namespace
@@ -62,70 +61,13 @@ namespace rvcx {
 hipStream_t Ctx::aux_stream() {
   if (!aux) {
     RVCX_HIP(hipSetDevice(device));
-    // RVCX_AUX_PRIO=1: the aux stream (HuBERT beside RMVPE) at the device's least priority, so the critical RMVPE
-    // chain's workgroups are dispatched first when both queues have work
-    static const int low = [] {
-      const char* e = rvcx_knob("RVCX_AUX_PRIO");
-      return e ? std::atoi(e) : 0;
-    }();
-    int least = 0, greatest = 0;
-    if (low && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess && least != greatest) {
-      RVCX_HIP(hipStreamCreateWithPriority(&aux, hipStreamNonBlocking, least));
-    } else {
-      (void)hipGetLastError();
-      RVCX_HIP(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
-    }
+    // (the aux stream at the device's least priority measured neutral: 18.22 vs 18.19 ms, round 3)
+    RVCX_HIP(hipStreamCreateWithFlags(&aux, hipStreamNonBlocking));
     RVCX_HIP(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
     RVCX_HIP(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
     RVCX_HIP(hipEventCreateWithFlags(&ev_gate, hipEventDisableTiming));
-    RVCX_HIP(hipEventCreateWithFlags(&ev_front, hipEventDisableTiming));
   }
   return aux;
-}
-
-hipStream_t Ctx::cu_stream(int ncu) {
-  if (aux_cu && aux_cu_n == ncu) return aux_cu;
-  if (aux_cu) {
-    RVCX_HIP(hipStreamSynchronize(aux_cu));
-    (void)hipStreamDestroy(aux_cu);
-    aux_cu = nullptr;
-  }
-  RVCX_HIP(hipSetDevice(device));
-  int ncus = 0;
-  RVCX_HIP(hipDeviceGetAttribute(&ncus, hipDeviceAttributeMultiprocessorCount, device));
-  if (ncus <= 0) ncus = 256;
-  std::vector<uint32_t> mask((size_t)(ncus + 31) / 32, 0u);
-  int taken = 0;
-  for (int i = 0; i < ncus; ++i)  // spread evenly over the CU index space (and so over the XCDs)
-    if ((long long)(i + 1) * ncu / ncus > (long long)i * ncu / ncus) {
-      mask[(size_t)i / 32] |= 1u << (i % 32);
-      ++taken;
-    }
-  if (taken == 0) mask[0] = 1u;
-  RVCX_HIP(hipExtStreamCreateWithCUMask(&aux_cu, (uint32_t)mask.size(), mask.data()));
-  if (!ev_cu_done) RVCX_HIP(hipEventCreateWithFlags(&ev_cu_done, hipEventDisableTiming));
-  aux_cu_n = ncu;
-  return aux_cu;
-}
-
-// split-K arrival counters, one array per stream (the aux stream's split launches run beside the caller's): zeroed
-// once here, and every launch leaves them zero (the last slice of a tile resets its counter). Outside the workspace
-// arena, which is rewound per call
-unsigned* Ctx::splitk_counters(hipStream_t s) {
-  auto& slot = fix_counters[s];
-  if (!slot) {
-    std::unique_ptr<DevBuf> b(new DevBuf());
-    const size_t bytes = sizeof(unsigned) * (size_t)SPLITK_COUNTERS;
-    if (hipMalloc(&b->p, bytes) != hipSuccess) {
-      (void)hipGetLastError();
-      throw Error(RVCX_E_OOM, "split-K counter allocation failed");
-    }
-    b->bytes = bytes;
-    RVCX_HIP(hipMemsetAsync(b->p, 0, bytes, s));
-    RVCX_HIP(hipStreamSynchronize(s));
-    slot = std::move(b);
-  }
-  return static_cast<unsigned*>(slot->p);
 }
 
 unsigned* Ctx::device_status() {
@@ -154,19 +96,15 @@ void Ctx::check_device_status() {
 
 Ctx::~Ctx() {
   if (status_host) (void)hipHostFree(status_host);
+  for (auto& kv : call_ev)
+    if (kv.second) (void)hipEventDestroy(kv.second);
   if (aux) {
     (void)hipStreamSynchronize(aux);
     (void)hipEventDestroy(ev_fork);
     (void)hipEventDestroy(ev_join);
     (void)hipEventDestroy(ev_gate);
-    (void)hipEventDestroy(ev_front);
     (void)hipStreamDestroy(aux);
   }
-  if (aux_cu) {
-    (void)hipStreamSynchronize(aux_cu);
-    (void)hipStreamDestroy(aux_cu);
-  }
-  if (ev_cu_done) (void)hipEventDestroy(ev_cu_done);
 }
 
 hipStream_t fork_aux(Ctx& c, hipStream_t s) {
@@ -224,17 +162,8 @@ const void* Ctx::rb_wsplit_for(const float* w, int C, int k, int wfmt, hipStream
   return slot->p;
 }
 
-void launch_rb_pair(Ctx& c, const RbPairArgs& a_in, hipStream_t s) {
-  static const int cfg = [] {
-    const char* e = rvcx_knob("RVCX_RB_CFG");
-    return e ? std::atoi(e) : 0;
-  }();
-  static const int flags = [] {
-    const char* e = rvcx_knob("RVCX_RB_FLAGS");
-    return e ? std::atoi(e) : 0;
-  }();
-  RbPairArgs a = a_in;
-  a.flags = flags;
+void launch_rb_pair(Ctx& c, const RbPairArgs& a, hipStream_t s) {
+  constexpr int cfg = 0;
   if (!c.prof) {
     check(rb_pair(a, cfg, s), "rb_pair");
     return;
@@ -293,10 +222,6 @@ void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double
     if (!a.wsplit) a.wsplit = c.wsplit_for(a, s);  // a caller-built image (rvcx_conv1d) is used as given
     a.wsplit_npad = conv_wsplit_npad(a.N);
   }
-  // the two-plane fp16 activation image (x_h16 / y_h16) exists only between weight-streamed fp16 launches
-  if ((a.x_h16 || a.y_h16) && (two_d || a.wsb != 1 || a.wsplit_fmt != WSPLIT_H16 || need > 0 || a.N % 32 != 0 ||
-                               (a.y_h16 && (a.ldy != a.N || a.acc_mode != ACC_STORE || a.mask || a.res))))
-    throw Error(RVCX_E_SHAPE, "conv: the fp16 activation image needs the weight-streamed fp16 kernel without split-K");
   // split-K slabs are per stream: the aux stream's convs run concurrently with the caller's
   // HuBERT's feature-encoder contractions (issued on the aux stream beside the U-Net, with ~1.5 ms of slack before the
   // BiGRU) take 64 KB more LDS per workgroup: one or two of them per CU at most, so the U-Net's latency-bound chain
@@ -310,10 +235,7 @@ void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double
   }();
   if (aux_lds > 0 && c.aux_front) a.lds_pad = aux_lds * 1024;
   if (need > 0) {
-    a.ws = c.buf<float>(c.aux && s == c.aux ? "conv.splitk.aux" : (c.aux_cu && s == c.aux_cu ? "conv.splitk.cu" : "conv.splitk"),
-                        (size_t)need, s);
-    a.fix_cnt = c.splitk_counters(s);  // the in-kernel combine's tile counters (the dispatcher decides per launch)
-    a.fix_cap = Ctx::SPLITK_COUNTERS;
+    a.ws = c.buf<float>(c.aux && s == c.aux ? "conv.splitk.aux" : "conv.splitk", (size_t)need, s);
   }
   if (flops < 0) {
     const double M = two_d ? (double)a.T_out * a.W_out : (double)a.T_out;
@@ -635,12 +557,15 @@ int rvcx_synth_infer_ex(rvcx_ctx* ctx, int B, int T, const float* d_phone, const
     if (ctx->scfg.f0 && (!d_pitch || !d_pitchf))
       throw Error(RVCX_E_INVALID, "rvcx_synth_infer_ex: a pitch-guided model needs pitch and pitchf");
     if (!ctx->scfg.f0) d_pitch = nullptr, d_pitchf = nullptr;
-    // head = int(z_p.shape[2] * (1.0 - rate)) (synthesizers.py:231); rate < 0: no rate
+    // head = int(z_p.shape[2] * (1.0 - rate)) (synthesizers.py:231), then Python's slice [head:]: a negative head
+    // (rate > 1) keeps the last -head frames (all T when -head >= T); rate < 0: no rate (None)
     int head = 0;
     if (rate >= 0.0) {
       const double h = (double)T * (1.0 - rate);
-      if (!(h < (double)T) || h < 0.0) throw Error(RVCX_E_INVALID, "rvcx_synth_infer_ex: rate must be in (0, 1]");
-      head = (int)h;
+      if (std::isnan(h)) throw Error(RVCX_E_INVALID, "rvcx_synth_infer_ex: rate is not a number");
+      const double ht = std::trunc(h);  // int(): toward zero
+      head = ht >= 0.0 ? (int)std::min(ht, (double)T) : (int)std::max(0.0, (double)T + ht);
+      if (head >= T) throw Error(RVCX_E_SHAPE, "rvcx_synth_infer_ex: rate keeps no frame (the reference's slice is empty)");
     }
     set_device(ctx);
     synth_forward(*ctx, B, T, d_phone, d_lengths, d_pitch, d_pitchf, d_sid, d_eps_z, d_eps_src, seed, d_out, d_zp,
@@ -869,8 +794,7 @@ int rvcx_config_info(const rvcx_ctx* ctx, char* buf, int64_t cap, int64_t* len) 
     std::string ve;
     for (char ch : v)
       if (ch != '"' && ch != '\\' && (unsigned char)ch >= 32) ve += ch;
-    const bool honoured = k == "RVCX_EXPERIMENTAL" || k == "RVCX_PROF_DUMP" || k == "RVCX_GRU_SPIN_LIMIT" ||
-                          k == "RVCX_LIB" || experimental_on();
+    const bool honoured = k == "RVCX_EXPERIMENTAL" || k == "RVCX_PROF_DUMP" || k == "RVCX_LIB" || experimental_on();
     j += std::string(first ? "" : ", ") + "\"" + k + "\": {\"value\": \"" + ve + "\", \"honoured\": " +
          (honoured ? "true" : "false") + "}";
     first = false;
@@ -943,7 +867,7 @@ int rvcx_conv2d3x3(rvcx_ctx* ctx, const float* d_x, int H, int W, int C_in, cons
   return guard(ctx, [&] {
     set_device(ctx);
     ctx->check_device_status();
-    if (!d_x || !d_w || !d_y || H <= 0 || W <= 0 || C_in <= 0 || N <= 0 || act < 0 || act > 1 || math < 0 || math > 3)
+    if (!d_x || !d_w || !d_y || H <= 0 || W <= 0 || C_in <= 0 || N <= 0 || act < 0 || act > 1 || math < 0 || math > 2)
       throw Error(RVCX_E_INVALID, "rvcx_conv2d3x3: bad argument");
     if ((int64_t)H * W * (C_in > N ? C_in : N) > INT32_MAX) throw Error(RVCX_E_SHAPE, "rvcx_conv2d3x3: size out of range");
     ConvArgs a;
@@ -953,16 +877,14 @@ int rvcx_conv2d3x3(rvcx_ctx* ctx, const float* d_x, int H, int W, int C_in, cons
     a.act = act ? ACT_RELU : ACT_NONE;
     a.math = math == 1 ? 1 : (math >= 2 ? 3 : 0);
     if (a.math == 0 && ctx->conv_math > 0) a.math = ctx->conv_math;
-    if (math >= 2) {
-      // the windowed gather-streamed kernels of the U-Net's deep levels in the two-plane fp16 split, split-K by the
-      // size policy: 2 = cfg 30 (64 x 64 tiles, K split over workgroups), 3 = cfg 33 (64 x 32 tiles, K split over
-      // the waves of a workgroup); a fresh image every call
+    if (math == 2) {
+      // the windowed gather-streamed kernel of the U-Net's deep levels in the two-plane fp16 split (64 x 64 tiles, K
+      // split over workgroups by the size policy); a fresh image every call
       a.wsb = 2;
       a.wsplit_fmt = WSPLIT_H16;
       if (!conv_gsw_eligible(a)) throw Error(RVCX_E_SHAPE, "rvcx_conv2d3x3: shape not eligible for the windowed kernel");
-      if (math == 3 && C_in < 128) throw Error(RVCX_E_SHAPE, "rvcx_conv2d3x3: the wave-split kernel needs C_in >= 128");
       a.w_static = 1;
-      a.force_cfg = math == 3 ? 33 : 30;
+      a.force_cfg = 30;
       void* img = ctx->buf<char>("conv.test.wsplit", (size_t)conv_wsplit_bytes(a), static_cast<hipStream_t>(stream));
       check(conv_wsplit_build(a, img, static_cast<hipStream_t>(stream)), "conv_wsplit_build");
       a.wsplit = img;
@@ -975,6 +897,51 @@ int rvcx_conv2d3x3(rvcx_ctx* ctx, const float* d_x, int H, int W, int C_in, cons
       a.wsplit = img;
     }
     launch_conv(*ctx, a, true, static_cast<hipStream_t>(stream), -1.0);
+  });
+}
+
+int rvcx_convtranspose2d_s2(rvcx_ctx* ctx, const float* d_x, int H, int W, int C_in, const float* d_w,
+                            const float* d_bias, int N, int act, int math, float* d_y, void* stream) {
+  return guard(ctx, [&] {
+    set_device(ctx);
+    ctx->check_device_status();
+    if (!d_x || !d_w || !d_y || H <= 0 || W <= 0 || C_in <= 0 || N <= 0 || act < 0 || act > 1 || math < 0 || math > 1)
+      throw Error(RVCX_E_INVALID, "rvcx_convtranspose2d_s2: bad argument");
+    if ((int64_t)4 * H * W * (C_in > 4 * N ? C_in : 4 * N) > INT32_MAX)
+      throw Error(RVCX_E_SHAPE, "rvcx_convtranspose2d_s2: size out of range");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    // the phase-conv weights (and its bias per virtual column) in test buffers, rebuilt every call
+    float* wp = ctx->buf<float>("conv.test.upw", (size_t)16 * N * C_in, s);
+    check(upconv_phase_pack(d_w, C_in, N, wp, s), "upconv_phase_pack");
+    float* bp = nullptr;
+    if (d_bias) {
+      bp = ctx->buf<float>("conv.test.upb", (size_t)4 * N, s);
+      for (int p = 0; p < 4; ++p)
+        RVCX_HIP(hipMemcpyAsync(bp + (size_t)p * N, d_bias, sizeof(float) * N, hipMemcpyDeviceToDevice, s));
+    }
+    ConvArgs a;  // runtime_fe.cpp's decoder up-conv
+    a.x = d_x; a.ldx = C_in; a.T_in = H; a.W_in = W; a.C_in = C_in;
+    a.w = wp; a.ldw = C_in; a.w_ts = (long long)4 * N * C_in; a.taps = 4; a.KH = 2; a.KW = 2;
+    a.y = d_y; a.ldy = N; a.T_out = H; a.W_out = W; a.N = 4 * N;
+    a.out_map = OUT_UPSAMPLE2D;
+    a.out_cv = N;
+    a.bias = bp;
+    a.act = act ? ACT_RELU : ACT_NONE;
+    a.math = math == 1 ? 1 : 0;
+    if (a.math == 0 && ctx->conv_math > 0) a.math = ctx->conv_math;
+    if (math == 0 && conv_math_of(a) >= 2) {
+      // the gather-streamed kernel the pipeline's policy routes the up-convs to, with a fresh image every call
+      a.wsb = 2;
+      a.wsplit_fmt = conv_math_of(a) == 3 ? WSPLIT_H16 : WSPLIT_BF16;
+      if (!conv_gs_eligible(a, true)) throw Error(RVCX_E_SHAPE, "rvcx_convtranspose2d_s2: shape not eligible");
+      a.w_static = 1;
+      a.force_cfg = 30;
+      void* img = ctx->buf<char>("conv.test.wsplit", (size_t)conv_wsplit_bytes(a), s);
+      check(conv_wsplit_build(a, img, s), "conv_wsplit_build");
+      a.wsplit = img;
+      a.wsplit_npad = conv_wsplit_npad(a.N);
+    }
+    launch_conv(*ctx, a, true, s, -1.0);
   });
 }
 

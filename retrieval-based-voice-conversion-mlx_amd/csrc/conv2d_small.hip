@@ -483,11 +483,8 @@ hipError_t small2d_wsplit_build(const ConvArgs& a, void* out, hipStream_t s) {
 }
 
 hipError_t conv2d_small(const ConvArgs& a, hipStream_t s) {
-  static const bool h16_ok = [] {  // RVCX_SMALL2D_F32=1: the exact-f32 form whatever the conv arithmetic (A/B aid)
-    const char* e = rvcx_knob("RVCX_SMALL2D_F32");
-    return !(e && std::atoi(e) != 0);
-  }();
-  if (h16_ok && conv_math_of(a) == 3 && a.wsplit && a.wsplit_fmt == WSPLIT_S2D) {
+  // the fp16 split (conv math 3) reads the pre-split image; the exact-f32 form serves conv math 1-2
+  if (conv_math_of(a) == 3 && a.wsplit && a.wsplit_fmt == WSPLIT_S2D) {
     hipError_t e = hipErrorInvalidValue;
     if (a.C_in == 16) e = a.N <= 16 ? launch_h16<16, 16>(a, s) : launch_h16<16, 32>(a, s);
     else e = a.N <= 16 ? launch_h16<32, 16>(a, s) : launch_h16<32, 32>(a, s);

@@ -97,87 +97,6 @@ __device__ __forceinline__ void noise_rows(const ConvArgs& a, int b, long long m
   }
 }
 
-// Split-K arrival (ConvArgs::fix_cnt): every thread's write-through slab stores have completed (vmcnt counts stores
-// on gfx9) before the workgroup counts its slice of the tile; true in the last slice to arrive, which resets the
-// counter for the next launch. No workgroup waits for another (nothing spins), so a slice that never runs cannot
-// hang the grid. Slab stores and the last slice's loads are sc1 (device-scope) accesses, coherent across the XCDs'
-// L2s without a release fence or an acquire (cdna_hip_programming.md Guideline 16, the counter row of the sc1 table)
-__device__ __forceinline__ bool splitk_last_arrival(unsigned* cnt, int ksplit) {
-  __shared__ unsigned s_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = old == (unsigned)ksplit - 1u;
-    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = last ? 1u : 0u;
-  }
-  __syncthreads();
-  return s_last != 0u;
-}
-
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-constexpr int BUF_SC1 = 16;  // buffer instruction aux bits: sc1 (write-through store / L2-coherent load)
-
-// The in-kernel split-K combine of store_tile16's tiles. The tile's slab is private to the tile and laid out as the
-// accumulators sit in registers ([slice][wave][tm][tn][lane] f32x4): one 16-B write-through store per accumulator and
-// one 16-B load per accumulator and slice in the last slice (the [row][column] slab of splitk_reduce_kernel needs
-// 4-B stores, ~6x slower per byte write-through). Returns false in every slice but the last; the last leaves the
-// ordered sum of all slices (0 + s0 + s1 + ..., splitk_reduce_kernel's arithmetic) in acc.
-template <int TM16, int TN16, int WM, int WN>
-__device__ __forceinline__ bool splitk_fixup(const ConvArgs& a, int m0, int n0, int b, int zsplit, int ksplit,
-                                             long long Mtot, f32x4 (&acc)[TM16][TN16]) {
-  constexpr int BM = TM16 * 16 * WM, BN = TN16 * 16 * WN;
-  constexpr int TILE = BM * BN;  // floats of one slice's partial tile
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const long long mt = (Mtot + BM - 1) / BM, nt = (a.N + BN - 1) / BN;
-  const long long tile = ((long long)b * mt + m0 / BM) * nt + n0 / BN;
-  const float* base = a.ws + tile * ksplit * TILE;
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)base);
-  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((uintptr_t)base >> 32));
-  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo), 0, ksplit * TILE * 4, 0x00020000);
-  const int lofs = (wave * TM16 * TN16 * 64 + lane) * 16;  // bytes: accumulator (tm, tn) at + (tm TN16 + tn) 1 KB
-#pragma unroll
-  for (int tm = 0; tm < TM16; ++tm)
-#pragma unroll
-    for (int tn = 0; tn < TN16; ++tn)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[tm][tn]), rsrc,
-                                             zsplit * TILE * 4 + lofs + (tm * TN16 + tn) * 1024, 0, BUF_SC1);
-  if (!splitk_last_arrival(a.fix_cnt + tile, ksplit)) return false;
-#pragma unroll
-  for (int tm = 0; tm < TM16; ++tm)
-#pragma unroll
-    for (int tn = 0; tn < TN16; ++tn) acc[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // four slices' loads in flight per group; a slice past the last reloads the last and adds +0 (exact: the running
-  // sum starts at +0 and is never -0), so every load is unconditional
-  for (int s = 0; s < ksplit; s += 4) {
-    f32x4 v[4][TM16][TN16];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int sj = min(s + j, ksplit - 1);
-#pragma unroll
-      for (int tm = 0; tm < TM16; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < TN16; ++tn)
-          v[j][tm][tn] = __builtin_bit_cast(
-              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, sj * TILE * 4 + lofs + (tm * TN16 + tn) * 1024, 0,
-                                                           BUF_SC1));
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const bool in = s + j < ksplit;
-#pragma unroll
-      for (int tm = 0; tm < TM16; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < TN16; ++tn)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[tm][tn][r] += in ? v[j][tm][tn][r] : 0.f;
-    }
-  }
-  return true;
-}
-
 // UP2D: the instantiation may see the ConvTranspose2d phase layout (OUT_UPSAMPLE2D: the 2-D gather-streamed kernel
 // only; compiled out elsewhere)
 template <int TM16, int TN16, int WM, int WN, bool UP2D = false>
@@ -186,9 +105,7 @@ __device__ __forceinline__ void store_tile16(const ConvArgs& a, int m0, int n0, 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int lc = lane & 15, lg = lane >> 4;
-  if (ksplit > 1 && a.fix_cnt) {
-    if (!splitk_fixup<TM16, TN16, WM, WN>(a, m0, n0, b, zsplit, ksplit, Mtot, acc)) return;
-  } else if (ksplit > 1) {
+  if (ksplit > 1) {
 #pragma unroll
     for (int tn = 0; tn < TN16; ++tn) {
       const int n = n0 + wn * TN16 * 16 + tn * 16 + lc;
@@ -290,27 +207,6 @@ __device__ __forceinline__ void store_tile16(const ConvArgs& a, int m0, int n0, 
           const long long m = mb + r;
           const long long oh = m / a.W_out, ow = m - oh * a.W_out;
           Y[((2 * oh + ph) * (2 * a.W_out) + (2 * ow + pw)) * a.ldy + co] = v[r];
-        }
-        continue;
-      }
-      if (a.y_h16) {
-        // the consumer's A operand as the two-plane fp16 image (split_bf16.h put_h16x4 of v * 2^-4): h = f16(x),
-        // l = f16((x - h) 2^11), at bytes [0, 64) and [64, 128) of the row's 32-channel chunk. Lanes 2j and 2j + 1 hold
-        // columns n, n + 1: one DPP swap of the packed {h, l} halves lets the even lane store the h pair and the odd
-        // lane the l pair, one dword each (as many store instructions as the fp32 path, not two 2-byte ones each)
-        const bool odd = (lc & 1) != 0;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float xs = v[r] * (1.f / 16.f);
-          const _Float16 h = (_Float16)xs;
-          const _Float16 l = (_Float16)((xs - (float)h) * 2048.f);
-          const unsigned hl = (unsigned)__builtin_bit_cast(unsigned short, h) |
-                              ((unsigned)__builtin_bit_cast(unsigned short, l) << 16);
-          const unsigned pv = (unsigned)__builtin_amdgcn_mov_dpp((int)hl, 0xB1, 0xF, 0xF, false);  // quad_perm 1,0,3,2
-          const unsigned word = odd ? ((pv >> 16) | (hl & 0xffff0000u)) : ((hl & 0xffffu) | (pv << 16));
-          unsigned* dst = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(Y + (mb + r) * a.ldy + (n & ~31)) +
-                                                      (odd ? 64 : 0) + ((n & 31) & ~1) * 2);
-          if (ok[r]) *dst = word;
         }
         continue;
       }

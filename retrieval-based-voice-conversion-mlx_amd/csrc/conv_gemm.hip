@@ -722,13 +722,9 @@ inline bool tiny_fits(const ConvArgs& a) {
 }
 
 // conv_rows1x1_kernel's shapes: a 1x1 / stride-1 conv (1-D or 2-D) with C_in a multiple of 4 up to 64, 16-B aligned
-// input rows, and conv_tiny_rows_kernel's epilogue conditions (RVCX_NO_ROWS1X1=1: off, A/B aid)
+// input rows, and conv_tiny_rows_kernel's epilogue conditions
 inline bool rows1x1_fits(const ConvArgs& a, bool two_d) {
-  static const bool off = [] {
-    const char* e = rvcx_knob("RVCX_NO_ROWS1X1");
-    return e && std::atoi(e) != 0;
-  }();
-  if (off || a.taps != 1 || a.stride != 1 || a.dil != 1 || a.pad != 0 || a.force_cfg >= 0) return false;
+  if (a.taps != 1 || a.stride != 1 || a.dil != 1 || a.pad != 0 || a.force_cfg >= 0) return false;
   if (two_d && (a.KH != 1 || a.KW != 1 || a.padh != 0 || a.padw != 0 || a.T_in != a.T_out || a.W_in != a.W_out))
     return false;
   const long long rows = two_d ? (long long)a.T_out * a.W_out : a.T_out;
@@ -773,14 +769,6 @@ hipError_t launch_tiny(const ConvArgs& a, bool two_d, hipStream_t s) {
   if (two_d) hipLaunchKernelGGL(conv_tiny_kernel<true>, dim3((unsigned)nb), dim3(256), 0, s, a);
   else hipLaunchKernelGGL(conv_tiny_kernel<false>, dim3((unsigned)nb), dim3(256), 0, s, a);
   return hipGetLastError();
-}
-
-bool xcd_enabled() {
-  static const bool v = [] {
-    const char* e = rvcx_knob("RVCX_NO_XCD");
-    return !(e && std::atoi(e) != 0);
-  }();
-  return v;
 }
 
 // the split-K combine of a gated WaveNet in_layer (ConvArgs::gate_h): the pair (c, c + H) of one output row per thread
@@ -862,7 +850,7 @@ hipError_t launch_cfg(const ConvArgs& a, hipStream_t s) {
   int ksplit = 1;
   if (a.ws && a.ksplit > 1) ksplit = a.ksplit;
   const int ntiles = (a.N + BN - 1) / BN;
-  const int ntn = xcd_enabled() ? ntiles : 0;
+  const int ntn = ntiles;  // XCD-contiguous tile runs (conv_block_coords)
   dim3 grid(ntn ? mtiles * ntiles : mtiles, ntn ? 1 : ntiles, a.batch * a.batch_inner * ksplit);
   auto kern = conv_gemm_kernel<BM, BN, WM, WN, TWO_D, PIPE, ASB, CKT>;
   static size_t smem_set = 64 * 1024;  // per instantiation: raise the dynamic-LDS limit once, not per launch
@@ -895,18 +883,10 @@ hipError_t launch_forced_asb(const ConvArgs& a, hipStream_t s) {
   }
 }
 
-// A-tile staging: serial (1) or 4 loads in flight per thread (4); RVCX_CONV_ASB overrides the default
-inline int default_asb() {
-  static const int v = [] {
-    const char* e = rvcx_knob("RVCX_CONV_ASB");
-    return e ? std::atoi(e) : 1;
-  }();
-  return v;
-}
-
+// A-tile staging: serial (1, the default) or 4 loads in flight per thread (ConvArgs::astage = 4)
 template <bool TWO_D, bool PIPE>
 hipError_t launch_forced(const ConvArgs& a, hipStream_t s) {
-  const int asb = a.astage > 0 ? a.astage : default_asb();
+  const int asb = a.astage > 0 ? a.astage : 1;
   if (!PIPE && asb >= 4) return launch_forced_asb<TWO_D, false, 4>(a, s);
   return launch_forced_asb<TWO_D, PIPE, 1>(a, s);
 }
@@ -915,7 +895,6 @@ hipError_t launch_forced(const ConvArgs& a, hipStream_t s) {
 // one 32x32 accumulator per wave with 4 waves per block beats the larger per-wave tiles in the pipeline:
 // 128x32 for N <= 32 and for the long-tap 1-D convs (the generator's dilated ResBlock convs), 64x64
 // otherwise; split-K when the output grid cannot fill 256 CUs.
-// RVCX_CFG_LONG / RVCX_CFG_SHORT / RVCX_CFG_NARROW override a class (measurement aid).
 inline int env_cfg(const char* name, int dflt) {
   const char* e = rvcx_knob(name);
   return e ? std::atoi(e) : dflt;
@@ -938,33 +917,24 @@ inline int conv_math(const ConvArgs& a) {
 // Tile per shape class in split mode, from build/bench_conv on MI355X (TF/s, split vs the native fp32 kernel):
 // long-tap convs 128x32 (C128 k11 155 vs 114, C256 k11 138 vs 106), short taps and GEMMs 64x64 (C128 k3 + residual
 // 101 vs 78, HuBERT qkv 52 vs 38), narrow short convs (N <= 32, taps < 5: the 32-channel ResBlock k=3, latency
-// bound) stay on the native kernel (53 vs 47): both arithmetics are fp32 accurate, so the choice is per shape.
-// RVCX_ECFG_* override a class (measurement aid; values < 10 select native tiles).
+// bound) stay on the native kernel (53 vs 47): both arithmetics are fp32 accurate, so the choice is per shape. The
+// U-Net's 3x3 convs: 64x64 (C2 26.7 -> 25.9 ms vs 128x64)
 template <bool TWO_D>
 int pick_emu(const ConvArgs& a) {
-  static const int c_long = env_cfg("RVCX_ECFG_LONG", 12);
-  static const int c_short = env_cfg("RVCX_ECFG_SHORT", 13);
-  static const int c_narrow = env_cfg("RVCX_ECFG_NARROW", 12);
-  static const int c_narrow_short = env_cfg("RVCX_ECFG_NARROW_SHORT", 1);
-  static const int c_gemm = env_cfg("RVCX_ECFG_GEMM", 13);
-  static const int c_2d = env_cfg("RVCX_ECFG_2D", 13);  // U-Net 3x3 convs: 64x64 (C2 26.7 -> 25.9 ms vs 128x64)
-  if (TWO_D) return a.N <= 32 ? 12 : c_2d;
-  if (a.N <= 32) return a.taps >= 5 ? c_narrow : c_narrow_short;
-  if (a.taps >= 5) return c_long;
-  if (a.taps == 1 && a.stride == 1) return c_gemm;
-  return c_short;
+  if (TWO_D) return a.N <= 32 ? 12 : 13;
+  if (a.N <= 32) return a.taps >= 5 ? 12 : 1;
+  if (a.taps >= 5) return 12;
+  return 13;
 }
 
 template <bool TWO_D>
 int pick_cfg(const ConvArgs& a) {
   if (a.force_cfg >= 0) return a.force_cfg;
   if (conv_math(a) >= 2) return pick_emu<TWO_D>(a);
-  static const int c_long = env_cfg("RVCX_CFG_LONG", 1);      // 1-D, taps >= 5, N > 32 (A/B: 32.8 vs 33.6 ms)
-  static const int c_short = env_cfg("RVCX_CFG_SHORT", 3);    // everything else with N > 32
-  static const int c_narrow = env_cfg("RVCX_CFG_NARROW", 1);  // N <= 32
-  if (a.N <= 32) return c_narrow;
-  if (!TWO_D && a.taps >= 5) return c_long;
-  return c_short;
+  // N <= 32 and the 1-D convs with taps >= 5 (A/B: 32.8 vs 33.6 ms): 128 x 32; everything else 64 x 64
+  if (a.N <= 32) return 1;
+  if (!TWO_D && a.taps >= 5) return 1;
+  return 3;
 }
 
 inline void cfg_tile(int cfg, int& BM, int& BN) {
@@ -973,14 +943,6 @@ inline void cfg_tile(int cfg, int& BM, int& BN) {
                                {64, 64}, {128, 32}, {128, 128}};
   BM = t[cfg][0];
   BN = t[cfg][1];
-}
-
-inline bool small2d_enabled() {
-  static const bool v = [] {
-    const char* e = rvcx_knob("RVCX_NO_SMALL2D");
-    return !(e && std::atoi(e) != 0);
-  }();
-  return v;
 }
 
 // weight-streamed split kernel (conv_wsb.hip) tiles: 256x32 for N <= 32, else 128x64 (2 x 2 waves of 64 x 32;
@@ -996,21 +958,18 @@ inline bool small2d_enabled() {
 // blocks), k = 7 / 11 at C_in <= 128 a little on 28 (C128 k11 244 -> 252), C256 k11 loses on 28 (208 -> 171). In the
 // C2 step (rocprof r03ab, weight-streamed time per step): 27 for k <= 3 7969 -> 7919 us, 28 for k = 7 / 11 +147 us
 // (cold activations, 2 workgroups per CU), so the long convs stay on 23 (RVCX_WCFG_LONG=28 to compare)
+// Round 6: the 128-channel k = 7 / 11 convs on 128 x 128 tiles (cfg 25, 2 x 2 waves of 64 x 64: C128 k11 402 vs 380
+// TF, k7 346 vs 340 in bench_conv r06a; same-box C2 12.91 / 12.99 vs 13.04 / 13.01 ms, r06b); at 256 input channels
+// (C256 k11 288 vs 330) and 64 output channels (half of each tile idle) cfg 23 stays. RVCX_WCFG_LONG forces one tile
+// for every long conv (A/B aid)
 inline int pick_wsb(const ConvArgs& a) {
-  static const int c_narrow = env_cfg("RVCX_WCFG_NARROW", 24);
-  static const int c_short = env_cfg("RVCX_WCFG_SHORT", 27);
-  static const int c_long = env_cfg("RVCX_WCFG_LONG", 23);
-  static const int c_wide = env_cfg("RVCX_WCFG_WIDE", 23);
-  static const int c_gs = env_cfg("RVCX_GCFG", 30);
-  // the U-Net's deep 3x3 levels (>= 4 chunks of 32 input channels) on the wave-K-split windowed kernel (cfg 33)
-  static const bool gswk = env_cfg("RVCX_GSWK", 0) != 0;
-  if (a.wsb == 2 && gswk && a.KH == 3 && a.C_in >= 4 * CK && conv_math(a) == 3 && conv_gsw_eligible(a)) return 33;
-  if (a.wsb == 2) return c_gs;  // gather-streamed (conv_gs.hip): the short contractions
-  if (a.N <= 32) return c_narrow;
-  if (a.taps <= 3) return c_short;
-  return a.C_in >= 256 ? c_wide : c_long;
+  static const int c_long = env_cfg("RVCX_WCFG_LONG", 0);
+  if (a.wsb == 2) return 30;  // gather-streamed (conv_gs.hip): the short contractions
+  if (a.N <= 32) return 24;
+  if (a.taps <= 3) return 27;
+  if (c_long > 0) return c_long;
+  return (a.C_in < 256 && a.N >= 128) ? 25 : 23;
 }
-inline bool cfg_is_gs(int cfg) { return cfg >= 30; }
 }  // namespace
 int conv_wsb_pick(const ConvArgs& a) {
   ConvArgs b = a;
@@ -1028,41 +987,16 @@ const char* conv_kind_name(int k) {
 
 namespace {
 
-// RVCX_SPLITK_FIXUP=1 (A/B aid, off by default): split-K launches of the store_tile16 kernels combine in-kernel (the
-// last slice of a tile sums the write-through slabs) instead of in a separate splitk_reduce_kernel launch. Correct
-// (the whole -m gpu suite passes with it on, r05n) but not faster here: the U-Net's deep-level convs went from
-// ~10 + 5 us (conv + combine launch) to 15-19 us per conv, the last slice's write-through drain, ticket and serial
-// slab read costing what the kernel boundary did; same-box C2 13.03 / 13.07 ms on vs 12.99 / 12.98 off
-bool splitk_fixup_on() {
-  static const bool v = [] {
-    const char* e = rvcx_knob("RVCX_SPLITK_FIXUP");
-    return e && std::atoi(e) != 0;
-  }();
-  return v;
-}
-
-// whether a split launch on BM x BN tiles may combine in-kernel (store_tile16's last-arrival fix-up): the plain
-// epilogue, and one arrival counter per tile within the caller's counter array
-bool fixup_fits(const ConvArgs& a, unsigned* cnt, int BM, int BN, bool two_d) {
-  if (!cnt || !splitk_fixup_on() || a.ln_g || a.gate_h > 0 || a.batch_inner != 1) return false;
-  const long long M = two_d ? (long long)a.T_out * a.W_out : (long long)a.T_out;
-  const long long tiles = (long long)a.batch * ((M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  return tiles <= a.fix_cap;
-}
-
 template <bool TWO_D>
 hipError_t dispatch(const ConvArgs& a_in, hipStream_t s) {
-  // the counters go only to the launches whose epilogue is store_tile16 (decided per path below)
-  ConvArgs a = a_in;
-  unsigned* const fix_cnt = a.fix_cnt;
-  a.fix_cnt = nullptr;
+  const ConvArgs& a = a_in;
   if (a.N <= 0 || a.T_out <= 0 || a.batch <= 0) return hipSuccess;
   if (a.C_in <= 0 || a.taps <= 0) return hipErrorInvalidValue;
   // the fused noise conv lives in store_tile16's unsplit epilogue only (the caller routes it to such a kernel)
   const bool nz = a.nz_har != nullptr;
   if (nz && (TWO_D || (a.ws && a.ksplit > 1) || a.nz_C <= 0 || a.nz_stride <= 0 ||
              a.nz_kk != 1 ||
-             a.N != a.nz_u * a.nz_C || a.out_map != OUT_ROWS || a.y_h16))
+             a.N != a.nz_u * a.nz_C || a.out_map != OUT_ROWS))
     return hipErrorInvalidValue;
   // the gate and the LayerNorm are applied by the combine
   if ((a.gate_h > 0 || a.ln_g) && !(a.ws && a.ksplit > 1)) return hipErrorInvalidValue;
@@ -1078,31 +1012,22 @@ hipError_t dispatch(const ConvArgs& a_in, hipStream_t s) {
   if (a.wsb == 2 && a.wsplit && conv_math(a) >= 2 && conv_gs_eligible(a, TWO_D)) {
     const int ks = (a.ws && a.ksplit > 1) ? a.ksplit : 1;
     const int cfg = a.force_cfg >= 30 ? a.force_cfg : pick_wsb(a);
-    g_conv_kind = (TWO_D && (cfg == 30 || cfg == 33) && conv_gsw_eligible(a)) ? CK_GSW : CK_GS;
-    int BM = 0, BN = 0;
-    conv_gs_tile(cfg, BM, BN);
-    ConvArgs f = a;
-    if (ks > 1 && fixup_fits(a, fix_cnt, BM, BN, TWO_D)) f.fix_cnt = fix_cnt;
-    hipError_t e = conv_gs_launch(f, cfg, xcd_enabled() ? 1 : 0, s, TWO_D, ks);
-    if (e == hipSuccess && ks > 1 && !f.fix_cnt) e = launch_splitk_reduce(a, ks, TWO_D, s);
+    g_conv_kind = (TWO_D && cfg == 30 && conv_gsw_eligible(a)) ? CK_GSW : CK_GS;
+    hipError_t e = conv_gs_launch(a, cfg, 1, s, TWO_D, ks);
+    if (e == hipSuccess && ks > 1) e = launch_splitk_reduce(a, ks, TWO_D, s);
     if (e != hipErrorInvalidValue) return e;
   }
   if (a.wsb == 1 && a.wsplit && conv_math(a) >= 2 && conv_wsb_eligible(a, TWO_D)) {
     const int ks = (a.ws && a.ksplit > 1) ? a.ksplit : 1;
-    const int cfg = TWO_D ? 21 : (a.force_cfg >= 20 ? a.force_cfg : pick_wsb(a));
-    if (nz && cfg < 23) return hipErrorInvalidValue;
-    g_conv_kind = cfg >= 23 ? CK_WSB16 : CK_WSB;
-    int BM = 0, BN = 0;
-    conv_wsb_tile(cfg, BM, BN);
-    ConvArgs f = a;  // the fp16 kernel's epilogue is store_tile16; the three-plane one's is conv_store_tile
-    if (ks > 1 && cfg >= 23 && !TWO_D && fixup_fits(a, fix_cnt, BM, BN, TWO_D)) f.fix_cnt = fix_cnt;
-    hipError_t e = conv_wsb_launch(f, cfg, xcd_enabled() ? 1 : 0, s, TWO_D, ks);
-    if (e == hipSuccess && ks > 1 && !f.fix_cnt) e = launch_splitk_reduce(a, ks, TWO_D, s);
+    const int cfg = a.force_cfg >= 20 ? a.force_cfg : pick_wsb(a);
+    g_conv_kind = CK_WSB16;
+    hipError_t e = conv_wsb_launch(a, cfg, 1, s, TWO_D, ks);
+    if (e == hipSuccess && ks > 1) e = launch_splitk_reduce(a, ks, TWO_D, s);
     if (e != hipErrorInvalidValue) return e;
   }
   if (nz) return hipErrorInvalidValue;  // no store_tile16 kernel took it
   // 3x3 convs with 16/32 channels: 16x16x4 MFMA fragments (conv2d_small.hip)
-  if (TWO_D && a.force_cfg < 0 && small2d_enabled() && conv2d_small_fits(a)) {
+  if (TWO_D && a.force_cfg < 0 && conv2d_small_fits(a)) {
     g_conv_kind = CK_SMALL2D;
     return conv2d_small(a, s);
   }
@@ -1110,18 +1035,14 @@ hipError_t dispatch(const ConvArgs& a_in, hipStream_t s) {
   g_conv_kind = cfg >= 10 ? CK_EMU : CK_GEMM;
   ConvArgs b = a;
   b.force_cfg = cfg;
-  // plain GEMMs (1-D, one tap, stride 1) take the double-buffered pipeline unless a.pipe < 0 or
-  // RVCX_NO_PIPE=1; a.pipe > 0 forces it (benchmarks)
-  static const bool pipe_env = [] {
-    const char* e = rvcx_knob("RVCX_NO_PIPE");
-    return !(e && std::atoi(e) != 0);
-  }();
+  // plain GEMMs (1-D, one tap, stride 1) take the double-buffered pipeline unless a.pipe < 0; a.pipe > 0 forces it
+  // (benchmarks)
   const bool gemm = !TWO_D && a.taps == 1 && a.stride == 1;
-  const bool pipe = gemm && (a.pipe > 0 || (a.pipe == 0 && pipe_env));
+  const bool pipe = gemm && a.pipe >= 0;
   if (cfg >= 10) {
     auto run = [&](int c, bool p) -> hipError_t {
       const int ksplit = (b.ws && b.ksplit > 1) ? b.ksplit : 1;
-      hipError_t e = conv_emu_launch(b, c, TWO_D, p, ksplit, xcd_enabled() ? 1 : 0, s);
+      hipError_t e = conv_emu_launch(b, c, TWO_D, p, ksplit, 1, s);
       if (e != hipSuccess || ksplit == 1) return e;
       return launch_splitk_reduce(b, ksplit, TWO_D, s);
     };
@@ -1156,12 +1077,12 @@ long long conv_plan_splitk(ConvArgs& a, bool two_d) {
   a.ksplit = 1;
   if (a.N <= 0 || a.T_out <= 0 || a.no_splitk) return 0;
   if (tiny_fits(a)) return 0;
-  if (two_d && a.force_cfg < 0 && small2d_enabled() && conv2d_small_fits(a)) return 0;
+  if (two_d && a.force_cfg < 0 && conv2d_small_fits(a)) return 0;
   int BM, BN;
   if (a.wsb == 2) {  // the gather-streamed tile
     conv_gs_tile(a.force_cfg >= 30 ? a.force_cfg : pick_wsb(a), BM, BN);
-  } else if (a.wsb) {  // the weight-streamed tile (pick_wsb; 2-D: 128 x 64)
-    conv_wsb_tile(two_d ? 21 : (a.force_cfg >= 20 ? a.force_cfg : pick_wsb(a)), BM, BN);
+  } else if (a.wsb) {  // the weight-streamed tile (pick_wsb)
+    if (!conv_wsb_tile(a.force_cfg >= 20 ? a.force_cfg : pick_wsb(a), BM, BN)) return 0;
   } else {
     cfg_tile(two_d ? pick_cfg<true>(a) : pick_cfg<false>(a), BM, BN);
   }
@@ -1175,18 +1096,6 @@ long long conv_plan_splitk(ConvArgs& a, bool two_d) {
   }
   const long long tiles = mtiles * ((a.N + BN - 1) / BN) * a.batch * a.batch_inner;
   const int iters = ((a.C_in + CK - 1) / CK) * a.taps;
-  if (a.wsb == 2 && two_d && BN == 32 && (a.force_cfg < 0 || a.force_cfg == 33) && a.gate_h == 0 && !a.ln_g) {
-    // cfg 33 (conv_gsw16k_kernel): workgroups split K over their 4 waves; split K over workgroups as well only until the
-    // grid reaches the target, and never below one chunk per wave
-    static const int t33 = env_cfg("RVCX_GSWK_TARGET", 256);
-    const int nch = (a.C_in + CK - 1) / CK;
-    int ks = (int)std::min<long long>((t33 + tiles - 1) / tiles, nch / 4);
-    if (ks < 2) return 0;
-    a.ksplit = ks;
-    a.ws_rows = (long long)a.T_out * a.W_out;
-    // the in-kernel combine's tile-private slabs cover whole tiles (store_tile16 splitk_fixup)
-    return std::max((long long)ks * a.ws_rows * a.N * a.batch * a.batch_inner, tiles * ks * BM * BN);
-  }
   const double M = two_d ? (double)a.T_out * a.W_out : (double)a.T_out;
   const double flops = 2.0 * M * a.N * (double)a.C_in * a.taps * a.batch * a.batch_inner;
   // split only where the output grid leaves CUs idle AND the contraction is long enough to pay
@@ -1196,9 +1105,9 @@ long long conv_plan_splitk(ConvArgs& a, bool two_d) {
   // steps = 264 us unsplit)
   // same-box A/B of C2 (round 2, with the 32-bit combine): (target, tiles, min_iters) = (512, 192, 4) 22.59 ms,
   // (768, 384, 8) 22.82, (512, 256, 4) 22.70, (384, 256, 4) 22.64, (1024, 384, 8) 23.33
-  static const int target = env_cfg("RVCX_SPLITK_TARGET", 512);   // workgroups a split launch aims for
-  static const int min_tiles = env_cfg("RVCX_SPLITK_TILES", 192);  // grids with at least this many tiles stay unsplit
-  static const int min_iters = env_cfg("RVCX_SPLITK_MINITERS", 4);  // shortest contraction worth a split
+  static const int target = env_cfg("RVCX_SPLITK_TARGET", 512);  // workgroups a split launch aims for
+  constexpr int min_tiles = 192;  // grids with at least this many tiles stay unsplit
+  constexpr int min_iters = 4;    // shortest contraction worth a split
   // a gated WaveNet in_layer always splits: its gate lives in the combine (ConvArgs::gate_h)
   const bool combine_epi = a.gate_h > 0 || a.ln_g;  // an epilogue only the combine applies: always split
   if (!combine_epi && (tiles >= min_tiles || iters < min_iters || (flops < 1.0e8 && iters < 16))) return 0;
@@ -1207,7 +1116,7 @@ long long conv_plan_splitk(ConvArgs& a, bool two_d) {
   // epilogue and the extra slab + combine launch cost more than the parallelism gains (bench_gs r03s, cold: HuBERT
   // 768 -> 768 ks 1 22.1 us vs ks 4 27.6, TextEncoder 1x1 ks 1 11.6 vs ks 3 14.4, U-Net 196 px ks 8 19.8 vs ks 16
   // 21.8, 3136 px ks 2 20.2 vs ks 6 27.3; the 3072 -> 768 linear keeps ks 4: 48.6 vs 62.8 unsplit)
-  static const int gs_min_steps = env_cfg("RVCX_GS_MINSTEPS", 8);  // same-box C2: 2 17.73, 8 17.72, 16 17.86, 24 17.97 ms
+  constexpr int gs_min_steps = 8;  // same-box C2: 2 17.73, 8 17.72, 16 17.86, 24 17.97 ms
   ks = std::min(ks, a.wsb == 2 ? iters / gs_min_steps : iters / 2);
   ks = std::min(ks, 32);
   // the windowed 2-D gather-streamed kernel splits by whole 32-channel chunks (bench_gs: U-Net 784 px ks 8 and 3136 px
@@ -1222,36 +1131,26 @@ long long conv_plan_splitk(ConvArgs& a, bool two_d) {
 }
 
 bool conv_wsb_wants(const ConvArgs& a) {
-  static const bool off = [] {
-    const char* e = rvcx_knob("RVCX_NO_WSB");
-    return e && std::atoi(e) != 0;
-  }();
-  if (off || conv_math(a) < 2 || !conv_wsb_eligible(a)) return false;
+  if (conv_math(a) < 2 || !conv_wsb_eligible(a)) return false;
   // where it measured faster (bench_conv, profiles/r02i_bench_conv.txt: 128 x 64 tiles of 2 x 2 waves of 64 x 32
   // with the register epilogue; C2 A/B): N >= 64 with >= 2 taps (ResBlock convs at 64-256 channels incl. k = 3, the
-  // polyphase ConvTranspose phases), on a grid that fills the chip (RVCX_WSB_MINN / _MINTAPS / _MINTILES: A/B aid)
-  static const int min_taps = env_cfg("RVCX_WSB_MINTAPS", 2);
-  static const int min_tiles = env_cfg("RVCX_WSB_MINTILES", 512);
-  static const int min_n = env_cfg("RVCX_WSB_MINN", 64);  // A/B: the 64-channel stage on 128x64 tiles beat the fused pair
+  // polyphase ConvTranspose phases; the 64-channel stage on 128x64 tiles beat the fused pair), on a grid that fills
+  // the chip
+  constexpr int min_taps = 2, min_tiles = 512, min_n = 64;
   if (a.N < min_n || a.taps < min_taps) return false;
   const long long tiles = (long long)((a.T_out + 127) / 128) * ((a.N + 63) / 64) * a.batch;
   return tiles >= min_tiles;
 }
 
 int conv_wsb_route(const ConvArgs& a, bool two_d) {
-  static const bool split_1d = env_cfg("RVCX_WSB_SPLIT", 0) != 0;  // small 1-D grids with split-K
-  static const bool route_2d = env_cfg("RVCX_WSB_2D", 0) != 0;     // 3x3 2-D convs, >= 64 channels
-  static const bool gs_on = env_cfg("RVCX_NO_GS", 0) == 0;         // the gather-streamed kernel (A/B aid)
-  static const int gs_min_n = env_cfg("RVCX_GS_MINN", 64);
   if (conv_math(a) < 2 || tiny_fits(a)) return 0;
-  if (two_d && small2d_enabled() && conv2d_small_fits(a)) return 0;
-  if (conv_wsb_eligible(a, two_d)) {
-    if (two_d && route_2d && a.N >= 64 && a.C_in >= 64) return 1;
-    if (!two_d && conv_wsb_wants(a)) return 1;
-    if (!two_d && split_1d && a.N >= 64) return 1;
-  }
+  if (two_d && conv2d_small_fits(a)) return 0;
+  // the weight-streamed kernel on small grids (split-K) and on the U-Net's 3x3 convs measured slower than the
+  // gather-streamed one (HuBERT / TextEncoder GEMMs +0.7 ms, U-Net +0.8 ms: with few M tiles every wave re-streams its
+  // B fragments from L2)
+  if (!two_d && conv_wsb_wants(a)) return 1;
   // everything else with a static weight, 32-channel chunks and >= 64 outputs: the short contractions
-  if (gs_on && a.N >= gs_min_n && conv_gs_eligible(a, two_d)) return 2;
+  if (a.N >= 64 && conv_gs_eligible(a, two_d)) return 2;
   return 0;
 }
 

@@ -319,15 +319,10 @@ hipError_t launch_gs(const ConvArgs& a, int ntn_enable, int ksplit, hipStream_t 
   const size_t smem = std::min((size_t)2 * BM * (h16 ? ERS_H : ERS) + (size_t)std::max(0, a.lds_pad),
                                std::max((size_t)2 * BM * (h16 ? ERS_H : ERS), (size_t)160 * 1024));
   // M-fastest tile runs when the pre-split weight (6 B per element) outweighs the activation operand (4 B)
-  static const int mf_env = [] {
-    const char* e = rvcx_knob("RVCX_GS_MFAST");
-    return e ? std::atoi(e) : -1;
-  }();
   const double wbytes = 6.0 * a.N * a.C_in * a.taps, abytes = 4.0 * (double)Mtot * a.C_in * a.batch;
-  const int mfast = mf_env >= 0 ? mf_env : (wbytes > abytes ? 1 : 0);
+  const int mfast = wbytes > abytes ? 1 : 0;
   const int mode = pre_mode(a.pre_act) | (!TWO_D && a.pre_mask ? 4 : 0) | (h16 ? 16 : 0);
-  if (h16 && !(BM == 64 && BN == 64)) return hipErrorInvalidValue;  // the fp16 instantiations: the policy's tile only
-  constexpr bool HI = BM == 64 && BN == 64;
+  constexpr bool HI = true;
   switch (mode) {
     case 0: launch_gs_mode<BM, BN, WM, WN, TWO_D, 0>(a, grid, smem, ntn, ksplit, mfast, s); break;
     case 1: launch_gs_mode<BM, BN, WM, WN, TWO_D, 1>(a, grid, smem, ntn, ksplit, mfast, s); break;
@@ -528,205 +523,6 @@ __global__ __launch_bounds__(CONV_THREADS, 2) void conv_gsw16_kernel(const ConvA
   store_tile16<TM16, TN16, WM, WN>(a, h0 * W, n0, b, zsplit, ksplit, (long long)H * W, acc);
 }
 
-// ---- The same windowed 3x3 convs with the K walk split over the WAVES of a workgroup (round 5, cfg 33; the U-Net's
-// deep levels). A 64 x 32 tile (64 pixels = 64 / W image rows, 32 output channels) per workgroup;
-// wave w takes the chunks c0 + w, c0 + w + 4, ... of the workgroup's chunk range and computes the WHOLE tile over
-// them: it stages its own chunk's window into its own LDS window (no workgroup barrier in the main loop), prefetching
-// its next chunk's window into registers during the 9 taps, B from the lane-major fp16 image one step ahead. The
-// four partial tiles are summed through LDS in a fixed order (deterministic) and stored by the four waves, 16 rows
-// each. Against cfg 30 (64 x 64 tiles, the K walk split over workgroups through HBM slabs and a combine launch)
-// the split-K slabs and combine launches of these levels go away or shrink four-fold.
-constexpr int GSWK_WV = (GSW_WROWS * EC4 + 63) / 64;  // float4 groups of one window per lane
-constexpr int GSWK_WIN = GSW_WROWS * ERS_H;           // LDS bytes of one wave's window
-constexpr int GSWK_RED_LD = 33;                       // floats per row of a partial tile in LDS (conflict padding)
-template <int MODE>
-__global__ __launch_bounds__(CONV_THREADS, 2) void conv_gsw16k_kernel(const ConvArgs a, const char* __restrict__ wsp,
-                                                                      const int Npad, const int ntn, const int ksplit,
-                                                                      const int mfast) {
-  constexpr int BN = 32, TM16 = 4, TN16 = 2, NQ = 2, RS = ERS_H;
-  constexpr int PA = MODE & 3;
-  extern __shared__ __attribute__((aligned(16))) char smem_gswk[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int lc = lane & 15, lg = lane >> 4;
-  int bx, by, bz;
-  conv_block_coords(ntn, bx, by, bz);
-  if (mfast && ntn > 0) {
-    const int t = bx * ntn + by;
-    const int mt = (int)gridDim.x / ntn;
-    bx = t % mt;
-    by = t / mt;
-  }
-  const int zsplit = bz % ksplit;
-  const int b = bz / ksplit;
-  const int n0 = by * BN;
-  const int W = a.W_out, H = a.T_out;
-  const int rh = 64 / W, aw = W + 2;
-  const int h0 = bx * rh;
-  const int nwin = (rh + 2) * aw;
-  const float* X = a.x + (long long)b * a.x_bs;
-  const int nch = a.C_in / EK;
-  const int pc = (nch + ksplit - 1) / ksplit;
-  const int c0 = zsplit * pc, c1 = min(nch, c0 + pc);
-  char* win = smem_gswk + wave * GSWK_WIN;
-
-  // ---- this wave's window staging: slot i = v * 64 + lane -> window pixel i / 8, channels 4 (i % 8) ..
-  f32x4 wr_[GSWK_WV];
-  unsigned wok = 0u;
-  auto load_win = [&](int ch) __attribute__((always_inline)) {
-    wok = 0u;
-#pragma unroll
-    for (int v = 0; v < GSWK_WV; ++v) {
-      const int i = v * 64 + lane;
-      const int r = i >> 3, c4 = (i & 7) << 2;
-      const int wh = r / aw, wc = r - wh * aw;
-      const int ih = h0 - 1 + wh, iw = wc - 1;
-      const bool ok = r < nwin && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
-      const unsigned g = ok ? (unsigned)(ih * W + iw) : 0u;
-      wr_[v] = *reinterpret_cast<const f32x4*>(X + ch * EK + c4 + g * (unsigned)a.ldx);  // branch-free
-      wok |= ok ? (1u << v) : 0u;
-    }
-  };
-  auto store_win = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int v = 0; v < GSWK_WV; ++v) {
-      const int i = v * 64 + lane;
-      const int r = i >> 3, c4 = (i & 7) << 2;
-      if (r < nwin) {
-        f32x4 val = wr_[v];
-        const bool ok = (wok >> v) & 1u;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) val[j] = ok ? pre_fn<PA>(val[j], a.pre_act, a.pre_slope) * H16_XS : 0.f;
-        put_h16x4<2>(win + r * RS, c4, val);
-      }
-    }
-  };
-  // ---- B: this wave's two 16-column groups of the image, one step ahead in registers
-  typedef bf16x8 BFrag[TN16][NQ];
-  const char* bp = wsp + (size_t)(n0 >> 4) * (NQ * GS_BLK) + lane * 16;
-  const size_t bstep = (size_t)Npad * NQ * PLANE;
-  auto load_b = [&](int st, BFrag& dst) __attribute__((always_inline)) {
-    const char* p = bp + (size_t)st * bstep;
-#pragma unroll
-    for (int tn = 0; tn < TN16; ++tn)
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) dst[tn][q] = *reinterpret_cast<const bf16x8*>(p + tn * (NQ * GS_BLK) + q * GS_BLK);
-  };
-  f32x4 acc[TM16][TN16], acc2[TM16][TN16];
-#pragma unroll
-  for (int tm = 0; tm < TM16; ++tm)
-#pragma unroll
-    for (int tn = 0; tn < TN16; ++tn) acc[tm][tn] = acc2[tm][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int aoff[TM16];
-#pragma unroll
-  for (int tm = 0; tm < TM16; ++tm) {
-    const int ml = tm * 16 + lc;
-    const int r = ml / W, c = ml - r * W;
-    aoff[tm] = (r * aw + c) * RS + lg * 16;
-  }
-  auto compute = [&](int tap, const BFrag& bf) __attribute__((always_inline)) {
-    const int toff = ((tap / 3) * aw + (tap % 3)) * RS;
-#pragma unroll
-    for (int tm = 0; tm < TM16; ++tm) {
-      bf16x8 af[NQ];
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) af[q] = *reinterpret_cast<const bf16x8*>(win + aoff[tm] + toff + q * PLANE);
-      mma_h16(af, bf, acc[tm], acc2[tm]);
-    }
-  };
-  const int my0 = c0 + wave;  // this wave's chunks: my0, my0 + 4, ... < c1
-  if (my0 < c1) {
-    BFrag b0, b1;
-    const int last = ((c1 - 1 - my0) / 4) * 4 + my0;  // this wave's last chunk
-    load_win(my0);
-    load_b(my0 * 9, b0);
-    for (int ch = my0; ch < c1; ch += 4) {
-      store_win();
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (ch + 4 < c1) load_win(ch + 4);
-      const int base = ch * 9;
-      const int nxt = ch + 4 < c1 ? (ch + 4) * 9 : last * 9 + 8;  // the step after this chunk's last (clamped)
-#pragma unroll
-      for (int tap = 0; tap < 9; tap += 2) {
-        load_b(tap + 1 < 9 ? base + tap + 1 : nxt, b1);
-        __builtin_amdgcn_sched_barrier(0);
-        compute(tap, b0);
-        if (tap + 1 < 9) {
-          load_b(tap + 2 < 9 ? base + tap + 2 : nxt, b0);
-          __builtin_amdgcn_sched_barrier(0);
-          compute(tap + 1, b1);
-        }
-      }
-      // taps 0..8: the odd count leaves the next chunk's first fragments in b1; move them to b0
-#pragma unroll
-      for (int tn = 0; tn < TN16; ++tn)
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) b0[tn][q] = b1[tn][q];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();  // every lane done reading this window before the next chunk's store
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-  }
-  // acc + 2^-11 acc2 times the column scales (h16_finish: this wave covers the whole 32-column tile, WN = 1)
-  h16_finish<TM16, TN16, 1>(wsp, (size_t)nch * 9 * bstep, n0, acc, acc2);
-  // ---- the four partial tiles through LDS (windows are dead after the barrier), summed in wave order
-  __syncthreads();
-  float* red = reinterpret_cast<float*>(smem_gswk);
-  float* mine = red + wave * 64 * GSWK_RED_LD;
-#pragma unroll
-  for (int tm = 0; tm < TM16; ++tm)
-#pragma unroll
-    for (int tn = 0; tn < TN16; ++tn)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) mine[(tm * 16 + 4 * lg + r) * GSWK_RED_LD + tn * 16 + lc] = acc[tm][tn][r];
-  __syncthreads();
-  f32x4 out[1][TN16];
-#pragma unroll
-  for (int tn = 0; tn < TN16; ++tn)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int o = (wave * 16 + 4 * lg + r) * GSWK_RED_LD + tn * 16 + lc;
-      out[0][tn][r] = ((red[o] + red[64 * GSWK_RED_LD + o]) + red[2 * 64 * GSWK_RED_LD + o]) + red[3 * 64 * GSWK_RED_LD + o];
-    }
-  store_tile16<1, TN16, 4, 1>(a, h0 * W, n0, b, zsplit, ksplit, (long long)H * W, out);
-}
-
-template <int MODE>
-void launch_gswk_mode(const ConvArgs& a, dim3 grid, size_t smem, int ntn, int ksplit, int mfast, hipStream_t s) {
-  auto kern = conv_gsw16k_kernel<MODE>;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              4 * GSWK_WIN);
-    attr = true;
-  }
-  hipLaunchKernelGGL(kern, grid, dim3(CONV_THREADS), smem, s, a, static_cast<const char*>(a.wsplit), a.wsplit_npad, ntn,
-                     ksplit, mfast);
-}
-
-hipError_t launch_gswk(const ConvArgs& a, int ntn_enable, int ksplit, hipStream_t s) {
-  const int W = a.W_out, rh = 64 / W;
-  const long long mtiles = (a.T_out + rh - 1) / rh;
-  if (a.wsplit_fmt != WSPLIT_H16 || a.wsplit_npad % 32 != 0 || ksplit < 1 || (ksplit > 1 && !a.ws) ||
-      mtiles > INT32_MAX / 64)
-    return hipErrorInvalidValue;
-  const int ntiles = (a.N + 31) / 32;
-  const int ntn = ntn_enable ? ntiles : 0;
-  dim3 grid((unsigned)(ntn ? mtiles * ntiles : mtiles), ntn ? 1 : ntiles, a.batch * ksplit);
-  const size_t smem = std::max((size_t)4 * GSWK_WIN, (size_t)4 * 64 * GSWK_RED_LD * sizeof(float));
-  const double wbytes = 4.0 * a.N * a.C_in * 9, abytes = 4.0 * (double)a.T_out * W * a.C_in * a.batch;
-  const int mfast = wbytes > abytes ? 1 : 0;
-  switch (pre_mode(a.pre_act)) {
-    case 0: launch_gswk_mode<16>(a, grid, smem, ntn, ksplit, mfast, s); break;
-    case 1: launch_gswk_mode<17>(a, grid, smem, ntn, ksplit, mfast, s); break;
-    default: launch_gswk_mode<18>(a, grid, smem, ntn, ksplit, mfast, s); break;
-  }
-  return hipGetLastError();
-}
-
 template <int MODE>
 void launch_gsw_mode(const ConvArgs& a, dim3 grid, size_t smem, int ntn, int ksplit, int mfast, hipStream_t s) {
   hipLaunchKernelGGL((conv_gsw16_kernel<MODE>), grid, dim3(CONV_THREADS), smem, s, a,
@@ -762,7 +558,7 @@ bool conv_gs_eligible(const ConvArgs& a, bool two_d) {
   // the 2x2-phase ConvTranspose2d output (OUT_UPSAMPLE2D, the U-Net decoder's up-convs, round 5) with the plain epilogue
   // (store_tile16 maps it; a split launch's combine does, as for the LDS-staged kernel)
   const bool up2d = two_d && a.out_map == OUT_UPSAMPLE2D && a.out_cv > 0 && a.N == 4 * a.out_cv && !a.res &&
-                    a.acc_mode == ACC_STORE && !a.mask && !a.y_h16 && !a.nz_har;
+                    a.acc_mode == ACC_STORE && !a.mask && !a.nz_har;
   const bool common = a.batch_inner == 1 && !a.b_kn && a.C_in % EK == 0 && a.C_in > 0 && a.taps >= 1 && vec_a &&
                       (a.out_map == OUT_ROWS || up2d) && a.stride >= 1 && a.dil >= 1;
   if (!common) return false;
@@ -773,44 +569,27 @@ bool conv_gs_eligible(const ConvArgs& a, bool two_d) {
   return a.taps == a.KH * a.KW && !a.pre_mask && a.stride == 1 && a.W_out >= 1 && a.W_in >= 1;
 }
 
-// cfg 30: 64 x 64 (2 x 2 waves of 32 x 32), 31: 128 x 64 (2 x 2 waves of 64 x 32), 32: 64 x 128 (2 x 2 of 32 x 64),
-// 33: 64 x 32 with the K walk split over the 4 waves (the windowed 3x3 form only, conv_gsw16k_kernel)
+// cfg 30: 64 x 64 (2 x 2 waves of 32 x 32). Round 5's 64 x 32 tiles with the K walk split over the 4 waves of a
+// workgroup (the windowed form, cfg 33) and the 128 x 64 / 64 x 128 tiles (31, 32) measured no faster and are gone
 bool conv_gs_tile(int cfg, int& BM, int& BN) {
-  static const int t[4][2] = {{64, 64}, {128, 64}, {64, 128}, {64, 32}};
-  if (cfg < 30 || cfg > 33) return false;
-  BM = t[cfg - 30][0];
-  BN = t[cfg - 30][1];
+  if (cfg != 30) return false;
+  BM = 64;
+  BN = 64;
   return true;
 }
 
 // the windowed 2-D kernel: 3x3 / pad 1 / stride 1, same-size images at most 32 pixels wide with 32 % W == 0
 bool conv_gsw_eligible(const ConvArgs& a) {
-  static const bool on = [] {
-    const char* e = rvcx_knob("RVCX_NO_GSW");
-    return !(e && std::atoi(e) != 0);
-  }();
-  return on && conv_gs_eligible(a, true) && a.KH == 3 && a.KW == 3 && a.padh == 1 && a.padw == 1 &&
+  return conv_gs_eligible(a, true) && a.KH == 3 && a.KW == 3 && a.padh == 1 && a.padw == 1 &&
          a.T_in == a.T_out && a.W_in == a.W_out && a.W_out <= GSW_MAXW && GSW_MAXW % a.W_out == 0 && a.W_out >= 4;
 }
 
 hipError_t conv_gs_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream_t s, bool two_d, int ksplit) {
   if (!a.wsplit || !conv_gs_eligible(a, two_d) || a.lowp) return hipErrorInvalidValue;
-  if (two_d && cfg == 30 && conv_gsw_eligible(a)) return launch_gsw(a, ntn_enable, ksplit, s);
-  if (cfg == 33) return (two_d && conv_gsw_eligible(a)) ? launch_gswk(a, ntn_enable, ksplit, s) : hipErrorInvalidValue;
-  if (two_d) {
-    switch (cfg) {
-      case 30: return launch_gs<64, 64, 2, 2, true>(a, ntn_enable, ksplit, s);
-      case 31: return launch_gs<128, 64, 2, 2, true>(a, ntn_enable, ksplit, s);
-      case 32: return launch_gs<64, 128, 2, 2, true>(a, ntn_enable, ksplit, s);
-      default: return hipErrorInvalidValue;
-    }
-  }
-  switch (cfg) {
-    case 30: return launch_gs<64, 64, 2, 2, false>(a, ntn_enable, ksplit, s);
-    case 31: return launch_gs<128, 64, 2, 2, false>(a, ntn_enable, ksplit, s);
-    case 32: return launch_gs<64, 128, 2, 2, false>(a, ntn_enable, ksplit, s);
-    default: return hipErrorInvalidValue;
-  }
+  if (cfg != 30) return hipErrorInvalidValue;
+  if (two_d && conv_gsw_eligible(a)) return launch_gsw(a, ntn_enable, ksplit, s);
+  return two_d ? launch_gs<64, 64, 2, 2, true>(a, ntn_enable, ksplit, s)
+               : launch_gs<64, 64, 2, 2, false>(a, ntn_enable, ksplit, s);
 }
 
 }  // namespace rvcx

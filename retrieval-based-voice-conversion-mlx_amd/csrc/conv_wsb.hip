@@ -1,10 +1,9 @@
 // fp32 implicit-GEMM convolution with the weights pre-split in HBM ("weight-streamed B"), for the long 1-D convs of
-// the generator (ResBlocks, ConvTranspose phases, conv_pre). Two arithmetics: the default, conv_wsb16_kernel with the
-// two-plane fp16 split (split_bf16.h put_h16x4: x = h + 2^-11 l, three v_mfma_f32_16x16x32_f16 products per step, the
-// weights from the per-column-scaled k_wsplit_h16 image), and the exact 3-plane bf16 split of conv_emu.hip
-// (x = x0 + x1 + x2, six plane products smallest first; conv_wsb_kernel and the bf16 instantiations of
-// conv_wsb16_kernel, rvcx_set_conv_math mode 2). Both are restructured so the (chunk, tap) loop has no barrier and no
-// conversion work:
+// the generator (ResBlocks, ConvTranspose phases, conv_pre). Two arithmetics in one kernel (conv_wsb16_kernel): the
+// default two-plane fp16 split (split_bf16.h put_h16x4: x = h + 2^-11 l, three v_mfma_f32_16x16x32_f16 products per
+// step, the weights from the per-column-scaled k_wsplit_h16 image), and the exact 3-plane bf16 split of conv_emu.hip
+// (x = x0 + x1 + x2, six plane products smallest first; rvcx_set_conv_math mode 2). The kernel is restructured so the
+// (chunk, tap) loop has no barrier and no conversion work:
 //   * the weights are split ONCE (k_wsplit / k_wsplit_h16, cached per weight tensor by the runtime) into lane-major
 //     1 KB plane blocks per (chunk, tap, 16-column group), so every lane loads its MFMA B fragments straight from
 //     L2/L1 as 16-byte vectors, one iteration ahead, into registers (two register sets);
@@ -23,16 +22,8 @@ namespace {
 
 using namespace splitbf16;
 
-#ifndef WSB_AFRAG_BATCH
-#define WSB_AFRAG_BATCH 0
-#endif
-#ifndef WSB_BPREFETCH_UNCOND
-#define WSB_BPREFETCH_UNCOND 1
-#endif
-
 constexpr int WROW = 3 * PLANE;  // bytes of one (chunk, tap, column) row of split weights in HBM
 constexpr int WSB_HALO = 64;     // max (taps - 1) * dil: the A prefetch registers cover BM + 64 rows
-constexpr int WSB_ROWS_2D = 224;  // 2-D: pixel-window rows the A prefetch registers cover (3x3 windows of 128 px)
 
 // w [tap][n][c] (ldw, w_ts) -> the pre-split image: per (chunk, tap) step, per 16-column group and plane a 1 KB
 // block laid out lane-major for the 16x16x32 MFMA B operand: 16-B slot g * 16 + j holds channels 8g..8g+7 of column
@@ -107,232 +98,18 @@ __global__ void k_wsplit_h16(const float* __restrict__ w, int ldw, long long w_t
   }
 }
 
-#ifndef WSB_EXP  // measurement aid (build/exp bench_conv only): 1 no A halo loads, 2 no B loads, 4 no A split (the halo
-                 // stored to LDS as loaded: the cost a producer-side pre-split image would remove)
-#define WSB_EXP 0
-#endif
-
-#ifndef WSB16_AFRAG  // A-fragment LDS reads of the fp16 kernel's step: 0 per row block, 1 all up front, 2 one block ahead
-#define WSB16_AFRAG 0
-#endif
-
-#ifndef WSB_WAVES_128x64
-#define WSB_WAVES_128x64 3
-#endif
-
-template <int BM, int BN, int WM, int WN, bool TWO_D>
-__global__ __launch_bounds__(CONV_THREADS, (BM == 128 && BN == 64 && !TWO_D) ? WSB_WAVES_128x64 : 2) void conv_wsb_kernel(const ConvArgs a, const char* __restrict__ wsp,
-                                                                   const int Npad, const int nrows_a, const int ntn,
-                                                                   const int ksplit, const int rw, const int rh,
-                                                                   const int tiles_w) {
-  constexpr int NT = CONV_THREADS;
-  constexpr int TM = BM / (WM * 32);
-  constexpr int TN = BN / (WN * 32);
-  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves, whole 32x32 sub-tiles");
-  extern __shared__ __attribute__((aligned(16))) char smem_w[];
-  char* const As = smem_w;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  const int li = lane & 31, hk = lane >> 5;
-  int bx, by, bz;
-  conv_block_coords(ntn, bx, by, bz);
-  const int zsplit = bz % ksplit;  // split-K slice
-  const int b = bz / ksplit;
-  const int n0 = by * BN;
-  int m0 = 0, h0 = 0, w0 = 0;
-  if (!TWO_D) {
-    m0 = bx * BM;
-  } else {
-    h0 = (bx / tiles_w) * rh;
-    w0 = (bx % tiles_w) * rw;
-  }
-  const float* X = a.x + (long long)b * a.x_bs;
-  const float* PM = (!TWO_D && a.pre_mask) ? a.pre_mask + (long long)b * a.pre_mask_bs : nullptr;
-  const int row0 = TWO_D ? 0 : m0 - a.pad;
-  const int aw = TWO_D ? rw + a.KW - 1 : 0;  // 2-D: the (rh + KH - 1) x (rw + KW - 1) pixel window, row-major
-
-  int aoff[TM];
-#pragma unroll
-  for (int tm = 0; tm < TM; ++tm) {
-    const int ml = wm * TM * 32 + tm * 32 + li;
-    const int r = !TWO_D ? ml : ((ml < rh * rw) ? (ml / rw) * aw + (ml % rw) : 0);
-    aoff[tm] = r * ERS + hk * 16;
-  }
-  // lane (column li, k-half hk): in the image block of its 16-column group, 16-B slot (2 s + hk) * 16 + li % 16
-  const char* bp[TN];
-#pragma unroll
-  for (int tn = 0; tn < TN; ++tn)
-    bp[tn] = wsp + (size_t)((n0 + wn * TN * 32 + tn * 32 + li) >> 4) * (3 * WBLK) + hk * 256 + (li & 15) * 16;
-  const size_t bstep = (size_t)Npad * WROW;  // one (chunk, tap) iteration
-
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-    for (int tn = 0; tn < TN; ++tn)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[tm][tn][r] = 0.f;
-
-  // ---- A: the chunk's nrows_a x 32 halo tile (1-D rows / 2-D pixel window), prefetched into registers one chunk
-  // ahead
-  constexpr int AP = ((TWO_D ? WSB_ROWS_2D : BM + WSB_HALO) * EC4 + NT - 1) / NT;
-  // branch-free prefetch (conv_gs.hip load_a): rows outside the input read row 0 and are zeroed when split into LDS
-  f32x4 apre[AP];
-  float apm[AP];
-  unsigned long long aok = 0ull;
-  const int arow = store_row(tid / EC4), ac4 = (tid % EC4) << 2;
-  auto load_a_regs = [&](int c0) __attribute__((always_inline)) {
-    const float* src0 = X + c0 + ac4;
-    aok = 0ull;
-#pragma unroll
-    for (int v = 0; v < AP; ++v) {
-      const int r = v * (NT / EC4) + arow;
-      long long g;
-      bool ok;
-      if constexpr (!TWO_D) {
-        g = row0 + r;
-        ok = r < nrows_a && g >= 0 && g < a.T_in;
-      } else {
-        const int ah = r / aw, awi = r - ah * aw;
-        const int gh = h0 - a.padh + ah, gw = w0 - a.padw + awi;
-        ok = r < nrows_a && gh >= 0 && gh < a.T_in && gw >= 0 && gw < a.W_in;
-        g = (long long)gh * a.W_in + gw;
-      }
-      const long long gc = ok ? g : 0;
-      apre[v] = *reinterpret_cast<const f32x4*>(src0 + gc * a.ldx);
-      apm[v] = PM ? PM[gc] : 1.f;
-      aok |= ok ? (1ull << v) : 0ull;
-    }
-  };
-  auto write_a_regs = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int v = 0; v < AP; ++v) {
-      const int r = v * (NT / EC4) + arow;
-      if (r < nrows_a) {
-        f32x4 val = apre[v];
-        const bool ok = (aok >> v) & 1ull;
-        if (a.pre_act != ACT_NONE) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) val[j] = act_fn(val[j], a.pre_act, a.pre_slope);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) val[j] = ok ? val[j] * apm[v] : 0.f;
-        put_split4(As + r * ERS, ac4, val);
-      }
-    }
-  };
-
-  // ---- B fragments of one iteration: [tn][s * 3 + plane], 16 B per lane each
-  typedef bf16x8 BFrag[TN][6];
-  auto load_b = [&](int it, BFrag& dst) __attribute__((always_inline)) {
-    const size_t o = (size_t)it * bstep;
-#pragma unroll
-    for (int tn = 0; tn < TN; ++tn)
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-          dst[tn][s * 3 + q] = *reinterpret_cast<const bf16x8*>(bp[tn] + o + q * WBLK + s * 512);
-  };
-  auto compute = [&](int tap, const BFrag& bf) __attribute__((always_inline)) {
-    const int toff = (TWO_D ? (tap / a.KW) * aw + (tap % a.KW) : tap * a.dil) * ERS;
-#if WSB_AFRAG_BATCH
-    // every A fragment of the step requested before the first MFMA (one exposed LDS latency per step)
-    bf16x8 af2[2][TM][3];
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-          af2[s][tm][q] = *reinterpret_cast<const bf16x8*>(As + aoff[tm] + toff + q * PLANE + s * 32);
-#endif
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-#if WSB_AFRAG_BATCH
-      auto& af = af2[s];
-#else
-      bf16x8 af[TM][3];
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-          af[tm][q] = *reinterpret_cast<const bf16x8*>(As + aoff[tm] + toff + q * PLANE + s * 32);
-#endif
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn) {
-          f32x16 c = acc[tm][tn];
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm][2], bf[tn][s * 3 + 0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm][1], bf[tn][s * 3 + 1], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm][0], bf[tn][s * 3 + 2], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm][1], bf[tn][s * 3 + 0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm][0], bf[tn][s * 3 + 1], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[tm][0], bf[tn][s * 3 + 0], c, 0, 0, 0);
-          acc[tm][tn] = c;
-        }
-    }
-  };
-
-  // (chunk, tap) iterations [it0, it1) of this split-K slice (an empty slice stores its zero partial tile)
-  const int taps = a.taps, total = (a.C_in / EK) * taps;
-  const int per = (total + ksplit - 1) / ksplit;
-  const int it0 = zsplit * per, it1 = min(total, it0 + per);
-  if (it0 < it1) {
-    BFrag b0, b1;
-    int ch = it0 / taps, tap = it0 - ch * taps;
-    load_a_regs(ch * EK);
-    write_a_regs();
-    if ((ch + 1) * taps < it1) load_a_regs((ch + 1) * EK);
-    load_b(it0, b0);
-    __syncthreads();
-    // one (chunk, tap) iteration: prefetch the next iteration's B, MFMAs on this one's, switch chunks after the
-    // last tap (every wave done reading the halo -> write the prefetched one -> prefetch the chunk after)
-    auto step = [&](int it, const BFrag& cur, BFrag& nxt) __attribute__((always_inline)) {
-#if WSB_BPREFETCH_UNCOND
-      // unconditional (the last step reloads its own fragments): with a conditional load the waitcnt pass merges
-      // the load-issued and load-skipped paths and waits for the prefetch itself inside this step; the scheduling
-      // barrier keeps the loads at the top of the step (the machine scheduler otherwise sinks them below the MFMAs,
-      // so the next step waits out their whole latency)
-      load_b(it + 1 < it1 ? it + 1 : it, nxt);
-      __builtin_amdgcn_sched_barrier(0);
-#else
-      if (it + 1 < it1) load_b(it + 1, nxt);
-#endif
-      compute(tap, cur);
-      if (++tap == taps) {
-        tap = 0;
-        if (++ch * taps < it1) {
-          __syncthreads();
-          write_a_regs();
-          if ((ch + 1) * taps < it1) load_a_regs((ch + 1) * EK);
-          __syncthreads();
-        }
-      }
-    };
-    for (int it = it0; it < it1; it += 2) {
-      step(it, b0, b1);
-      if (it + 1 < it1) step(it + 1, b1, b0);
-    }
-  }
-
-  conv_store_tile<TM, TN, WM, WN, TWO_D>(a, TilePos{m0, h0, w0, rw, rh, n0, b, 0, b, zsplit, ksplit}, acc,
-                                         reinterpret_cast<float*>(smem_w));
-}
-
-// ---- the same contraction on v_mfma_f32_16x16x32_bf16 (1-D only). One MFMA covers a whole 32-channel chunk (lane
-// group g = lane / 16 holds channels 8g..8g+7 of its row / column), so a (chunk, tap) step is, per wave of TM16 x TN16
-// 16x16 tiles, 3*TM16 LDS reads, 3*TN16 global B loads and 6*TM16*TN16 MFMAs of 16 cycles: the same bytes and MFMA
-// cycles per step as the 32x32x16 form at the same wave tile. The chip sustains a higher clock on this shape under
-// power-limited load (MI355X_MICROARCH.md "DVFS give-back" item 7), which is the point.
+// ---- the contraction on v_mfma_f32_16x16x32 (1-D). One MFMA covers a whole 32-channel chunk (lane group g = lane / 16
+// holds channels 8g..8g+7 of its row / column), so a (chunk, tap) step is, per wave of TM16 x TN16 16x16 tiles,
+// NQ*TM16 LDS reads, NQ*TN16 global B loads and 3 (fp16) or 6 (bf16) x TM16*TN16 MFMAs of 16 cycles. The chip holds a
+// higher clock on this shape than on 32x32x16 under power-limited load (MI355X_MICROARCH.md "DVFS give-back" item 7):
+// a 32x32x16 form of the fp16 kernel (round 6, same tile and image) measured slower on every generator shape (C128 k11
+// 352 vs 380 TF, k7 317 vs 340, C2 +0.2 ms; profiles/r06a_bench_conv_wsb32h.txt) although an MFMA of it blocks vector
+// issue for 8 of 32 cycles instead of 8 of 16.
 // C layout of a 16x16 tile: lane l holds column l % 16, rows 4 (l / 16) + r, r = 0..3.
 // MODE: bits 0-1 the pre-activation (pre_fn), bit 2 a pre-mask row multiplier (conv_gs.hip's MODE), bit 4 the
 // two-plane fp16 arithmetic (split_bf16.h put_h16x4; weights from the k_wsplit_h16 image), bit 3 (with bit 4) the
-// opt-in reduced precision: the fp16 hi planes' product alone
+// opt-in reduced precision: the fp16 hi planes' product alone. The weight image comes from k_wsplit (bf16) or
+// k_wsplit_h16 (fp16); only the activation halo goes through LDS (split once per 32-channel chunk, reused by every tap)
 template <int BM, int BN, int WM, int WN, int MODE>
 __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 : 3) void conv_wsb16_kernel(const ConvArgs a, const char* __restrict__ wsp,
                                                                      const int Npad, const int nrows_a, const int ntn,
@@ -342,7 +119,6 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
   constexpr bool PMASK = (MODE & 4) != 0;
   constexpr bool H16 = (MODE & 16) != 0;
   constexpr bool LOWP = H16 && (MODE & 8) != 0;
-  constexpr bool PRESPLIT = H16 && (MODE & 32) != 0;  // A arrives as the h16 image (ConvArgs::x_h16): copied, not split
   constexpr int NQ = LOWP ? 1 : (H16 ? 2 : 3);  // planes an MFMA step reads
   constexpr int NQI = H16 ? 2 : 3;               // planes of the weight image
   constexpr int RS = H16 ? ERS_H : ERS;          // LDS row stride
@@ -388,7 +164,7 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
   constexpr int AP = ((BM + WSB_HALO) * EC4 + NT - 1) / NT;
   f32x4 apre[AP];
   float apm[AP];
-  unsigned aok = 0u;  // branch-free prefetch, as conv_wsb_kernel's
+  unsigned aok = 0u;  // branch-free prefetch: rows outside the input read row 0 and are zeroed when split into LDS
   const int arow = store_row(tid / EC4), ac4 = (tid % EC4) << 2;
   auto load_a_regs = [&](int c0) __attribute__((always_inline)) {
     const float* src0 = X + c0 + ac4;
@@ -399,11 +175,7 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
       const long long g = row0 + r;
       const bool ok = r < nrows_a && g >= 0 && g < a.T_in;
       const long long gc = ok ? g : 0;
-#if WSB_EXP & 1
-      apre[v] = f32x4{1.f, 2.f, 3.f, (float)(c0 + v)};
-#else
       apre[v] = *reinterpret_cast<const f32x4*>(src0 + gc * a.ldx);
-#endif
       if constexpr (PMASK) apm[v] = PM[gc];
       aok |= ok ? (1u << v) : 0u;
     }
@@ -415,12 +187,6 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
       if (r < nrows_a) {
         f32x4 val = apre[v];
         const bool ok = (aok >> v) & 1u;
-        if constexpr (PRESPLIT) {
-          // the 16 bytes at this slot already hold the row's planes in the LDS row layout (slot ac4 / 4 of 8)
-          const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-          *reinterpret_cast<f32x4*>(As + r * RS + ac4 * 4) = ok ? val : zero;
-          continue;
-        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) val[j] = pre_fn<PA>(val[j], a.pre_act, a.pre_slope);
         if constexpr (PMASK) {
@@ -431,13 +197,9 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
           for (int j = 0; j < 4; ++j) val[j] = ok ? val[j] : 0.f;
         }
         if constexpr (H16) {
-#if WSB_EXP & 4
-          *reinterpret_cast<f32x4*>(As + r * RS + ac4 * 4) = apre[v];
-#else
 #pragma unroll
           for (int j = 0; j < 4; ++j) val[j] *= H16_XS;
           put_h16x4<NQ>(As + r * RS, ac4, val);
-#endif
         } else {
           put_split4(As + r * RS, ac4, val);
         }
@@ -450,53 +212,10 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
 #pragma unroll
     for (int tn = 0; tn < TN16; ++tn)
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-#if WSB_EXP & 2
-        const int u = it + tn + q;
-        dst[tn][q] = __builtin_bit_cast(bf16x8, (int4){u, u + 1, u + 2, u + 3});
-#else
-        dst[tn][q] = *reinterpret_cast<const bf16x8*>(bp[tn] + o + q * WBLK);
-#endif
-      }
+      for (int q = 0; q < NQ; ++q) dst[tn][q] = *reinterpret_cast<const bf16x8*>(bp[tn] + o + q * WBLK);
   };
   auto compute = [&](int tap, const BFrag& bf) __attribute__((always_inline)) {
     const int toff = tap * a.dil * RS;
-#if WSB16_AFRAG
-    if constexpr (H16) {
-      // the step's A fragments requested ahead of their MFMAs (1: all TM16 at the top; 2: one row block ahead)
-      bf16x8 afa[WSB16_AFRAG == 1 ? TM16 : 2][NQ];
-#pragma unroll
-      for (int tm = 0; tm < (WSB16_AFRAG == 1 ? TM16 : 1); ++tm)
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) afa[tm][q] = *reinterpret_cast<const bf16x8*>(As + aoff[tm] + toff + q * PLANE);
-      __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler otherwise sinks them to their MFMAs)
-#pragma unroll
-      for (int tm = 0; tm < TM16; ++tm) {
-        const int sl = WSB16_AFRAG == 1 ? tm : (tm & 1);
-        if constexpr (WSB16_AFRAG == 2) {
-          if (tm + 1 < TM16) {
-#pragma unroll
-            for (int q = 0; q < NQ; ++q)
-              afa[(tm + 1) & 1][q] = *reinterpret_cast<const bf16x8*>(As + aoff[tm + 1] + toff + q * PLANE);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
-        const f16x8 ah = __builtin_bit_cast(f16x8, afa[sl][0]);
-#pragma unroll
-        for (int tn = 0; tn < TN16; ++tn) {
-          const f16x8 bh = __builtin_bit_cast(f16x8, bf[tn][0]);
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc[tm][tn], 0, 0, 0);
-          if constexpr (!LOWP) {
-            f32x4 c = acc2[tm][tn];
-            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, afa[sl][NQ - 1]), bh, c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, __builtin_bit_cast(f16x8, bf[tn][NQ - 1]), c, 0, 0, 0);
-            acc2[tm][tn] = c;
-          }
-        }
-      }
-      return;
-    }
-#endif
 #pragma unroll
     for (int tm = 0; tm < TM16; ++tm) {
       bf16x8 af[NQ];
@@ -543,7 +262,11 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
     load_b(it0, b0);
     __syncthreads();
     auto step = [&](int it, const BFrag& cur, BFrag& nxt) __attribute__((always_inline)) {
-      load_b(it + 1 < it1 ? it + 1 : it, nxt);  // unconditional and pinned at the top (see conv_wsb_kernel)
+      // unconditional (the last step reloads its own fragments): with a conditional load the waitcnt pass merges the
+      // load-issued and load-skipped paths and waits for the prefetch itself inside this step; the scheduling barrier
+      // keeps the loads at the top of the step (the machine scheduler otherwise sinks them below the MFMAs, so the
+      // next step waits out their whole latency)
+      load_b(it + 1 < it1 ? it + 1 : it, nxt);
       __builtin_amdgcn_sched_barrier(0);
       compute(tap, cur);
       if (++tap == taps) {
@@ -580,7 +303,7 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
   store_tile16<TM16, TN16, WM, WN>(a, m0, n0, b, zsplit, ksplit, (long long)a.T_out, acc);
 }
 
-template <int BM, int BN, int WM, int WN, bool H16OK = false>
+template <int BM, int BN, int WM, int WN>
 hipError_t launch_wsb16(const ConvArgs& a, int ntn_enable, int ksplit, hipStream_t s) {
   const int nrows_a = BM + (a.taps - 1) * a.dil;
   const int mtiles = (a.T_out + BM - 1) / BM;
@@ -588,67 +311,31 @@ hipError_t launch_wsb16(const ConvArgs& a, int ntn_enable, int ksplit, hipStream
   const size_t smem = (size_t)nrows_a * (h16 ? ERS_H : ERS);
   if (a.wsplit_npad % BN != 0 || ksplit < 1 || (ksplit > 1 && !a.ws)) return hipErrorInvalidValue;
   if (a.lowp && !h16) return hipErrorInvalidValue;  // the reduced-precision mode reads the fp16 image's hi plane
-  if (h16 && !H16OK) return hipErrorInvalidValue;   // fp16 instantiations only for the tiles the policy picks
   const int ntiles = (a.N + BN - 1) / BN;
   const int ntn = ntn_enable ? ntiles : 0;
   dim3 grid(ntn ? mtiles * ntiles : mtiles, ntn ? 1 : ntiles, a.batch * ksplit);
   // the reduced-precision opt-in only without a pre-mask (the generator's convs)
-  // the pre-split A image: the fp16 arithmetic without a pre-activation or pre-mask, rows of exactly C_in channels
-  if (a.x_h16 && (!h16 || a.pre_act != ACT_NONE || a.pre_mask || a.ldx != a.C_in)) return hipErrorInvalidValue;
-  const int mode = pre_mode(a.pre_act) | (a.pre_mask ? 4 : 0) | (h16 ? 16 : 0) | (h16 && a.lowp && !a.pre_mask ? 8 : 0) |
-                   (a.x_h16 ? 32 : 0);
+  const int mode = pre_mode(a.pre_act) | (a.pre_mask ? 4 : 0) | (h16 ? 16 : 0) | (h16 && a.lowp && !a.pre_mask ? 8 : 0);
   void (*kern)(const ConvArgs, const char*, int, int, int, int);
   switch (mode) {
 #define WSB16_CASE(M) \
-  case M: kern = conv_wsb16_kernel<BM, BN, WM, WN, (H16OK || M < 16) ? M : 0>; break;
+  case M: kern = conv_wsb16_kernel<BM, BN, WM, WN, M>; break;
     WSB16_CASE(0) WSB16_CASE(1) WSB16_CASE(2) WSB16_CASE(4) WSB16_CASE(5) WSB16_CASE(6)
     WSB16_CASE(16) WSB16_CASE(17) WSB16_CASE(18) WSB16_CASE(20) WSB16_CASE(21) WSB16_CASE(22)
-    WSB16_CASE(24) WSB16_CASE(25) WSB16_CASE(26) WSB16_CASE(48) WSB16_CASE(56)
+    WSB16_CASE(24) WSB16_CASE(25) WSB16_CASE(26)
 #undef WSB16_CASE
     default: return hipErrorInvalidValue;
   }
   // per instantiation: raise the dynamic-LDS limit once, not per launch
-  static size_t smem_set[64] = {};
-  if (smem > 64 * 1024 && smem > smem_set[mode & 63]) {
+  static size_t smem_set[32] = {};
+  if (smem > 64 * 1024 && smem > smem_set[mode & 31]) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
-    smem_set[mode & 63] = smem;
+    smem_set[mode & 31] = smem;
   }
   hipLaunchKernelGGL(kern, grid, dim3(CONV_THREADS), smem, s, a, static_cast<const char*>(a.wsplit), a.wsplit_npad,
                      nrows_a, ntn, ksplit);
-  return hipGetLastError();
-}
-
-template <int BM, int BN, int WM, int WN, bool TWO_D>
-hipError_t launch_wsb(const ConvArgs& a, int ntn_enable, int ksplit, hipStream_t s) {
-  int nrows_a, rw = 0, rh = 0, tiles_w = 1, mtiles;
-  if (!TWO_D) {
-    nrows_a = BM + (a.taps - 1) * a.dil;
-    mtiles = (a.T_out + BM - 1) / BM;
-  } else {
-    rw = a.W_out < BM ? a.W_out : BM;
-    rh = BM / rw;
-    tiles_w = (a.W_out + rw - 1) / rw;
-    mtiles = ((a.T_out + rh - 1) / rh) * tiles_w;
-    nrows_a = (rh + a.KH - 1) * (rw + a.KW - 1);
-    if (nrows_a > WSB_ROWS_2D) return hipErrorInvalidValue;  // the window outgrows the A prefetch registers
-  }
-  const size_t smem = std::max((size_t)nrows_a * ERS, (size_t)4 * 32 * 33 * sizeof(float));
-  if (a.wsplit_npad % BN != 0 || ksplit < 1 || (ksplit > 1 && !a.ws)) return hipErrorInvalidValue;
-  const int ntiles = (a.N + BN - 1) / BN;
-  const int ntn = ntn_enable ? ntiles : 0;
-  dim3 grid(ntn ? mtiles * ntiles : mtiles, ntn ? 1 : ntiles, a.batch * ksplit);
-  auto kern = conv_wsb_kernel<BM, BN, WM, WN, TWO_D>;
-  static size_t smem_set = 64 * 1024;
-  if (smem > smem_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    if (e != hipSuccess) return e;
-    smem_set = smem;
-  }
-  hipLaunchKernelGGL(kern, grid, dim3(CONV_THREADS), smem, s, a, static_cast<const char*>(a.wsplit), a.wsplit_npad,
-                     nrows_a, ntn, ksplit, rw, rh, tiles_w);
   return hipGetLastError();
 }
 
@@ -656,13 +343,8 @@ hipError_t launch_wsb(const ConvArgs& a, int ntn_enable, int ksplit, hipStream_t
 
 bool conv_wsb_eligible(const ConvArgs& a, bool two_d) {
   const bool vec_a = ((a.ldx & 3) == 0) && ((reinterpret_cast<uintptr_t>(a.x) & 15) == 0) && ((a.x_bs & 3) == 0);
-  const bool common = a.batch_inner == 1 && !a.b_kn && a.C_in % EK == 0 && a.C_in > 0 && a.taps >= 1 && vec_a &&
-                      a.out_map == OUT_ROWS;
-  if (!two_d) return common && a.stride == 1 && (a.taps - 1) * a.dil <= WSB_HALO && a.dil >= 1;
-  // 2-D: stride 1, taps = KH x KW, the window of a 128-pixel tile within the prefetch registers
-  if (!common || a.taps != a.KH * a.KW || a.W_out < 1 || a.pre_mask) return false;
-  const int rw = a.W_out < 128 ? a.W_out : 128, rh = 128 / rw;
-  return a.W_out == a.W_in && a.T_out == a.T_in && (rh + a.KH - 1) * (rw + a.KW - 1) <= WSB_ROWS_2D;
+  return !two_d && a.batch_inner == 1 && !a.b_kn && a.C_in % EK == 0 && a.C_in > 0 && a.taps >= 1 && vec_a &&
+         a.out_map == OUT_ROWS && a.stride == 1 && (a.taps - 1) * a.dil <= WSB_HALO && a.dil >= 1;
 }
 
 int conv_wsplit_npad(int N) { return (N + 127) / 128 * 128; }
@@ -694,37 +376,30 @@ hipError_t conv_wsplit_build(const ConvArgs& a, void* out, hipStream_t s) {
   return hipGetLastError();
 }
 
-// cfg 20: 256 x 32 (4 x 1 waves of 64 x 32), 21: 128 x 64 (2 x 2 waves of 64 x 32), 22: 128 x 128 (2 x 2 of 64 x 64);
-// cfg 23 / 24: the 21 / 20 tiles on v_mfma_f32_16x16x32_bf16 (1-D); 25: 128 x 128 (2 x 2 waves of 64 x 64), 26: 256 x 64
-// (4 x 1 waves of 64 x 64) on 16x16x32; 27: 128 x 64 as 1 x 4 waves of 128 x 16, 28: 256 x 64 as 2 x 2 waves of 128 x 32
-// (16x16x32). A persistent form of the 16x16x32
-// kernel (contiguous tile runs per workgroup, A halos and B prefetched across tile boundaries) measured slower on every
-// shape (bench_conv r03k: C128 k3 118 vs 129 TF, k11 198 vs 219, up-phases 88-111 vs 97-128): three independent
-// one-tile workgroups per CU already overlap each other's prologue and epilogue
+// cfg 23: 128 x 64 as 2 x 2 waves of 64 x 32, 24: 256 x 32 as 4 x 1 waves of 64 x 32 (N <= 32), 25: 128 x 128 as
+// 2 x 2 waves of 64 x 64 (round 6: the 128-channel k = 7 / 11 convs, C128 k11 402 vs 380 TF, k7 346 vs 340 in
+// bench_conv r06a; C2 -0.05 to -0.1 ms same box), 27: 128 x 64 as 1 x 4 waves of 128 x 16 (k <= 3). The 32x32x16
+// bf16 kernel of rounds 2-3 (cfg 20-22), 256 x 64 tiles (26, 28) and a 32x32x16 fp16 form (r06a) measured slower and
+// are gone. A persistent form of the kernel (contiguous tile runs per workgroup, A halos and B prefetched across tile
+// boundaries) measured slower on every shape (bench_conv r03k: C128 k3 118 vs 129 TF, k11 198 vs 219, up-phases 88-111
+// vs 97-128): three independent one-tile workgroups per CU already overlap each other's prologue and epilogue
 bool conv_wsb_tile(int cfg, int& BM, int& BN) {
-  static const int t[9][2] = {{256, 32}, {128, 64}, {128, 128}, {128, 64}, {256, 32}, {128, 128}, {256, 64},
-                              {128, 64}, {256, 64}};
-  if (cfg < 20 || cfg > 28) return false;
-  BM = t[cfg - 20][0];
-  BN = t[cfg - 20][1];
-  return true;
+  switch (cfg) {
+    case 23: BM = 128; BN = 64; return true;
+    case 24: BM = 256; BN = 32; return true;
+    case 25: BM = 128; BN = 128; return true;
+    case 27: BM = 128; BN = 64; return true;
+    default: return false;
+  }
 }
 
 hipError_t conv_wsb_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream_t s, bool two_d, int ksplit) {
   if (!a.wsplit || !conv_wsb_eligible(a, two_d)) return hipErrorInvalidValue;
-  // the fp16 image only on the 16x16x32 kernel (1-D)
-  if (a.wsplit_fmt == WSPLIT_H16 && (two_d || cfg < 23)) return hipErrorInvalidValue;
-  if (two_d) return cfg == 21 ? launch_wsb<128, 64, 2, 2, true>(a, ntn_enable, ksplit, s) : hipErrorInvalidValue;
   switch (cfg) {
-    case 20: return launch_wsb<256, 32, 4, 1, false>(a, ntn_enable, ksplit, s);
-    case 21: return launch_wsb<128, 64, 2, 2, false>(a, ntn_enable, ksplit, s);
-    case 22: return launch_wsb<128, 128, 2, 2, false>(a, ntn_enable, ksplit, s);
-    case 23: return launch_wsb16<128, 64, 2, 2, true>(a, ntn_enable, ksplit, s);
-    case 24: return launch_wsb16<256, 32, 4, 1, true>(a, ntn_enable, ksplit, s);
-    case 25: return launch_wsb16<128, 128, 2, 2, true>(a, ntn_enable, ksplit, s);
-    case 26: return launch_wsb16<256, 64, 4, 1>(a, ntn_enable, ksplit, s);
-    case 27: return launch_wsb16<128, 64, 1, 4, true>(a, ntn_enable, ksplit, s);
-    case 28: return launch_wsb16<256, 64, 2, 2, true>(a, ntn_enable, ksplit, s);
+    case 23: return launch_wsb16<128, 64, 2, 2>(a, ntn_enable, ksplit, s);
+    case 24: return launch_wsb16<256, 32, 4, 1>(a, ntn_enable, ksplit, s);
+    case 25: return launch_wsb16<128, 128, 2, 2>(a, ntn_enable, ksplit, s);
+    case 27: return launch_wsb16<128, 64, 1, 4>(a, ntn_enable, ksplit, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -7,9 +7,9 @@
 // fragment needs an LDS transpose: S^T = K Q^T (A = K rows, B = Q^T; MFMA C layout puts one query per lane
 // column), the softmax statistics of a query are a lane's own 16 registers plus its partner lane (lane ^ 32),
 // and O^T = V^T P^T takes P^T straight from the S^T registers as the B fragment (the K16 slots of a lane are its
-// C rows, the same key permutation on the A side). Every product uses the exact 3-plane bf16 split of
-// conv_emu.hip (fp32 accurate). Key splits write unnormalised partials (O, running max, running sum) that
-// k_flash_combine merges; the relative-value band is folded into each split's O before it is written.
+// C rows, the same key permutation on the A side). Every product uses the two-plane fp16 split (below; fp32
+// accurate). Key splits write unnormalised partials (O, running max, running sum) that k_flash_combine merges; the
+// relative-value band is folded into each split's O before it is written.
 #include <algorithm>
 #include <cstdlib>
 #include <cmath>
@@ -27,278 +27,13 @@ constexpr int FA_Q = 32;    // queries per wave
 constexpr int FA_K = 32;    // keys per block
 constexpr int FA_NW = 32;   // max relative window 2w+1 (LDS table width)
 
-__device__ __forceinline__ void split8(const float (&v)[8], bf16x8 (&out)[3]) {
-  char buf[3 * 16];
-  // reuse the 4-wide splitter on a private 3-plane row of 8 channels
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    f32x4 x = {v[4 * h], v[4 * h + 1], v[4 * h + 2], v[4 * h + 3]};
-    uint2 hi, mi, lo;
-    hi.x = pk_bf16(x[0], x[1]);
-    hi.y = pk_bf16(x[2], x[3]);
-    float r0 = x[0] - lo_f(hi.x), r1 = x[1] - hi_f(hi.x), r2 = x[2] - lo_f(hi.y), r3 = x[3] - hi_f(hi.y);
-    mi.x = pk_bf16(r0, r1);
-    mi.y = pk_bf16(r2, r3);
-    r0 -= lo_f(mi.x);
-    r1 -= hi_f(mi.x);
-    r2 -= lo_f(mi.y);
-    r3 -= hi_f(mi.y);
-    lo.x = pk_bf16(r0, r1);
-    lo.y = pk_bf16(r2, r3);
-    *reinterpret_cast<uint2*>(buf + 8 * h) = hi;
-    *reinterpret_cast<uint2*>(buf + 16 + 8 * h) = mi;
-    *reinterpret_cast<uint2*>(buf + 32 + 8 * h) = lo;
-  }
-#pragma unroll
-  for (int q = 0; q < 3; ++q) out[q] = *reinterpret_cast<const bf16x8*>(buf + 16 * q);
-}
-
-__device__ __forceinline__ f32x16 mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 c) {
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
-  return c;
-}
-
 // key row of C register r for the half-wave hk (MFMA 32x32 C layout)
 __device__ __forceinline__ int crow(int r, int hk) { return (r & 3) + 8 * (r >> 2) + 4 * hk; }
 
-// qkv [B][T][ldq]: q at col h*DK, k at H + h*DK, v at 2H + h*DK. part_o [nsplit][BH][T][DK], part_ml
-// [nsplit][BH][T][2] (running max, running sum).
-template <int DK>
-__global__ __launch_bounds__(64) void k_flash_attn(const float* __restrict__ qkv, int ldq, int T, int nh, int H,
-                                                   float qscale, int kb_per_split, const float* __restrict__ rel_k,
-                                                   const float* __restrict__ rel_v, int window,
-                                                   const float* __restrict__ mask, float* __restrict__ part_o,
-                                                   float* __restrict__ part_ml) {
-  constexpr int NS = DK / 16;  // K16 steps over the head dimension
-  constexpr int NT = DK / 32;  // 32-dim tiles of O^T
-  __shared__ float relq[FA_Q][FA_NW + 1];
-  __shared__ float pband[FA_Q][FA_NW + 1];
-  const int lane = threadIdx.x, li = lane & 31, hk = lane >> 5;
-  const int q0 = blockIdx.x * FA_Q, split = blockIdx.y, bh = blockIdx.z;
-  const int b = bh / nh, h = bh % nh;
-  const int nsplit = gridDim.y;
-  const int BH = gridDim.z;
-  const float* base = qkv + (long long)b * T * ldq;
-  const int i = q0 + li;
-  const bool qok = i < T;
-  const int nw = rel_k ? 2 * window + 1 : 0;
-  const float* mk = mask ? mask + (long long)b * T : nullptr;
-  const float mi = (mk && qok) ? mk[i] : 1.f;
-
-  // Q^T fragments (scaled), kept for the whole key range
-  bf16x8 qf[NS][3];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (qok) {
-      const float4* src = reinterpret_cast<const float4*>(base + (long long)i * ldq + h * DK + 16 * s + 8 * hk);
-      const float4 x0 = src[0], x1 = src[1];
-      v[0] = x0.x * qscale; v[1] = x0.y * qscale; v[2] = x0.z * qscale; v[3] = x0.w * qscale;
-      v[4] = x1.x * qscale; v[5] = x1.y * qscale; v[6] = x1.z * qscale; v[7] = x1.w * qscale;
-    }
-    split8(v, qf[s]);
-  }
-  const int nkb = (T + FA_K - 1) / FA_K;
-  const int kb0 = split * kb_per_split, kb1 = min(nkb, kb0 + kb_per_split);
-  // does this split's key range reach the relative-position band of this query block?
-  const bool band_split = nw && kb0 < kb1 && (kb1 * FA_K - 1 >= q0 - window) && (kb0 * FA_K <= q0 + FA_Q - 1 + window);
-  // relative key logits of this wave's queries as one MFMA tile: relq^T[o][i] = rel_k[o] . (q_i * qscale)
-  if (band_split) {
-    f32x16 rq;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) rq[r] = 0.f;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (li < nw) {
-        const float* src = rel_k + li * DK + 16 * s + 8 * hk;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = src[e];
-      }
-      bf16x8 rf[3];
-      split8(v, rf);
-      rq = mfma6(rf, qf[s], rq);
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int od = crow(r, hk);
-      relq[li][od] = rq[r];
-      pband[li][od] = 0.f;
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-  f32x16 o[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
-  float m_run = -INFINITY, l_run = 0.f;
-
-  for (int kb = kb0; kb < kb1; ++kb) {
-    const int j0 = kb * FA_K;
-    // S^T = K Q^T for keys j0.. (rows) x this wave's queries (columns)
-    f32x16 sc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) sc[r] = 0.f;
-    {
-      const int j = j0 + li;
-      const bool kok = j < T;
-      const float* kr = base + (long long)j * ldq + H + h * DK + 8 * hk;
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        if (kok) {
-          const float4 x0 = *reinterpret_cast<const float4*>(kr + 16 * s);
-          const float4 x1 = *reinterpret_cast<const float4*>(kr + 16 * s + 4);
-          v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w;
-          v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
-        }
-        bf16x8 kf[3];
-        split8(v, kf);
-        sc = mfma6(kf, qf[s], sc);
-      }
-    }
-    // relative-position band, mask fill (-1e4), keys past T excluded
-    float mloc = -INFINITY;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int j = j0 + crow(r, hk);
-      float v = sc[r];
-      if (nw) {
-        const int od = j - i + window;
-        if (od >= 0 && od < nw) v = v + relq[li][od];
-      }
-      if (mk && j < T && mi * mk[j] == 0.f) v = -1e4f;
-      if (j >= T) v = -INFINITY;
-      sc[r] = v;
-      mloc = fmaxf(mloc, v);
-    }
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 32));
-    const float m_new = fmaxf(m_run, mloc);
-    const float alpha = expf(m_run - m_new);
-    float lsum = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      sc[r] = expf(sc[r] - m_new);
-      lsum += sc[r];
-    }
-    lsum += __shfl_xor(lsum, 32);
-    l_run = l_run * alpha + lsum;
-    m_run = m_new;
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
-    if (band_split) {
-      // keys of this block inside the band: rescale the band sums (once per query), then add
-      const bool band = (j0 + FA_K - 1 >= q0 - window) && (j0 <= q0 + FA_Q - 1 + window);
-      if (hk == 0)
-        for (int od = 0; od < nw; ++od) pband[li][od] *= alpha;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (band) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int od = j0 + crow(r, hk) - i + window;
-          if (od >= 0 && od < nw) pband[li][od] += sc[r];
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    // O^T += V^T P^T: the B fragment of K16 step s2 is P^T's registers 8 s2 .. 8 s2 + 7 (keys crow(.)+16 s2)
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      float pv[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) pv[e] = sc[8 * s2 + e];
-      bf16x8 pf[3];
-      split8(pv, pf);
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        float v[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int j = j0 + crow(8 * s2 + e, hk);
-          v[e] = j < T ? base[(long long)j * ldq + 2 * H + h * DK + 32 * t + li] : 0.f;
-        }
-        bf16x8 vf[3];
-        split8(v, vf);
-        o[t] = mfma6(vf, pf, o[t]);
-      }
-    }
-  }
-  // the relative-value band of this split as MFMAs: O^T[d][i] += sum_o rel_v^T[d][o] pband^T[o][i] (o < 32)
-  if (band_split) {
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      float pv[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) pv[e] = pband[li][16 * s2 + 8 * hk + e];
-      bf16x8 pf[3];
-      split8(pv, pf);
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        float v[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int od = 16 * s2 + 8 * hk + e;
-          v[e] = od < nw ? rel_v[od * DK + 32 * t + li] : 0.f;
-        }
-        bf16x8 vf[3];
-        split8(v, vf);
-        o[t] = mfma6(vf, pf, o[t]);
-      }
-    }
-  }
-  // O^T leaves the registers one query per lane column: stored directly, every store instruction would write 64
-  // scattered 4-B words (one per query row, 48 instructions for DK = 96). Each 32-dim tile goes through LDS instead
-  // (relq's 32 x 33 floats, free once the band is folded in) and out as float4 rows: 4 instructions of 8 whole 128-B
-  // row segments each.
-  float* ot = &relq[0][0];
-  const long long slab = ((long long)split * BH + bh) * T;
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int r = 0; r < 16; ++r) ot[li * (FA_NW + 1) + crow(r, hk)] = o[t][r];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int idx = k * 64 + lane, rr = idx >> 3, c4 = (idx & 7) * 4;
-      if (q0 + rr < T) {
-        const float* src = ot + rr * (FA_NW + 1) + c4;
-        const f32x4 v = {src[0], src[1], src[2], src[3]};
-        *reinterpret_cast<f32x4*>(part_o + (slab + q0 + rr) * DK + 32 * t + c4) = v;
-      }
-    }
-  }
-  if (qok && hk == 0) {
-    const long long row = slab + i;
-    part_ml[2 * row] = m_run;
-    part_ml[2 * row + 1] = l_run;
-  }
-  (void)nsplit;
-}
-
-// ---- The same attention in the two-plane fp16 split (split_bf16.h put_h16x4; the default since round 4): three
-// v_mfma_f32_32x32x16_f16 products per step into two accumulators (h h' and l h' + h l', combined as acc + 2^-11 acc2)
-// instead of six bf16 products, and K / V from fragment-major images built once per call by k_kv_split16 (every
-// query-block wave of the bf16 kernel re-split the same K and V blocks: ~30 VALU per 8 values per wave). q, k, v and
+// ---- The arithmetic: the two-plane fp16 split (split_bf16.h put_h16x4; since round 4): three v_mfma_f32_32x32x16_f16
+// products per step into two accumulators (h h' and l h' + h l', combined as acc + 2^-11 acc2) instead of the six bf16
+// products of rounds 2-3's three-plane kernel (removed in round 6), and K / V from fragment-major images built once
+// per call by k_kv_split16 (every query-block wave of the bf16 kernel re-split the same K and V blocks). q, k, v and
 // the relative tables are scaled by 2^-4 before the split (inputs up to 2^20 stay finite fp16; the softmax
 // probabilities need none) and the scales are multiplied back exactly: S by 2^8, O by 2^4.
 // Image of one (batch x head, 32-key block): K: [NS][plane][64 lanes][8 fp16] (lane (li, hk): key li, dims
@@ -735,16 +470,7 @@ int flash_attn_splits(int B, int nh, int T) {
   return ns;
 }
 
-// RVCX_FA_MATH=split: the three-plane bf16 kernel (A/B aid); default the two-plane fp16 split with K / V images
-static bool fa_h16() {
-  static const bool v = [] {
-    const char* e = rvcx_knob("RVCX_FA_MATH");
-    return !(e && std::string(e) == "split");
-  }();
-  return v;
-}
-
-// part_o's floats: the split partials, then (fp16 form) the K / V fragment images
+// part_o's floats: the split partials, then the K / V fragment images
 long long flash_attn_ws_floats(int B, int nh, int T, int dk, int nsplit) {
   const long long parts = (long long)nsplit * B * nh * T * dk;
   const long long nkb = (T + FA_K - 1) / FA_K;
@@ -762,21 +488,16 @@ hipError_t flash_attn(const float* qkv, int ldq, int B, int T, int nh, int dk, f
   if ((reinterpret_cast<uintptr_t>(rel_k) & 15) != 0) return hipErrorInvalidValue;  // float4 rel_k rows (h16 kernel)
   const int H = nh * dk;
   const int qb = (T + FA_Q - 1) / FA_Q, kb = (T + FA_K - 1) / FA_K;
-  const int per = (kb + nsplit - 1) / nsplit;
-  dim3 grid(qb, nsplit, B * nh);
   if (dk != 64 && dk != 96) return hipErrorInvalidValue;
   int nparts = nsplit;  // partials the combine merges
-  if (fa_h16()) {
+  {
     // the K / V images after the partials (the caller sized part_o with flash_attn_ws_floats)
     uint4* img = reinterpret_cast<uint4*>(part_o + (long long)nsplit * B * nh * T * dk);
     if ((reinterpret_cast<uintptr_t>(img) & 15) != 0) return hipErrorInvalidValue;
     dim3 g2(kb, B * nh, dk / 16 + dk / 16);  // NS K steps + 2 NT V^T pairs (NS = 2 NT)
-    // NW key splits per block merged in LDS (RVCX_FA_NW 1: one wave per split, every split a partial)
-    static const int nw_env = [] {
-      const char* e = rvcx_knob("RVCX_FA_NW");
-      return e ? std::atoi(e) : 4;
-    }();
-    const int NWB = (nw_env == 4 && nsplit >= 4) ? 4 : 1;
+    // four key splits per block merged in LDS (one wave per split, every split a partial, below four splits; four
+    // waves per block cut the HBM partials and the combine's reads 4-fold: TE combine 17.0 -> 6.7 us, r04zg)
+    const int NWB = nsplit >= 4 ? 4 : 1;
     nparts = (nsplit + NWB - 1) / NWB;
     const int per_w = (kb + nparts * NWB - 1) / (nparts * NWB);
     dim3 gw(qb, nparts, B * nh);
@@ -797,12 +518,6 @@ hipError_t flash_attn(const float* qkv, int ldq, int B, int T, int nh, int dk, f
         hipLaunchKernelGGL((k_flash_attn_h16<96, 1>), gw, dim3(64), 0, s, qkv, ldq, T, nh, H, qscale, per_w, rel_k,
                            rel_v, window, mask, img, part_o, part_ml);
     }
-  } else if (dk == 64) {
-    hipLaunchKernelGGL(k_flash_attn<64>, grid, dim3(64), 0, s, qkv, ldq, T, nh, H, qscale, per, rel_k, rel_v, window,
-                       mask, part_o, part_ml);
-  } else {
-    hipLaunchKernelGGL(k_flash_attn<96>, grid, dim3(64), 0, s, qkv, ldq, T, nh, H, qscale, per, rel_k, rel_v, window,
-                       mask, part_o, part_ml);
   }
   const long long rows = (long long)B * nh * T;
   if (rows * nsplit * dk >= (1LL << 31) || (ldo & 3) != 0 || (reinterpret_cast<uintptr_t>(out) & 15) != 0)

@@ -5,14 +5,10 @@
 // with W_hh = 768 x 256 fp32 (786 KB per direction: more than one CU's VGPRs + LDS can hold).
 //
 // Design: 4 working workgroups per sequence = 2 directions x 2 halves of the hidden units (partners on one XCD). A workgroup
-// owns 128 hidden units = 384 rows of W_hh (its units' r, z, n rows) and keeps ALL of them in
-// VGPRs: 768 threads, thread (j, r) holds 128 columns of row r: columns [64j, 64j+64) of its OWN
-// half of h and the same 64 columns of the PARTNER's half, as packed pairs for v_pk_fma_f32.
-// Per step every wave first takes the dot with its own columns (h_own is local), then waits for
-// the 64 partner values it needs and takes the second dot: the partner-dependent work after the
-// hand-off is 64 packed FMAs spread over all 12 waves (3 per SIMD), not 128 FMAs on half of them.
-// The gate threads add both halves. Measured (build/gru/bench_gru, T = 1568): 1.37 us/step, from 2.18
-// for 128 columns per thread split own/partner by wave (the partner half on 6 waves, 2 on some SIMDs).
+// owns 128 hidden units = 384 rows of W_hh (its units' r, z, n rows) and keeps ALL of them in VGPRs (768 threads, 128
+// weights each, as packed pairs for v_pk_fma_f32; layout below). Per step every wave first takes the dot with its own
+// half of h (local), then waits for the partner values it needs and takes the second dot, so the partner-dependent
+// work after the hand-off is spread over all 12 waves (3 per SIMD).
 // Hand-off: 8-byte {tag = step + 1, value} granules stored with agent-scope relaxed atomics (the
 // data IS the flag; MI355X_MICROARCH.md, hand-off "R2"), double-buffered by step parity; each
 // wave polls the 64 granules its lanes need (one per lane) with agent-scope relaxed loads (sc1,
@@ -33,7 +29,6 @@ constexpr int H = 256;
 constexpr int UNITS = 128;  // hidden units per workgroup
 constexpr int ROWS = 3 * UNITS;
 constexpr int NT = 2 * ROWS;  // 768 threads
-constexpr int HALF = UNITS / 2;  // columns of each half a thread covers
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr unsigned SPIN_LIMIT = 1u << 22;  // default bound on the polls of one hand-off (RVCX_GRU_SPIN_LIMIT overrides)
 
@@ -43,161 +38,20 @@ __device__ __forceinline__ float sigm(float v) { return __frcp_rn(1.f + __expf(-
 __device__ __forceinline__ float tanh_g(float v) { return 1.f - 2.f * __frcp_rn(1.f + __expf(2.f * v)); }
 }  // namespace
 
-// MODE (measurement aid, RVCX_GRU_MODE; bench_gru): 0 the recurrence; 1 the hand-off alone (no W_hh dots: the
-// partner poll, the gates and the publish of every step); 2 the math alone (the dots and gates, no poll: partner
-// values read as published by nobody)
-template <int MODE>
-__global__ __launch_bounds__(NT, 1) void k_gru_bidir(const float* __restrict__ gi, const float* whh_f,
-                                                     const float* bhh_f, const float* whh_b, const float* bhh_b,
-                                                     int T, float* out, unsigned long long* xchg,
-                                                     unsigned* status, unsigned spin_limit, unsigned tag0,
-                                                     int adjacent) {
-  __shared__ __attribute__((aligned(16))) float h_own[UNITS];
-  __shared__ __attribute__((aligned(16))) float h_pw[NT / 64][HALF];  // per-wave copy of its partner columns
-  __shared__ float part[2][ROWS];
-  __shared__ float bias_h[ROWS];
-  __shared__ int abort_flag;
-
-  // 16 blocks per sequence, 4 of them working: block w = 0 / 8 are direction 0's two halves, 1 / 9 direction 1's.
-  // Blocks are dealt round-robin to the 8 XCDs (MI355X_MICROARCH.md), so each partner pair shares one XCD and its
-  // L2: the per-step hand-off stays inside that L2 instead of crossing XCDs through memory.
-  const int w = blockIdx.x & 15;
-  if (adjacent ? w > 3 : (w & 7) > 1) return;
-  const int d = adjacent ? w >> 1 : w & 1;  // direction
-  const int q = adjacent ? w & 1 : w >> 3;  // half
-  const int seq = blockIdx.x >> 4;  // independent sequence (batched streams / utterances of one length)
-  gi += (long long)seq * T * 6 * H;
-  out += (long long)seq * T * 2 * H;
-  xchg += (long long)seq * 4 * 2 * UNITS;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int j = tid / ROWS;        // column quarter within each half (wave-uniform: ROWS % 64 == 0)
-  const int r = tid - j * ROWS;    // local row: gate r / 128, unit r % 128
-  const float* whh = d ? whh_b : whh_f;
-  const float* bhh = d ? bhh_b : bhh_f;
-  unsigned long long* mine = xchg + ((long long)(d * 2 + q) * 2) * UNITS;          // [2][128]
-  unsigned long long* theirs = xchg + ((long long)(d * 2 + (1 - q)) * 2) * UNITS;  // [2][128]
-
-  const int gate = r / UNITS, unit = r % UNITS;
-  const int grow = gate * H + q * UNITS + unit;
-  // this thread's columns: HALF of the workgroup's own units and the same HALF of the partner's
-  const int own0 = q * UNITS + j * HALF, par0 = (1 - q) * UNITS + j * HALF;
-  f32x2 wo[HALF / 2], wp[HALF / 2];
-#pragma unroll
-  for (int k = 0; k < HALF; k += 4) {
-    const float4 v = *reinterpret_cast<const float4*>(&whh[(long long)grow * H + own0 + k]);
-    wo[k / 2] = f32x2{v.x, v.y};
-    wo[k / 2 + 1] = f32x2{v.z, v.w};
-    const float4 u = *reinterpret_cast<const float4*>(&whh[(long long)grow * H + par0 + k]);
-    wp[k / 2] = f32x2{u.x, u.y};
-    wp[k / 2 + 1] = f32x2{u.z, u.w};
-  }
-  if (tid < UNITS) h_own[tid] = 0.f;
-  if (tid == 0) abort_flag = 0;
-  const int gunit = q * UNITS + tid;  // gate threads: tid < 128
-  if (tid < ROWS) bias_h[tid] = bhh[(tid / UNITS) * H + q * UNITS + tid % UNITS];
-  __syncthreads();
-
-  // dot of HALF weights with HALF values in LDS (broadcast float4 reads), two packed-FMA chains
-#define RVCX_GRU_DOT(W, HV, OUT)                                                      \
-  do {                                                                               \
-    f32x2 a0_ = {0.f, 0.f}, a1_ = {0.f, 0.f};                                        \
-    _Pragma("unroll") for (int k = 0; k < HALF; k += 4) {                            \
-      const float4 x_ = *reinterpret_cast<const float4*>(&(HV)[k]);                  \
-      a0_ = __builtin_elementwise_fma(W[k / 2], f32x2{x_.x, x_.y}, a0_);             \
-      a1_ = __builtin_elementwise_fma(W[k / 2 + 1], f32x2{x_.z, x_.w}, a1_);         \
-    }                                                                                \
-    OUT = (a0_.x + a1_.x) + (a0_.y + a1_.y);                                         \
-  } while (0)
-
-  // input gates of step s: issued at the top of the step, consumed after the hand-off (a prefetch one step
-  // ahead measured slower: its registers pushed the kernel into scratch)
-  auto load_ig = [&](int s, float& ir, float& iz, float& in) {
-    const int t = d ? (T - 1 - s) : s;
-    const int o = t * (6 * H) + d * 3 * H + gunit;  // 32-bit offset from the uniform base (T * 1536 < 2^31)
-    ir = gi[o];
-    iz = gi[o + H];
-    in = gi[o + 2 * H];
-  };
-  float ig_r = 0.f, ig_z = 0.f, ig_n = 0.f;
-  for (int s = 0; s < T; ++s) {
-    const int t = d ? (T - 1 - s) : s;
-    if (tid < UNITS) load_ig(s, ig_r, ig_z, ig_n);
-    // ---- phase A: own columns from h_own(s-1) right away, then each wave fetches the 64 partner values of
-    // h(s-1) it needs (one granule per lane) and takes its partner columns. (One polling wave + a barrier
-    // measured slower: 2.4 vs 1.9 us/step.)
-    float own = 0.f, par = 0.f;
-    if constexpr (MODE != 1) RVCX_GRU_DOT(wo, h_own + j * HALF, own);
-    asm volatile("" : "+v"(own));  // finish the own-column dot before polling (else it is sunk past the spin)
-    {
-      float* hp = h_pw[wave];
-      if (MODE != 2 && s > 0) {
-        const unsigned epoch = tag0 + (unsigned)s;
-        const unsigned long long* slot = theirs + ((s - 1) & 1) * UNITS + j * HALF;
-        unsigned long long gv = 0;
-#pragma nounroll
-        for (unsigned spins = 0;; ++spins) {
-          // the limit is checked before the poll, so spin_limit 0 (test hook) fails the first hand-off
-          // deterministically instead of racing the partner
-          if (spins >= spin_limit) {
-            abort_flag = 1;
-            break;
-          }
-          gv = __hip_atomic_load(&slot[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((unsigned)(gv >> 32) == epoch) break;
-          __builtin_amdgcn_s_sleep(1);
-        }
-        hp[lane] = __uint_as_float((unsigned)gv);
-      } else {
-        hp[lane] = 0.f;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if constexpr (MODE != 1) RVCX_GRU_DOT(wp, hp, par);
-    }
-    part[j][r] = own + par;
-    __syncthreads();
-    if (abort_flag) {
-      // status is host-mapped pinned memory (the context's device-status word): a plain system-scope store
-      // (idempotent: every aborting workgroup writes the same 1), read by the host after it synchronises
-      if (tid == 0) __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return;
-    }
-    // ---- phase B: gates for the 128 own units, publish h(s)
-    if (tid < UNITS) {
-      const float hr = (part[0][tid] + part[1][tid]) + bias_h[tid];
-      const float hz = (part[0][UNITS + tid] + part[1][UNITS + tid]) + bias_h[UNITS + tid];
-      const float hn = (part[0][2 * UNITS + tid] + part[1][2 * UNITS + tid]) + bias_h[2 * UNITS + tid];
-      const float rr = sigm(hr + ig_r);
-      const float zz = sigm(hz + ig_z);
-      const float nn = tanh_g(ig_n + hn * rr);
-      const float hprev = h_own[tid];
-      const float hnew = (hprev - nn) * zz + nn;
-      h_own[tid] = hnew;
-      out[(long long)t * (2 * H) + d * H + gunit] = hnew;
-      const unsigned long long g =
-          ((unsigned long long)(tag0 + (unsigned)(s + 1)) << 32) | (unsigned long long)__float_as_uint(hnew);
-      __hip_atomic_store(&mine[(s & 1) * UNITS + tid], g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-  }
-#undef RVCX_GRU_DOT
-}
-
-// Gate-major layout (round 5): the same 4 workgroups x 768 threads and the same W_hh-in-VGPRs budget (128 weights per
-// thread), but a wave owns ONE gate of all 128 units of its workgroup and a 32-column group of each half of h: wave w
-// = (gate g = w / 4, column group cg = w % 4), lane l holds rows (g, unit l) and (g, unit 64 + l) over own columns
-// [32 cg, 32 cg + 32) and the same 32 partner columns. Every h value a wave reads now feeds two rows, so the per-step
-// LDS broadcast reads of h halve (16 ds_read_b128 per wave instead of 32; they were ~1500 of the CU's LDS cycles per
-// step, the larger part of the math phase), the partner work after the hand-off stays 32 packed FMAs on every wave,
-// and the gate threads sum four column-group partials instead of two.
+// Gate-major layout (round 5): a wave owns ONE gate of all 128 units of its workgroup and a 32-column group of each
+// half of h: wave w = (gate g = w / 4, column group cg = w % 4), lane l holds rows (g, unit l) and (g, unit 64 + l)
+// over own columns [32 cg, 32 cg + 32) and the same 32 partner columns (128 weights per thread). Every h value a wave
+// reads feeds two rows, so the per-step LDS broadcast reads of h are 16 ds_read_b128 per wave (32 in rounds 2-4's
+// row-major waves, which were the larger part of the math phase: 1.405 -> 1.24 us per step), the partner work after
+// the hand-off is 32 packed FMAs on every wave, and the gate threads sum four column-group partials.
+// MODE (measurement aid, RVCX_GRU_MODE; bench_gru): 0 the recurrence; 1 the hand-off alone (no W_hh dots: the partner
+// poll, the gates and the publish of every step); 2 the math alone (the dots and gates, no poll: partner values read
+// as published by nobody)
 template <int MODE>
 __global__ __launch_bounds__(NT, 1) void k_gru_bidir_g(const float* __restrict__ gi, const float* whh_f,
                                                        const float* bhh_f, const float* whh_b, const float* bhh_b,
                                                        int T, float* out, unsigned long long* xchg,
-                                                       unsigned* status, unsigned spin_limit, unsigned tag0,
-                                                       int adjacent) {
+                                                       unsigned* status, unsigned spin_limit, unsigned tag0) {
   constexpr int CG = 32;  // columns of each half per wave
   __shared__ __attribute__((aligned(16))) float h_own[UNITS];
   __shared__ __attribute__((aligned(16))) float h_pw[NT / 64][CG];  // per-wave copy of its partner columns
@@ -206,9 +60,9 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir_g(const float* __restrict__
   __shared__ int abort_flag;
 
   const int w = blockIdx.x & 15;
-  if (adjacent ? w > 3 : (w & 7) > 1) return;
-  const int d = adjacent ? w >> 1 : w & 1;
-  const int q = adjacent ? w & 1 : w >> 3;
+  if ((w & 7) > 1) return;  // partners w and w + 8 share an XCD under round-robin placement (speed only)
+  const int d = w & 1;       // direction
+  const int q = w >> 3;      // half
   const int seq = blockIdx.x >> 4;
   gi += (long long)seq * T * 6 * H;
   out += (long long)seq * T * 2 * H;
@@ -349,26 +203,17 @@ hipError_t gru_bidir(const float* gi, const float* whh_f, const float* bhh_f, co
     tag0 = 1;
   }
   *next_tag = tag0 + (unsigned)T + 1;
-  static const int adj = [] {  // RVCX_GRU_ADJACENT=1: partners in adjacent blocks (different XCDs; A/B aid)
-    const char* e = rvcx_knob("RVCX_GRU_ADJACENT");
-    return e ? std::atoi(e) : 0;
-  }();
-  // fault-injection test hook, read without the RVCX_EXPERIMENTAL opt-in (it cannot change a result, only force the
-  // loud timeout path): a tiny RVCX_GRU_SPIN_LIMIT makes the hand-off time out
+  // fault-injection hook (RVCX_EXPERIMENTAL=1 RVCX_GRU_SPIN_LIMIT=0 forces the loud timeout path; read per call so a
+  // test can set and clear it)
   unsigned spin = SPIN_LIMIT;
-  if (const char* e = std::getenv("RVCX_GRU_SPIN_LIMIT")) spin = (unsigned)std::strtoul(e, nullptr, 10);
+  if (const char* e = rvcx_knob("RVCX_GRU_SPIN_LIMIT")) spin = (unsigned)std::strtoul(e, nullptr, 10);
   static const int mode = [] {
     const char* e = rvcx_knob("RVCX_GRU_MODE");
     return e ? std::atoi(e) : 0;
   }();
-  static const int layout = [] {  // RVCX_GRU_LAYOUT: 0 row-major waves (rounds 2-4), 1 gate-major waves (default)
-    const char* e = rvcx_knob("RVCX_GRU_LAYOUT");
-    return e ? std::atoi(e) : 1;
-  }();
-  auto kern = layout == 0 ? (mode == 1 ? k_gru_bidir<1> : (mode == 2 ? k_gru_bidir<2> : k_gru_bidir<0>))
-                          : (mode == 1 ? k_gru_bidir_g<1> : (mode == 2 ? k_gru_bidir_g<2> : k_gru_bidir_g<0>));
+  auto kern = mode == 1 ? k_gru_bidir_g<1> : (mode == 2 ? k_gru_bidir_g<2> : k_gru_bidir_g<0>);
   hipLaunchKernelGGL(kern, dim3(16 * B), dim3(NT), 0, s, gi, whh_f, bhh_f, whh_b, bhh_b, T, out, xchg, status, spin,
-                     tag0, adj);
+                     tag0);
   return hipGetLastError();
 }
 

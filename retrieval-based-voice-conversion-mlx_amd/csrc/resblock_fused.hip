@@ -321,12 +321,11 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
   int tile = blockIdx.x * per;
   const int tile_end = min(total, tile + per);
   if (tile >= tile_end) return;
-  // the first job's weights and the first tile's x are in flight together
-  const bool pre = (a.flags & 1) != 0;  // contiguous runs: the next tile mostly sits in L2 already (A/B: off 22.19, on 22.30 ms)
-  if (pre) load_x(tile);
+  // (a next-tile x prefetch into registers measured slower: contiguous runs find the next tile in L2 already, and the
+  // first weight wait after it stalls on the HBM load, A/B 22.30 vs 22.19 ms)
 #pragma unroll 1
   for (; tile < tile_end; ++tile) {
-  if (!pre) load_x(tile);
+  load_x(tile);
   const int b = tile / ntiles;
   const int t0 = (tile - b * ntiles) * TT;
   const float* X = a.x + (long long)b * a.x_bs;
@@ -334,7 +333,6 @@ __global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, c
   // conv1 (writing TS) after every wave's conv2 of the previous tile (reading TS)
   write_x();
   __syncthreads();
-  if (pre && tile + 1 < tile_end) load_x(tile + 1);
   float* Y = a.y + (long long)b * a.y_bs;
 #pragma unroll 1
   for (int job = 0; job < 2 * UPW; ++job) {
@@ -513,8 +511,10 @@ hipError_t rb_wsplit_build(const float* w, int C, int k, void* out, hipStream_t 
   return hipGetLastError();
 }
 
-// cfg 0 = default per C; otherwise (C, NBT, TN) = 32: 1 (4,1) 2 (8,2); 64: 1 (2,1) 2 (4,2)
+// (C, NBT, TN) = 32: (4, 1), 64: (2, 1). The (8, 2) / (4, 2) tiles (two time blocks per wave) measured slower (+0.35 ms
+// in the C2 step) and are gone: cfg must be 0
 hipError_t rb_pair(const RbPairArgs& a, int cfg, hipStream_t s) {
+  if (cfg != 0) return hipErrorInvalidValue;
   if (!rb_pair_fits(a.C, a.k, a.d) || a.T < 1 || a.B < 1 || !a.x || !a.y || !a.w1s || !a.w2s || !a.b1 || !a.b2 ||
       a.x == a.y)
     return hipErrorInvalidValue;
@@ -522,8 +522,8 @@ hipError_t rb_pair(const RbPairArgs& a, int cfg, hipStream_t s) {
       (a.y_bs & 3))
     return hipErrorInvalidValue;
   switch (a.C) {
-    case 32: return cfg == 2 ? launch_rb<32, 8, 2>(a, s) : launch_rb<32, 4, 1>(a, s);
-    case 64: return cfg == 2 ? launch_rb<64, 4, 2>(a, s) : launch_rb<64, 2, 1>(a, s);
+    case 32: return launch_rb<32, 4, 1>(a, s);
+    case 64: return launch_rb<64, 2, 1>(a, s);
     default: return hipErrorInvalidValue;
   }
 }

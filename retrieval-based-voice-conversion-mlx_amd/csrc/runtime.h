@@ -140,26 +140,12 @@ struct Ctx {
   // set while HuBERT's feature encoder is being issued (runtime_pipeline.cpp issue_front): the launches RVCX_AUX_LDS
   // throttles
   bool aux_front = false;
-  // split-K tile arrival counters per stream (ConvArgs::fix_cnt), allocated and zeroed on a stream's first split launch
-  static constexpr int SPLITK_COUNTERS = 16384;
-  std::map<hipStream_t, std::unique_ptr<DevBuf>> fix_counters;
-  unsigned* splitk_counters(hipStream_t s);
   // second stream for work independent of the caller's stream (HuBERT beside RMVPE), created lazily
   hipStream_t aux = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_gate = nullptr, ev_front = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_gate = nullptr;
   hipStream_t aux_stream();
-  // a third stream restricted to ncu of the device's CUs (hipExtStreamCreateWithCUMask), for work that should leave
-  // the rest of the chip to the critical path (HuBERT's feature encoder beside the U-Net); created on first use
-  hipStream_t aux_cu = nullptr;
-  int aux_cu_n = 0;
-  hipEvent_t ev_cu_done = nullptr;
-  hipStream_t cu_stream(int ncu);
   // issued by RMVPE's E2E right before the BiGRU launch (host callback, cleared when taken)
   std::function<void(hipStream_t)> before_gru;
-  // issued by RMVPE's E2E after U-Net encoder level unet_hook_level (or, if the U-Net has no such level, before the
-  // BiGRU launch); host callback, cleared when taken
-  std::function<void(hipStream_t)> at_unet_level;
-  int unet_hook_level = -1;
   // device-side fault flags in pinned host-mapped memory (bit 0: a BiGRU partner hand-off timed out).
   // Kernels store into it; the host reads it after a synchronisation: every compute entry point checks
   // it on entry (faults of earlier, completed calls), the pipeline at its own sync points, and
@@ -201,11 +187,36 @@ struct Ctx {
   size_t arena_bytes = 0, arena_used = 0;
   size_t carved = 0;  // bytes the pool has taken since the last release (every region, regrown ones included)
   bool sizing_plan = false;  // rvcx_workspace_bytes: long inputs take the worst-case chunk plan (runtime_pipeline.cpp)
-  // Arena mode: every API call carves its regions from offset 0 again (called by the entry points before any work),
-  // so a call never inherits the regions earlier calls regrew. No device synchronisation: a call's work is enqueued
-  // after the previous call's on the caller's stream (the aux stream forks from it), so reuse is stream-ordered -- as
-  // for the named pool without an arena. The marks describing buffer contents go with the regions (a caller that
-  // wrote into its arena between calls cannot leave a stale zeroed buffer or memoised scalar behind).
+  // Call-to-call ordering: every compute entry point starts with begin_call(), which records an event on
+  // each stream the previous call took pool buffers on; the first pool buffer a call takes on a stream makes that
+  // stream wait for the previous call's events on OTHER streams. A call on stream B therefore never overwrites a
+  // region (arena mode: the same offsets under other names; pool mode: the same named buffers) that a call still
+  // running on stream A uses; calls on one stream stay ordered by the stream itself (no wait is issued).
+  std::vector<hipStream_t> call_streams;                              // streams the current call took buffers on
+  std::vector<std::pair<hipStream_t, hipEvent_t>> prev_call_events;  // the previous call's, recorded at begin_call
+  std::map<hipStream_t, hipEvent_t> call_ev;                           // one reusable event per stream
+  void begin_call() {
+    prev_call_events.clear();
+    for (hipStream_t st : call_streams) {
+      hipEvent_t& e = call_ev[st];
+      if (!e) RVCX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      RVCX_HIP(hipEventRecord(e, st));
+      prev_call_events.emplace_back(st, e);
+    }
+    call_streams.clear();
+    arena_rewind();
+  }
+  void touch_stream(hipStream_t s) {
+    for (hipStream_t st : call_streams)
+      if (st == s) return;
+    call_streams.push_back(s);
+    for (const auto& pe : prev_call_events)
+      if (pe.first != s) RVCX_HIP(hipStreamWaitEvent(s, pe.second, 0));
+  }
+  // Arena mode: every API call carves its regions from offset 0 again (begin_call, before any work), so a call never
+  // inherits the regions earlier calls regrew; reuse is ordered by the caller's stream and, across streams, by
+  // begin_call's events. The marks describing buffer contents go with the regions (a caller that wrote into its arena
+  // between calls cannot leave a stale zeroed buffer or memoised scalar behind).
   void arena_rewind() {
     if (!arena) return;
     ws.clear();
@@ -238,6 +249,7 @@ T* Ctx::buf(const std::string& name, size_t count, hipStream_t s) {
   size_t bytes = count * sizeof(T);
   if (bytes == 0) bytes = 16;
   bytes = (bytes + 255) & ~size_t(255);
+  touch_stream(s);
   auto& slot = ws[name];
   if (!slot || slot->bytes < bytes) {
     if (slot && slot->p) RVCX_HIP(hipStreamSynchronize(s));
@@ -357,8 +369,8 @@ void set_i32_once(Ctx& c, const std::string& name, int32_t* p, int32_t v, hipStr
 // far (or s itself when overlap is off: kernel timing on, or RVCX_NO_OVERLAP=1); join_aux makes s wait for
 // everything queued on the aux stream so far.
 hipStream_t fork_aux(Ctx& c, hipStream_t s);
-// whether launch_conv would run this 1-D contraction on the weight-streamed fp16 kernel without split-K (the only
-// producer / consumer of the two-plane fp16 activation image, ConvArgs::y_h16 / x_h16)
+// whether launch_conv would run this 1-D contraction on the weight-streamed fp16 kernel without split-K (the kernels
+// whose epilogue takes the fused NSF noise conv, ConvArgs::nz_*)
 bool conv_routes_wsb16(Ctx& c, const ConvArgs& a);
 // marks a synth_forward call whose rows all have the full length T (Ctx::synth_full_lengths) for its lifetime
 struct ScopedFullLengths {
@@ -371,26 +383,6 @@ void join_aux(Ctx& c, hipStream_t s, hipStream_t ax);
 void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double flops = -1.0);
 // one fused ResBlock pair (resblock_fused.hip) with optional event timing (counted with the conv family)
 void launch_rb_pair(Ctx& c, const RbPairArgs& a, hipStream_t s);
-// the fused pair is used for every ResBlock pair rb_pair_fits accepts; RVCX_NO_RBFUSE=1 restores two conv launches
-// (A/B measurement aid), RVCX_RB_CFG picks a tile configuration
-inline bool rb_fuse_enabled() {
-  static const bool v = [] {
-    const char* e = rvcx_knob("RVCX_NO_RBFUSE");
-    return !(e && std::atoi(e) != 0);
-  }();
-  return v;
-}
-
-// fused attention (flash_attn.hip) for the TextEncoder and HuBERT; RVCX_NO_FLASH=1 restores the materialised
-// score path (A/B measurement aid)
-inline bool flash_enabled() {
-  static const bool v = [] {
-    const char* e = rvcx_knob("RVCX_NO_FLASH");
-    return !(e && std::atoi(e) != 0);
-  }();
-  return v;
-}
-
 inline void check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw Error(RVCX_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }

@@ -223,52 +223,19 @@ void hubert_layers(Ctx& c, const HubertRun& run, int l0, int l1, hipStream_t s) 
   float* hs = c.buf<float>("hb.hs", (size_t)BL * HD, s);
   float* hs2 = c.buf<float>("hb.hs2", (size_t)BL * HD, s);
   float* qkv = c.buf<float>("hb.qkv", (size_t)BL * 3 * HD, s);
-  const bool fused = flash_enabled();
   const int nsplit = flash_attn_splits(B, HHEADS, L);
-  float* sc = fused ? nullptr : c.buf<float>("hb.scores", (size_t)B * HHEADS * L * L, s);
-  float* part_o =
-      fused ? c.buf<float>("hb.fa_o", (size_t)flash_attn_ws_floats(B, HHEADS, L, HD / HHEADS, nsplit), s) : nullptr;
-  float* part_ml = fused ? c.buf<float>("hb.fa_ml", (size_t)nsplit * B * HHEADS * L * 2, s) : nullptr;
+  float* part_o = c.buf<float>("hb.fa_o", (size_t)flash_attn_ws_floats(B, HHEADS, L, HD / HHEADS, nsplit), s);
+  float* part_ml = c.buf<float>("hb.fa_ml", (size_t)nsplit * B * HHEADS * L * 2, s);
   float* att = c.buf<float>("hb.att", (size_t)BL * HD, s);
   float* ff = c.buf<float>("hb.ff", (size_t)BL * HFF, s);
   const int hd = HD / HHEADS;
   for (int i = l0; i < l1; ++i) {
     const std::string q = "hb." + std::to_string(i);
     run1(c, lin(hs, HD, BL, HD, c.W(q + ".qkv.w"), 3 * HD, c.W(q + ".qkv.b"), qkv, 3 * HD), s);
-    if (fused) {  // softmax((q * hd^-0.5) k^T) v per head in one pass (flash_attn.hip): no [B][12][L][L] scores
-      check(flash_attn(qkv, 3 * HD, B, L, HHEADS, hd, (float)std::pow((double)hd, -0.5), nullptr, nullptr, 0, nullptr,
-                       part_o, part_ml, nsplit, att, HD, s),
-            "flash_attn");
-    } else {
-    {
-      ConvArgs a1 = lin(qkv, 3 * HD, L, hd, qkv + HD, L, nullptr, sc, L);
-      a1.ldw = 3 * HD;
-      a1.alpha = (float)std::pow((double)hd, -0.5);
-      a1.batch_inner = HHEADS;
-      a1.x_bs2 = hd;
-      a1.w_bs2 = hd;
-      a1.y_bs2 = (long long)L * L;
-      a1.batch = B;
-      a1.x_bs = a1.w_bs = (long long)L * 3 * HD;
-      a1.y_bs = (long long)HHEADS * L * L;
-      run1(c, a1, s);
-    }
-    check(softmax_rows(sc, B * HHEADS * L, L, s), "softmax");
-    {
-      ConvArgs a2 = lin(sc, L, L, L, qkv + 2 * HD, hd, nullptr, att, HD);
-      a2.ldw = 3 * HD;
-      a2.b_kn = 1;
-      a2.batch_inner = HHEADS;
-      a2.x_bs2 = (long long)L * L;
-      a2.w_bs2 = hd;
-      a2.y_bs2 = hd;
-      a2.batch = B;
-      a2.x_bs = (long long)HHEADS * L * L;
-      a2.w_bs = (long long)L * 3 * HD;
-      a2.y_bs = (long long)L * HD;
-      run1(c, a2, s);
-    }
-    }
+    // softmax((q * hd^-0.5) k^T) v per head in one pass (flash_attn.hip): no [B][12][L][L] scores
+    check(flash_attn(qkv, 3 * HD, B, L, HHEADS, hd, (float)std::pow((double)hd, -0.5), nullptr, nullptr, 0, nullptr,
+                     part_o, part_ml, nsplit, att, HD, s),
+          "flash_attn");
     {
       ConvArgs a3 = lin(att, HD, BL, HD, c.W(q + ".o.w"), HD, c.W(q + ".o.b"), hs2, HD);
       a3.res = hs;
@@ -581,11 +548,6 @@ static void e2e_chunk(Ctx& c, float* img, int Fc, float* sal, hipStream_t s, int
     }
     float* pooled = c.buf<float>("rm.pool" + std::to_string(i), (size_t)B * (H / 2) * (W / 2) * cout, s);
     check(avgpool2(catb[i] + cout, B * H, W, cout, 2 * cout, pooled, s), "avgpool");
-    if (c.at_unet_level && i == c.unet_hook_level) {  // work the caller wants issued from this point of the U-Net on
-      auto h = std::move(c.at_unet_level);
-      c.at_unet_level = nullptr;
-      h(s);
-    }
     x = pooled;
     ldx = cout;
     H /= 2;
@@ -678,11 +640,6 @@ static void e2e_chunk(Ctx& c, float* img, int Fc, float* sal, hipStream_t s, int
   // work the caller wants issued beside the BiGRU (which occupies 4 CUs): the gate event marks this point of the
   // stream, the BiGRU goes out first and the hook's (many) launches after it, so the host time spent issuing
   // them overlaps the BiGRU instead of delaying its launch
-  if (c.at_unet_level) {  // a hook level the U-Net does not have: issue it now, before the BiGRU's
-    auto h = std::move(c.at_unet_level);
-    c.at_unet_level = nullptr;
-    h(s);
-  }
   std::function<void(hipStream_t)> hook = std::move(c.before_gru);
   c.before_gru = nullptr;
   if (hook && c.ev_gate) RVCX_HIP(hipEventRecord(c.ev_gate, s));

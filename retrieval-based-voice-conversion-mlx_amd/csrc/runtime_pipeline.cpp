@@ -309,14 +309,6 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
   const bool guided = c.scfg.f0;
   const int split = (ax != s && guided) ? gate_layer : HUBERT_LAYERS;
   std::vector<HubertRun> hruns(chunks.size());
-  // HuBERT's feature encoder is issued beside the U-Net from encoder level front_level on (its convs slowed the
-  // U-Net's wide first levels, which are on the critical path, while the deep levels leave most CUs idle); -1:
-  // from the start. Single-chunk RMVPE calls only.
-  static const int front_level = [] {
-    const char* e = rvcx_knob("RVCX_HUBERT_FRONT_LEVEL");
-    return e ? std::atoi(e) : -1;
-  }();
-  const bool delay_front = ax != s && guided && chunks.size() == 1 && o.f0_method == 0 && front_level >= 0;
   // chunks are processed longest first: every later chunk fits the shared work buffers the first one grew, so a
   // call regrows nothing past its first chunk (a caller-sized arena, rvcx_workspace_bytes, holds any split plan);
   // the per-chunk noise offsets, seeds and output positions keep the reference's order (computed up front below)
@@ -325,55 +317,26 @@ int64_t pipeline_forward_ex(Ctx& c, const double* audio, int64_t n, const rvcx_p
   std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) {
     return chunks[x].a1 - chunks[x].a0 > chunks[y].a1 - chunks[y].a0;
   });
-  // HuBERT's feature encoder (and the layers before the gate) on a stream restricted to front_cus CUs, so the U-Net
-  // keeps the rest of the chip (RVCX_FRONT_CUS; 0: the aux stream, all CUs). The aux stream waits for it before the
-  // gated layers.
-  static const int front_cus = [] {
-    const char* e = rvcx_knob("RVCX_FRONT_CUS");
-    return e ? std::atoi(e) : 0;
-  }();
-  hipStream_t afront = ax;
-  if (ax != s && guided && chunks.size() == 1 && front_cus > 0) {
-    afront = c.cu_stream(front_cus);
-    RVCX_HIP(hipStreamWaitEvent(afront, c.ev_fork, 0));  // ordered after the padded input (fork_aux's event)
-  }
-  auto issue_front = [&]() {
-    c.aux_front = afront != s;  // reset below and by FrontScope (an exception mid-issue)
+  // HuBERT's feature encoder (and the layers before the gate) on the aux stream beside the U-Net. Measured and removed:
+  // issuing it from a later U-Net level on (neutral) and on a CU-masked stream of 64 / 128 CUs (+3.6 ms)
+  {
+    struct FrontScope {  // the throttle ends with the front end's issue, also when an exception ends it
+      Ctx& c;
+      ~FrontScope() { c.aux_front = false; }
+    } front_scope{c};
+    c.aux_front = ax != s;
     for (size_t i : order) {
       const int64_t len = chunks[i].a1 - chunks[i].a0;
       const int64_t cap_rows = len / 320 + 8;
-      cfeats[i] = c.buf<float>("pl.hb" + std::to_string(i), (size_t)cap_rows * E, afront);
-      hruns[i] = hubert_front(c, pad32 + chunks[i].a0, len, len, 1, hubert_version_for(c), cfeats[i], cap_rows, afront);
+      cfeats[i] = c.buf<float>("pl.hb" + std::to_string(i), (size_t)cap_rows * E, ax);
+      hruns[i] = hubert_front(c, pad32 + chunks[i].a0, len, len, 1, hubert_version_for(c), cfeats[i], cap_rows, ax);
       if (chunks.size() == 1) {
-        hubert_layers(c, hruns[i], 0, split, afront);
+        hubert_layers(c, hruns[i], 0, split, ax);
       } else {  // several chunks share the HuBERT workspace: each runs to completion before the next
-        hubert_layers(c, hruns[i], 0, HUBERT_LAYERS, afront);
-        cL[i] = hubert_tail(c, hruns[i], afront);
+        hubert_layers(c, hruns[i], 0, HUBERT_LAYERS, ax);
+        cL[i] = hubert_tail(c, hruns[i], ax);
       }
     }
-    c.aux_front = false;
-    if (afront != ax) {
-      RVCX_HIP(hipEventRecord(c.ev_cu_done, afront));
-      RVCX_HIP(hipStreamWaitEvent(ax, c.ev_cu_done, 0));
-    }
-  };
-  struct FrontScope {
-    Ctx& c;
-    ~FrontScope() {
-      c.at_unet_level = nullptr;
-      c.unet_hook_level = -1;
-      c.aux_front = false;
-    }
-  } front_scope{c};
-  if (delay_front) {
-    c.unet_hook_level = front_level;
-    c.at_unet_level = [&](hipStream_t main) {
-      RVCX_HIP(hipEventRecord(c.ev_front, main));
-      RVCX_HIP(hipStreamWaitEvent(afront, c.ev_front, 0));
-      issue_front();
-    };
-  } else {
-    issue_front();
   }
   // the caller records c.ev_gate on `main` where the rest may start (gate_here), then calls this
   auto gate_here = [&](hipStream_t main) {

@@ -433,12 +433,8 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
       if (npad > HAR_PAD || ntap * stride - npad > HAR_PAD + stride)
         throw Error(RVCX_E_SHAPE, "noise conv stride too large for the source padding");
       nn = "dec.noise_convs." + std::to_string(i);
-      static const bool nz_on = [] {  // RVCX_NOISE_FUSE=0: always the separate noise launch (A/B aid)
-        const char* e = rvcx_knob("RVCX_NOISE_FUSE");
-        return !(e && std::atoi(e) == 0);
-      }();
       const int kk = ntap * stride;
-      if (nz_on && kk == 1 && conv_routes_wsb16(c, a)) {
+      if (kk == 1 && conv_routes_wsb16(c, a)) {
         a.nz_har = har + HAR_PAD - npad;
         a.nz_bs = har_ld;
         a.nz_stride = stride;
@@ -474,13 +470,9 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
       const auto& dil = cf.rb_d[j];
       const std::string rb = "dec.resblocks." + std::to_string(i * nk + j);
       const float* r_in = y;
-      static const int rb_maxc = [] {
-        // widest stage taking the fused pair: 32 channels (same-box A/B of C2: fused 32 + weight-streamed 64
-        // 21.97 ms, fused 32 + 64 22.46, weight-streamed both 23.07; RVCX_RB_MAXC overrides)
-        const char* e = rvcx_knob("RVCX_RB_MAXC");
-        return e ? std::atoi(e) : 32;
-      }();
-      bool fuse = rb_fuse_enabled() && C <= rb_maxc;
+      // widest stage taking the fused pair: 32 channels (same-box A/B of C2: fused 32 + weight-streamed 64 21.97 ms,
+      // fused 32 + 64 22.46, weight-streamed both 23.07; again +0.1 ms at 64 in round 5)
+      bool fuse = C <= 32;
       for (int d : dil) fuse = fuse && rb_pair_fits(C, k, d);
       if (fuse) {
         // each dilation pair as one fused kernel (resblock_fused.hip); pairs ping-pong between RR and T1 (a pair
@@ -515,15 +507,8 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
         }
         continue;
       }
-      // c1 hands its output to c2 as the two-plane fp16 image when both run on the weight-streamed fp16 kernel: c2's
-      // input has no pre-activation (c1's epilogue applies the leaky ReLU) and no other reader, so the image (the
-      // same 4 B per element) replaces the fp32 tensor and c2's halo staging is a copy instead of a split.
-      // Off by default (RVCX_PRESPLIT=1 turns it on): same-box C2 A/Bs measured it within noise of the fp32 hand-off
-      // (13.03/13.06 ms on vs 12.996/12.954 off), the epilogue's extra split costing what c2's staging saves
-      static const bool presplit_on = [] {
-        const char* e = rvcx_knob("RVCX_PRESPLIT");
-        return e && std::atoi(e) != 0;
-      }();
+      // (c1 handing its output to c2 as a two-plane fp16 image, so that c2's halo staging is a copy instead of a split,
+      // measured within noise of the fp32 hand-off in round 5: 13.03 / 13.06 ms vs 12.996 / 12.954; removed)
       for (size_t m = 0; m < dil.size(); ++m) {
         const int d = dil[m];
         const std::string n1 = rb + ".convs1." + std::to_string(m);
@@ -540,10 +525,6 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
         ConvArgs a2 = conv(T1, C, Ti, C, c.W(n2 + ".w"), C, k, 1, (k - 1) / 2, c.W(n2 + ".b"), dst, C, Ti, B);
         a2.w_static = 1;
         a2.lowp = gen_lowp;
-        if (presplit_on && C % 32 == 0 && conv_routes_wsb16(c, a1) && conv_routes_wsb16(c, a2)) {
-          a1.y_h16 = 1;
-          a2.x_h16 = 1;
-        }
         run(c, a1, s);
         a2.res = r_in;
         a2.ldr = C;
@@ -572,7 +553,7 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
                    float* out, float* zp_out, float* z_out, hipStream_t s, int gen_lowp, int head, float* mp_out,
                    float* logsp_out) {
   const SynthCfg& cf = c.scfg;
-  const int H = cf.H, I = cf.I, F = cf.F, E = cf.emb_dim, nh = cf.n_heads, dk = H / nh, nw = 2 * cf.window + 1;
+  const int H = cf.H, I = cf.I, F = cf.F, E = cf.emb_dim, nh = cf.n_heads, dk = H / nh;
   const long long BT = (long long)B * T;
   float* mask = c.buf<float>("te.mask", BT, s);
   check(seq_mask(lengths, mask, B, T, s), "seq_mask");
@@ -598,13 +579,9 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
     run(c, a, s);
   }
   float* qkv = c.buf<float>("te.qkv", BT * 3 * H, s);
-  const bool fused = flash_enabled();
   const int nsplit = flash_attn_splits(B, nh, T);
-  float* sc = fused ? nullptr : c.buf<float>("te.scores", (size_t)B * nh * T * T, s);
-  float* rel = fused ? nullptr : c.buf<float>("te.rel", (size_t)B * nh * T * nw, s);
-  float* pband = fused ? nullptr : c.buf<float>("te.pband", (size_t)B * nh * T * nw, s);
-  float* part_o = fused ? c.buf<float>("te.fa_o", (size_t)flash_attn_ws_floats(B, nh, T, dk, nsplit), s) : nullptr;
-  float* part_ml = fused ? c.buf<float>("te.fa_ml", (size_t)nsplit * B * nh * T * 2, s) : nullptr;
+  float* part_o = c.buf<float>("te.fa_o", (size_t)flash_attn_ws_floats(B, nh, T, dk, nsplit), s);
+  float* part_ml = c.buf<float>("te.fa_ml", (size_t)nsplit * B * nh * T * 2, s);
   float* att = c.buf<float>("te.att", BT * H, s);
   float* o = c.buf<float>("te.o", BT * H, s);
   float* h1 = c.buf<float>("te.h1", BT * F, s);
@@ -612,68 +589,12 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
   for (int i = 0; i < cf.n_layers; ++i) {
     const std::string q = "te." + std::to_string(i);
     run(c, lin(x, H, (int)BT, H, c.W(q + ".qkv.w"), 3 * H, c.W(q + ".qkv.b"), qkv, 3 * H), s);
-    if (fused) {  // attentions.py:79-185 in one pass per query block (flash_attn.hip): no [B][nh][T][T] scores
-      // the key mask only where a row is shorter than T: with every length T it is all ones, and its per-element loads
-      // in the key loop cost the TextEncoder's attention ~1/3 of its time (the fill never fires: identical results)
-      check(flash_attn(qkv, 3 * H, B, T, nh, dk, qscale, c.W(q + ".rel_k"), c.W(q + ".rel_v"), cf.window,
-                       c.synth_full_lengths ? nullptr : mask, part_o,
-                       part_ml, nsplit, att, H, s),
-            "flash_attn");
-    } else {
-    {  // scores = (q / sqrt(dk)) k^T   (attentions.py:96)
-      ConvArgs a = lin(qkv, 3 * H, T, dk, qkv + H, T, nullptr, sc, T);
-      a.ldw = 3 * H;
-      a.alpha = qscale;
-      a.batch = B;
-      a.batch_inner = nh;
-      a.x_bs = (long long)T * 3 * H;
-      a.x_bs2 = dk;
-      a.w_bs = (long long)T * 3 * H;
-      a.w_bs2 = dk;
-      a.y_bs = (long long)nh * T * T;
-      a.y_bs2 = (long long)T * T;
-      run(c, a, s);
-    }
-    {  // relative key logits (attentions.py:127-132)
-      ConvArgs a = lin(qkv, 3 * H, T, dk, c.W(q + ".rel_k"), nw, nullptr, rel, nw);
-      a.alpha = qscale;
-      a.batch = B;
-      a.batch_inner = nh;
-      a.x_bs = (long long)T * 3 * H;
-      a.x_bs2 = dk;
-      a.y_bs = (long long)nh * T * nw;
-      a.y_bs2 = (long long)T * nw;
-      run(c, a, s);
-    }
-    check(softmax_rel(sc, T, nh, B, rel, cf.window, mask, pband, 0, s), "softmax_rel");
-    {  // p v   (attentions.py:120)
-      ConvArgs a = lin(sc, T, T, T, qkv + 2 * H, dk, nullptr, att, H);
-      a.ldw = 3 * H;
-      a.b_kn = 1;
-      a.batch = B;
-      a.batch_inner = nh;
-      a.x_bs = (long long)nh * T * T;
-      a.x_bs2 = (long long)T * T;
-      a.w_bs = (long long)T * 3 * H;
-      a.w_bs2 = dk;
-      a.y_bs = (long long)T * H;
-      a.y_bs2 = dk;
-      run(c, a, s);
-    }
-    {  // + relative values (attentions.py:122-123, 134-141)
-      ConvArgs a = lin(pband, nw, T, nw, c.W(q + ".rel_v"), dk, nullptr, att, H);
-      a.ldw = dk;
-      a.b_kn = 1;
-      a.batch = B;
-      a.batch_inner = nh;
-      a.x_bs = (long long)nh * T * nw;
-      a.x_bs2 = (long long)T * nw;
-      a.y_bs = (long long)T * H;
-      a.y_bs2 = dk;
-      a.acc_mode = ACC_ADD;
-      run(c, a, s);
-    }
-    }
+    // attentions.py:79-185 in one pass per query block (flash_attn.hip): no [B][nh][T][T] scores. The key mask only
+    // where a row is shorter than T: with every length T it is all ones, and its per-element loads in the key loop
+    // cost the TextEncoder's attention ~1/3 of its time (the fill never fires: identical results)
+    check(flash_attn(qkv, 3 * H, B, T, nh, dk, qscale, c.W(q + ".rel_k"), c.W(q + ".rel_v"), cf.window,
+                     c.synth_full_lengths ? nullptr : mask, part_o, part_ml, nsplit, att, H, s),
+          "flash_attn");
     run(c, lin(att, H, (int)BT, H, c.W(q + ".o.w"), H, c.W(q + ".o.b"), o, H), s);
     check(layernorm_rows(x, o, x, c.W(q + ".ln1.g"), c.W(q + ".ln1.b"), (int)BT, H, 1e-5f, nullptr, s), "ln1");
     {  // FFN (attentions.py:221-231): conv_1(pad(x*mask)) -> relu -> conv_2(pad(.*mask)) * mask

@@ -57,10 +57,6 @@ struct ConvArgs {
   int C_in = 0;         // contraction channels per tap
   int pre_act = ACT_NONE;
   float pre_slope = 0.f;
-  // x is the two-plane fp16 image an h16 epilogue wrote (y_h16 below): per row and 32-channel chunk 128 B = the h
-  // plane (32 fp16) then the 2^11-scaled residual plane, of the values times 2^-4 -- the weight-streamed kernel's LDS
-  // row layout, so its A staging is a plain copy (conv_wsb16_kernel only; ldx = C_in, no pre_act / pre_mask)
-  int x_h16 = 0;
   const float* pre_mask = nullptr;  // [b][row] multiplier applied to input rows (1-D only)
   long long pre_mask_bs = 0;
   // B operand (weights): NK: w + tap*w_ts + n*ldw + c ; KN: w + tap*w_ts + c*ldw + n
@@ -96,9 +92,6 @@ struct ConvArgs {
   long long mask_bs = 0;
   int acc_mode = ACC_STORE;
   float acc_div = 1.f;
-  // write y as that two-plane fp16 image instead of fp32 (after bias / act; ldy = N, N % 32 == 0, ACC_STORE, no mask,
-  // no residual, no split-K; a consumer takes it with x_h16)
-  int y_h16 = 0;
   // WaveNet gate (commons.py:88-103) in the split-K combine: N = 2 gate_h columns; y[m][c] (c < gate_h) =
   // tanh(v[c] + g[c]) * sigmoid(v[c + gate_h] + g[c + gate_h]), v = acc + bias, g = gate_g + b * gate_g_bs. Forces a
   // split (ksplit >= 2); no other epilogue field may be set.
@@ -116,10 +109,10 @@ struct ConvArgs {
   int batch = 1;
   int batch_inner = 1;
   long long x_bs2 = 0, w_bs2 = 0, y_bs2 = 0, res_bs2 = 0, bias_bs2 = 0;
-  // tuning / benchmarking: force a tile configuration (0..5) and the software pipeline on/off
+  // tuning / benchmarking: force a tile configuration and the software pipeline on/off
   int force_cfg = -1;
   int pipe = 0;
-  int astage = 0;  // A-tile staging batch: 0 = default (RVCX_CONV_ASB or 1), 1 = serial, 4 = 4 loads in flight
+  int astage = 0;  // A-tile staging batch: 0 = default (1), 1 = serial, 4 = 4 loads in flight
   int math = 0;    // contraction arithmetic: 0 = default (RVCX_CONV_MATH), 1 = native fp32 MFMA, 2 = fp32 via 3 bf16 planes
   // split-K: set by conv_plan_splitk; ws holds ksplit partial [rows][N] tiles per batch entry
   // weight-streamed split kernel (conv_wsb.hip): w pre-split into bf16 planes, set by the runtime for static weights
@@ -136,12 +129,6 @@ struct ConvArgs {
   int lowp = 0;
   long long ws_rows = 0;
   float* ws = nullptr;
-  // split-K without the combine launch (round 5): one arrival counter per output tile (zero between launches). Each
-  // slice writes its partial tile with device-scope stores and counts the tile; the last slice to arrive sums the
-  // slices in slice order (splitk_reduce_kernel's arithmetic) and runs the epilogue. Set by the dispatcher only for
-  // the kernels whose epilogue is store_tile16 and the plain epilogue (no gate, no LayerNorm); fix_cap counters
-  unsigned* fix_cnt = nullptr;
-  int fix_cap = 0;
   // + the NSF noise conv of this output (hifigan_nsf.py:196-199: x = ups(x) + noise_convs(har)), fused into the
   // epilogue of the polyphase ConvTranspose (1-D, unsplit, store_tile16 kernels, plain bias epilogue; one tap,
   // nz_kk = 1, the only length the dispatcher admits): output row m,
@@ -167,7 +154,7 @@ const char* conv_kind_name(int k);
 int conv_math_of(const ConvArgs& a);
 hipError_t conv2d(const ConvArgs& a, hipStream_t s);
 // 3x3/pad-1 2-D convs with C_in, N in {16, 32} on 16x16x4 MFMA fragments (conv2d_small.hip); conv2d routes
-// the shapes conv2d_small_fits accepts there (RVCX_NO_SMALL2D=1 disables)
+// the shapes conv2d_small_fits accepts there
 bool conv2d_small_fits(const ConvArgs& a);
 hipError_t conv2d_small(const ConvArgs& a, hipStream_t s);
 // their WSPLIT_S2D image (the fp16-split form reads it; built by conv_wsplit_build for that format)
@@ -184,13 +171,13 @@ hipError_t channel_flip(const float* x, float* y, int rows, int C, hipStream_t s
 hipError_t gather_rows(const float* table, int ld_table, const int32_t* idx, float* y, int rows, int C,
                        hipStream_t s);
 hipError_t seq_mask(const int32_t* lengths, float* mask, int B, int T, hipStream_t s);
+// ConvTranspose2d 3x3 / stride 2 / pad 1 / output pad 1 weights w [C][co][3][3] -> the 2x2-tap phase conv's
+// [4][4 co][C] (virtual column (ph 2 + pw) co + o; ConvArgs::out_map OUT_UPSAMPLE2D scatters the phases)
+hipError_t upconv_phase_pack(const float* w, int C, int co, float* out, hipStream_t s);
 hipError_t layernorm_rows(const float* x, const float* r, float* y, const float* gamma, const float* beta,
                           int rows, int D, float eps, const float* mask, hipStream_t s);
 hipError_t gate_tanh_sigmoid(const float* xin, int ldx, const float* g, long long g_bs, float* acts, int B,
                              int T, int H, hipStream_t s);
-hipError_t softmax_rel(float* scores, int T, int n_heads, int B, const float* rel, int window,
-                       const float* mask, float* pband, int rows_scaled_by_band, hipStream_t s);
-hipError_t softmax_rows(float* scores, int rows, int cols, hipStream_t s);
 // y[b][t][c] += nb[c] + sum_{q < taps*stride} wf[(q / stride) * C + c][q % stride] * har[b*har_bs + t*stride + q]
 // (the NSF noise conv, hifigan_nsf.py:196-199, in its framed form); C % 4 == 0, taps*stride <= 16
 // weight-streamed split conv (conv_wsb.hip): eligibility (1-D, stride 1, C_in % 32 == 0, halo <= 64 rows, no
@@ -198,15 +185,15 @@ hipError_t softmax_rows(float* scores, int rows, int cols, hipStream_t s);
 // large enough to fill the chip (conv_gemm.hip policy)
 bool conv_wsb_eligible(const ConvArgs& a, bool two_d = false);
 bool conv_wsb_wants(const ConvArgs& a);
-// route a contraction with a static weight to the weight-streamed kernel: the big 1-D grids (conv_wsb_wants), and
-// behind RVCX_WSB_SPLIT / RVCX_WSB_2D the small 1-D grids (with split-K) and the 3x3 2-D convs with >= 64 channels
+// route a contraction with a static weight to the weight-streamed kernel (the big 1-D grids, conv_wsb_wants) or the
+// gather-streamed one (the rest with 32-channel chunks and >= 64 outputs)
 // 0: not routed (conv_emu / conv_gemm), 1: conv_wsb.hip, 2: conv_gs.hip
 int conv_wsb_route(const ConvArgs& a, bool two_d);
-bool conv_wsb_tile(int cfg, int& BM, int& BN);  // cfg 20..28 -> tile
+bool conv_wsb_tile(int cfg, int& BM, int& BN);  // cfg 23, 24, 25, 27 -> tile
 int conv_wsb_pick(const ConvArgs& a);  // the weight-streamed tile cfg the size policy picks for a
 // gather-streamed split conv (conv_gs.hip) for the short contractions: pre-split weights (the conv_wsb image) in a
 // register ring, A gathered per (chunk, tap) step; 1-D (any stride / dilation) and 2-D (stride 1, OUT_ROWS), C_in % 32
-// == 0, split-K capable. cfg 30..32 -> tile
+// == 0, split-K capable. cfg 30 -> its 64 x 64 tile
 bool conv_gs_eligible(const ConvArgs& a, bool two_d);
 bool conv_gsw_eligible(const ConvArgs& a);  // the windowed 2-D form (split-K slices of whole 32-channel chunks)
 bool conv_gs_tile(int cfg, int& BM, int& BN);
@@ -231,7 +218,6 @@ struct RbPairArgs {
   long long y_bs = 0;
   int acc_mode = ACC_STORE;
   float acc_div = 1.f;
-  int flags = 0;  // bit 0: next-tile x prefetch into registers (measurement aid, RVCX_RB_FLAGS)
   int wfmt = 0;   // RB_WBF16: w1s / w2s are three-plane bf16 images (the exact split); RB_WF16: two-plane fp16 images
   int lowp = 0;   // opt-in reduced precision (rvcx_rt_opts::gen_precision): the fp16 images' hi planes alone
 };
@@ -380,12 +366,10 @@ struct SosPlan {
   const double* pow(int j) const { return coef(j) + 16; }
   const double* ca(int j) const { return coef(j) + 64; }
 };
-size_t sos_ws_doubles(long long n_ext, int L);
 // filtfilt over the odd-extended input ext [ne] as two passes of the whole cascade (p.casc), trimmed and reflect-padded
 hipError_t casc_filtfilt_pad(const SosPlan& p, const double* ext, long long ne, int padlen, long long n,
                              long long t_pad, double* ws, double* pad64, float* pad32, hipStream_t s);
 size_t casc_ws_doubles(long long ne, int L);
-hipError_t sos_pass(const SosPlan& p, const double* x, long long n, int rev, double* out, double* ws, hipStream_t s);
 // filtfilt (odd padding 3*(order+1)) through the SOS plan + reflect pad t_pad (pipeline.py:439, :459)
 hipError_t filtfilt_sos_pad(const SosPlan& p, int order, const double* x, long long n, long long t_pad, double* ws,
                             double* pad64, float* pad32, hipStream_t s);

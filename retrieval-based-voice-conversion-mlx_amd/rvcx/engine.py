@@ -583,8 +583,8 @@ class Engine:
     def conv2d3x3(self, x, w, bias=None, relu: bool = False, math: str = "default"):
         """torch.nn.functional.conv2d(x.permute(2, 0, 1)[None], w, bias, padding=1)[0].permute(1, 2, 0) on the device
         kernel: x [H][W][C_in] (NHWC), w [N][C_in][3][3] (torch layout) -> [H][W][N] fp32 (rvcx_conv2d3x3); math
-        "default" = the context's arithmetic, "f32" = exact fp32, "gsw" / "gswk" = the U-Net deep levels' windowed
-        kernels in the fp16 split (K split over workgroups / over the waves of a workgroup)."""
+        "default" = the context's arithmetic, "f32" = exact fp32, "gsw" = the U-Net deep levels' windowed kernel in the
+        fp16 split (K split over workgroups)."""
         torch = self.torch
         x = self._dev(x, torch.float32)
         w = torch.as_tensor(w, dtype=torch.float32)
@@ -593,9 +593,26 @@ class Engine:
         b = self._dev(bias, torch.float32) if bias is not None else None
         H, W = int(x.shape[0]), int(x.shape[1])
         y = torch.empty((H, W, N), dtype=torch.float32, device=self.device)
-        m = {"default": 0, "f32": 1, "gsw": 2, "gswk": 3}[math]
+        m = {"default": 0, "f32": 1, "gsw": 2}[math]
         self._check(self.lib.rvcx_conv2d3x3(self.ctx, _ptr(x), H, W, C, _ptr(wk), _ptr(b), N, 1 if relu else 0, m,
                                             _ptr(y), self.stream()), "conv2d3x3")
+        return y
+
+    def convtranspose2d_s2(self, x, w, bias=None, relu: bool = False, math: str = "default"):
+        """torch.nn.functional.conv_transpose2d(x.permute(2, 0, 1)[None], w, bias, stride=2, padding=1,
+        output_padding=1)[0].permute(1, 2, 0) on the device (rvcx_convtranspose2d_s2, the U-Net decoder's up-conv as
+        the pipeline runs it): x [H][W][C_in] (NHWC), w [C_in][N][3][3] (torch layout) -> [2H][2W][N] fp32; math
+        "default" = the context's arithmetic, "f32" = exact fp32."""
+        torch = self.torch
+        x = self._dev(x, torch.float32)
+        wd = self._dev(torch.as_tensor(w, dtype=torch.float32).contiguous(), torch.float32)
+        C, N = int(wd.shape[0]), int(wd.shape[1])
+        b = self._dev(bias, torch.float32) if bias is not None else None
+        H, W = int(x.shape[0]), int(x.shape[1])
+        y = torch.empty((2 * H, 2 * W, N), dtype=torch.float32, device=self.device)
+        m = {"default": 0, "f32": 1}[math]
+        self._check(self.lib.rvcx_convtranspose2d_s2(self.ctx, _ptr(x), H, W, C, _ptr(wd), _ptr(b), N,
+                                                     1 if relu else 0, m, _ptr(y), self.stream()), "convtranspose2d_s2")
         return y
 
     def resblock_pair(self, x, w1, b1, w2, b2, dilation: int, acc=None, acc_mode: int = 0, acc_div: float = 1.0,

@@ -78,8 +78,9 @@ class Synthesizer:
 
     def infer(self, phone, phone_lengths, pitch, nsff0, sid, rate=None, eps_z=None, eps_src=None, seed: int = 0):
         """synthesizers.py:206-243: -> (o [B][1][T' upp], x_mask [B][1][T'], (z, z_p, m_p, logs_p)) with z / z_p
-        [B][I][T'] and m_p / logs_p [B][I][T]; rate (a float or a one-element tensor) keeps frames
-        int(T (1 - rate)) .. T - 1 before the flow (T' = T without it)."""
+        [B][I][T'] and m_p / logs_p [B][I][T]; rate (a float or a one-element tensor) slices z_p, x_mask and nsff0
+        [:, head:] before the flow with head = int(T (1 - rate)) and Python's slice semantics (rate > 1: a negative
+        head keeps the last -head frames; T' = T without a rate)."""
         ph = _np(phone).astype(np.float32)
         B, T = ph.shape[0], ph.shape[1]
         guided = bool(self.engine.synth_cfg.use_f0)  # synthesizers.py:233-239: pitch ignored without f0

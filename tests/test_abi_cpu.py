@@ -127,7 +127,7 @@ def test_env_knobs_need_the_experimental_opt_in(experimental):
 
     env = {k: v for k, v in os.environ.items() if not k.startswith("RVCX_")}
     env["RVCX_CONV_MATH"] = "f32"
-    env["RVCX_NO_WSB"] = "1"
+    env["RVCX_NO_OVERLAP"] = "1"
     if experimental:
         env["RVCX_EXPERIMENTAL"] = "1"
     out = subprocess.run([sys.executable, "-c", _KNOB_PROBE, _lib.LIB_PATH], env=env, capture_output=True, text=True,
@@ -136,4 +136,4 @@ def test_env_knobs_need_the_experimental_opt_in(experimental):
     assert info["experimental"] is experimental
     assert info["conv_math_default"] == ("f32" if experimental else "h16")
     assert info["env"]["RVCX_CONV_MATH"] == {"value": "f32", "honoured": experimental}
-    assert info["env"]["RVCX_NO_WSB"]["honoured"] is experimental
+    assert info["env"]["RVCX_NO_OVERLAP"]["honoured"] is experimental

@@ -160,24 +160,33 @@ def test_unet_small_2d_convs_are_fp32_accurate(engine, H, W, C, N, spread, wsp):
     assert errs["default"] < 1e-6 and errs["default"] <= 4.0 * errs["f32"] + 1e-8, errs
 
 
-DEEP2D = [  # H, W, C_in, N: the RMVPE U-Net's deep levels (windowed gather-streamed kernels, conv_gs.hip)
-    (49, 4, 512, 512),    # intermediate (196 px)
-    (98, 8, 256, 256),    # level 3 (784 px)
-    (196, 16, 128, 128),  # level 2 (3136 px)
-    (33, 8, 256, 80),     # ragged rows and a partial 32-column tile
-    (20, 32, 128, 64),
+DEEP2D = [  # H, W, C_in, N, weight spread: the RMVPE U-Net's deep levels (windowed gather-streamed kernel, conv_gs.hip)
+    (49, 4, 512, 512, 0),    # intermediate (196 px)
+    (98, 8, 256, 256, 0),    # level 3 (784 px)
+    (196, 16, 128, 128, 0),  # level 2 (3136 px)
+    (33, 8, 256, 80, 0),     # ragged rows and a partial 32-column tile
+    (20, 32, 128, 64, 0),
+    # per-column weight scales (the windowed kernel shares h16_finish's per-column inverse scales)
+    (49, 4, 512, 512, "ch12"),
+    (98, 8, 256, 256, "dead20"),
+    (196, 16, 128, 128, "ch12"),
+    (33, 8, 256, 80, "dead20"),
 ]
 
 
-@pytest.mark.parametrize("H,W,C,N", DEEP2D)
-def test_unet_deep_level_windowed_kernels(engine, H, W, C, N):
-    """cfg 30 (64 x 64 tiles, K split over workgroups) and cfg 33 (64 x 32 tiles, K split over the 4 waves of a
-    workgroup, partials summed in LDS) against fp64, per output element relative to its own sum |x w|: both within
-    1e-6 and at most 4x the exact-f32 kernel's error."""
+@pytest.mark.parametrize("H,W,C,N,wsp", DEEP2D)
+def test_unet_deep_level_windowed_kernels(engine, H, W, C, N, wsp):
+    """The windowed gather-streamed kernel (64 x 64 tiles, K split over workgroups by the size policy) against fp64,
+    per output element relative to its own sum |x w|: within 1e-6 and at most 4x the exact-f32 kernel's error, also
+    with per-column weight scales over 2^+-12 and a column at 2^-20 of the tensor max."""
     rng = np.random.Generator(np.random.PCG64(H * 7 + W + C + N))
     x = rng.standard_normal((H, W, C)).astype(np.float32)
     w = (rng.standard_normal((N, C, 3, 3)) / np.sqrt(9 * C)).astype(np.float32)
     bias = rng.standard_normal(N).astype(np.float32)
+    if wsp:
+        cs = _wspread(rng, N, wsp)
+        w = (w * cs[:, None, None, None]).astype(np.float32)
+        bias = (bias * cs).astype(np.float32)
     xd = torch.from_numpy(x.astype(np.float64)).permute(2, 0, 1)[None]
     wd = torch.from_numpy(w.astype(np.float64))
     ref = torch.relu(torch.nn.functional.conv2d(xd, wd, torch.from_numpy(bias.astype(np.float64)), padding=1))
@@ -185,59 +194,54 @@ def test_unet_deep_level_windowed_kernels(engine, H, W, C, N):
     ref = ref[0].permute(1, 2, 0).numpy()
     mag = mag[0].permute(1, 2, 0).numpy() + 1e-300
     errs = {}
-    for mode in ("f32", "gsw", "gswk"):
+    for mode in ("f32", "gsw"):
         y = engine.conv2d3x3(x, w, bias, relu=True, math=mode).cpu().numpy()
         assert y.shape == ref.shape
         errs[mode] = float(np.max(np.abs(y - ref) / mag))
-    print(f"\n2-D deep {H}x{W} {C}->{N}: " + " ".join(f"{k} {v:.2e}" for k, v in errs.items()))
+    print(f"\n2-D deep {H}x{W} {C}->{N} {wsp or ''}: " + " ".join(f"{k} {v:.2e}" for k, v in errs.items()))
     assert errs["f32"] < 1e-6, errs
-    for k in ("gsw", "gswk"):
-        assert errs[k] < 1e-6 and errs[k] <= 4.0 * errs["f32"] + 1e-8, errs
+    assert errs["gsw"] < 1e-6 and errs["gsw"] <= 4.0 * errs["f32"] + 1e-8, errs
 
 
-_FIXUP_CHILD = r"""
-import sys
-import numpy as np
-sys.path[:0] = [sys.argv[1], sys.argv[2]]
-from rvcx.engine import Engine
-d = np.load(sys.argv[3])
-e = Engine(0)
-out = {}
-for i in range(int(d["n"])):
-    for mode in ("gsw", "gswk"):
-        out[f"{mode}{i}"] = e.conv2d3x3(d[f"x{i}"], d[f"w{i}"], d[f"b{i}"], relu=True, math=mode).cpu().numpy()
-e.close()
-np.savez(sys.argv[4], **out)
-"""
+UPCONV = [  # H, W, C_in, N, weight spread: the U-Net decoder's ConvTranspose2d (3x3, stride 2, pad 1, output pad 1)
+    (49, 4, 512, 256, 0),     # decoder level 0 (the intermediate's output)
+    (98, 8, 256, 128, 0),
+    (196, 16, 128, 64, 0),
+    (392, 32, 64, 32, 0),
+    (33, 8, 256, 40, 0),      # ragged rows, 4 x 40 virtual columns (a partial tile)
+    (98, 8, 256, 128, "ch12"),
+    (196, 16, 128, 64, "dead20"),
+    (49, 4, 512, 256, "ch12"),
+]
 
 
-def test_splitk_in_kernel_combine_is_bit_identical(engine, tmp_path):
-    """The opt-in in-kernel split-K combine (RVCX_SPLITK_FIXUP=1: the last slice of a tile to arrive sums the
-    write-through slabs, conv_common.h splitk_fixup) against the default combine launch, on the U-Net's split deep
-    levels with both windowed kernels: bit-identical (same slice order, same epilogue). The knob is read once per
-    process, so the in-kernel side runs in a child process."""
-    import os
-    import subprocess
-    import sys
-
-    from conftest import PKG, REPO
-
-    shapes = DEEP2D[:4]
-    inp, ref = {"n": np.array(len(shapes))}, {}
-    for i, (H, W, C, N) in enumerate(shapes):
-        rng = np.random.Generator(np.random.PCG64(1000 + i))
-        inp[f"x{i}"] = rng.standard_normal((H, W, C)).astype(np.float32)
-        inp[f"w{i}"] = (rng.standard_normal((N, C, 3, 3)) / np.sqrt(9 * C)).astype(np.float32)
-        inp[f"b{i}"] = rng.standard_normal(N).astype(np.float32)
-        for mode in ("gsw", "gswk"):
-            ref[f"{mode}{i}"] = engine.conv2d3x3(inp[f"x{i}"], inp[f"w{i}"], inp[f"b{i}"], relu=True,
-                                                 math=mode).cpu().numpy()
-    src, dst = str(tmp_path / "in.npz"), str(tmp_path / "out.npz")
-    np.savez(src, **inp)
-    env = dict(os.environ, RVCX_EXPERIMENTAL="1", RVCX_SPLITK_FIXUP="1")
-    r = subprocess.run([sys.executable, "-c", _FIXUP_CHILD, PKG, REPO, src, dst], env=env, capture_output=True,
-                       text=True, timeout=110)
-    assert r.returncode == 0, r.stderr[-2000:]
-    out = np.load(dst)
-    for k, v in ref.items():
-        assert np.array_equal(out[k], v), (k, float(np.max(np.abs(out[k] - v))))
+@pytest.mark.parametrize("H,W,C,N,wsp", UPCONV)
+def test_unet_upconv_phase_gather_kernel(engine, H, W, C, N, wsp):
+    """the decoder's up-convs run as a 2x2-tap phase conv with 4 N virtual columns on the
+    fp16-split gather kernel, whose epilogue maps the phase layout (store_tile16 OUT_UPSAMPLE2D). Against fp64
+    torch.nn.functional.conv_transpose2d (RMVPE.py ResDecoderBlock conv1: stride 2, padding 1, output_padding 1),
+    per output element relative to its own sum |x w|: within 1e-6 and at most 4x the exact-f32 kernel's error, also
+    with per-output-channel weight scales over 2^+-12 and a channel at 2^-20 of the tensor max."""
+    rng = np.random.Generator(np.random.PCG64(H * 11 + W + C + N))
+    x = rng.standard_normal((H, W, C)).astype(np.float32)
+    w = (rng.standard_normal((C, N, 3, 3)) / np.sqrt(9 * C)).astype(np.float32)  # torch layout [C_in][N][kh][kw]
+    bias = rng.standard_normal(N).astype(np.float32)
+    if wsp:
+        cs = _wspread(rng, N, wsp)
+        w = (w * cs[None, :, None, None]).astype(np.float32)
+        bias = (bias * cs).astype(np.float32)
+    xd = torch.from_numpy(x.astype(np.float64)).permute(2, 0, 1)[None]
+    wd = torch.from_numpy(w.astype(np.float64))
+    ct = torch.nn.functional.conv_transpose2d
+    ref = torch.relu(ct(xd, wd, torch.from_numpy(bias.astype(np.float64)), stride=2, padding=1, output_padding=1))
+    mag = ct(xd.abs(), wd.abs(), None, stride=2, padding=1, output_padding=1) + np.abs(bias)[None, :, None, None]
+    ref = ref[0].permute(1, 2, 0).numpy()
+    mag = mag[0].permute(1, 2, 0).numpy() + 1e-300
+    errs = {}
+    for mode in ("f32", "default"):
+        y = engine.convtranspose2d_s2(x, w, bias, relu=True, math=mode).cpu().numpy()
+        assert y.shape == ref.shape, (y.shape, ref.shape)
+        errs[mode] = float(np.max(np.abs(y - ref) / mag))
+    print(f"\nup-conv {H}x{W} {C}->{N} {wsp or ''}: " + " ".join(f"{k} {v:.2e}" for k, v in errs.items()))
+    assert errs["f32"] < 1e-6, errs
+    assert errs["default"] < 1e-6 and errs["default"] <= 4.0 * errs["f32"] + 1e-8, errs

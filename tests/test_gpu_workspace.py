@@ -115,3 +115,31 @@ def test_workspace_arena_short_then_long_call(engine):
         assert torch.equal(engine.pipeline_ex(a_long, o, seed=1).cpu(), ref_long)
     finally:
         engine.set_workspace(None)
+
+
+@pytest.mark.parametrize("with_arena", [True, False])
+def test_calls_on_two_streams_do_not_share_live_regions(engine, with_arena):
+    """a call enqueued on stream B right after a call on stream A (no host synchronisation between them)
+    must not overwrite the regions A's call still uses -- in arena mode every call carves from offset 0, and in pool
+    mode both calls take the same named buffers. begin_call orders the second call after the first one's streams, so
+    both results equal their serial runs."""
+    engine.set_pipeline_highpass()
+    n_long, n_short = 6 * 16000, int(2.5 * 16000)
+    a_long, a_short = _audio(n_long, 4), _audio(n_short, 5)
+    ref_long = engine.pipeline(a_long, seed=3).cpu()
+    ref_short = engine.pipeline(a_short, seed=4).cpu()
+    arena = torch.empty(engine.workspace_bytes(n_long), dtype=torch.uint8, device=engine.device) if with_arena else None
+    sa, sb = torch.cuda.Stream(engine.device), torch.cuda.Stream(engine.device)
+    try:
+        engine.set_workspace(arena)
+        torch.cuda.synchronize(engine.device)
+        for _ in range(2):
+            with torch.cuda.stream(sa):
+                out_a = engine.pipeline(a_long, seed=3)
+            with torch.cuda.stream(sb):
+                out_b = engine.pipeline(a_short, seed=4)
+            torch.cuda.synchronize(engine.device)
+            assert torch.equal(out_a.cpu(), ref_long)
+            assert torch.equal(out_b.cpu(), ref_short)
+    finally:
+        engine.set_workspace(None)
