@@ -437,6 +437,18 @@ int rvcx_conv2d3x3(rvcx_ctx* ctx, const float* d_x, int H, int W, int C_in, cons
 int rvcx_convtranspose2d_s2(rvcx_ctx* ctx, const float* d_x, int H, int W, int C_in, const float* d_w,
                             const float* d_bias, int N, int act, int math, float* d_y, void* stream);
 
+/* Multi-head attention core on the fused kernel (csrc/flash_attn.hip), time-major: d_qkv [B][T][3 H] (q | k | v, head
+ * h at columns h dk .. of each, H = n_heads dk), d_out [B][T][H]: per head softmax(qscale q k^T + band) v + band(p)
+ * rel_v, where, with d_rel_k / d_rel_v [2 window + 1][dk] (both or neither), band adds qscale q . rel_k[j - i + window]
+ * to the logit of key j of query i for |j - i| <= window and band(p) is the probabilities of those keys
+ * (MultiHeadAttention.attention with window_size, rvc/lib/algorithm/attentions.py:79-185), and d_mask [B][T]
+ * (optional) fills the logits of masked query-key pairs with -1e4 (:106-107). Without the relative tables it is
+ * HuBERT's attention (modeling_hubert.py HubertAttention: softmax((q dk^-0.5) k^T) v). dk 64 or 96, window <= 15.
+ * Exposed for the numerics tests. */
+int rvcx_flash_attention(rvcx_ctx* ctx, const float* d_qkv, int B, int T, int n_heads, int dk, float qscale,
+                         const float* d_rel_k, const float* d_rel_v, int window, const float* d_mask, float* d_out,
+                         void* stream);
+
 /* One ResBlock dilation pair as one fused kernel (csrc/resblock_fused.hip), time-major: d_x, d_y [B][T][C] (distinct
  * buffers), d_w1 / d_w2 [k][C][C] (torch weight [C][C][k] permuted), d_b1 / d_b2 [C]:
  *     out = conv2(lrelu(conv1_d(lrelu(x), 0.1) + b1, 0.1)) + b2 + x     (zero padding; conv2 dilation 1)

@@ -945,6 +945,26 @@ int rvcx_convtranspose2d_s2(rvcx_ctx* ctx, const float* d_x, int H, int W, int C
   });
 }
 
+int rvcx_flash_attention(rvcx_ctx* ctx, const float* d_qkv, int B, int T, int n_heads, int dk, float qscale,
+                         const float* d_rel_k, const float* d_rel_v, int window, const float* d_mask, float* d_out,
+                         void* stream) {
+  return guard(ctx, [&] {
+    set_device(ctx);
+    ctx->check_device_status();
+    if (!d_qkv || !d_out || B <= 0 || T <= 0 || n_heads <= 0 || (dk != 64 && dk != 96) || window < 0 ||
+        (d_rel_k != nullptr) != (d_rel_v != nullptr))
+      throw Error(RVCX_E_INVALID, "rvcx_flash_attention: bad argument");
+    if ((long long)B * T * 3 * n_heads * dk > INT32_MAX) throw Error(RVCX_E_SHAPE, "rvcx_flash_attention: too large");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int nsplit = flash_attn_splits(B, n_heads, T);
+    float* po = ctx->buf<float>("att.test.o", (size_t)flash_attn_ws_floats(B, n_heads, T, dk, nsplit), s);
+    float* pml = ctx->buf<float>("att.test.ml", (size_t)nsplit * B * n_heads * T * 2, s);
+    check(flash_attn(d_qkv, 3 * n_heads * dk, B, T, n_heads, dk, qscale, d_rel_k, d_rel_v, window, d_mask, po, pml,
+                     nsplit, d_out, n_heads * dk, s),
+          "flash_attn");
+  });
+}
+
 int rvcx_resblock_pair(rvcx_ctx* ctx, const float* d_x, int B, int64_t T, int C, const float* d_w1, const float* d_b1,
                        const float* d_w2, const float* d_b2, int k, int dilation, int acc_mode, float acc_div, int cfg,
                        float* d_y, void* stream) {

@@ -615,6 +615,22 @@ class Engine:
                                                      1 if relu else 0, m, _ptr(y), self.stream()), "convtranspose2d_s2")
         return y
 
+    def flash_attention(self, qkv, n_heads: int, qscale: float, rel_k=None, rel_v=None, window: int = 0, mask=None):
+        """The fused attention core (rvcx_flash_attention): qkv [B][T][3 H] time-major (q | k | v, heads of dk inside
+        each), optional relative tables rel_k / rel_v [2 window + 1][dk] and key/query mask [B][T] -> [B][T][H]."""
+        torch = self.torch
+        q = self._dev(qkv, torch.float32)
+        B, T, H3 = (int(v) for v in q.shape)
+        dk = H3 // 3 // n_heads
+        rk = None if rel_k is None else self._dev(rel_k, torch.float32)
+        rv = None if rel_v is None else self._dev(rel_v, torch.float32)
+        mk = None if mask is None else self._dev(mask, torch.float32)
+        y = torch.empty((B, T, H3 // 3), dtype=torch.float32, device=self.device)
+        self._check(self.lib.rvcx_flash_attention(self.ctx, _ptr(q), B, T, int(n_heads), dk, float(qscale), _ptr(rk),
+                                                  _ptr(rv), int(window), _ptr(mk), _ptr(y), self.stream()),
+                    "flash_attention")
+        return y
+
     def resblock_pair(self, x, w1, b1, w2, b2, dilation: int, acc=None, acc_mode: int = 0, acc_div: float = 1.0,
                       cfg: int = 0):
         """One ResBlock dilation pair on the fused kernel (rvcx_resblock_pair): x [B][T][C] time-major, w1/w2
