@@ -6,6 +6,9 @@
 //   graph     the nop256 chain captured once and replayed as a hipGraph
 //   busy      nop256 while a second stream keeps a long kernel resident on part of the chip (the step's HuBERT /
 //             BiGRU overlap)
+//   ahead     the nop256 chain (and one with a 512-byte kernel argument, the size of ConvArgs) enqueued behind a
+//             5 ms single-workgroup kernel, timed from that kernel's end: the GPU-side cost per launch with the host
+//             far ahead (the eager nop chains above are host-bound: ~3.6 us of enqueue per launch)
 // Run it bare and under `rocprofv3 --kernel-trace --stats` to compare the tracer's per-kernel duration with the
 // event-timed cost per launch.
 #include <hip/hip_runtime.h>
@@ -27,6 +30,13 @@
 
 __global__ void k_nop(int* p, int v) {
   if (threadIdx.x == 0) p[blockIdx.x] = v + p[blockIdx.x + 4096];
+}
+
+struct BigArg {
+  int v[128];
+};
+__global__ void k_nop_big(int* p, BigArg a) {
+  if (threadIdx.x == 0) p[blockIdx.x] = a.v[blockIdx.x & 127] + p[blockIdx.x + 4096];
 }
 
 // writes n float4 (dirty bytes for the next launch) and reads one line of the previous launch's output
@@ -135,6 +145,67 @@ int main(int argc, char** argv) {
       const double us = chain_us(s, n, [&] { hipLaunchKernelGGL(k_nop, dim3(256), dim3(256), 0, s, w, ++v); });
       CK_(hipStreamSynchronize(s2));
       printf("busy%-4d %7.2f us per launch (nop256 beside %d resident workgroups)\n", wgs, us, wgs);
+    }
+  }
+  {
+    // host far ahead: a 5 ms one-workgroup kernel first, then the chain; events around the chain only
+    for (int big = 0; big < 2; ++big) {
+      BigArg ba;
+      for (int i = 0; i < 128; ++i) ba.v[i] = i;
+      hipEvent_t e0, e1;
+      CK_(hipEventCreate(&e0));
+      CK_(hipEventCreate(&e1));
+      for (int rep = 0; rep < 2; ++rep) {
+        hipLaunchKernelGGL(k_busy, dim3(1), dim3(64), 0, s, bo, 3000000);
+        CK_(hipEventRecord(e0, s));
+        auto h0 = std::chrono::steady_clock::now();
+        for (int i = 0; i < n; ++i) {
+          if (big) hipLaunchKernelGGL(k_nop_big, dim3(256), dim3(256), 0, s, w, ba);
+          else hipLaunchKernelGGL(k_nop, dim3(256), dim3(256), 0, s, w, ++v);
+        }
+        auto h1 = std::chrono::steady_clock::now();
+        CK_(hipEventRecord(e1, s));
+        CK_(hipEventSynchronize(e1));
+        float ms = 0.f, busy_ms = 0.f;
+        CK_(hipEventElapsedTime(&ms, e0, e1));
+        const double host = std::chrono::duration<double, std::micro>(h1 - h0).count() / n;
+        if (rep == 1)
+          printf("ahead%s %7.2f us per launch on the GPU (host enqueue %.2f us per launch, %s)\n", big ? "512" : "   ",
+                 ms * 1e3 / n, host, ms * 1e3 > host * n ? "host ahead" : "HOST-BOUND: lengthen the busy kernel");
+        (void)busy_ms;
+      }
+      CK_(hipEventDestroy(e0));
+      CK_(hipEventDestroy(e1));
+    }
+  }
+  {
+    // marginal cost of a trivial launch between real kernels (host ahead): a chain of 2 MB-writing kernels with and
+    // without a nop256 after each
+    for (int with_nop = 0; with_nop < 2; ++with_nop) {
+      hipEvent_t e0, e1;
+      CK_(hipEventCreate(&e0));
+      CK_(hipEventCreate(&e1));
+      int flip = 0;
+      for (int rep = 0; rep < 2; ++rep) {
+        hipLaunchKernelGGL(k_busy, dim3(1), dim3(64), 0, s, bo, 3000000);
+        CK_(hipEventRecord(e0, s));
+        for (int i = 0; i < n / 2; ++i) {
+          float4* dst = flip ? d1 : d0;
+          const float4* src = flip ? d0 : d1;
+          flip ^= 1;
+          hipLaunchKernelGGL(k_dirty, dim3(1024), dim3(256), 0, s, dst, src, (2ll << 20) / 16, ++v);
+          if (with_nop) hipLaunchKernelGGL(k_nop, dim3(256), dim3(256), 0, s, w, ++v);
+        }
+        CK_(hipEventRecord(e1, s));
+        CK_(hipEventSynchronize(e1));
+        float ms = 0.f;
+        CK_(hipEventElapsedTime(&ms, e0, e1));
+        if (rep == 1)
+          printf("real2MB%s %7.2f us per real kernel%s\n", with_nop ? "+nop" : "    ", ms * 1e3 / (n / 2),
+                 with_nop ? " (with a nop256 after each)" : "");
+      }
+      CK_(hipEventDestroy(e0));
+      CK_(hipEventDestroy(e1));
     }
   }
   CK_(hipDeviceSynchronize());
