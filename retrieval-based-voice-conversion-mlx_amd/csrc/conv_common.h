@@ -126,47 +126,32 @@ __device__ __forceinline__ void store_tile16(const ConvArgs& a, int m0, int n0, 
   const bool need_r = R && a.res_mode != RES_NONE;
   const bool need_d = a.acc_mode != ACC_STORE;
   const int act = a.act;
-  // the residual / accumulate / mask operands of up to EG row blocks are gathered before any of their arithmetic and
-  // stores: every element is read and written by this lane only, so the reorder is exact, and one load latency is
-  // exposed per group instead of per 16-row block (the stores may alias the loads -- an in-place residual -- so the
-  // compiler cannot hoist them across the stores itself)
-  constexpr int EG = TM16 < 4 ? TM16 : 4;
 #pragma unroll
   for (int tn = 0; tn < TN16; ++tn) {
     const int n = n0 + wn * TN16 * 16 + tn * 16 + lc;
     const bool n_ok = n < a.N;
     const float bn = (bias && n_ok) ? bias[n] : 0.f;
 #pragma unroll
-    for (int tg = 0; tg < TM16; tg += EG) {
-    f32x4 rvg[EG], dvg[EG], mvg[EG];
-#pragma unroll
-    for (int e = 0; e < EG; ++e) {
-      const long long mb = (long long)m0 + wm * TM16 * 16 + (tg + e) * 16 + 4 * lg;
-      rvg[e] = f32x4{0.f, 0.f, 0.f, 0.f};
-      dvg[e] = f32x4{0.f, 0.f, 0.f, 0.f};
-      mvg[e] = f32x4{1.f, 1.f, 1.f, 1.f};
-      if (need_r) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) rvg[e][r] = (n_ok && mb + r < Mtot) ? R[(mb + r) * a.ldr + n] : 0.f;
-      }
-      if (need_d) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dvg[e][r] = (n_ok && mb + r < Mtot) ? Y[(mb + r) * a.ldy + n] : 0.f;
-      }
-      if (MK) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) mvg[e][r] = (n_ok && mb + r < Mtot) ? MK[mb + r] : 1.f;
-      }
-    }
-#pragma unroll
-    for (int e = 0; e < EG; ++e) {
-      const int tm = tg + e;
+    for (int tm = 0; tm < TM16; ++tm) {
       const long long mb = (long long)m0 + wm * TM16 * 16 + tm * 16 + 4 * lg;
       bool ok[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) ok[r] = n_ok && mb + r < Mtot;
       f32x4 v = acc[tm][tn];
-      const f32x4 rv = rvg[e], dv = dvg[e], mv = mvg[e];
+      f32x4 rv = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f}, mv = {1.f, 1.f, 1.f, 1.f};
+      // gather first (residual / accumulate / mask operands), then the arithmetic, then the stores
+      if (need_r) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rv[r] = ok[r] ? R[(mb + r) * a.ldr + n] : 0.f;
+      }
+      if (need_d) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dv[r] = ok[r] ? Y[(mb + r) * a.ldy + n] : 0.f;
+      }
+      if (MK) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mv[r] = ok[r] ? MK[mb + r] : 1.f;
+      }
       if (bias) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] += bn;
@@ -228,7 +213,6 @@ __device__ __forceinline__ void store_tile16(const ConvArgs& a, int m0, int n0, 
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         if (ok[r]) Y[(mb + r) * a.ldy + n] = v[r];
-    }
     }
   }
 }
