@@ -418,6 +418,18 @@ int rvcx_set_generator_precision(rvcx_ctx* ctx, int precision);
 int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const float* d_w, const float* d_bias, int N,
                 int taps, int dilation, int pad, int stride, int math, float* d_y, int64_t T_out, void* stream);
 
+/* The generator's fused conv form, time-major (rvcx_conv1d's layouts, stride 1, T_out = T + 2 pad - (taps - 1)
+ * dilation): y = acc(act(conv(pre(x)) + bias) + res), pre = leaky ReLU(pre_slope) when pre_act = 1 (else identity),
+ * act = leaky ReLU(slope) when act = 1, res
+ * optional ([T_out][N]), acc_mode 0 store, 1 y + v, 2 (y + v) / acc_div -- one ResBlock conv (residuals.py:71-80:
+ * convs1 with act, convs2 with the residual and the ResBlock mean on the last pair) or one ConvTranspose phase group
+ * (hifigan_nsf.py:184-199) in the two-plane fp16 split. kernel 0 = the size policy's route, 1 = the weight-streamed
+ * kernel (conv_wsb.hip, the tile the policy picks), 2 = the weight-stationary kernel (conv_wst.hip: C_in = N in {64,
+ * 128}, 2-3 taps, (taps - 1) dilation <= 16, else RVCX_E_SHAPE). Exposed for numerics tests; C_in % 32 == 0. */
+int rvcx_conv1d_gen(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const float* d_w, const float* d_bias,
+                    int N, int taps, int dilation, int pad, int pre_act, float pre_slope, int act, float slope,
+                    const float* d_res, int acc_mode, float acc_div, int kernel, float* d_y, void* stream);
+
 /* One 3x3 / pad-1 Conv2d forward, NHWC: d_x [H][W][C_in], d_w [9][N][C_in] (torch weight [N][C_in][3][3] permuted to
  * (kh * 3 + kw, N, C_in)), d_bias [N] (optional), d_y [H][W][N]; act 0 none, 1 ReLU. The RMVPE U-Net's conv
  * (RMVPE.py:13-57 ConvBlockRes, torch.nn.Conv2d(kernel 3, padding 1)), exposed for the numerics tests of its

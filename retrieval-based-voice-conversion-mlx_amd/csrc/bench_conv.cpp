@@ -203,7 +203,7 @@ int main(int argc, char** argv) {
     const double flops = 2.0 * cs.T * cs.N * (double)cs.Cin * cs.taps;
     // variants: (cfg, math, pipe); cfg -1 = the library's policy for that math
     struct V { int cfg, math, pipe; };
-    std::vector<V> vars = {{-1, 2, 0}, {23, 2, -1}, {24, 2, -1}, {27, 2, -1}, {23, 3, -1}, {24, 3, -1},
+    std::vector<V> vars = {{-1, 2, 0}, {23, 2, -1}, {24, 2, -1}, {27, 2, -1}, {23, 3, -1}, {24, 3, -1}, {40, 3, -1},
                            {27, 3, -1}, {25, 3, -1}, {23, 4, -1}, {27, 4, -1}, {13, 2, -1}, {1, 1, -1}};
     if (cs.taps == 1)
       for (int c : {10, 12, 13, 14, 15}) vars.push_back({c, 2, 1});

@@ -207,8 +207,9 @@ void launch_conv(Ctx& c, const ConvArgs& a_in, bool two_d, hipStream_t s, double
   // the policy for a packed (static) weight; decided before the split-K plan, whose geometry depends on it
   const bool stat = a.w_static || c.is_weight(a.w);
   a.wsb = !stat ? 0
-          : (a.force_cfg >= 30 ? 2
+          : (a.force_cfg >= 30 && a.force_cfg < 40 ? 2
              : (a.force_cfg >= 20 && !two_d) ? 1 : (a.force_cfg < 0 ? conv_wsb_route(a, two_d) : 0));
+  if (a.force_cfg == 40 && !two_d && stat) a.wsb = 1;  // the weight-stationary kernel (conv_wst.hip), forced
   const long long need = conv_plan_splitk(a, two_d);
   // the few-channel 3x3 convs' fp16-split form reads a pre-split image (conv2d_small.hip)
   if (two_d && !a.wsb && stat && !a.wsplit && conv_math_of(a) == 3 && conv2d_small_fits(a)) {
@@ -858,6 +859,53 @@ int rvcx_conv1d(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const floa
       check(conv_wsplit_build(a, img, static_cast<hipStream_t>(stream)), "conv_wsplit_build");
       a.wsplit = img;
     }
+    launch_conv(*ctx, a, false, static_cast<hipStream_t>(stream), -1.0);
+  });
+}
+
+int rvcx_conv1d_gen(rvcx_ctx* ctx, const float* d_x, int64_t T, int C_in, const float* d_w, const float* d_bias,
+                    int N, int taps, int dilation, int pad, int pre_act, float pre_slope, int act, float slope,
+                    const float* d_res, int acc_mode, float acc_div, int kernel, float* d_y, void* stream) {
+  return guard(ctx, [&] {
+    set_device(ctx);
+    ctx->check_device_status();
+    if (!d_x || !d_w || !d_y || T <= 0 || C_in <= 0 || N <= 0 || taps <= 0 || dilation <= 0 || pad < 0 || act < 0 ||
+        act > 1 || pre_act < 0 || pre_act > 1 || acc_mode < 0 || acc_mode > 2 || kernel < 0 || kernel > 2 || (d_res && d_res == d_x))
+      throw Error(RVCX_E_INVALID, "rvcx_conv1d_gen: bad argument");
+    const int64_t T_out = T + 2 * (int64_t)pad - (int64_t)(taps - 1) * dilation;
+    if (T_out <= 0 || T > INT32_MAX || (int64_t)taps * N * C_in > INT32_MAX)
+      throw Error(RVCX_E_SHAPE, "rvcx_conv1d_gen: size out of range");
+    ConvArgs a;
+    a.x = d_x; a.ldx = C_in; a.T_in = (int)T; a.C_in = C_in;
+    a.w = d_w; a.ldw = C_in; a.w_ts = (long long)N * C_in; a.taps = taps; a.dil = dilation; a.pad = pad;
+    a.y = d_y; a.ldy = N; a.T_out = (int)T_out; a.N = N; a.bias = d_bias;
+    a.pre_act = pre_act ? ACT_LRELU : ACT_NONE;
+    a.pre_slope = pre_slope;
+    a.act = act ? ACT_LRELU : ACT_NONE;
+    a.slope = slope;
+    if (d_res) {
+      a.res = d_res;
+      a.ldr = N;
+      a.res_mode = RES_ADD_POST;
+    }
+    a.acc_mode = acc_mode == 0 ? ACC_STORE : (acc_mode == 1 ? ACC_ADD : ACC_ADD_DIV);
+    a.acc_div = acc_div;
+    a.math = 3;
+    a.wsplit_fmt = WSPLIT_H16;
+    a.w_static = 1;
+    a.no_splitk = 1;
+    if (!conv_wsb_eligible(a)) throw Error(RVCX_E_SHAPE, "rvcx_conv1d_gen: shape not eligible for the weight-streamed kernel");
+    // 0: the size policy's route, 1: the weight-streamed tile the policy would pick, 2: the weight-stationary kernel
+    a.force_cfg = kernel == 1 ? conv_wsb_pick(a) : (kernel == 2 ? 40 : -1);
+    // a fresh image every call (rvcx_conv1d's reason)
+    a.wsplit_npad = conv_wsplit_npad(a.N);
+    void* img = ctx->buf<char>("conv.test.wsplit", (size_t)conv_wsplit_bytes(a), static_cast<hipStream_t>(stream));
+    check(conv_wsplit_build(a, img, static_cast<hipStream_t>(stream)), "conv_wsplit_build");
+    a.wsplit = img;
+    ConvArgs b = a;
+    b.wsb = 1;
+    if (kernel == 2 && !conv_wst_fits(b, false))
+      throw Error(RVCX_E_SHAPE, "rvcx_conv1d_gen: shape not eligible for the weight-stationary kernel");
     launch_conv(*ctx, a, false, static_cast<hipStream_t>(stream), -1.0);
   });
 }

@@ -981,7 +981,8 @@ int conv_last_kind() { return g_conv_kind; }
 const char* conv_kind_name(int k) {
   static const char* const names[CK_COUNT] = {"conv_wsb16_kernel", "conv_wsb_kernel", "conv_gs16_kernel",
                                               "conv_gsw16_kernel", "k_rb_pair", "k_conv2d_h16/k_conv2d_small",
-                                              "conv_emu_kernel", "conv_gemm_kernel", "conv_tiny_kernel", "other"};
+                                              "conv_emu_kernel", "conv_gemm_kernel", "conv_tiny_kernel",
+                                              "conv_wst16_kernel", "other"};
   return (k >= 0 && k < CK_COUNT) ? names[k] : "other";
 }
 
@@ -1019,7 +1020,14 @@ hipError_t dispatch(const ConvArgs& a_in, hipStream_t s) {
   }
   if (a.wsb == 1 && a.wsplit && conv_math(a) >= 2 && conv_wsb_eligible(a, TWO_D)) {
     const int ks = (a.ws && a.ksplit > 1) ? a.ksplit : 1;
-    const int cfg = a.force_cfg >= 20 ? a.force_cfg : pick_wsb(a);
+    // the short 64 / 128-channel convs on the weight-stationary kernel (conv_wst.hip; force_cfg 20..39 keeps a
+    // weight-streamed tile for comparisons)
+    if (ks == 1 && (a.force_cfg < 20 || a.force_cfg == 40) && conv_wst_fits(a, TWO_D)) {
+      g_conv_kind = CK_WST;
+      hipError_t e = conv_wst_launch(a, s);
+      if (e != hipErrorInvalidValue) return e;
+    }
+    const int cfg = a.force_cfg >= 20 && a.force_cfg < 40 ? a.force_cfg : pick_wsb(a);
     g_conv_kind = CK_WSB16;
     hipError_t e = conv_wsb_launch(a, cfg, 1, s, TWO_D, ks);
     if (e == hipSuccess && ks > 1) e = launch_splitk_reduce(a, ks, TWO_D, s);

@@ -144,7 +144,7 @@ __device__ __forceinline__ float lrelu01(float v) { return v > 0.f ? v : v * 0.1
 // MODE: bits 0-1 the accumulate mode ACCM; bits 2-3 the arithmetic FMT (RbFmt: the exact bf16 split, the two-plane
 // fp16 split, or the realtime hop's reduced-precision fp16 hi planes)
 template <int C, int NBT, int TN, int MODE>
-__global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair(const RbPairArgs a, const int ntiles) {
+__global__ __launch_bounds__(RB_THREADS, 3) void k_rb_pair(const RbPairArgs a, const int ntiles) {
   constexpr int ACCM = MODE & 3;
   constexpr int FMT = (MODE >> 2) & 3;
   constexpr bool H16 = FMT != RB_BF16X3;
@@ -460,7 +460,7 @@ hipError_t launch_rb_acc(const RbPairArgs& a, hipStream_t s) {
                                                  hipSuccess || ncu <= 0)
       ncu = 256;
   }
-  const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / smem)));
+  const int per_cu = std::max(1, std::min(3, (int)((160 * 1024) / smem)));
   const long long tiles = (long long)ntiles * a.B;
   const int grid = (int)std::min<long long>(tiles, (long long)ncu * per_cu);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(RB_THREADS), smem, s, a, ntiles);

@@ -146,8 +146,8 @@ struct ConvArgs {
 
 hipError_t conv1d(const ConvArgs& a, hipStream_t s);
 // the kernel family the last conv1d / conv2d on this host thread launched (kernel-timing records, rvcx_profile)
-enum ConvKind : int { CK_WSB16 = 0, CK_WSB, CK_GS, CK_GSW, CK_RBPAIR, CK_SMALL2D, CK_EMU, CK_GEMM, CK_TINY, CK_OTHER,
-                      CK_COUNT };
+enum ConvKind : int { CK_WSB16 = 0, CK_WSB, CK_GS, CK_GSW, CK_RBPAIR, CK_SMALL2D, CK_EMU, CK_GEMM, CK_TINY, CK_WST,
+                      CK_OTHER, CK_COUNT };
 int conv_last_kind();
 const char* conv_kind_name(int k);
 // the contraction arithmetic a launch gets: ConvArgs::math, else RVCX_CONV_MATH (1 fp32 MFMA, 2 bf16 split, 3 fp16 split)
@@ -203,6 +203,12 @@ long long conv_wsplit_bytes(const ConvArgs& a);
 hipError_t conv_wsplit_build(const ConvArgs& a, void* out, hipStream_t s);
 hipError_t conv_wsb_launch(const ConvArgs& a, int cfg, int ntn_enable, hipStream_t s, bool two_d = false,
                            int ksplit = 1);
+// weight-stationary form of the fp16-split conv (conv_wst.hip) for the short 64 / 128-channel convs (k = 3 ResBlock
+// convs, ConvTranspose phases): 1-D, C_in = N in {64, 128}, 2-3 taps, halo <= 16, no or leaky-ReLU pre-activation,
+// the WSPLIT_H16 image, bias / leaky-ReLU / RES_ADD_POST / acc modes / the fused noise conv; bit-identical to
+// conv_wsb16_kernel. The dispatcher takes it ahead of the weight-streamed tiles
+bool conv_wst_fits(const ConvArgs& a, bool two_d);
+hipError_t conv_wst_launch(const ConvArgs& a, hipStream_t s);
 // fused ResBlock dilation pair (resblock_fused.hip): y (acc_mode) <- conv2(lrelu(conv1_d(lrelu(x)) + b1)) + b2 + x,
 // x / y [B][T][C] (x != y), C in {32, 64}, odd k, (k - 1) / 2 * d <= 30; w1s / w2s are rb_wsplit_build images
 // of [k][C][C] fp32 weights

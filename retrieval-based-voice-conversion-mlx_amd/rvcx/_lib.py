@@ -29,7 +29,7 @@ EXPORTS = [
     "rvcx_index_retrieve", "rvcx_rt_default_desc", "rvcx_rt_default_opts", "rvcx_rt_create", "rvcx_rt_destroy",
     "rvcx_rt_geometry", "rvcx_rt_reset", "rvcx_rt_process", "rvcx_hubert_batch", "rvcx_rmvpe_batch",
     "rvcx_pipeline_batch", "rvcx_set_highpass_sos", "rvcx_highpass_pad", "rvcx_device_status", "rvcx_index_parse",
-    "rvcx_set_conv_math", "rvcx_conv1d", "rvcx_conv2d3x3", "rvcx_convtranspose2d_s2", "rvcx_flash_attention", "rvcx_resblock_pair", "rvcx_crepe", "rvcx_split_audio",
+    "rvcx_set_conv_math", "rvcx_conv1d", "rvcx_conv1d_gen", "rvcx_conv2d3x3", "rvcx_convtranspose2d_s2", "rvcx_flash_attention", "rvcx_resblock_pair", "rvcx_crepe", "rvcx_split_audio",
     "rvcx_workspace_bytes", "rvcx_set_workspace", "rvcx_workspace_info", "rvcx_crepe_ex",
     "rvcx_crepe_decode",
 ]
@@ -168,6 +168,8 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
                                           P(i64)]),
         "rvcx_profile_kind_name": (ctypes.c_char_p, [i32]),
         "rvcx_conv1d": (i32, [vp, vp, i64, i32, vp, vp, i32, i32, i32, i32, i32, i32, vp, i64, vp]),
+        "rvcx_conv1d_gen": (i32, [vp, vp, i64, i32, vp, vp, i32, i32, i32, i32, i32, f32, i32, f32, vp, i32, f32, i32,
+                                  vp, vp]),
         "rvcx_conv2d3x3": (i32, [vp, vp, i32, i32, i32, vp, vp, i32, i32, i32, vp, vp]),
         "rvcx_convtranspose2d_s2": (i32, [vp, vp, i32, i32, i32, vp, vp, i32, i32, i32, vp, vp]),
         "rvcx_flash_attention": (i32, [vp, vp, i32, i32, i32, i32, ctypes.c_float, vp, vp, i32, vp, vp, vp]),

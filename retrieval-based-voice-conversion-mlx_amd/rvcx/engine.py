@@ -580,6 +580,35 @@ class Engine:
                                          m, _ptr(y), T_out, self.stream()), "conv1d")
         return y
 
+    def conv1d_gen(self, x, w, bias=None, dilation: int = 1, padding: int = 0, pre_slope: float = 0.1,
+                   slope=None, res=None, acc=None, acc_mode: int = 0, acc_div: float = 1.0,
+                   kernel: str = "policy"):
+        """The generator's fused conv (rvcx_conv1d_gen): y = acc(act(conv1d(pre(x), w, bias)) + res), pre = leaky
+        ReLU(pre_slope) unless pre_slope is None, act = leaky ReLU(slope) unless slope is None, acc_mode 0 store / 1 add
+        / 2 add-then-divide into `acc` (the
+        initial y); kernel "policy", "wsb" (weight-streamed) or "wst" (weight-stationary). x [T][C_in], w [N][C_in][taps]
+        -> [T_out][N] fp32 in the two-plane fp16 split."""
+        torch = self.torch
+        x = self._dev(x, torch.float32)
+        w = torch.as_tensor(w, dtype=torch.float32)
+        N, C, K = (int(v) for v in w.shape)
+        wk = self._dev(w.permute(2, 0, 1).contiguous(), torch.float32)
+        b = self._dev(bias, torch.float32) if bias is not None else None
+        r = self._dev(res, torch.float32) if res is not None else None
+        T = int(x.shape[0])
+        T_out = T + 2 * padding - dilation * (K - 1)
+        if acc is not None:
+            y = self._dev(acc, torch.float32).clone()
+        else:
+            y = torch.empty((T_out, N), dtype=torch.float32, device=self.device)
+        kn = {"policy": 0, "wsb": 1, "wst": 2}[kernel]
+        self._check(self.lib.rvcx_conv1d_gen(self.ctx, _ptr(x), T, C, _ptr(wk), _ptr(b), N, K, dilation, padding,
+                                             0 if pre_slope is None else 1,
+                                             0.0 if pre_slope is None else float(pre_slope), 0 if slope is None else 1,
+                                             0.0 if slope is None else float(slope), _ptr(r), int(acc_mode),
+                                             float(acc_div), kn, _ptr(y), self.stream()), "conv1d_gen")
+        return y
+
     def conv2d3x3(self, x, w, bias=None, relu: bool = False, math: str = "default"):
         """torch.nn.functional.conv2d(x.permute(2, 0, 1)[None], w, bias, padding=1)[0].permute(1, 2, 0) on the device
         kernel: x [H][W][C_in] (NHWC), w [N][C_in][3][3] (torch layout) -> [H][W][N] fp32 (rvcx_conv2d3x3); math

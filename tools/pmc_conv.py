@@ -8,7 +8,7 @@ import glob
 import sys
 
 tag = sys.argv[1] if len(sys.argv) > 1 else "pmc_c3_g23"
-kern = sys.argv[2:] or ["conv_gemm", "conv_emu", "conv_wsb", "conv_gs", "k_rb_pair"]
+kern = sys.argv[2:] or ["conv_gemm", "conv_emu", "conv_wsb", "conv_wst", "conv_gs", "k_rb_pair"]
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 cnt = collections.defaultdict(collections.Counter)
 for f in sorted(glob.glob(f"gpurun_out/{tag}_p*/**/*counter_collection.csv", recursive=True)):
