@@ -17,8 +17,12 @@
 //
 // Arithmetic: exactly conv_wsb16_kernel's (split_bf16.h put_h16x4 activations at 2^-4, the per-column-scaled
 // k_wsplit_h16 image, three v_mfma_f32_16x16x32_f16 products per (chunk, tap) step in the same order, acc + 2^-11 acc2
-// times the column's inverse scale, then store_tile16's epilogue order): the two kernels are bit-identical
-// (tests/test_gpu_conv_math.py::test_wst_matches_wsb).
+// times the column's inverse scale, then store_tile16's epilogue order), with the MFMA operands swapped (D = W X^T, so
+// a lane's accumulators are four channels of one time row): the two kernels are bit-identical
+// (tests/test_gpu_conv_wst.py compares them element for element). Measured against the weight-streamed tile it
+// replaces (profiles/r06t_ab_wst.txt): bench_conv C128 k3 198 -> 262 TF, the up3 phase group 151 -> 224, C2 -0.2 ms.
+// What bounds it (r06v/w variants): the MFMA loop alone runs 43 us of the 70 us C128 k3 launch and the loads, split
+// and stores alone 34 us (5.6 TB/s); a ping-pong schedule meant to overlap them measured slower (r06r/s).
 #include <algorithm>
 
 #include "conv_common.h"
@@ -63,7 +67,11 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wst16_kernel(const ConvArgs a
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lc = lane & 15, lg = lane >> 4;
-  const int n = wave * 16 + lc;  // the lane's output column
+  // MFMA orientation D[out channel][time] (A = the weight fragment, B = the activation fragment): accumulator element r
+  // of lane (lc, lg) is output channel n0 + r of time row lc of its 16-row block, so the epilogue moves 16 B per lane
+  // (four channels) where the [time][channel] orientation stored one float per lane and instruction (the epilogue's
+  // store issue, not HBM, was its cost)
+  const int n0 = wave * 16 + 4 * lg;  // the lane's four output channels
   const int per = (total + (int)gridDim.x - 1) / (int)gridDim.x;
   const int t_begin = blockIdx.x * per, t_end = min(total, t_begin + per);
   if (t_begin >= t_end) return;
@@ -78,9 +86,13 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wst16_kernel(const ConvArgs a
     for (int q = 0; q < 2; ++q)
       wr[it][q] = *reinterpret_cast<const f16x8*>(wsp + it * bstep + (size_t)wave * 2 * WST_WBLK + q * WST_WBLK +
                                                   lane * 16);
-  const float iv = reinterpret_cast<const float*>(wsp + NSTEP * bstep)[n];
+  const f32x4 iv = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(wsp + NSTEP * bstep) + n0);
   const bool has_bias = a.bias != nullptr;
-  const float bn = has_bias ? a.bias[n] : 0.f;
+  f32x4 bn = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (has_bias) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bn[r] = a.bias[n0 + r];
+  }
 
   // ---- tile cursors: a run's tiles are consecutive (batch-major), so each consumer (the row prefetch, the residual
   // prefetch, the epilogue) steps its own (batch, row tile) pair instead of dividing; element offsets inside one batch
@@ -135,17 +147,15 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wst16_kernel(const ConvArgs a
   f32x4 rv[TM16], dv[TM16];
   const int tlast_row = a.T_out - 1;
   auto load_rd = [&](const Cur& c) __attribute__((always_inline)) {
-    const float* R = NEED_R ? a.res + (long long)c.b * a.res_bs + n : nullptr;
-    const float* Y = a.y + (long long)c.b * a.y_bs + n;
-    const int m0 = c.mi * WST_BM + 4 * lg;
+    const float* R = NEED_R ? a.res + (long long)c.b * a.res_bs + n0 : nullptr;
+    const float* Y = a.y + (long long)c.b * a.y_bs + n0;
+    const int m0 = c.mi * WST_BM + lc;
 #pragma unroll
-    for (int tm = 0; tm < TM16; ++tm)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const unsigned m = (unsigned)min(m0 + tm * 16 + r, tlast_row);
-        if constexpr (NEED_R) rv[tm][r] = R[__umul24(m, (unsigned)a.ldr)];
-        if constexpr (NEED_D) dv[tm][r] = Y[__umul24(m, (unsigned)a.ldy)];
-      }
+    for (int tm = 0; tm < TM16; ++tm) {
+      const unsigned m = (unsigned)min(m0 + tm * 16, tlast_row);
+      if constexpr (NEED_R) rv[tm] = *reinterpret_cast<const f32x4*>(R + __umul24(m, (unsigned)a.ldr));
+      if constexpr (NEED_D) dv[tm] = *reinterpret_cast<const f32x4*>(Y + __umul24(m, (unsigned)a.ldy));
+    }
   };
 
   f32x4 acc[TM16], acc2[TM16];
@@ -175,35 +185,36 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wst16_kernel(const ConvArgs a
       __builtin_amdgcn_sched_barrier(0);
       const int it = u / TM16, tm = u - it * TM16;
       const f16x8 ah = af[u % RING][0], al = af[u % RING][1];
-      acc[tm] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wr[it][0], acc[tm], 0, 0, 0);
+      acc[tm] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[it][0], ah, acc[tm], 0, 0, 0);
       f32x4 c = acc2[tm];
-      c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, wr[it][0], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wr[it][1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[it][0], al, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[it][1], ah, c, 0, 0, 0);
       acc2[tm] = c;
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  // store_tile16's order of operations (bit-identical): (acc + 2^-11 acc2) * inv, + bias, act, + residual, accumulate,
-  // + the fused noise conv
+  // store_tile16's order of operations, per element: (acc + 2^-11 acc2) * inv, + bias, act, + residual, accumulate,
+  // + the fused noise conv (one tap: k_noise_add's y + (w x + b))
   auto epilogue = [&](const Cur& c) __attribute__((always_inline)) {
-    const int b = c.b, m0 = c.mi * WST_BM;
-    float* Yn = a.y + (long long)b * a.y_bs + n;
+    const int b = c.b;
+    float* Yn = a.y + (long long)b * a.y_bs + n0;
+    // the noise conv of these four columns (one phase p of nz_u: C % 4 == 0) -- conv_wst_fits admits nz_kk = 1 only
+    const float* hb = a.nz_har ? a.nz_har + (long long)b * a.nz_bs : nullptr;
+    const int nzp = a.nz_har ? n0 / a.nz_C : 0, nzc = a.nz_har ? n0 - nzp * a.nz_C : 0;
 #pragma unroll
     for (int tm = 0; tm < TM16; ++tm) {
-      const int mb = m0 + tm * 16 + 4 * lg;
-      bool ok[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) ok[r] = mb + r < a.T_out;
+      const int m = c.mi * WST_BM + tm * 16 + lc;
+      const bool ok = m < a.T_out;
       f32x4 v;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float x = acc[tm][r];
         x += acc2[tm][r] * H16_LO_INV;
-        v[r] = x * iv;
+        v[r] = x * iv[r];
       }
       if (has_bias) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += bn;
+        for (int r = 0; r < 4; ++r) v[r] += bn[r];
       }
       if (a.act == ACT_LRELU) {
 #pragma unroll
@@ -222,10 +233,15 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wst16_kernel(const ConvArgs a
           for (int r = 0; r < 4; ++r) v[r] = (dv[tm][r] + v[r]) / a.acc_div;
         }
       }
-      if (a.nz_har) noise_rows<1>(a, b, mb, n, ok, v);
+      if (hb) {
+        const float hx = hb[((long long)(ok ? m : 0) * a.nz_u + nzp) * a.nz_stride];
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (ok[r]) Yn[__umul24((unsigned)(mb + r), (unsigned)a.ldy)] = v[r];
+        for (int r = 0; r < 4; ++r) {
+          const float w = a.nz_w[(long long)(nzc + r) * a.nz_stride];
+          v[r] = v[r] + (fmaf(w, hx, 0.f) + a.nz_b[nzc + r]);
+        }
+      }
+      if (ok) *reinterpret_cast<f32x4*>(Yn + __umul24((unsigned)m, (unsigned)a.ldy)) = v;
     }
   };
 
@@ -305,9 +321,14 @@ hipError_t launch_wst_epi(const ConvArgs& a, hipStream_t s) {
 
 bool conv_wst_fits(const ConvArgs& a, bool two_d) {
   const bool vec_a = ((a.ldx & 3) == 0) && ((reinterpret_cast<uintptr_t>(a.x) & 15) == 0) && ((a.x_bs & 3) == 0);
+  // 16-byte epilogue operands: y / res rows (and their batch strides) 16-B aligned
+  const bool vec_y = ((reinterpret_cast<uintptr_t>(a.y) & 15) == 0) && (a.ldy & 3) == 0 && (a.y_bs & 3) == 0 &&
+                     (a.res_mode == RES_NONE ||
+                      (((reinterpret_cast<uintptr_t>(a.res) & 15) == 0) && (a.ldr & 3) == 0 && (a.res_bs & 3) == 0)) &&
+                     (!a.nz_har || (a.nz_C % 4 == 0 && a.nz_kk == 1));
   const bool shape = (a.C_in == 128 && a.N == 128 && (a.taps == 3 || a.taps == 2)) ||
                      (a.C_in == 64 && a.N == 64 && (a.taps == 3 || a.taps == 2));
-  return !two_d && shape && vec_a && a.wsb == 1 && a.wsplit && a.wsplit_fmt == WSPLIT_H16 && !a.lowp &&
+  return !two_d && shape && vec_a && vec_y && a.wsb == 1 && a.wsplit && a.wsplit_fmt == WSPLIT_H16 && !a.lowp &&
          a.wsplit_npad >= a.N && a.batch_inner == 1 && !a.b_kn && a.out_map == OUT_ROWS && a.stride == 1 &&
          a.dil >= 1 && (a.taps - 1) * a.dil <= WST_HMAX && (a.pre_act == ACT_LRELU || a.pre_act == ACT_NONE) &&
          !a.pre_mask && a.alpha == 1.f &&
