@@ -217,6 +217,151 @@ __device__ __forceinline__ void store_tile16(const ConvArgs& a, int m0, int n0, 
   }
 }
 
+// store_tile16 for the transposed accumulator layout D = W X^T (conv_wsb.hip): lane (lc, lg) of a 16x16 tile holds
+// row lc, columns 4 lg + r, so the residual / accumulate operands and the outputs move as one 16-byte vector per lane
+// and tile where the rows are 16-byte aligned (vec: N, the row strides and the bases multiples of 4 floats) -- a
+// quarter of store_tile16's memory instructions, whose issue rate, not HBM, bounded the epilogue. Same per-element
+// order of operations (bit-identical results); 1-D OUT_ROWS only.
+template <int TM16, int TN16, int WM, int WN>
+__device__ __forceinline__ void store_tile16t(const ConvArgs& a, int m0, int n0, int b, int zsplit, int ksplit,
+                                              long long Mtot, f32x4 (&acc)[TM16][TN16]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int lc = lane & 15, lg = lane >> 4;
+  const bool nvec = (a.N & 3) == 0;
+  if (ksplit > 1) {
+    float* W = a.ws + ((long long)b * ksplit + zsplit) * a.ws_rows * a.N;
+#pragma unroll
+    for (int tm = 0; tm < TM16; ++tm) {
+      const long long m = (long long)m0 + wm * TM16 * 16 + tm * 16 + lc;
+      if (m >= Mtot) continue;
+#pragma unroll
+      for (int tn = 0; tn < TN16; ++tn) {
+        const int n = n0 + wn * TN16 * 16 + tn * 16 + 4 * lg;
+        float* dst = W + m * a.N + n;
+        if (nvec && n + 3 < a.N) {
+          *reinterpret_cast<f32x4*>(dst) = acc[tm][tn];
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (n + r < a.N) dst[r] = acc[tm][tn][r];
+        }
+      }
+    }
+    return;
+  }
+  const float* bias = a.bias ? a.bias + (long long)b * a.bias_bs : nullptr;
+  const float* R = a.res ? a.res + (long long)b * a.res_bs : nullptr;
+  const float* MK = a.mask ? a.mask + (long long)b * a.mask_bs : nullptr;
+  float* Y = a.y + (long long)b * a.y_bs;
+  const bool need_r = R && a.res_mode != RES_NONE;
+  const bool need_d = a.acc_mode != ACC_STORE;
+  const int act = a.act;
+  const bool vec = nvec && ((reinterpret_cast<uintptr_t>(Y) & 15) == 0) && (a.ldy & 3) == 0 &&
+                   (!need_r || (((reinterpret_cast<uintptr_t>(R) & 15) == 0) && (a.ldr & 3) == 0));
+#pragma unroll
+  for (int tn = 0; tn < TN16; ++tn) {
+    const int n = n0 + wn * TN16 * 16 + tn * 16 + 4 * lg;
+    f32x4 bn = {0.f, 0.f, 0.f, 0.f};
+    if (bias) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bn[r] = n + r < a.N ? bias[n + r] : 0.f;
+    }
+#pragma unroll
+    for (int tm = 0; tm < TM16; ++tm) {
+      const long long m = (long long)m0 + wm * TM16 * 16 + tm * 16 + lc;
+      const bool m_ok = m < Mtot;
+      const bool full = m_ok && n + 3 < a.N;
+      bool ok[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ok[r] = m_ok && n + r < a.N;
+      f32x4 v = acc[tm][tn];
+      f32x4 rv = {0.f, 0.f, 0.f, 0.f}, dv = {0.f, 0.f, 0.f, 0.f};
+      float mv = 1.f;
+      // gather first (residual / accumulate / mask operands), then the arithmetic, then the stores
+      if (need_r) {
+        const float* src = R + m * a.ldr + n;
+        if (vec && full) {
+          rv = *reinterpret_cast<const f32x4*>(src);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) rv[r] = ok[r] ? src[r] : 0.f;
+        }
+      }
+      if (need_d) {
+        const float* src = Y + m * a.ldy + n;
+        if (vec && full) {
+          dv = *reinterpret_cast<const f32x4*>(src);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dv[r] = ok[r] ? src[r] : 0.f;
+        }
+      }
+      if (MK) mv = m_ok ? MK[m] : 1.f;
+      if (bias) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += bn[r];
+      }
+      if (a.res_mode == RES_ADD_PRE) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = v[r] + rv[r];
+      }
+      if (a.alpha != 1.f) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] *= a.alpha;
+      }
+      if (act == ACT_LRELU) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * a.slope;
+      } else if (act == ACT_RELU) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
+      } else if (act != ACT_NONE) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = act_fn_slow(v[r], act, a.slope);
+      }
+      if (a.res_mode == RES_ADD_POST) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = v[r] + rv[r];
+      } else if (a.res_mode == RES_RSUB_POST) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = rv[r] - v[r];
+      }
+      if (a.acc_mode == ACC_ADD) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = dv[r] + v[r];
+      } else if (a.acc_mode == ACC_ADD_DIV) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (dv[r] + v[r]) / a.acc_div;
+      }
+      if (a.nz_har) {
+        // the NSF noise conv of these 4 outputs, one tap (the dispatcher admits nz_kk = 1 only): k_noise_add's
+        // arithmetic, y + (w x + b)
+        const float* hb = a.nz_har + (long long)b * a.nz_bs;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          if (!ok[r]) continue;
+          const int p = (n + r) / a.nz_C, c = n + r - p * a.nz_C;
+          const float x = hb[(m * a.nz_u + p) * a.nz_stride];
+          v[r] = v[r] + (fmaf(a.nz_w[(long long)c * a.nz_stride], x, 0.f) + a.nz_b[c]);
+        }
+      }
+      if (MK) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] *= mv;
+      }
+      float* dst = Y + m * a.ldy + n;
+      if (vec && full) {
+        *reinterpret_cast<f32x4*>(dst) = v;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (ok[r]) dst[r] = v[r];
+      }
+    }
+  }
+}
+
 // Where a block tile sits: output rows m0.. (1-D) or the rh x rw pixel window at (h0, w0) (2-D), output channels
 // n0.., outer/inner batch (b, bi), split-K slice zsplit of ksplit for batch entry zb.
 struct TilePos {

@@ -105,7 +105,9 @@ __global__ void k_wsplit_h16(const float* __restrict__ w, int ldw, long long w_t
 // a 32x32x16 form of the fp16 kernel (round 6, same tile and image) measured slower on every generator shape (C128 k11
 // 352 vs 380 TF, k7 317 vs 340, C2 +0.2 ms; profiles/r06a_bench_conv_wsb32h.txt) although an MFMA of it blocks vector
 // issue for 8 of 32 cycles instead of 8 of 16.
-// C layout of a 16x16 tile: lane l holds column l % 16, rows 4 (l / 16) + r, r = 0..3.
+// The MFMA runs D = W X^T (weight fragment as the A operand): lane l of a 16x16 tile holds row (time) l % 16, columns
+// (output channels) 4 (l / 16) + r, r = 0..3, so the epilogue (store_tile16t) moves 16 B per lane (a [time][channel]
+// D held one float per lane and store: C128 k7 / k11 and C64 k11 ... r06 A/B in profiles/r06t_ab_wst.txt).
 // MODE: bits 0-1 the pre-activation (pre_fn), bit 2 a pre-mask row multiplier (conv_gs.hip's MODE), bit 4 the
 // two-plane fp16 arithmetic (split_bf16.h put_h16x4; weights from the k_wsplit_h16 image), bit 3 (with bit 4) the
 // opt-in reduced precision: the fp16 hi planes' product alone. The weight image comes from k_wsplit (bf16) or
@@ -226,11 +228,11 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
 #pragma unroll
         for (int tn = 0; tn < TN16; ++tn) {
           const f16x8 bh = __builtin_bit_cast(f16x8, bf[tn][0]);
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc[tm][tn], 0, 0, 0);
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, ah, acc[tm][tn], 0, 0, 0);
           if constexpr (!LOWP) {
             f32x4 c = acc2[tm][tn];
-            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, af[NQ - 1]), bh, c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, __builtin_bit_cast(f16x8, bf[tn][NQ - 1]), c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(bh, __builtin_bit_cast(f16x8, af[NQ - 1]), c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, bf[tn][NQ - 1]), ah, c, 0, 0, 0);
             acc2[tm][tn] = c;
           }
         }
@@ -239,12 +241,12 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
 #pragma unroll
       for (int tn = 0; tn < TN16; ++tn) {
         f32x4 c = acc[tm][tn];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[NQ - 1], bf[tn][0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[NQ / 2], bf[tn][NQ / 2], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[tn][NQ - 1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[NQ / 2], bf[tn][0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[tn][NQ / 2], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], bf[tn][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[tn][0], af[NQ - 1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[tn][NQ / 2], af[NQ / 2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[tn][NQ - 1], af[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[tn][0], af[NQ / 2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[tn][NQ / 2], af[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[tn][0], af[0], c, 0, 0, 0);
         acc[tm][tn] = c;
       }
     }
@@ -286,21 +288,22 @@ __global__ __launch_bounds__(CONV_THREADS, (BM / WM) * (BN / WN) > 64 * 32 ? 2 :
   }
   if constexpr (H16) {
     // acc + 2^-11 acc2, times 1 / (column weight scale x activation scale) from the image tail: exact powers of two
-    const float* inv = reinterpret_cast<const float*>(wsp + (size_t)total * bstep) + n0 + wn * TN16 * 16 + lc;
+    // (the image's padded columns carry scales too, so the 4-column vector is always in bounds)
+    const float* inv = reinterpret_cast<const float*>(wsp + (size_t)total * bstep) + n0 + wn * TN16 * 16 + 4 * lg;
 #pragma unroll
     for (int tn = 0; tn < TN16; ++tn) {
-      const float iv = inv[tn * 16];
+      const f32x4 iv = *reinterpret_cast<const f32x4*>(inv + tn * 16);
 #pragma unroll
       for (int tm = 0; tm < TM16; ++tm)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float v = acc[tm][tn][r];
           if constexpr (!LOWP) v += acc2[tm][tn][r] * H16_LO_INV;
-          acc[tm][tn][r] = v * iv;
+          acc[tm][tn][r] = v * iv[r];
         }
     }
   }
-  store_tile16<TM16, TN16, WM, WN>(a, m0, n0, b, zsplit, ksplit, (long long)a.T_out, acc);
+  store_tile16t<TM16, TN16, WM, WN>(a, m0, n0, b, zsplit, ksplit, (long long)a.T_out, acc);
 }
 
 template <int BM, int BN, int WM, int WN>
