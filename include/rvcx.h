@@ -467,8 +467,9 @@ int rvcx_flash_attention(rvcx_ctx* ctx, const float* d_qkv, int B, int T, int n_
  *     acc_mode 0: y = out; 1: y = y + out; 2: y = (y + out) / acc_div
  * Replaces one iteration of ResBlock.forward (rvc/lib/algorithm/residuals.py:71-80) and MRFLayer.forward
  * (generators/hifigan_mrf.py:45-50), plus the ResBlock mean of HiFiGANNSFGenerator.forward (hifigan_nsf.py:190-207)
- * on the last pair. C in {32, 64}, odd k, (k - 1) / 2 * dilation <= 30, else RVCX_E_SHAPE. cfg bits 0-3: the tile
- * (must be 0: the default tile); bits 4-5 the arithmetic: 0 the exact 3-plane bf16 split, 1 the two-plane
+ * on the last pair. C in {32, 64}, odd k, (k - 1) / 2 * dilation <= 30, else RVCX_E_SHAPE. cfg bits 0-3: 0 the
+ * default kernels (the k = 3, 32-channel fp16 pairs on the weight-resident form), 1 the streamed-weight kernel for
+ * every shape (comparisons; bit-identical results); bits 4-5 the arithmetic: 0 the exact 3-plane bf16 split, 1 the two-plane
  * fp16 split, 2 fp16 hi planes alone (the realtime reduced-precision mode). Exposed for numerics tests and A/B timing. */
 int rvcx_resblock_pair(rvcx_ctx* ctx, const float* d_x, int B, int64_t T, int C, const float* d_w1, const float* d_b1,
                        const float* d_w2, const float* d_b2, int k, int dilation, int acc_mode, float acc_div, int cfg,

@@ -437,6 +437,228 @@ __global__ __launch_bounds__(RB_THREADS, 3) void k_rb_pair(const RbPairArgs a, c
   }  // tiles
 }
 
+// The k = 3 pairs at 32 channels in the two-plane fp16 split (the 32-channel stage's first ResBlock, residuals.py:71-80
+// with d = 1, 3, 5): both convs' images -- 3 taps x 2 chunks x 2 planes, one 16-byte A fragment each per lane, 96
+// VGPRs -- are loaded into registers once per persistent workgroup, so the conv loops issue no global loads and the
+// next tile's x rows are prefetched into registers across both convs (in the streamed-weight form such a prefetch
+// stalled the first weight wait behind its HBM latency: vmcnt retires in issue order). Biases and inverse weight
+// scales sit in LDS. Same tile (128 rows, 126 outputs), the same MFMA sequence and epilogue order as k_rb_pair: the
+// results are bit-identical to it (tests/test_gpu_resblock_fused.py::test_k3_pair_matches_streamed_form).
+template <int ACCM>
+__global__ __launch_bounds__(RB_THREADS, 2) void k_rb_pair3(const RbPairArgs a, const int ntiles) {
+  constexpr int C = 32, NBT = 4, NCH = 2, NQ = 2, CB = NQ * 32, ROW = RbGeo<C, RB_F16X2>::ROW, NST = 3 * NCH;
+  constexpr int C4 = C / 4;
+  constexpr int XITER = ((NBT * 32 + 2 * RB_MAXH1) * C4 + RB_THREADS - 1) / RB_THREADS;
+  constexpr size_t QS = (size_t)C * 32;
+  typedef _Float16 f16x8_ __attribute__((ext_vector_type(8)));
+  extern __shared__ __attribute__((aligned(16))) char rb_smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, hk = lane >> 5;
+  const int h1 = a.d;  // conv1 halo (k = 3); conv2's is 1
+  const int nx = NBT * 32 + 2 * h1;
+  constexpr int TT = NBT * 32 - 2;
+  char* const XS = rb_smem;
+  char* const TS = rb_smem + (size_t)nx * ROW;
+  float* const prm = reinterpret_cast<float*>(TS + (size_t)(NBT * 32 + 2) * ROW);  // b1, inv1, b2, inv2
+  const int total = ntiles * a.B;
+  const int per = (total + (int)gridDim.x - 1) / (int)gridDim.x;
+  int tile = blockIdx.x * per;
+  const int tile_end = min(total, tile + per);
+  if (tile >= tile_end) return;
+
+  // ---- once: the weight fragments (A operand: out channel li, slots hk * 8 ..) and the per-channel constants
+  f16x8_ w1r[NST][NQ], w2r[NST][NQ];
+  {
+    const char* p1 = static_cast<const char*>(a.w1s) + (size_t)li * 32 + hk * 16;
+    const char* p2 = static_cast<const char*>(a.w2s) + (size_t)li * 32 + hk * 16;
+#pragma unroll
+    for (int st = 0; st < NST; ++st)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        w1r[st][q] = *reinterpret_cast<const f16x8_*>(p1 + (size_t)st * 2 * QS + q * QS);
+        w2r[st][q] = *reinterpret_cast<const f16x8_*>(p2 + (size_t)st * 2 * QS + q * QS);
+      }
+  }
+  if (tid < 4 * C) {
+    const int which = tid / C, c = tid % C;
+    const float* inv1 = reinterpret_cast<const float*>(static_cast<const char*>(a.w1s) + NST * 2 * QS);
+    const float* inv2 = reinterpret_cast<const float*>(static_cast<const char*>(a.w2s) + NST * 2 * QS);
+    prm[tid] = which == 0 ? a.b1[c] : which == 1 ? inv1[c] : which == 2 ? a.b2[c] : inv2[c];
+  }
+
+  // ---- x tile -> XS = split(lrelu(x)); row r <-> time t0 - 1 - h1 + r, zero outside [0, T) (conv1's padding)
+  f32x4 xv[XITER];
+  unsigned xok = 0u;  // rows outside [0, T) are loaded from row 0 and zeroed when split (no select on the loads)
+  auto load_x = [&](int tl) __attribute__((always_inline)) {
+    const int bb = tl / ntiles, tb = (tl - bb * ntiles) * TT - 1 - h1;
+    const float* Xb = a.x + (long long)bb * a.x_bs;
+    xok = 0u;
+#pragma unroll
+    for (int it = 0; it < XITER; ++it) {
+      const int i = it * RB_THREADS + tid;
+      const int r = i / C4, c4 = (i % C4) * 4;
+      const int t = tb + r;
+      const bool ok = r < nx && t >= 0 && t < a.T;
+      xv[it] = *reinterpret_cast<const f32x4*>(Xb + (long long)(ok ? t : 0) * C + c4);
+      xok |= ok ? (1u << it) : 0u;
+    }
+  };
+  auto write_x = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int it = 0; it < XITER; ++it) {
+      const int i = it * RB_THREADS + tid;
+      const int r = i / C4, c4 = (i % C4) * 4;
+      if (r < nx) {
+        const int s = c4 >> 4, o = c4 & 15;
+        const int slot = ((o >> 2) & 1) * 8 + (o >> 3) * 4;
+        char* row = XS + (size_t)r * ROW + s * CB + slot * 2;
+        const bool ok = (xok >> it) & 1u;
+        const float y0 = ok ? lrelu01(xv[it][0]) * RB_XS : 0.f, y1 = ok ? lrelu01(xv[it][1]) * RB_XS : 0.f,
+                    y2 = ok ? lrelu01(xv[it][2]) * RB_XS : 0.f, y3 = ok ? lrelu01(xv[it][3]) * RB_XS : 0.f;
+        uint2 hh, ll;
+        hh.x = pk_f16(y0, y1);
+        hh.y = pk_f16(y2, y3);
+        ll.x = pk_f16((y0 - f16lo_f(hh.x)) * H16_LO, (y1 - f16hi_f(hh.x)) * H16_LO);
+        ll.y = pk_f16((y2 - f16lo_f(hh.y)) * H16_LO, (y3 - f16hi_f(hh.y)) * H16_LO);
+        *reinterpret_cast<uint2*>(row) = hh;
+        *reinterpret_cast<uint2*>(row + 32) = ll;
+      }
+    }
+  };
+  // one conv over the wave's 32-row block: B fragments from LDS one step ahead (two register slots)
+  auto conv = [&](const char* bl, int dil, const f16x8_(&w)[NST][NQ], f32x16& acc, f32x16& acc2)
+                  __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = acc2[r] = 0.f;
+    f16x8_ bf[2][NQ];
+    auto load_b = [&](int st, f16x8_(&f)[NQ]) __attribute__((always_inline)) {
+      const int tap = st / NCH, s = st - tap * NCH;
+      const char* bp = bl + (size_t)tap * dil * ROW + s * CB;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) f[q] = *reinterpret_cast<const f16x8_*>(bp + q * 32);
+    };
+    load_b(0, bf[0]);
+#pragma unroll
+    for (int st = 0; st < NST; ++st) {
+      if (st + 1 < NST) load_b(st + 1, bf[(st + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      const f16x8_ bh = bf[st & 1][0];
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[st][0], bh, acc, 0, 0, 0);
+      acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[st][1], bh, acc2, 0, 0, 0);
+      acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[st][0], bf[st & 1][1], acc2, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // acc + 2^-11 acc2 times 1 / (channel weight scale x activation scale): element r is channel 8 (r / 4) + 4 hk + r % 4
+  auto finish = [&](f32x16& acc, const f32x16& acc2, const float* inv) __attribute__((always_inline)) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const f32x4 iv = *reinterpret_cast<const f32x4*>(inv + 8 * m + 4 * hk);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[4 * m + e] = (acc[4 * m + e] + acc2[4 * m + e] * H16_LO_INV) * iv[e];
+    }
+  };
+
+  load_x(tile);
+#pragma unroll 1
+  for (; tile < tile_end; ++tile) {
+    const int b = tile / ntiles;
+    const int t0 = (tile - b * ntiles) * TT;
+    write_x();
+    __syncthreads();  // XS complete; TS free (every wave's conv2 of the previous tile is done)
+    // this tile's residual (and accumulate) operands, then the next tile's rows: issued in the order they are used
+    const float* X = a.x + (long long)b * a.x_bs;
+    float* Y = a.y + (long long)b * a.y_bs;
+    const int o = wave * 32 + li;
+    const int t = t0 + o;
+    const bool out_ok = o < TT && t < a.T;
+    const long long off = (long long)(out_ok ? t : 0) * C + 4 * hk;
+    f32x4 rv[4], dv[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      rv[m] = *reinterpret_cast<const f32x4*>(X + off + 8 * m);
+      if constexpr (ACCM != ACC_STORE) dv[m] = *reinterpret_cast<const f32x4*>(Y + off + 8 * m);
+    }
+    load_x(min(tile + 1, tile_end - 1));
+    // conv1 -> TS = split(lrelu(conv1 + b1)); TS row p <-> time t0 - 1 + p, zero outside [0, T)
+    {
+      f32x16 acc, acc2;
+      conv(XS + (size_t)(wave * 32 + li) * ROW + hk * 16, a.d, w1r, acc, acc2);
+      finish(acc, acc2, prm + C);
+      const int p = wave * 32 + li;
+      const int tp = t0 - 1 + p;
+      const bool ok = tp >= 0 && tp < a.T;
+      char* row = TS + (size_t)p * ROW + hk * 16;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int r = 8 * hh + i;
+          const float bv = prm[8 * (r >> 2) + 4 * hk + (r & 3)];
+          const float x = lrelu01(acc[r] + bv);
+          v[i] = ok ? x * RB_XS : 0.f;
+        }
+        uint4 Hh, Ll;
+        split8_h16(v, Hh, Ll);
+        char* dst = row + hh * CB;
+        *reinterpret_cast<uint4*>(dst) = Hh;
+        *reinterpret_cast<uint4*>(dst + 32) = Ll;
+      }
+    }
+    __syncthreads();  // TS complete; XS free
+    // conv2 + b2 + x -> y (acc mode); output row o <-> time t0 + o
+    {
+      f32x16 acc, acc2;
+      conv(TS + (size_t)(wave * 32 + li) * ROW + hk * 16, 1, w2r, acc, acc2);
+      finish(acc, acc2, prm + 3 * C);
+      if (out_ok) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const f32x4 bv = *reinterpret_cast<const f32x4*>(prm + 2 * C + 8 * m + 4 * hk);
+          f32x4 o4;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float v = acc[4 * m + e] + bv[e];
+            v = v + rv[m][e];
+            if constexpr (ACCM == ACC_ADD) v = dv[m][e] + v;
+            else if constexpr (ACCM == ACC_ADD_DIV) v = (dv[m][e] + v) / a.acc_div;
+            o4[e] = v;
+          }
+          *reinterpret_cast<f32x4*>(Y + off + 8 * m) = o4;
+        }
+      }
+    }
+  }
+}
+
+template <int ACCM>
+hipError_t launch_rb3(const RbPairArgs& a, hipStream_t s) {
+  constexpr int ROW = RbGeo<32, RB_F16X2>::ROW;
+  const int TT = 4 * 32 - 2;
+  const size_t smem = (size_t)(4 * 32 + 2 * a.d) * ROW + (size_t)(4 * 32 + 2) * ROW + 4 * 32 * sizeof(float);
+  auto kern = k_rb_pair3<ACCM>;
+  static size_t smem_set = 64 * 1024;
+  if (smem > smem_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)smem);
+    if (e != hipSuccess) return e;
+    smem_set = smem;
+  }
+  const int ntiles = (a.T + TT - 1) / TT;
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || ncu <= 0)
+      ncu = 256;
+  }
+  const long long tiles = (long long)ntiles * a.B;
+  const int grid = (int)std::min<long long>(tiles, (long long)ncu * 2);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(RB_THREADS), smem, s, a, ntiles);
+  return hipGetLastError();
+}
+
 template <int C, int NBT, int TN, int MODE>
 hipError_t launch_rb_acc(const RbPairArgs& a, hipStream_t s) {
   constexpr int ROW = RbGeo<C, (MODE >> 2) & 3>::ROW;
@@ -512,15 +734,24 @@ hipError_t rb_wsplit_build(const float* w, int C, int k, void* out, hipStream_t 
 }
 
 // (C, NBT, TN) = 32: (4, 1), 64: (2, 1). The (8, 2) / (4, 2) tiles (two time blocks per wave) measured slower (+0.35 ms
-// in the C2 step) and are gone: cfg must be 0
+// in the C2 step) and are gone. cfg 0: the k = 3, 32-channel fp16 pairs on the weight-resident kernel (k_rb_pair3),
+// the rest on k_rb_pair; cfg 1: k_rb_pair for every shape (comparisons)
 hipError_t rb_pair(const RbPairArgs& a, int cfg, hipStream_t s) {
-  if (cfg != 0) return hipErrorInvalidValue;
+  if (cfg != 0 && cfg != 1) return hipErrorInvalidValue;
   if (!rb_pair_fits(a.C, a.k, a.d) || a.T < 1 || a.B < 1 || !a.x || !a.y || !a.w1s || !a.w2s || !a.b1 || !a.b2 ||
       a.x == a.y)
     return hipErrorInvalidValue;
   if ((reinterpret_cast<uintptr_t>(a.x) & 15) || (reinterpret_cast<uintptr_t>(a.y) & 15) || (a.x_bs & 3) ||
       (a.y_bs & 3))
     return hipErrorInvalidValue;
+  if (cfg == 0 && a.C == 32 && a.k == 3 && a.wfmt == RB_WF16 && !a.lowp) {
+    switch (a.acc_mode) {
+      case ACC_STORE: return launch_rb3<ACC_STORE>(a, s);
+      case ACC_ADD: return launch_rb3<ACC_ADD>(a, s);
+      case ACC_ADD_DIV: return launch_rb3<ACC_ADD_DIV>(a, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
   switch (a.C) {
     case 32: return launch_rb<32, 4, 1>(a, s);
     case 64: return launch_rb<64, 2, 1>(a, s);

@@ -149,3 +149,31 @@ def test_fused_pair_fp16_per_channel_weight_spread(engine, C, k, d):
         print(f"\nfused pair C{C} k{k} spread, cfg {cfg}: worst channel {err.max():.2e} (ch {int(err.argmax())}), "
               f"2^-20 channel {err[7]:.2e}")
         assert err.max() < bar, (cfg, float(err.max()), int(err.argmax()))
+
+
+@pytest.mark.parametrize("B,T,d,mode", [(1, 5000, 1, 0), (2, 4111, 3, 1), (1, 3001, 5, 2), (1, 17, 5, 0), (3, 127, 1, 2),
+                                        (1, 252, 3, 0), (1, 200003, 5, 1)])
+def test_k3_pair_matches_streamed_form(engine, B, T, d, mode):
+    """The k = 3, 32-channel fp16 pairs run on the weight-resident kernel (resblock_fused.hip k_rb_pair3: both convs'
+    images in registers, the next tile's rows prefetched across the convs). Same tile, MFMA sequence and epilogue
+    order as the streamed-weight kernel (cfg 1 forces it): bit-identical, on ragged lengths, batches, T below the halo,
+    exact multiples of the 126-row tile, a long run of tiles per workgroup, every dilation and accumulate mode; and
+    within the fp16 split's fp64 bar."""
+    rng = np.random.Generator(np.random.PCG64(31 * T + d + mode))
+    C, k = 32, 3
+    x = rng.standard_normal((B, T, C)).astype(np.float32)
+    acc = rng.standard_normal((B, T, C)).astype(np.float32) if mode else None
+    w1, b1, w2, b2 = _weights(rng, C, k)
+    y_res = engine.resblock_pair(x, w1, b1, w2, b2, d, acc=acc, acc_mode=mode, acc_div=3.0, cfg=1 << 4).cpu().numpy()
+    y_str = engine.resblock_pair(x, w1, b1, w2, b2, d, acc=acc, acc_mode=mode, acc_div=3.0,
+                                 cfg=(1 << 4) | 1).cpu().numpy()
+    assert np.array_equal(y_res, y_str), float(np.abs(y_res - y_str).max())
+    if T > 10000:
+        return
+    ref = _ref(x, w1, b1, w2, b2, d)
+    if mode:
+        ref = acc.astype(np.float64) + ref
+        if mode == 2:
+            ref = ref / 3.0
+    err = float(np.abs(y_res - ref).max() / np.abs(ref).max())
+    assert err < 6e-6, err
