@@ -180,6 +180,7 @@ int main(int argc, char** argv) {
       {"gen.s2 C128 k3 d1 res", 186000, 128, 128, 3, 1, 1},
       {"gen.up1 1550 512->12x256 t2", 1550, 512, 3072, 2, 1}, {"gen.up2 18600 256->10x128 t2", 18600, 256, 1280, 2, 1},
       {"gen.up3 186000 128->2x64 t2", 186000, 128, 128, 2, 1},
+      {"gen.s1 C256 k3 d1 res", 18600, 256, 256, 3, 1, 1}, {"gen.up2 18600 256->10x128 t3", 18600, 256, 1280, 3, 1},
   };
   for (size_t ci = 0; ci < cases.size(); ++ci) {
     if (only_case >= 0 && (int)ci != only_case) continue;
@@ -203,7 +204,7 @@ int main(int argc, char** argv) {
     const double flops = 2.0 * cs.T * cs.N * (double)cs.Cin * cs.taps;
     // variants: (cfg, math, pipe); cfg -1 = the library's policy for that math
     struct V { int cfg, math, pipe; };
-    std::vector<V> vars = {{-1, 2, 0}, {23, 2, -1}, {24, 2, -1}, {27, 2, -1}, {23, 3, -1}, {24, 3, -1}, {40, 3, -1},
+    std::vector<V> vars = {{-1, 2, 0}, {23, 2, -1}, {24, 2, -1}, {27, 2, -1}, {23, 3, -1}, {24, 3, -1}, {40, 3, -1}, {-1, 3, -1},
                            {27, 3, -1}, {25, 3, -1}, {23, 4, -1}, {27, 4, -1}, {13, 2, -1}, {1, 1, -1}};
     if (cs.taps == 1)
       for (int c : {10, 12, 13, 14, 15}) vars.push_back({c, 2, 1});
