@@ -19,6 +19,6 @@ for name, s, e in rows:
 tot = sum(fam.values())
 for k, v in sorted(fam.items(), key=lambda kv: -kv[1])[:12]:
     print(f"  {v:9.1f} us/step  {k[:90]}")
-for fam_name in ("conv_wsb16", "conv_gs", "k_rb_pair"):
+for fam_name in ("conv_wsb16", "conv_wst16", "conv_gs", "k_rb_pair"):
     print(f"  {sum(v for k, v in fam.items() if k.startswith(fam_name)):9.1f} us/step  all {fam_name}*")
 print(f"  {tot:9.1f} us/step  total over {n} steps")

@@ -14,7 +14,8 @@ import glob
 import os
 import sys
 
-FAMILY = ("conv_emu_kernel", "conv_wsb_kernel", "conv_wsb16_kernel", "conv_gs16_kernel", "conv_gsw16_kernel", "k_rb_pair",
+FAMILY = ("conv_emu_kernel", "conv_wsb_kernel", "conv_wsb16_kernel", "conv_wst16_kernel", "conv_gs16_kernel",
+          "conv_gsw16_kernel", "k_rb_pair",
           "conv_gemm_kernel", "conv_tiny", "k_conv2d_")  # conv_tiny(_rows)_kernel, k_conv2d_small / _h16
 
 

@@ -34,8 +34,8 @@ def load(d, counter):
 def main():
     d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
     keys = (sys.argv[2] if len(sys.argv) > 2 else
-            "conv_emu_kernel,conv_wsb_kernel,conv_wsb16_kernel,conv_gs16_kernel,conv_gsw16_kernel,k_rb_pair,conv_gemm_kernel,"
-            "conv_tiny,k_conv2d_").split(",")
+            "conv_emu_kernel,conv_wsb_kernel,conv_wsb16_kernel,conv_wst16_kernel,conv_gs16_kernel,conv_gsw16_kernel,k_rb_pair,"
+            "conv_gemm_kernel,conv_tiny,k_conv2d_").split(",")
     key = ",".join(keys)
     fam = lambda k: any(s in k for s in keys)  # noqa: E731
     bytes_fam = lambda k: fam(k) or "splitk_reduce" in k  # noqa: E731
@@ -50,7 +50,8 @@ def main():
            "note": "FETCH_SIZE doubled (gfx950 16-B/lane reads), WRITE_SIZE as is; KB counters x 1024"}
     # per kernel family (the names bench.py's roofline.dominant uses, rvcx_profile_kind_name): HBM bytes per launch of
     # the family's own kernels (its split-K combines are separate kernels, not attributed)
-    famnames = {"conv_wsb16_kernel": "conv_wsb16_kernel", "conv_wsb_kernel": "conv_wsb_kernel<",
+    famnames = {"conv_wsb16_kernel": "conv_wsb16_kernel", "conv_wst16_kernel": "conv_wst16_kernel",
+                "conv_wsb_kernel": "conv_wsb_kernel<",
                 "conv_gs16_kernel": "conv_gs16_kernel", "conv_gsw16_kernel": "conv_gsw16_kernel", "k_rb_pair": "k_rb_pair",
                 "k_conv2d_h16/k_conv2d_small": "k_conv2d_", "conv_emu_kernel": "conv_emu_kernel",
                 "conv_gemm_kernel": "conv_gemm_kernel", "conv_tiny_kernel": "conv_tiny"}
