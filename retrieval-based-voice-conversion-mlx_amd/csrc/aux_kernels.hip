@@ -680,6 +680,86 @@ hipError_t groupnorm_time_gelu(float* x, int T, int C, const float* gamma, const
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ HuBERT conv0 + GroupNorm + GELU, fused
+// conv_layers.0 (modeling_hubert.py HubertGroupNormConvLayer: Conv1d(1, C, 10, stride 5, bias=False) -> GroupNorm(C, C)
+// -> GELU). The conv is 10 MACs per output, so the statistics pass recomputes it instead of reading a stored copy, and
+// the apply pass computes it a third time and writes the normalized, activated output once: no conv output in HBM,
+// no read-modify-write pass (round 6; before: the conv on the 3-plane MFMA kernel at K = 5 x 2 taps, 65 us, then
+// k_gn_stats / k_gn_finalize / k_gn_apply over the stored 101 MB, 96 us). Every pass evaluates hconv0_at, one fp32 fma
+// chain over the 10 taps, so the statistics are those of the values the apply pass normalizes.
+__device__ __forceinline__ float hconv0_at(const float* __restrict__ xr, const float (&wr)[10]) {
+  float v = 0.f;
+#pragma unroll
+  for (int k = 0; k < 10; ++k) v = fmaf(wr[k], xr[k], v);
+  return v;
+}
+// grid (C/64, nchunks, B), block 256 = 64 channels x 4 row lanes: k_gn_stats's partial-sum layout (k_gn_finalize reads it)
+__global__ __launch_bounds__(256) void k_hconv0_stats(const float* __restrict__ x, long long ldx, const float* __restrict__ w,
+                                                      int T, int C, int chunk, double* __restrict__ ws) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;
+  const int t0 = blockIdx.y * chunk;
+  const int t1 = min(T, t0 + chunk);
+  x += (long long)blockIdx.z * ldx;
+  ws += (long long)blockIdx.z * gridDim.y * C * 2;
+  float wr[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) wr[k] = w[(long long)c * 10 + k];
+  double s = 0.0, q = 0.0;
+  for (int t = t0 + rl; t < t1; t += 4) {
+    const double v = hconv0_at(x + 5LL * t, wr);
+    s += v;
+    q += v * v;
+  }
+  __shared__ double ss[4][64], qq[4][64];
+  ss[rl][threadIdx.x & 63] = s;
+  qq[rl][threadIdx.x & 63] = q;
+  __syncthreads();
+  if (rl == 0) {
+    s = ss[0][threadIdx.x] + ss[1][threadIdx.x] + ss[2][threadIdx.x] + ss[3][threadIdx.x];
+    q = qq[0][threadIdx.x] + qq[1][threadIdx.x] + qq[2][threadIdx.x] + qq[3][threadIdx.x];
+    ws[((long long)blockIdx.y * C + c) * 2] = s;
+    ws[((long long)blockIdx.y * C + c) * 2 + 1] = q;
+  }
+}
+// block C/4 threads (thread = 4 channels, its 40 weights in registers), grid (rows, B): rows t = blockIdx.x + k gridDim.x
+__global__ void k_hconv0_apply(const float* __restrict__ x, long long ldx, const float* __restrict__ w, int T, int C,
+                               const float* __restrict__ ss, float* __restrict__ y) {
+  const int c0 = threadIdx.x * 4;
+  x += (long long)blockIdx.y * ldx;
+  y += (long long)blockIdx.y * T * C;
+  ss += (long long)blockIdx.y * 2 * C;
+  float wr[4][10];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int k = 0; k < 10; ++k) wr[j][k] = w[(long long)(c0 + j) * 10 + k];
+  const f32x4v sc = *reinterpret_cast<const f32x4v*>(ss + c0);
+  const f32x4v sh = *reinterpret_cast<const f32x4v*>(ss + C + c0);
+  for (int t = blockIdx.x; t < T; t += gridDim.x) {
+    const float* xr = x + 5LL * t;
+    f32x4v v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float u = hconv0_at(xr, wr[j]) * sc[j] + sh[j];  // k_gn_apply's arithmetic
+      v[j] = 0.5f * u * (1.f + erff(u * 0.70710678118654752440f));
+    }
+    *reinterpret_cast<f32x4v*>(y + (long long)t * C + c0) = v;
+  }
+}
+hipError_t hubert_conv0_gn_gelu(const float* x, long long ldx, const float* w10, int T, int C, const float* gamma,
+                                const float* beta, float eps, double* ws, float* y, hipStream_t s, int B) {
+  // ws: groupnorm_ws_doubles(C, B); x row b at x + b ldx holds >= 5 (T - 1) + 10 samples; y [B][T][C]
+  if (C % 64 || C > 1024 || B < 1 || B > 65535 || T < 1 || (reinterpret_cast<uintptr_t>(y) & 15)) return hipErrorInvalidValue;
+  const int nchunks = GN_CHUNKS;
+  const int chunk = (T + nchunks - 1) / nchunks;
+  float* ss = reinterpret_cast<float*>(ws + (size_t)B * nchunks * C * 2);
+  hipLaunchKernelGGL(k_hconv0_stats, dim3(C / 64, nchunks, B), dim3(256), 0, s, x, ldx, w10, T, C, chunk, ws);
+  hipLaunchKernelGGL(k_gn_finalize, dim3(C / 64, B), dim3(256), 0, s, ws, nchunks, T, C, gamma, beta, eps, ss);
+  hipLaunchKernelGGL(k_hconv0_apply, dim3((unsigned)std::min(T, 2048), B), dim3(C / 4), 0, s, x, ldx, w10, T, C, ss, y);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ RMVPE front end
 // grid.y = sequence: x rows of stride ldx, y rows of stride ldy
 // (a row stride ldy past the padded length gets its tail zeroed here: no fill launch before)

@@ -33,9 +33,12 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr unsigned SPIN_LIMIT = 1u << 22;  // default bound on the polls of one hand-off (RVCX_GRU_SPIN_LIMIT overrides)
 
 // gate activations on the hardware exp/rcp (v_exp_f32, v_rcp_f32): the libm expf/tanhf and IEEE divisions
-// were 0.14 us of every 1.5 us step; error <= ~2e-6 relative on sigmoid, ~1e-7 absolute on tanh
-__device__ __forceinline__ float sigm(float v) { return __frcp_rn(1.f + __expf(-v)); }
-__device__ __forceinline__ float tanh_g(float v) { return 1.f - 2.f * __frcp_rn(1.f + __expf(2.f * v)); }
+// were 0.14 us of every 1.5 us step (and __frcp_rn, used until round 6, is still the IEEE division sequence: three
+// dependent 10-instruction chains per step on the hand-off path); error <= ~2e-6 relative on sigmoid, ~1e-7 absolute
+// on tanh
+__device__ __forceinline__ float rcp_hw(float v) { return __builtin_amdgcn_rcpf(v); }
+__device__ __forceinline__ float sigm(float v) { return rcp_hw(1.f + __expf(-v)); }
+__device__ __forceinline__ float tanh_g(float v) { return 1.f - 2.f * rcp_hw(1.f + __expf(2.f * v)); }
 }  // namespace
 
 // Gate-major layout (round 5): a wave owns ONE gate of all 128 units of its workgroup and a 32-column group of each
@@ -57,6 +60,7 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir_g(const float* __restrict__
   __shared__ __attribute__((aligned(16))) float h_pw[NT / 64][CG];  // per-wave copy of its partner columns
   __shared__ float part[4][ROWS];
   __shared__ float bias_h[ROWS];
+  __shared__ float igl[3][UNITS];  // this step's input gates (staged from registers after the poll)
   __shared__ int abort_flag;
 
   const int w = blockIdx.x & 15;
@@ -116,17 +120,26 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir_g(const float* __restrict__
     O1 = (b0_.x + b1_.x) + (b0_.y + b1_.y);                                          \
   } while (0)
 
-  auto load_ig = [&](int s, float& ir, float& iz, float& in) {
+  auto load_ig = [&](int s, float (&ig)[3]) {
     const int t = d ? (T - 1 - s) : s;
     const int o = t * (6 * H) + d * 3 * H + gunit;
-    ir = gi[o];
-    iz = gi[o + H];
-    in = gi[o + 2 * H];
+    ig[0] = gi[o];
+    ig[1] = gi[o + H];
+    ig[2] = gi[o + 2 * H];
   };
-  float ig_r = 0.f, ig_z = 0.f, ig_n = 0.f;
+  // The input gates of step s + 1 are loaded right after step s's poll into `ig` (the gate threads), and staged to
+  // LDS right after step s + 1's poll, whose wait (vmcnt(0): the poll load is the newest) has retired them a whole step
+  // after their issue. Loaded at the top of their own step (round 5), their latency sat on the hand-off path: the
+  // poll's wait retires them in order, a few hundred ns after the issue.
+  float ig[3] = {0.f, 0.f, 0.f};
+  if (tid < UNITS) load_ig(0, ig);
+  const int oofs = d * H + gunit;
+  // retire every load issued so far (the W_hh registers) before the loop: otherwise the wait-count pass, merging the
+  // loop's entry with its back edge, keeps the weights "pending" and waits for them inside the loop with counts that
+  // also retire the input-gate loads just issued (vmcnt(0) in the partner dots)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt / lgkmcnt untouched (gfx9 encoding)
   for (int s = 0; s < T; ++s) {
     const int t = d ? (T - 1 - s) : s;
-    if (tid < UNITS) load_ig(s, ig_r, ig_z, ig_n);
     float own0 = 0.f, own1 = 0.f, par0v = 0.f, par1v = 0.f;
     if constexpr (MODE != 1) RVCX_GRU_DOT2(wo0, wo1, h_own + cg * CG, own0, own1);
     asm volatile("" : "+v"(own0), "+v"(own1));  // finish the own-column dots before polling
@@ -151,6 +164,12 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir_g(const float* __restrict__
       } else if (lane < CG) {
         hp[lane] = 0.f;
       }
+      if (tid < UNITS) {
+        igl[0][tid] = ig[0];
+        igl[1][tid] = ig[1];
+        igl[2][tid] = ig[2];
+        if (s + 1 < T) load_ig(s + 1, ig);
+      }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -170,13 +189,13 @@ __global__ __launch_bounds__(NT, 1) void k_gru_bidir_g(const float* __restrict__
       const float hn = ((part[0][2 * UNITS + tid] + part[1][2 * UNITS + tid]) +
                         (part[2][2 * UNITS + tid] + part[3][2 * UNITS + tid])) +
                        bias_h[2 * UNITS + tid];
-      const float rr = sigm(hr + ig_r);
-      const float zz = sigm(hz + ig_z);
-      const float nn = tanh_g(ig_n + hn * rr);
+      const float rr = sigm(hr + igl[0][tid]);
+      const float zz = sigm(hz + igl[1][tid]);
+      const float nn = tanh_g(igl[2][tid] + hn * rr);
       const float hprev = h_own[tid];
       const float hnew = (hprev - nn) * zz + nn;
       h_own[tid] = hnew;
-      out[(long long)t * (2 * H) + d * H + gunit] = hnew;
+      out[t * (2 * H) + oofs] = hnew;  // 32-bit offset on the scalar base (a 64-bit lane pointer spilled)
       const unsigned long long gg =
           ((unsigned long long)(tag0 + (unsigned)(s + 1)) << 32) | (unsigned long long)__float_as_uint(hnew);
       __hip_atomic_store(&mine[(s & 1) * UNITS + tid], gg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

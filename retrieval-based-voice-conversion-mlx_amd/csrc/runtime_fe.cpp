@@ -63,15 +63,8 @@ constexpr int POS_K = 128, POS_G = 16;
 // ================================================================== HuBERT
 void finalize_hubert(Ctx& c) {
   const int M = 1;
-  // conv0 (C_in 1, k 10, s 5) viewed as a 2-tap conv over 5-sample rows: W'[t][o][c] = W[o][0][5t + c]
-  {
-    auto& w = getw(c, M, "feature_extractor.conv_layers.0.conv.weight", {HCONV, 1, HK[0]});
-    std::vector<float> v((size_t)2 * HCONV * 5);
-    for (int t = 0; t < 2; ++t)
-      for (int o = 0; o < HCONV; ++o)
-        for (int cc = 0; cc < 5; ++cc) v[((size_t)t * HCONV + o) * 5 + cc] = w.v[(size_t)o * HK[0] + 5 * t + cc];
-    c.alloc_weight("hb.conv0", v);
-  }
+  // conv0 (C_in 1, k 10, s 5): [512][1][10] as is, the fused conv + GroupNorm + GELU kernel's [c][k] layout
+  c.alloc_weight("hb.conv0", getw(c, M, "feature_extractor.conv_layers.0.conv.weight", {HCONV, 1, HK[0]}).v);
   for (int i = 1; i < 7; ++i)
     c.alloc_weight("hb.conv" + std::to_string(i),
                    pack_conv1d(getw(c, M, "feature_extractor.conv_layers." + std::to_string(i) + ".conv.weight",
@@ -152,18 +145,10 @@ HubertRun hubert_front(Ctx& c, const float* audio, int64_t n, int64_t lda, int B
   float* a = c.buf<float>("hb.a", (size_t)B * T[1] * HCONV, s);
   float* b = c.buf<float>("hb.b", (size_t)B * T[2] * HCONV, s);
   double* gnws = c.buf<double>("hb.gnws", groupnorm_ws_doubles(HCONV, B), s);
-  {  // conv0 over 5-sample rows (2 taps)
-    ConvArgs a0 = lin(audio, 5, (int)(n / 5), 5, c.W("hb.conv0"), HCONV, nullptr, a, HCONV);
-    a0.taps = 2;
-    a0.w_ts = (long long)HCONV * 5;
-    a0.ldw = 5;
-    a0.T_out = (int)T[1];
-    a0.batch = B;
-    a0.x_bs = lda;
-    a0.y_bs = T[1] * HCONV;
-    run1(c, a0, s);
-  }
-  check(groupnorm_time_gelu(a, (int)T[1], HCONV, c.W("hb.gn.g"), c.W("hb.gn.b"), 1e-5f, gnws, s, B), "groupnorm");
+  // conv0 -> GroupNorm(512, 512) -> GELU in three launches (statistics, finalize, apply), the conv recomputed by each
+  check(hubert_conv0_gn_gelu(audio, lda, c.W("hb.conv0"), (int)T[1], HCONV, c.W("hb.gn.g"), c.W("hb.gn.b"), 1e-5f, gnws,
+                             a, s, B),
+        "hubert_conv0");
   float* cur = a;
   float* nxt = b;
   for (int i = 1; i < 7; ++i) {
@@ -221,7 +206,6 @@ HubertRun hubert_front(Ctx& c, const float* audio, int64_t n, int64_t lda, int B
 void hubert_layers(Ctx& c, const HubertRun& run, int l0, int l1, hipStream_t s) {
   const int B = run.B, L = run.L, BL = B * L;
   float* hs = c.buf<float>("hb.hs", (size_t)BL * HD, s);
-  float* hs2 = c.buf<float>("hb.hs2", (size_t)BL * HD, s);
   float* qkv = c.buf<float>("hb.qkv", (size_t)BL * 3 * HD, s);
   const int nsplit = flash_attn_splits(B, HHEADS, L);
   float* part_o = c.buf<float>("hb.fa_o", (size_t)flash_attn_ws_floats(B, HHEADS, L, HD / HHEADS, nsplit), s);
@@ -236,14 +220,15 @@ void hubert_layers(Ctx& c, const HubertRun& run, int l0, int l1, hipStream_t s) 
     check(flash_attn(qkv, 3 * HD, B, L, HHEADS, hd, (float)std::pow((double)hd, -0.5), nullptr, nullptr, 0, nullptr,
                      part_o, part_ml, nsplit, att, HD, s),
           "flash_attn");
-    {
-      ConvArgs a3 = lin(att, HD, BL, HD, c.W(q + ".o.w"), HD, c.W(q + ".o.b"), hs2, HD);
+    {  // hs = LN(hs + out_proj(att)) (layer_norm) in the split-K combine, in place: one combine block per row reads
+       // the row's residual before it writes the row (round 6: the combine + a separate LayerNorm pass before)
+      ConvArgs a3 = lin(att, HD, BL, HD, c.W(q + ".o.w"), HD, c.W(q + ".o.b"), hs, HD);
       a3.res = hs;
       a3.ldr = HD;
-      a3.res_mode = RES_ADD_POST;
+      a3.ln_g = c.W(q + ".ln1.g");
+      a3.ln_b = c.W(q + ".ln1.b");
       run1(c, a3, s);
     }
-    check(layernorm_rows(hs2, nullptr, hs, c.W(q + ".ln1.g"), c.W(q + ".ln1.b"), BL, HD, 1e-5f, nullptr, s), "ln1");
     {
       ConvArgs f1 = lin(hs, HD, BL, HD, c.W(q + ".ff1.w"), HFF, c.W(q + ".ff1.b"), ff, HFF);
       f1.act = ACT_GELU;

@@ -287,6 +287,10 @@ constexpr int GN_CHUNKS = 256;
 inline size_t groupnorm_ws_doubles(int C, int B = 1) { return (size_t)B * (GN_CHUNKS * C * 2 + C); }
 hipError_t groupnorm_time_gelu(float* x, int T, int C, const float* gamma, const float* beta, float eps,
                                double* ws, hipStream_t s, int B = 1);
+// HuBERT conv_layers.0 fused: y[b][t][c] = GELU(GroupNorm_c(sum_k w10[c][k] x[b ldx + 5t + k])), T rows, C % 64 == 0,
+// C <= 1024, y 16-byte aligned; ws as above (aux_kernels.hip)
+hipError_t hubert_conv0_gn_gelu(const float* x, long long ldx, const float* w10, int T, int C, const float* gamma,
+                                const float* beta, float eps, double* ws, float* y, hipStream_t s, int B = 1);
 hipError_t act_inplace(float* x, long long n, int act, float slope, hipStream_t s);
 hipError_t reflect_pad_1d(const float* x, int n, int pad_l, int pad_r, float* y, hipStream_t s, int B = 1,
                           long long ldx = 0, long long ldy = 0);

@@ -1,6 +1,7 @@
 """Critical-path view of one C2 step from a rocprofv3 kernel-trace database: per stream, the busy time and the
 span of each phase (high-pass, RMVPE, HuBERT, synthesizer) of step STEP (0-based, k_odd_ext marks a step start).
-usage: python tools/timeline.py RUN.db [STEP]"""
+usage: python tools/timeline.py RUN.db [STEP] [-v] [--mark=KERNEL] (--mark: another kernel marks a step start, e.g.
+k_reflect1d for a stand-alone RMVPE trace)"""
 import sqlite3
 import sys
 from collections import defaultdict
@@ -20,10 +21,11 @@ def phase(name):
 
 
 def main():
-    db, step = sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    db, step = sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2].isdigit() else 1
+    mark = next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--mark=")), "k_odd_ext")
     con = sqlite3.connect(db)
     rows = con.execute("select name, start, end, stream_id, queue_id from kernels order by start").fetchall()
-    starts = [r[1] for r in rows if "k_odd_ext" in r[0]]
+    starts = [r[1] for r in rows if mark in r[0]]
     t0 = starts[step]
     t1 = starts[step + 1] if step + 1 < len(starts) else max(r[2] for r in rows)
     sel = [r for r in rows if t0 <= r[1] < t1]
