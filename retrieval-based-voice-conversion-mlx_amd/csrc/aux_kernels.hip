@@ -280,7 +280,10 @@ hipError_t upconv_phase_pack(const float* w, int C, int co, float* out, hipStrea
 // read once for the 4 channels, y is read and written as one float4 (coalesced along the row). The weights are
 // staged once per block into LDS as [q][C] so each (q, 4 channels) is one 16-byte read. The per-channel sum runs
 // over q in order as an fma chain, then + bias, then + y (the separate-launch order it replaces).
+// STORE: y = sum + bias (the noise branch computed ahead into its own buffer, added later as the ConvTranspose's
+// residual: y_up + (sum + bias), the same single addition)
 constexpr int NOISE_LDS_FLOATS = 4096;
+template <bool STORE>
 __global__ __launch_bounds__(256) void k_noise_add(const float* __restrict__ har, long long har_bs, int stride,
                                                    int taps, const float* __restrict__ wf,
                                                    const float* __restrict__ nb, float* __restrict__ y, int B, int T,
@@ -318,21 +321,26 @@ __global__ __launch_bounds__(256) void k_noise_add(const float* __restrict__ har
       }
     }
     float4* yp = reinterpret_cast<float4*>(y + (long long)bt * C + c);
-    float4 v = *yp;
-    v.x = v.x + (acc.x + nb[c]);
-    v.y = v.y + (acc.y + nb[c + 1]);
-    v.z = v.z + (acc.z + nb[c + 2]);
-    v.w = v.w + (acc.w + nb[c + 3]);
-    *yp = v;
+    if constexpr (STORE) {
+      *yp = make_float4(acc.x + nb[c], acc.y + nb[c + 1], acc.z + nb[c + 2], acc.w + nb[c + 3]);
+    } else {
+      float4 v = *yp;
+      v.x = v.x + (acc.x + nb[c]);
+      v.y = v.y + (acc.y + nb[c + 1]);
+      v.z = v.z + (acc.z + nb[c + 2]);
+      v.w = v.w + (acc.w + nb[c + 3]);
+      *yp = v;
+    }
   }
 }
 hipError_t noise_conv_add(const float* har, long long har_bs, int stride, int taps, const float* wf, const float* nb,
-                          float* y, int B, int T, int C, hipStream_t s) {
+                          float* y, int B, int T, int C, hipStream_t s, bool store) {
   if (C % 4 != 0 || taps * stride > 16 || taps * stride < 1 || (reinterpret_cast<uintptr_t>(y) & 15) != 0 ||
       (long long)B * T * (C / 4) >= (1LL << 31) || taps * stride * C > NOISE_LDS_FLOATS)
     return hipErrorInvalidValue;
   // grid-stride over a capped grid: each block stages the weights once
-  hipLaunchKernelGGL(k_noise_add, dim3(std::min(nblocks((long long)B * T * (C / 4)), 4096u)), dim3(TB), 0, s, har,
+  hipLaunchKernelGGL(store ? k_noise_add<true> : k_noise_add<false>,
+                     dim3(std::min(nblocks((long long)B * T * (C / 4)), 4096u)), dim3(TB), 0, s, har,
                      har_bs, stride,
                      taps, wf, nb, y, B, T, C);
   return hipGetLastError();

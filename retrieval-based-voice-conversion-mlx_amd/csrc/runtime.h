@@ -319,8 +319,15 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
 // T - head frames (out [B][(T - head) upp], zp_out / z_out [B][T - head][I]); mp_out / logsp_out [B][T][I]
 // gen_lowp: the generator's weight-streamed convs and fused ResBlock pairs on fp16 operands (one MFMA product per
 // step): the realtime hop's opt-in (rvcx_rt_opts::gen_precision), never set by an offline entry point
+// noise_pre: the NSF source and the noise convs of the multi-tap stages were computed ahead by dec_noise_prepare (same
+// B, T, f0, eps_src, seed), on a stream this one has joined since; the ConvTransposes add them as their residual
 void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, const float* f0, const float* g,
-                 const float* eps_src, uint64_t seed, float* out, hipStream_t s, int gen_lowp = 0);
+                 const float* eps_src, uint64_t seed, float* out, hipStream_t s, int gen_lowp = 0,
+                 bool noise_pre = false);
+// the NSF harmonic source (SineGen) and every multi-tap noise conv (hifigan_nsf.py:196-199) into their own buffers:
+// the synthesizer issues it on the aux stream beside the TextEncoder and flow, which leave most of the GPU idle.
+// Returns false (nothing issued) for configurations without the NSF noise branch.
+bool dec_noise_prepare(Ctx& c, int B, int T, const float* f0, const float* eps_src, uint64_t seed, hipStream_t s);
 
 void set_highpass(Ctx& c, const double* b, const double* a, const double* zi, int order);
 void set_highpass_sos(Ctx& c, const double* sos, int nsec);

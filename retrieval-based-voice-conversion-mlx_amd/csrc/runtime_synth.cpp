@@ -345,37 +345,97 @@ void finalize_synth(Ctx& c) {
 
 // ------------------------------------------------------------------ generator
 // HiFiGANNSFGenerator.forward (generators/hifigan_nsf.py:173-212); z_btc [B][T][I] time-major.
+namespace {
+// noise_convs[i]'s framing for stage i (hifigan_nsf.py:184-199): stride = the product of the later upsample rates,
+// kernel 2 stride - stride % 2 (1 at the last stage), read from har at HAR_PAD - npad; ntap taps of `stride` samples
+struct NoiseFrame {
+  int stride = 1, kern = 1, npad = 0, ntap = 1;
+};
+NoiseFrame noise_frame(const SynthCfg& cf, size_t i) {
+  NoiseFrame f;
+  for (size_t j = i + 1; j < cf.ups.size(); ++j) f.stride *= cf.ups[j];
+  f.kern = f.stride == 1 ? 1 : f.stride * 2 - f.stride % 2;
+  f.npad = f.stride == 1 ? 0 : (f.kern - f.stride) / 2;
+  f.ntap = f.kern == 1 ? 1 : 2;
+  if (f.npad > HAR_PAD || f.ntap * f.stride - f.npad > HAR_PAD + f.stride)
+    throw Error(RVCX_E_SHAPE, "noise conv stride too large for the source padding");
+  return f;
+}
+bool noise_row_kernel(const NoiseFrame& f, int B, long long Ti, int C) {  // k_noise_add's limits
+  return f.ntap * f.stride <= 16 && C % 4 == 0 && (long long)B * Ti * (C / 4) < (1LL << 31) && f.ntap * f.stride * C <= 4096;
+}
+// NSF source (SineGen + l_linear + tanh) into the zero-padded rows of "dec.har"
+float* dec_source(Ctx& c, int B, int T, const float* f0, const float* eps_src, uint64_t seed, hipStream_t s) {
+  const SynthCfg& cf = c.scfg;
+  const int upp = cf.upp();
+  const long long Nh = (long long)T * upp;
+  // har rows carry HAR_PAD zeros on both sides so every framed noise-conv read stays in its row
+  const long long har_ld = Nh + 2 * HAR_PAD;
+  float* har = c.buf<float>("dec.har", (size_t)(B * har_ld), s);
+  // the pad columns stay zero from call to call (the sources write the interior only)
+  c.zero_once("dec.har", har, sizeof(float) * (size_t)(B * har_ld), har_ld * 65536 + B, s);
+  const auto& lin_wb = c.host[0].at("__src_lin__").v;
+  const uint64_t sseed = splitmix(seed ^ 0x5352434e4f495345ull);
+  if (cf.vocoder == 0) {  // NSF SineGen, harmonic_num 0 (hifigan.py:156-228)
+    double* cum = c.buf<double>("dec.cum", (size_t)B * T, s);
+    check(sine_source(f0, B, T, upp, (float)cf.sr, eps_src, sseed, lin_wb[0], lin_wb[1], cum, har + HAR_PAD, har_ld, s),
+          "sine_source");
+  } else {  // MRF: 9 harmonics, per-sample phase accumulation (hifigan_mrf.py:120-230)
+    const int Hs = cf.src_harmonics();
+    double* ws = c.buf<double>("dec.harm_ws", harm_source_ws_doubles(B, T, upp, Hs), s);
+    const float* ini = eps_src ? eps_src + (size_t)B * cf.src_noise_row(T) : nullptr;
+    check(harm_source(f0, B, T, upp, (float)cf.sr, Hs, 0, eps_src, ini, sseed, c.W("dec.src.w"), lin_wb[1], ws,
+                      har + HAR_PAD, har_ld, s),
+          "harm_source");
+  }
+  return har;
+}
+}  // namespace
+
+bool dec_noise_prepare(Ctx& c, int B, int T, const float* f0, const float* eps_src, uint64_t seed, hipStream_t s) {
+  const SynthCfg& cf = c.scfg;
+  if (!cf.f0 || cf.vocoder == 2 || !f0) return false;
+  const long long har_ld = (long long)T * cf.upp() + 2 * HAR_PAD;
+  float* har = dec_source(c, B, T, f0, eps_src, seed, s);
+  long long Ti = T;
+  for (size_t i = 0; i < cf.ups.size(); ++i) {
+    const int C = c.ups[i].cout;
+    Ti *= cf.ups[i];
+    const NoiseFrame f = noise_frame(cf, i);
+    if (f.ntap * f.stride == 1) continue;  // the one-tap stage stays in its ConvTranspose's epilogue (dec_forward)
+    const std::string nn = "dec.noise_convs." + std::to_string(i);
+    float* nz = c.buf<float>("dec.nz" + std::to_string(i), (size_t)B * Ti * C, s);
+    if (noise_row_kernel(f, B, Ti, C)) {
+      check(noise_conv_add(har + HAR_PAD - f.npad, har_ld, f.stride, f.ntap, c.W(nn + ".wf"), c.W(nn + ".b"), nz, B,
+                           (int)Ti, C, s, true),
+            "noise_conv");
+    } else {
+      ConvArgs an = conv(har + HAR_PAD - f.npad, f.stride, (int)Ti + f.ntap - 1, f.stride, c.W(nn + ".wf"), C, f.ntap, 1,
+                         0, c.W(nn + ".b"), nz, C, (int)Ti, B);
+      an.x_bs = har_ld;
+      run(c, an, s, 2.0 * B * (double)Ti * C * f.kern);
+    }
+  }
+  return true;
+}
+
+// ------------------------------------------------------------------ generator
+// HiFiGANNSFGenerator.forward (generators/hifigan_nsf.py:173-212); z_btc [B][T][I] time-major.
 void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, const float* f0, const float* g,
-                 const float* eps_src, uint64_t seed, float* out, hipStream_t s, int gen_lowp) {
+                 const float* eps_src, uint64_t seed, float* out, hipStream_t s, int gen_lowp, bool noise_pre) {
   const SynthCfg& cf = c.scfg;
   if (cf.f0 && cf.vocoder == 2) {
     refinegan_forward(c, B, T, z_btc, mask, f0, g, eps_src, seed, out, s);
     return;
   }
-  const int I = cf.I, C0 = cf.C0, upp = cf.upp();
-  const long long Nh = (long long)T * upp;
-  // NSF source (SineGen + l_linear + tanh)
-  // har rows carry HAR_PAD zeros on both sides so every framed noise-conv read stays in its row
-  const long long har_ld = Nh + 2 * HAR_PAD;
+  const int I = cf.I, C0 = cf.C0;
+  const long long har_ld = (long long)T * cf.upp() + 2 * HAR_PAD;
   float* har = nullptr;
   if (cf.f0) {
-    har = c.buf<float>("dec.har", (size_t)(B * har_ld), s);
-    // the pad columns stay zero from call to call (the sources write the interior only)
-    c.zero_once("dec.har", har, sizeof(float) * (size_t)(B * har_ld), har_ld * 65536 + B, s);
-    const auto& lin_wb = c.host[0].at("__src_lin__").v;
-    const uint64_t sseed = splitmix(seed ^ 0x5352434e4f495345ull);
-    if (cf.vocoder == 0) {  // NSF SineGen, harmonic_num 0 (hifigan.py:156-228)
-      double* cum = c.buf<double>("dec.cum", (size_t)B * T, s);
-      check(sine_source(f0, B, T, upp, (float)cf.sr, eps_src, sseed, lin_wb[0], lin_wb[1], cum, har + HAR_PAD,
-                        har_ld, s),
-            "sine_source");
-    } else {  // MRF: 9 harmonics, per-sample phase accumulation (hifigan_mrf.py:120-230)
-      const int Hs = cf.src_harmonics();
-      double* ws = c.buf<double>("dec.harm_ws", harm_source_ws_doubles(B, T, upp, Hs), s);
-      const float* ini = eps_src ? eps_src + (size_t)B * cf.src_noise_row(T) : nullptr;
-      check(harm_source(f0, B, T, upp, (float)cf.sr, Hs, 0, eps_src, ini, sseed, c.W("dec.src.w"), lin_wb[1], ws,
-                        har + HAR_PAD, har_ld, s),
-            "harm_source");
+    if (noise_pre) {
+      har = c.buf<float>("dec.har", (size_t)(B * har_ld), s);  // written by dec_noise_prepare
+    } else {
+      har = dec_source(c, B, T, f0, eps_src, seed, s);
     }
   }
   // conv_pre + cond(g)
@@ -422,19 +482,26 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
     // kernels (<= 16 taps) by a coalesced row kernel after it, one pass over y (in the epilogue, their 4 / 8 taps of
     // per-element loads cost more than the pass: stage 1 120 + 39 -> 173 us, stage 2 93 + 37 -> 130, r05q); the
     // long first-stage kernel as a framed implicit GEMM
-    int stride = 1, kern = 1, npad = 0, ntap = 1;
+    NoiseFrame nf;
+    int& stride = nf.stride;
+    int& kern = nf.kern;
+    int& npad = nf.npad;
+    int& ntap = nf.ntap;
     std::string nn;
     bool nz_fused = false;
     if (cf.f0) {
-      for (size_t j = i + 1; j < cf.ups.size(); ++j) stride *= cf.ups[j];
-      kern = stride == 1 ? 1 : stride * 2 - stride % 2;
-      npad = stride == 1 ? 0 : (kern - stride) / 2;
-      ntap = kern == 1 ? 1 : 2;
-      if (npad > HAR_PAD || ntap * stride - npad > HAR_PAD + stride)
-        throw Error(RVCX_E_SHAPE, "noise conv stride too large for the source padding");
+      nf = noise_frame(cf, i);
       nn = "dec.noise_convs." + std::to_string(i);
       const int kk = ntap * stride;
-      if (kk == 1 && conv_routes_wsb16(c, a)) {
+      if (noise_pre && kk > 1) {
+        // computed ahead (dec_noise_prepare): y = ups(x) + nz, the residual of this ConvTranspose's epilogue -- the
+        // same single addition as the accumulate pass after it (k_noise_add / the ACC_ADD conv), bit-identical
+        a.res = c.buf<float>("dec.nz" + std::to_string(i), (size_t)B * Ti * C, s);
+        a.ldr = u * C;
+        a.res_bs = (long long)Ti * C;
+        a.res_mode = RES_ADD_POST;
+        nz_fused = true;
+      } else if (kk == 1 && conv_routes_wsb16(c, a)) {
         a.nz_har = har + HAR_PAD - npad;
         a.nz_bs = har_ld;
         a.nz_stride = stride;
@@ -448,7 +515,7 @@ void dec_forward(Ctx& c, int B, int T, const float* z_btc, const float* mask, co
     }
     run(c, a, s, 2.0 * B * curT * (double)Cin * C * L.k);
     if (cf.f0 && !nz_fused) {
-      if (ntap * stride <= 16 && C % 4 == 0 && (long long)B * Ti * (C / 4) < (1LL << 31) && ntap * stride * C <= 4096) {
+      if (noise_row_kernel(nf, B, Ti, C)) {
         check(noise_conv_add(har + HAR_PAD - npad, har_ld, stride, ntap, c.W(nn + ".wf"), c.W(nn + ".b"), y, B, Ti,
                              C, s),
               "noise_conv_add");
@@ -660,6 +727,15 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
     maskf = m2;
   }
   if (zp_out) RVCX_HIP(hipMemcpyAsync(zp_out, z, BTf * I * sizeof(float), hipMemcpyDeviceToDevice, s));
+  // the decoder's NSF source and multi-tap noise convs depend on f0 alone: issued now on the aux stream, beside the
+  // flow's latency-bound chain, instead of between the decoder's ConvTransposes (kernel timing and RVCX_NO_OVERLAP
+  // keep them on this stream, fork_aux)
+  hipStream_t nax = s;
+  bool noise_pre = false;
+  if (cf.f0 && cf.vocoder != 2 && pitchff) {
+    nax = fork_aux(c, s);
+    noise_pre = dec_noise_prepare(c, B, Tf, pitchff, eps_src, seed, nax);
+  }
   // ---- flow reverse (residuals.py:151-164, 233-258; modules.py:78-109)
   // hs [BTf][2H]: the WaveNet residual stream h (columns [0, H)) and its skip sum (columns [H, 2H))
   float* hs = c.buf<float>("flow.hs", BTf * 2 * H, s);
@@ -719,7 +795,8 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
   }
   if (z_out) RVCX_HIP(hipMemcpyAsync(z_out, z, BTf * I * sizeof(float), hipMemcpyDeviceToDevice, s));
   // ---- dec(z * mask, nsff0, g)
-  dec_forward(c, B, Tf, z, maskf, pitchff, g, eps_src, seed, out, s, gen_lowp);
+  join_aux(c, s, nax);
+  dec_forward(c, B, Tf, z, maskf, pitchff, g, eps_src, seed, out, s, gen_lowp, noise_pre);
 }
 
 }  // namespace rvcx

@@ -256,8 +256,9 @@ constexpr int CREPE_RVC_BATCH = 512;  // rvc/lib/predictors/f0.py:38
 hipError_t crepe_decode_viterbi(const float* probs, int F, int minidx, int maxidx, const float* dither, float thr,
                                 float* lp, int* ptr, int* bins, float* f0_raw, float* per_raw, float* f0, double* f0d,
                                 float* per, hipStream_t s, int seg = CREPE_RVC_BATCH);
+// (store: y = the noise conv itself, not accumulated)
 hipError_t noise_conv_add(const float* har, long long har_bs, int stride, int taps, const float* wf, const float* nb,
-                          float* y, int B, int T, int C, hipStream_t s);
+                          float* y, int B, int T, int C, hipStream_t s, bool store = false);
 hipError_t upsample2_protect(const float* feats, const float* feats0, int L, int D, float* out, int T, const float* pitchf,
                              float protect,
                              hipStream_t s);

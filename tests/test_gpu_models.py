@@ -52,6 +52,21 @@ def test_dec_vs_reference(engine):
     assert rel_err(o, ref) < 2e-3, rel_err(o, ref)
 
 
+@pytest.mark.parametrize("name", ["synth_t64.npz", "synth_b2_ragged.npz"])
+def test_synth_noise_branch_ahead_is_bit_identical(engine, name):
+    """synth_infer issues the NSF source and the multi-tap noise convs ahead, on the aux stream beside the flow, and adds
+    them as the ConvTransposes' residual (runtime_synth.cpp dec_noise_prepare); dec_only keeps the in-line passes
+    (k_noise_add / the accumulating framed conv). The same single addition either way: the same bits for the same z,
+    f0 and seed (B = 1 and a ragged B = 2, whose masked z tails are zero in both)."""
+    g = golden(name)
+    out, zp, z = engine.synth_infer(g["phone"], g["lengths"], g["pitch"], g["f0"], g["sid"], eps_z=g["eps_z"], seed=77,
+                                    want_latents=True)
+    ref = engine.dec_only(z.transpose(1, 2).contiguous(), g["f0"], g["sid"], seed=77)
+    torch.cuda.synchronize()
+    assert out.shape == ref.shape
+    assert torch.equal(out, ref), float((out - ref).abs().max())
+
+
 def test_hubert_vs_reference(engine):
     g = golden("hubert_1s.npz")
     f = engine.hubert(g["audio"]).cpu().numpy()
