@@ -966,6 +966,9 @@ inline int pick_wsb(const ConvArgs& a) {
   static const int c_long = env_cfg("RVCX_WCFG_LONG", 0);
   if (a.wsb == 2) return 30;  // gather-streamed (conv_gs.hip): the short contractions
   if (a.N <= 32) return 24;
+  // the wide ConvTranspose phase group of the second upsample (18600 rows x 1280 columns, 2 taps) on 128 x 128 tiles:
+  // bench_conv r06a h25 254.6 vs h27 232.2 TF (the first one, 1550 rows x 3072, loses there: 189 vs 206)
+  if (a.taps <= 3 && a.N >= 1024 && a.T_out >= 8192 && a.C_in < 512 && c_long == 0) return 25;
   if (a.taps <= 3) return 27;
   if (c_long > 0) return c_long;
   return (a.C_in < 256 && a.N >= 128) ? 25 : 23;

@@ -650,7 +650,6 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
   float* part_o = c.buf<float>("te.fa_o", (size_t)flash_attn_ws_floats(B, nh, T, dk, nsplit), s);
   float* part_ml = c.buf<float>("te.fa_ml", (size_t)nsplit * B * nh * T * 2, s);
   float* att = c.buf<float>("te.att", BT * H, s);
-  float* o = c.buf<float>("te.o", BT * H, s);
   float* h1 = c.buf<float>("te.h1", BT * F, s);
   const float qscale = (float)(1.0 / std::sqrt((double)dk));
   for (int i = 0; i < cf.n_layers; ++i) {
@@ -662,8 +661,15 @@ void synth_forward(Ctx& c, int B, int T, const float* phone, const int32_t* leng
     check(flash_attn(qkv, 3 * H, B, T, nh, dk, qscale, c.W(q + ".rel_k"), c.W(q + ".rel_v"), cf.window,
                      c.synth_full_lengths ? nullptr : mask, part_o, part_ml, nsplit, att, H, s),
           "flash_attn");
-    run(c, lin(att, H, (int)BT, H, c.W(q + ".o.w"), H, c.W(q + ".o.b"), o, H), s);
-    check(layernorm_rows(x, o, x, c.W(q + ".ln1.g"), c.W(q + ".ln1.b"), (int)BT, H, 1e-5f, nullptr, s), "ln1");
+    {  // x = LN(x + conv_o(att)) (norm_layers_1, attentions.py:57-62) in the split-K combine, in place (one combine
+       // block per row reads the row's residual before writing it): one launch instead of the GEMM + a LayerNorm pass
+      ConvArgs a = lin(att, H, (int)BT, H, c.W(q + ".o.w"), H, c.W(q + ".o.b"), x, H);
+      a.res = x;
+      a.ldr = H;
+      a.ln_g = c.W(q + ".ln1.g");
+      a.ln_b = c.W(q + ".ln1.b");
+      run(c, a, s);
+    }
     {  // FFN (attentions.py:221-231): conv_1(pad(x*mask)) -> relu -> conv_2(pad(.*mask)) * mask
       ConvArgs a = conv(x, H, T, H, c.W(q + ".ffn1.w"), F, cf.ksize, 1, (cf.ksize - 1) / 2, c.W(q + ".ffn1.b"), h1,
                         F, T, B);
