@@ -340,7 +340,7 @@ hipError_t noise_conv_add(const float* har, long long har_bs, int stride, int ta
     return hipErrorInvalidValue;
   // grid-stride over a capped grid: each block stages the weights once
   hipLaunchKernelGGL(store ? k_noise_add<true> : k_noise_add<false>,
-                     dim3(std::min(nblocks((long long)B * T * (C / 4)), 4096u)), dim3(TB), 0, s, har,
+                     dim3(std::min(nblocks((long long)B * T * (C / 4)), store ? 512u : 4096u)), dim3(TB), 0, s, har,
                      har_bs, stride,
                      taps, wf, nb, y, B, T, C);
   return hipGetLastError();

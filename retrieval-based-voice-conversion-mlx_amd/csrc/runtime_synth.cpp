@@ -413,6 +413,7 @@ bool dec_noise_prepare(Ctx& c, int B, int T, const float* f0, const float* eps_s
       ConvArgs an = conv(har + HAR_PAD - f.npad, f.stride, (int)Ti + f.ntap - 1, f.stride, c.W(nn + ".wf"), C, f.ntap, 1,
                          0, c.W(nn + ".b"), nz, C, (int)Ti, B);
       an.x_bs = har_ld;
+      an.lds_pad = 64 * 1024;  // beside the flow's latency-bound chain: at most two of its workgroups per CU
       run(c, an, s, 2.0 * B * (double)Ti * C * f.kern);
     }
   }
